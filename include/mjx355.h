@@ -1,0 +1,212 @@
+/*
+ * mjx355 — MI355X-native batched humanoid physics step (C ABI).
+ *
+ * This header is the drop-in boundary for the reference's hot path. Each entry
+ * point names the reference interface it replaces. The reference calls MJX, a JAX library
+ * (mujoco-mjx==3.3.6, requirements.txt:27), from Python:
+ *
+ *   mujoco.MjModel.from_xml_path + mjx.put_model   src/training_utils.py:80,105
+ *                                                  mjx_humanoid_speed_test.py:25,28,44
+ *   mjx.make_data + mjx.forward                    src/envs.py:108-113 (single_pipeline_init)
+ *   mjx.step                                       src/envs.py:345, mjx_humanoid_speed_test.py:54
+ *   v_step = jit(vmap(single_step))                src/envs.py:333-495
+ *   v_reset + merge_if_done (auto-reset)           src/envs.py:115-202,494; train_ppo.py:149-161
+ *
+ * Conventions
+ *   - All device buffers are float32, C-contiguous, shape [nenv, dim] (one row per env).
+ *   - `stream` is a hipStream_t passed as void* (NULL = default stream). Calls are asynchronous.
+ *   - Return value 0 = OK; otherwise an error code and mjl_last_error() holds a message.
+ *   - A batch is thread-compatible, not thread-safe. One process per GPU.
+ *   - No allocation happens in step/forward/env calls (they can be captured in a hipGraph).
+ */
+#ifndef MJX355_H_
+#define MJX355_H_
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ---------------------------------------------------------------------------------------------
+ * Model descriptor: compiled model constants (float64), the data that mjx.put_model uploads.
+ * Filled by the host-side MJCF compiler (mjx_amd/mjcf.py). Capacities below bound the models
+ * the kernels accept; larger models are rejected at load time (MJL_ERR_UNSUPPORTED).
+ * ------------------------------------------------------------------------------------------- */
+#define MJL_MAXBODY 32
+#define MJL_MAXJNT 32
+#define MJL_MAXQ 48
+#define MJL_MAXV 32
+#define MJL_MAXGEOM 32
+#define MJL_MAXSITE 8
+#define MJL_MAXU 32
+#define MJL_MAXTENDON 4
+#define MJL_MAXTENWRAP 4
+#define MJL_MAXPAIR 256
+#define MJL_MAXSENSOR 4
+#define MJL_MAXOBS 64
+
+/* enums (MuJoCo numbering where one exists) */
+enum { MJL_GEOM_PLANE = 0, MJL_GEOM_SPHERE = 2, MJL_GEOM_CAPSULE = 3, MJL_GEOM_BOX = 6 };
+enum { MJL_JNT_FREE = 0, MJL_JNT_HINGE = 3 };
+enum { MJL_SOLVER_CG = 1, MJL_SOLVER_NEWTON = 2 };
+enum { MJL_INT_EULER = 0, MJL_INT_IMPLICITFAST = 3 };
+enum { MJL_COL_PLANE_SPHERE = 0, MJL_COL_PLANE_CAPSULE = 1, MJL_COL_SPHERE_SPHERE = 2,
+       MJL_COL_SPHERE_CAPSULE = 3, MJL_COL_CAPSULE_CAPSULE = 4 };
+enum { MJL_SENS_TOUCH = 0 };
+
+typedef struct mjlModelDesc {
+  int32_t nq, nv, nu, nbody, njnt, ngeom, nsite, ntendon, npair, nsensor, nsensordata;
+  int32_t iterations, ls_iterations, solver, integrator, eulerdamp;
+  double timestep, gravity[3], impratio, tolerance, ls_tolerance, meaninertia;
+
+  int32_t body_parentid[MJL_MAXBODY], body_rootid[MJL_MAXBODY], body_weldid[MJL_MAXBODY];
+  int32_t body_jntadr[MJL_MAXBODY], body_jntnum[MJL_MAXBODY];
+  int32_t body_dofadr[MJL_MAXBODY], body_dofnum[MJL_MAXBODY];
+  int32_t body_subtree_end[MJL_MAXBODY], body_level[MJL_MAXBODY];
+  double body_pos[MJL_MAXBODY][3], body_quat[MJL_MAXBODY][4], body_ipos[MJL_MAXBODY][3];
+  double body_inertia[MJL_MAXBODY][6]; /* body-frame tensor about ipos: xx yy zz xy xz yz */
+  double body_mass[MJL_MAXBODY], body_invweight0[MJL_MAXBODY][2];
+
+  int32_t jnt_type[MJL_MAXJNT], jnt_qposadr[MJL_MAXJNT], jnt_dofadr[MJL_MAXJNT];
+  int32_t jnt_bodyid[MJL_MAXJNT], jnt_limited[MJL_MAXJNT];
+  double jnt_pos[MJL_MAXJNT][3], jnt_axis[MJL_MAXJNT][3], jnt_range[MJL_MAXJNT][2];
+  double jnt_stiffness[MJL_MAXJNT], jnt_margin[MJL_MAXJNT];
+  double jnt_solref[MJL_MAXJNT][2], jnt_solimp[MJL_MAXJNT][5];
+
+  int32_t dof_bodyid[MJL_MAXV], dof_jntid[MJL_MAXV], dof_parentid[MJL_MAXV];
+  double dof_damping[MJL_MAXV], dof_armature[MJL_MAXV], dof_invweight0[MJL_MAXV];
+  double qpos0[MJL_MAXQ], qpos_spring[MJL_MAXQ];
+
+  int32_t geom_type[MJL_MAXGEOM], geom_bodyid[MJL_MAXGEOM];
+  double geom_pos[MJL_MAXGEOM][3], geom_quat[MJL_MAXGEOM][4], geom_size[MJL_MAXGEOM][3];
+
+  int32_t pair_geom1[MJL_MAXPAIR], pair_geom2[MJL_MAXPAIR], pair_kind[MJL_MAXPAIR];
+  int32_t pair_condim[MJL_MAXPAIR];
+  double pair_friction[MJL_MAXPAIR][5], pair_solref[MJL_MAXPAIR][2], pair_solimp[MJL_MAXPAIR][5];
+  double pair_margin[MJL_MAXPAIR], pair_gap[MJL_MAXPAIR];
+
+  int32_t site_type[MJL_MAXSITE], site_bodyid[MJL_MAXSITE];
+  double site_pos[MJL_MAXSITE][3], site_quat[MJL_MAXSITE][4], site_size[MJL_MAXSITE][3];
+
+  int32_t actuator_trnid[MJL_MAXU], actuator_ctrllimited[MJL_MAXU];
+  double actuator_gear[MJL_MAXU], actuator_ctrlrange[MJL_MAXU][2];
+
+  int32_t tendon_num[MJL_MAXTENDON], tendon_jnt[MJL_MAXTENDON][MJL_MAXTENWRAP];
+  int32_t tendon_limited[MJL_MAXTENDON];
+  double tendon_coef[MJL_MAXTENDON][MJL_MAXTENWRAP], tendon_range[MJL_MAXTENDON][2];
+  double tendon_margin[MJL_MAXTENDON], tendon_solref[MJL_MAXTENDON][2];
+  double tendon_solimp[MJL_MAXTENDON][5], tendon_invweight0[MJL_MAXTENDON];
+
+  int32_t sensor_type[MJL_MAXSENSOR], sensor_objid[MJL_MAXSENSOR], sensor_adr[MJL_MAXSENSOR];
+} mjlModelDesc;
+
+/* Env configuration: EnvConfig (reference src/config.py:29-66) with the flip permutation
+ * tables already expanded the way create_env_functions builds them (src/envs.py:48-74). */
+typedef struct mjlEnvConfig {
+  float progress_weight, electricity_cost, stall_torque_cost, posture_penalty_weight;
+  float tall_height_threshold, tall_bonus_weight, target_threshold, target_dist;
+  float stance_time_reward_weight, random_joint_noise, random_vel_noise, initial_velocity_max;
+  float terminate_height, terminate_reward;
+  int32_t stop_frames, max_episode_steps, random_flip;
+  int32_t pelvis_body_id, head_body_id, touch_sensor_right_id, touch_sensor_left_id;
+  int32_t obs_dim;
+  int32_t act_perm[MJL_MAXU];
+  float act_sign[MJL_MAXU];
+  int32_t obs_perm[MJL_MAXOBS];
+  float obs_sign[MJL_MAXOBS];
+} mjlEnvConfig;
+
+#define MJL_AUX_DIM 9 /* [flip, tx, ty, tz, close_count, stance, stance_time, last_pot, episode_step] */
+
+/* error codes */
+enum { MJL_OK = 0, MJL_ERR_ARG = 1, MJL_ERR_UNSUPPORTED = 2, MJL_ERR_HIP = 3, MJL_ERR_NOGPU = 4 };
+
+/* readable per-env fields (mjl_get / mjl_set) */
+enum {
+  MJL_FIELD_QPOS = 0,          /* [nq]   Data.qpos */
+  MJL_FIELD_QVEL = 1,          /* [nv]   Data.qvel */
+  MJL_FIELD_QACC_WARMSTART = 2,/* [nv]   Data.qacc_warmstart */
+  MJL_FIELD_TIME = 3,          /* [1]    Data.time */
+  MJL_FIELD_CTRL = 4,          /* [nu]   Data.ctrl */
+  MJL_FIELD_QACC = 5,          /* [nv]   Data.qacc (constrained forward acceleration) */
+  MJL_FIELD_XPOS = 6,          /* [nbody*3] Data.xpos (from the last forward pass) */
+  MJL_FIELD_XQUAT = 7,         /* [nbody*4] Data.xquat */
+  MJL_FIELD_QFRC_ACTUATOR = 8, /* [nv]   Data.qfrc_actuator */
+  MJL_FIELD_SENSORDATA = 9,    /* [nsensordata] Data.sensordata */
+  MJL_FIELD_AUX = 10,          /* [9]    env aux state (src/envs.py:15) */
+  MJL_FIELD_STATS = 11,        /* [4]    ncon_active, nefc_active, solver_iter, nan_flag */
+  MJL_FIELD_QFRC_BIAS = 12,    /* [nv]   Data.qfrc_bias */
+  MJL_FIELD_QFRC_PASSIVE = 13, /* [nv]   Data.qfrc_passive */
+  MJL_FIELD_QFRC_CONSTRAINT = 14, /* [nv] Data.qfrc_constraint */
+  MJL_FIELD_QACC_SMOOTH = 15,  /* [nv]   Data.qacc_smooth */
+  MJL_NFIELD = 16
+};
+
+typedef struct mjlModel mjlModel;
+typedef struct mjlBatch mjlBatch;
+
+/* Message of the last failing call on this thread. */
+const char* mjl_last_error(void);
+/* Library version string. */
+const char* mjl_version(void);
+
+/* Replaces mjx.put_model(MjModel) (src/training_utils.py:105): validate + upload constants.
+ * Host only; does not need a GPU until mjl_batch_create. */
+int mjl_model_create(const mjlModelDesc* desc, mjlModel** out);
+void mjl_model_destroy(mjlModel* model);
+/* Max constraint rows the model can produce (contacts + limits); sizes per-env scratch. */
+int mjl_model_nefc_max(const mjlModel* model);
+
+/* Replaces the batched mjx.make_data pytree (src/envs.py:110): owns per-env state on `device`,
+ * initialised like make_data (qpos = qpos0, everything else zero). */
+int mjl_batch_create(const mjlModel* model, int nenv, int device, mjlBatch** out);
+void mjl_batch_destroy(mjlBatch* batch);
+int mjl_batch_nenv(const mjlBatch* batch);
+
+/* Batch options. MJL_OPT_STORE_DERIVED (default 1): step/env kernels also write the derived
+ * per-env outputs (xpos, xquat, qacc, forces, sensordata, stats) readable with mjl_get; set 0 to
+ * keep only the state + env outputs in the hot loop. */
+enum { MJL_OPT_STORE_DERIVED = 0 };
+int mjl_batch_set_option(mjlBatch* batch, int option, int value);
+
+/* Copy a per-env field to / from a device buffer [nenv, dim] (async on stream). `mask` (device,
+ * float [nenv], may be NULL) restricts mjl_set to envs with mask > 0.5. */
+int mjl_get(mjlBatch* batch, int field, float* dst, void* stream);
+int mjl_set(mjlBatch* batch, int field, const float* src, const float* mask, void* stream);
+
+/* Replaces mjx.forward (src/envs.py:112): full forward pass, no integration, on envs with
+ * mask > 0.5 (mask may be NULL = all). Results readable via mjl_get. */
+int mjl_forward(mjlBatch* batch, const float* mask, void* stream);
+
+/* Replaces mjx.step (src/envs.py:345): ctrl (device [nenv, nu], may be NULL = keep current)
+ * -> forward + integrate, state updated in place. */
+int mjl_step(mjlBatch* batch, const float* ctrl, void* stream);
+
+/* Speed-test step (mjx_humanoid_speed_test.py:48-57): for each env e, a fresh make_data state
+ * with qvel[0] = vel[e], one step, out[e] = new qpos[0]. Stateless: does not touch the batch
+ * state (the batch only provides scratch and the model). */
+int mjl_speedtest_step(mjlBatch* batch, const float* vel, float* out, void* stream);
+
+/* Replaces create_env_functions' EnvConfig capture (src/envs.py:26-87). */
+int mjl_env_config(mjlBatch* batch, const mjlEnvConfig* cfg);
+
+/* Replaces v_step (src/envs.py:333-495) fused with the PPO auto-reset merge
+ * (train_ppo.py:147-161): act [nenv, nu] -> obs [nenv, obs_dim], rew/term/trunc [nenv].
+ * If auto_reset != 0, envs with max(term, trunc) > 0.5 are re-initialised in the same launch
+ * (single_reset semantics, src/envs.py:115-202, RNG stream (seed, counter, env)) and obs holds
+ * the post-reset observation, exactly as merge_if_done does; rew/term/trunc stay the step's. */
+int mjl_env_step(mjlBatch* batch, const float* act, float* obs, float* rew, float* term,
+                 float* trunc, int auto_reset, uint64_t seed, uint64_t counter, void* stream);
+
+/* Replaces v_reset (src/envs.py:115-202,494) restricted to envs with mask > 0.5 (mask may be
+ * NULL = all). obs [nenv, obs_dim] is written for reset envs only. `noise` (device, may be NULL)
+ * overrides the on-device RNG with explicit draws [nenv, nq-7 + nv + 2] in [0,1):
+ * joint-noise uniforms, velocity-noise uniforms, flip uniform, initial-speed uniform. */
+int mjl_env_reset(mjlBatch* batch, const float* mask, uint64_t seed, uint64_t counter,
+                  const float* noise, float* obs, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* MJX355_H_ */

@@ -1,0 +1,438 @@
+// mjx355 C ABI (include/mjx355.h): model upload, batch state ownership, kernel launches.
+// Host side only; the kernels live in physics.hip (same translation unit).
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <new>
+#include <string>
+
+#include "physics.hip"
+
+using namespace mjl;
+
+namespace {
+
+thread_local std::string g_err;
+
+int fail(int code, const char* fmt, ...) __attribute__((format(printf, 2, 3)));
+int fail(int code, const char* fmt, ...) {
+  char buf[512];
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(buf, sizeof(buf), fmt, ap);
+  va_end(ap);
+  g_err = buf;
+  return code;
+}
+
+#define HIPCHK(expr)                                                                   \
+  do {                                                                                 \
+    hipError_t e_ = (expr);                                                            \
+    if (e_ != hipSuccess) return fail(MJL_ERR_HIP, "%s: %s", #expr, hipGetErrorString(e_)); \
+  } while (0)
+
+}  // namespace
+
+struct mjlModel {
+  mjlModelDesc desc;
+  ModelF mf;
+  int nefc_max, ncon_max, nvc;
+};
+
+struct mjlBatch {
+  const mjlModel* model;
+  int device, nenv, store_derived;
+  ModelF* d_model;
+  mjlEnvConfig* d_env;
+  int has_env, obs_dim;
+  float* d_state;  // one slab holding every per-env field
+  StateBuf s;
+  int dim[MJL_NFIELD];
+  float* field_ptr[MJL_NFIELD];
+  float* d_scratch;
+  int scratch_stride, gmax_efc, gmax_con;
+};
+
+extern "C" {
+
+const char* mjl_last_error(void) { return g_err.c_str(); }
+const char* mjl_version(void) { return "mjx355 0.1 (gfx950)"; }
+
+static void q2m_host(const double* q, double* m) {
+  double w = q[0], x = q[1], y = q[2], z = q[3];
+  m[0] = 1 - 2 * (y * y + z * z); m[1] = 2 * (x * y - w * z); m[2] = 2 * (x * z + w * y);
+  m[3] = 2 * (x * y + w * z); m[4] = 1 - 2 * (x * x + z * z); m[5] = 2 * (y * z - w * x);
+  m[6] = 2 * (x * z - w * y); m[7] = 2 * (y * z + w * x); m[8] = 1 - 2 * (x * x + y * y);
+}
+
+int mjl_model_create(const mjlModelDesc* d, mjlModel** out) {
+  if (!d || !out) return fail(MJL_ERR_ARG, "null argument");
+  *out = nullptr;
+  if (d->nbody > MJL_MAXBODY || d->njnt > MJL_MAXJNT || d->nv > MJL_MAXV || d->nq > MJL_MAXQ ||
+      d->ngeom > MJL_MAXGEOM || d->nsite > MJL_MAXSITE || d->nu > MJL_MAXU || d->ntendon > MJL_MAXTENDON ||
+      d->npair > MJL_MAXPAIR || d->nsensor > MJL_MAXSENSOR || d->nbody < 2 || d->nv < 1)
+    return fail(MJL_ERR_UNSUPPORTED, "model sizes exceed kernel capacities");
+  if (d->nq - 7 + d->nv + 2 > 64) return fail(MJL_ERR_UNSUPPORTED, "too many reset draws for one wave");
+  if (d->solver != MJL_SOLVER_NEWTON && d->solver != MJL_SOLVER_CG)
+    return fail(MJL_ERR_UNSUPPORTED, "solver %d not supported (Newton, CG)", d->solver);
+  if (d->integrator != MJL_INT_EULER && d->integrator != MJL_INT_IMPLICITFAST)
+    return fail(MJL_ERR_UNSUPPORTED, "integrator %d not supported (Euler, implicitfast)", d->integrator);
+  mjlModel* M = new (std::nothrow) mjlModel();
+  if (!M) return fail(MJL_ERR_ARG, "out of host memory");
+  M->desc = *d;
+  ModelF& f = M->mf;
+  std::memset(&f, 0, sizeof(f));
+  f.nq = d->nq; f.nv = d->nv; f.nu = d->nu; f.nbody = d->nbody; f.njnt = d->njnt; f.ngeom = d->ngeom;
+  f.nsite = d->nsite; f.ntendon = d->ntendon; f.npair = d->npair; f.nsensor = d->nsensor;
+  f.nsensordata = d->nsensordata; f.iterations = d->iterations; f.ls_iterations = d->ls_iterations;
+  f.solver = d->solver; f.integrator = d->integrator; f.eulerdamp = d->eulerdamp;
+  f.timestep = (float)d->timestep; f.impratio = (float)d->impratio; f.tolerance = (float)d->tolerance;
+  f.ls_tolerance = (float)d->ls_tolerance; f.meaninertia = (float)d->meaninertia;
+  f.scale = (float)(1.0 / (d->meaninertia * (d->nv > 1 ? d->nv : 1)));
+  for (int i = 0; i < 3; i++) f.gravity[i] = (float)d->gravity[i];
+  int maxlevel = 0;
+  for (int b = 0; b < d->nbody; b++) {
+    f.body_parentid[b] = d->body_parentid[b]; f.body_rootid[b] = d->body_rootid[b];
+    f.body_jntadr[b] = d->body_jntadr[b]; f.body_jntnum[b] = d->body_jntnum[b];
+    f.body_dofadr[b] = d->body_dofadr[b]; f.body_dofnum[b] = d->body_dofnum[b];
+    f.body_subtree_end[b] = d->body_subtree_end[b]; f.body_level[b] = d->body_level[b];
+    if (d->body_level[b] > maxlevel) maxlevel = d->body_level[b];
+    for (int i = 0; i < 3; i++) { f.body_pos[b][i] = (float)d->body_pos[b][i]; f.body_ipos[b][i] = (float)d->body_ipos[b][i]; }
+    for (int i = 0; i < 4; i++) f.body_quat[b][i] = (float)d->body_quat[b][i];
+    for (int i = 0; i < 6; i++) f.body_inertia[b][i] = (float)d->body_inertia[b][i];
+    f.body_mass[b] = (float)d->body_mass[b];
+    f.body_invweight0[b][0] = (float)d->body_invweight0[b][0];
+    f.body_invweight0[b][1] = (float)d->body_invweight0[b][1];
+    if (b > 0 && d->body_parentid[b] >= b) { delete M; return fail(MJL_ERR_ARG, "bodies must be in DFS order"); }
+  }
+  f.maxlevel = maxlevel;
+  // dof masks along ancestor chains
+  for (int b = 1; b < d->nbody; b++) {
+    uint32_t mask = 0;
+    for (int bb = b; bb > 0; bb = d->body_parentid[bb])
+      for (int k = d->body_dofadr[bb]; k < d->body_dofadr[bb] + d->body_dofnum[bb]; k++) mask |= 1u << k;
+    f.body_dofmask[b] = mask;
+  }
+  int nlim = 0;
+  for (int j = 0; j < d->njnt; j++) {
+    if (d->jnt_type[j] != MJL_JNT_FREE && d->jnt_type[j] != MJL_JNT_HINGE) {
+      delete M; return fail(MJL_ERR_UNSUPPORTED, "joint type %d not supported", d->jnt_type[j]);
+    }
+    if (d->jnt_type[j] == MJL_JNT_FREE && d->body_jntadr[d->jnt_bodyid[j]] != j) {
+      delete M; return fail(MJL_ERR_UNSUPPORTED, "free joint must be the first joint of its body");
+    }
+    f.jnt_type[j] = d->jnt_type[j]; f.jnt_qposadr[j] = d->jnt_qposadr[j]; f.jnt_dofadr[j] = d->jnt_dofadr[j];
+    f.jnt_limited[j] = d->jnt_limited[j];
+    nlim += (d->jnt_limited[j] && d->jnt_type[j] == MJL_JNT_HINGE);
+    for (int i = 0; i < 3; i++) { f.jnt_pos[j][i] = (float)d->jnt_pos[j][i]; f.jnt_axis[j][i] = (float)d->jnt_axis[j][i]; }
+    f.jnt_range[j][0] = (float)d->jnt_range[j][0]; f.jnt_range[j][1] = (float)d->jnt_range[j][1];
+    f.jnt_stiffness[j] = (float)d->jnt_stiffness[j]; f.jnt_margin[j] = (float)d->jnt_margin[j];
+    f.jnt_solref[j][0] = (float)d->jnt_solref[j][0]; f.jnt_solref[j][1] = (float)d->jnt_solref[j][1];
+    for (int i = 0; i < 5; i++) f.jnt_solimp[j][i] = (float)d->jnt_solimp[j][i];
+  }
+  int anyd = 0;
+  for (int k = 0; k < d->nv; k++) {
+    f.dof_bodyid[k] = d->dof_bodyid[k]; f.dof_jntid[k] = d->dof_jntid[k]; f.dof_parentid[k] = d->dof_parentid[k];
+    f.dof_damping[k] = (float)d->dof_damping[k]; f.dof_armature[k] = (float)d->dof_armature[k];
+    f.dof_invweight0[k] = (float)d->dof_invweight0[k];
+    anyd |= d->dof_damping[k] > 0;
+  }
+  f.any_damping = anyd;
+  for (int i = 0; i < d->nq; i++) { f.qpos0[i] = (float)d->qpos0[i]; f.qpos_spring[i] = (float)d->qpos_spring[i]; }
+  for (int g = 0; g < d->ngeom; g++) {
+    f.geom_type[g] = d->geom_type[g]; f.geom_bodyid[g] = d->geom_bodyid[g];
+    double gm[9];
+    q2m_host(d->geom_quat[g], gm);
+    for (int i = 0; i < 3; i++) {
+      f.geom_pos[g][i] = (float)d->geom_pos[g][i];
+      f.geom_zaxis[g][i] = (float)gm[3 * i + 2];
+      f.geom_size[g][i] = (float)d->geom_size[g][i];
+    }
+  }
+  int ncon_max = 0, nefc_max = nlim;
+  for (int p = 0; p < d->npair; p++) {
+    int kind = d->pair_kind[p];
+    if (kind < MJL_COL_PLANE_SPHERE || kind > MJL_COL_CAPSULE_CAPSULE) {
+      delete M; return fail(MJL_ERR_UNSUPPORTED, "collision kind %d not supported", kind);
+    }
+    if (d->pair_condim[p] != 1 && d->pair_condim[p] != 3) {
+      delete M; return fail(MJL_ERR_UNSUPPORTED, "condim %d not supported", d->pair_condim[p]);
+    }
+    f.pair_geom1[p] = d->pair_geom1[p]; f.pair_geom2[p] = d->pair_geom2[p]; f.pair_kind[p] = kind;
+    f.pair_condim[p] = d->pair_condim[p];
+    f.pair_mu[p] = (float)d->pair_friction[p][0];
+    f.pair_solref[p][0] = (float)d->pair_solref[p][0]; f.pair_solref[p][1] = (float)d->pair_solref[p][1];
+    for (int i = 0; i < 5; i++) f.pair_solimp[p][i] = (float)d->pair_solimp[p][i];
+    f.pair_includemargin[p] = (float)(d->pair_margin[p] - d->pair_gap[p]);
+    int b1 = d->geom_bodyid[d->pair_geom1[p]], b2 = d->geom_bodyid[d->pair_geom2[p]];
+    double tran = d->body_invweight0[b1][0] + d->body_invweight0[b2][0];
+    if (d->pair_condim[p] == 1) f.pair_invweight[p] = (float)tran;
+    else {  // pyramidal: common invweight for every edge (constraint._efc_contact_pyramidal)
+      double mu = d->pair_friction[p][0];
+      double iw = tran + mu * mu * tran;
+      f.pair_invweight[p] = (float)(iw * 2 * mu * mu / d->impratio);
+    }
+    int nc = kind == MJL_COL_PLANE_CAPSULE ? 2 : 1;
+    ncon_max += nc;
+    nefc_max += nc * (d->pair_condim[p] == 1 ? 1 : 2 * (d->pair_condim[p] - 1));
+  }
+  for (int s = 0; s < d->nsite; s++) {
+    f.site_bodyid[s] = d->site_bodyid[s];
+    double sm[9];
+    q2m_host(d->site_quat[s], sm);
+    for (int i = 0; i < 9; i++) f.site_mat[s][i] = (float)sm[i];
+    for (int i = 0; i < 3; i++) { f.site_pos[s][i] = (float)d->site_pos[s][i]; f.site_size[s][i] = (float)d->site_size[s][i]; }
+  }
+  for (int u = 0; u < d->nu; u++) {
+    int j = d->actuator_trnid[u];
+    if (j < 0 || j >= d->njnt || d->jnt_type[j] != MJL_JNT_HINGE) {
+      delete M; return fail(MJL_ERR_UNSUPPORTED, "actuator %d: only hinge joint transmission supported", u);
+    }
+    f.actuator_dof[u] = d->jnt_dofadr[j];
+    f.actuator_ctrllimited[u] = d->actuator_ctrllimited[u];
+    f.actuator_gear[u] = (float)d->actuator_gear[u];
+    f.actuator_ctrlrange[u][0] = (float)d->actuator_ctrlrange[u][0];
+    f.actuator_ctrlrange[u][1] = (float)d->actuator_ctrlrange[u][1];
+  }
+  for (int t = 0; t < d->ntendon; t++) {
+    f.tendon_num[t] = d->tendon_num[t]; f.tendon_limited[t] = d->tendon_limited[t];
+    for (int w = 0; w < d->tendon_num[t]; w++) {
+      int j = d->tendon_jnt[t][w];
+      f.tendon_qadr[t][w] = d->jnt_qposadr[j];
+      f.tendon_dof[t][w] = d->jnt_dofadr[j];
+      f.tendon_coef[t][w] = (float)d->tendon_coef[t][w];
+    }
+    f.tendon_range[t][0] = (float)d->tendon_range[t][0]; f.tendon_range[t][1] = (float)d->tendon_range[t][1];
+    f.tendon_margin[t] = (float)d->tendon_margin[t];
+    f.tendon_solref[t][0] = (float)d->tendon_solref[t][0]; f.tendon_solref[t][1] = (float)d->tendon_solref[t][1];
+    for (int i = 0; i < 5; i++) f.tendon_solimp[t][i] = (float)d->tendon_solimp[t][i];
+    f.tendon_invweight0[t] = (float)d->tendon_invweight0[t];
+    nefc_max += d->tendon_limited[t];
+  }
+  for (int s = 0; s < d->nsensor; s++) {
+    if (d->sensor_type[s] != MJL_SENS_TOUCH) { delete M; return fail(MJL_ERR_UNSUPPORTED, "sensor type"); }
+    f.sensor_type[s] = d->sensor_type[s]; f.sensor_objid[s] = d->sensor_objid[s]; f.sensor_adr[s] = d->sensor_adr[s];
+  }
+  M->nefc_max = nefc_max;
+  M->ncon_max = ncon_max;
+  M->nvc = d->nv <= 27 ? 27 : 32;
+  if (d->nv < 27 && M->nvc == 27) M->nvc = 27;  // padded path handles nv < NVC
+  *out = M;
+  return MJL_OK;
+}
+
+void mjl_model_destroy(mjlModel* m) { delete m; }
+int mjl_model_nefc_max(const mjlModel* m) { return m ? m->nefc_max : -1; }
+
+int mjl_batch_create(const mjlModel* model, int nenv, int device, mjlBatch** out) {
+  if (!model || !out || nenv <= 0) return fail(MJL_ERR_ARG, "bad argument");
+  *out = nullptr;
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) return fail(MJL_ERR_NOGPU, "no HIP device available");
+  if (device < 0 || device >= ndev) return fail(MJL_ERR_ARG, "device %d out of range", device);
+  HIPCHK(hipSetDevice(device));
+  mjlBatch* B = new (std::nothrow) mjlBatch();
+  if (!B) return fail(MJL_ERR_ARG, "out of host memory");
+  std::memset(B, 0, sizeof(*B));
+  B->model = model; B->device = device; B->nenv = nenv; B->store_derived = 1;
+  const mjlModelDesc& d = model->desc;
+  int* dim = B->dim;
+  dim[MJL_FIELD_QPOS] = d.nq; dim[MJL_FIELD_QVEL] = d.nv; dim[MJL_FIELD_QACC_WARMSTART] = d.nv;
+  dim[MJL_FIELD_TIME] = 1; dim[MJL_FIELD_CTRL] = d.nu; dim[MJL_FIELD_QACC] = d.nv;
+  dim[MJL_FIELD_XPOS] = d.nbody * 3; dim[MJL_FIELD_XQUAT] = d.nbody * 4; dim[MJL_FIELD_QFRC_ACTUATOR] = d.nv;
+  dim[MJL_FIELD_SENSORDATA] = d.nsensordata > 0 ? d.nsensordata : 1; dim[MJL_FIELD_AUX] = MJL_AUX_DIM;
+  dim[MJL_FIELD_STATS] = 4; dim[MJL_FIELD_QFRC_BIAS] = d.nv; dim[MJL_FIELD_QFRC_PASSIVE] = d.nv;
+  dim[MJL_FIELD_QFRC_CONSTRAINT] = d.nv; dim[MJL_FIELD_QACC_SMOOTH] = d.nv;
+  size_t total = 0;
+  for (int f = 0; f < MJL_NFIELD; f++) total += (size_t)dim[f] * nenv;
+  hipError_t e = hipMalloc(&B->d_state, total * sizeof(float));
+  if (e != hipSuccess) { delete B; return fail(MJL_ERR_HIP, "hipMalloc state: %s", hipGetErrorString(e)); }
+  size_t off = 0;
+  for (int f = 0; f < MJL_NFIELD; f++) { B->field_ptr[f] = B->d_state + off; off += (size_t)dim[f] * nenv; }
+  StateBuf& s = B->s;
+  s.qpos = B->field_ptr[MJL_FIELD_QPOS]; s.qvel = B->field_ptr[MJL_FIELD_QVEL];
+  s.qacc_warmstart = B->field_ptr[MJL_FIELD_QACC_WARMSTART]; s.time = B->field_ptr[MJL_FIELD_TIME];
+  s.ctrl = B->field_ptr[MJL_FIELD_CTRL]; s.aux = B->field_ptr[MJL_FIELD_AUX]; s.qacc = B->field_ptr[MJL_FIELD_QACC];
+  s.xpos = B->field_ptr[MJL_FIELD_XPOS]; s.xquat = B->field_ptr[MJL_FIELD_XQUAT];
+  s.qfrc_actuator = B->field_ptr[MJL_FIELD_QFRC_ACTUATOR]; s.sensordata = B->field_ptr[MJL_FIELD_SENSORDATA];
+  s.stats = B->field_ptr[MJL_FIELD_STATS]; s.qfrc_bias = B->field_ptr[MJL_FIELD_QFRC_BIAS];
+  s.qfrc_passive = B->field_ptr[MJL_FIELD_QFRC_PASSIVE]; s.qfrc_constraint = B->field_ptr[MJL_FIELD_QFRC_CONSTRAINT];
+  s.qacc_smooth = B->field_ptr[MJL_FIELD_QACC_SMOOTH];
+  // make_data: zeros, qpos = qpos0
+  e = hipMemset(B->d_state, 0, total * sizeof(float));
+  if (e == hipSuccess) {
+    float* q = new float[(size_t)d.nq * nenv];
+    for (int i = 0; i < nenv; i++)
+      for (int k = 0; k < d.nq; k++) q[(size_t)i * d.nq + k] = (float)d.qpos0[k];
+    e = hipMemcpy(s.qpos, q, sizeof(float) * d.nq * nenv, hipMemcpyHostToDevice);
+    delete[] q;
+  }
+  if (e == hipSuccess) e = hipMalloc(&B->d_model, sizeof(ModelF));
+  if (e == hipSuccess) e = hipMemcpy(B->d_model, &model->mf, sizeof(ModelF), hipMemcpyHostToDevice);
+  if (e == hipSuccess) e = hipMalloc(&B->d_env, sizeof(mjlEnvConfig));
+  // global overflow rows for envs whose active constraints exceed the LDS capacity
+  int LD = model->nvc <= 28 ? 28 : 36;
+  B->gmax_efc = model->nefc_max > 0 ? model->nefc_max : 1;
+  B->gmax_con = model->ncon_max > 0 ? model->ncon_max : 1;
+  B->scratch_stride = B->gmax_efc * (LD + 8) + B->gmax_con * (CONW + 2);
+  B->scratch_stride = (B->scratch_stride + 3) & ~3;
+  if (e == hipSuccess) e = hipMalloc(&B->d_scratch, (size_t)B->scratch_stride * nenv * sizeof(float));
+  if (e != hipSuccess) {
+    (void)hipFree(B->d_state); (void)hipFree(B->d_model); (void)hipFree(B->d_env); (void)hipFree(B->d_scratch);
+    delete B;
+    return fail(MJL_ERR_HIP, "batch allocation: %s", hipGetErrorString(e));
+  }
+  *out = B;
+  return MJL_OK;
+}
+
+void mjl_batch_destroy(mjlBatch* B) {
+  if (!B) return;
+  (void)hipSetDevice(B->device);
+  (void)hipFree(B->d_state); (void)hipFree(B->d_model); (void)hipFree(B->d_env); (void)hipFree(B->d_scratch);
+  delete B;
+}
+
+int mjl_batch_nenv(const mjlBatch* B) { return B ? B->nenv : -1; }
+
+int mjl_batch_set_option(mjlBatch* B, int option, int value) {
+  if (!B) return fail(MJL_ERR_ARG, "null batch");
+  if (option == MJL_OPT_STORE_DERIVED) { B->store_derived = value != 0; return MJL_OK; }
+  return fail(MJL_ERR_ARG, "unknown option %d", option);
+}
+
+}  // extern "C"
+
+__global__ void masked_copy_kernel(float* dst, const float* src, const float* mask, int nenv, int dim) {
+  long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  long n = (long)nenv * dim;
+  if (i >= n) return;
+  int env = (int)(i / dim);
+  if (!mask || mask[env] > 0.5f) dst[i] = src[i];
+}
+
+extern "C" int mjl_get(mjlBatch* B, int field, float* dst, void* stream) {
+  if (!B || !dst || field < 0 || field >= MJL_NFIELD) return fail(MJL_ERR_ARG, "bad argument");
+  HIPCHK(hipSetDevice(B->device));
+  HIPCHK(hipMemcpyAsync(dst, B->field_ptr[field], sizeof(float) * (size_t)B->dim[field] * B->nenv,
+                        hipMemcpyDeviceToDevice, (hipStream_t)stream));
+  return MJL_OK;
+}
+
+extern "C" int mjl_set(mjlBatch* B, int field, const float* src, const float* mask, void* stream) {
+  if (!B || !src || field < 0 || field >= MJL_NFIELD) return fail(MJL_ERR_ARG, "bad argument");
+  HIPCHK(hipSetDevice(B->device));
+  long n = (long)B->dim[field] * B->nenv;
+  if (!mask) {
+    HIPCHK(hipMemcpyAsync(B->field_ptr[field], src, sizeof(float) * n, hipMemcpyDeviceToDevice, (hipStream_t)stream));
+  } else {
+    int threads = 256;
+    long blocks = (n + threads - 1) / threads;
+    hipLaunchKernelGGL(masked_copy_kernel, dim3((unsigned)blocks), dim3(threads), 0, (hipStream_t)stream,
+                       B->field_ptr[field], src, mask, B->nenv, B->dim[field]);
+    HIPCHK(hipGetLastError());
+  }
+  return MJL_OK;
+}
+
+static KParams make_params(mjlBatch* B) {
+  KParams P;
+  std::memset(&P, 0, sizeof(P));
+  P.m = B->d_model;
+  P.env = B->d_env;
+  P.s = B->s;
+  P.nenv = B->nenv;
+  P.store_derived = B->store_derived;
+  P.scratch = B->d_scratch;
+  P.scratch_stride = B->scratch_stride;
+  P.gmax_efc = B->gmax_efc;
+  P.gmax_con = B->gmax_con;
+  return P;
+}
+
+template <int MODE> static int launch(mjlBatch* B, const KParams& P, void* stream) {
+  HIPCHK(hipSetDevice(B->device));
+  dim3 grid(B->nenv), block(64);
+  if (B->model->nvc == 27)
+    hipLaunchKernelGGL((step_kernel<27, MODE>), grid, block, 0, (hipStream_t)stream, P);
+  else
+    hipLaunchKernelGGL((step_kernel<32, MODE>), grid, block, 0, (hipStream_t)stream, P);
+  HIPCHK(hipGetLastError());
+  return MJL_OK;
+}
+
+extern "C" {
+
+int mjl_forward(mjlBatch* B, const float* mask, void* stream) {
+  if (!B) return fail(MJL_ERR_ARG, "null batch");
+  KParams P = make_params(B);
+  P.mask = mask;
+  return launch<MODE_FORWARD>(B, P, stream);
+}
+
+int mjl_step(mjlBatch* B, const float* ctrl, void* stream) {
+  if (!B) return fail(MJL_ERR_ARG, "null batch");
+  KParams P = make_params(B);
+  P.in_ctrl = ctrl;
+  return launch<MODE_STEP>(B, P, stream);
+}
+
+int mjl_speedtest_step(mjlBatch* B, const float* vel, float* out, void* stream) {
+  if (!B || !vel || !out) return fail(MJL_ERR_ARG, "bad argument");
+  KParams P = make_params(B);
+  P.vel = vel;
+  P.out_speed = out;
+  P.store_derived = 0;
+  return launch<MODE_SPEEDTEST>(B, P, stream);
+}
+
+int mjl_env_config(mjlBatch* B, const mjlEnvConfig* cfg) {
+  if (!B || !cfg) return fail(MJL_ERR_ARG, "bad argument");
+  const mjlModelDesc& d = B->model->desc;
+  if (cfg->obs_dim <= 0 || cfg->obs_dim > 64) return fail(MJL_ERR_ARG, "obs_dim must be in 1..64");
+  if (cfg->obs_dim != 1 + 3 + (d.nq - 7) + d.nv + 2) return fail(MJL_ERR_ARG, "obs_dim does not match the model");
+  if (cfg->pelvis_body_id <= 0 || cfg->pelvis_body_id >= d.nbody || cfg->head_body_id <= 0 ||
+      cfg->head_body_id >= d.nbody)
+    return fail(MJL_ERR_ARG, "pelvis/head body id out of range");
+  if (cfg->touch_sensor_right_id < 0 || cfg->touch_sensor_right_id >= d.nsensordata ||
+      cfg->touch_sensor_left_id < 0 || cfg->touch_sensor_left_id >= d.nsensordata)
+    return fail(MJL_ERR_ARG, "touch sensor id out of range");
+  if (d.nbody < 2 || d.jnt_type[0] != MJL_JNT_FREE) return fail(MJL_ERR_UNSUPPORTED, "env needs a free-floating root");
+  for (int i = 0; i < d.nu; i++)
+    if (cfg->act_perm[i] < 0 || cfg->act_perm[i] >= d.nu) return fail(MJL_ERR_ARG, "act_perm out of range");
+  for (int i = 0; i < cfg->obs_dim; i++)
+    if (cfg->obs_perm[i] < 0 || cfg->obs_perm[i] >= cfg->obs_dim) return fail(MJL_ERR_ARG, "obs_perm out of range");
+  HIPCHK(hipSetDevice(B->device));
+  HIPCHK(hipMemcpy(B->d_env, cfg, sizeof(mjlEnvConfig), hipMemcpyHostToDevice));
+  B->has_env = 1;
+  B->obs_dim = cfg->obs_dim;
+  return MJL_OK;
+}
+
+int mjl_env_step(mjlBatch* B, const float* act, float* obs, float* rew, float* term, float* trunc, int auto_reset,
+                 uint64_t seed, uint64_t counter, void* stream) {
+  if (!B || !act || !obs || !rew || !term || !trunc) return fail(MJL_ERR_ARG, "bad argument");
+  if (!B->has_env) return fail(MJL_ERR_ARG, "mjl_env_config not called");
+  KParams P = make_params(B);
+  P.in_ctrl = act; P.obs = obs; P.rew = rew; P.term = term; P.trunc = trunc;
+  P.auto_reset = auto_reset;
+  P.seed_lo = (uint32_t)seed; P.seed_hi = (uint32_t)(seed >> 32);
+  P.ctr_lo = (uint32_t)counter; P.ctr_hi = (uint32_t)(counter >> 32);
+  return launch<MODE_ENV_STEP>(B, P, stream);
+}
+
+int mjl_env_reset(mjlBatch* B, const float* mask, uint64_t seed, uint64_t counter, const float* noise, float* obs,
+                  void* stream) {
+  if (!B) return fail(MJL_ERR_ARG, "null batch");
+  if (!B->has_env) return fail(MJL_ERR_ARG, "mjl_env_config not called");
+  KParams P = make_params(B);
+  P.mask = mask; P.noise = noise; P.obs = obs;
+  P.seed_lo = (uint32_t)seed; P.seed_hi = (uint32_t)(seed >> 32);
+  P.ctr_lo = (uint32_t)counter; P.ctr_hi = (uint32_t)(counter >> 32);
+  return launch<MODE_ENV_RESET>(B, P, stream);
+}
+
+}  // extern "C"

@@ -1,0 +1,83 @@
+// Device-side model constants (float32) and kernel parameter block.
+// Built on the host from mjlModelDesc (include/mjx355.h) by mjl_model_create; lives in device
+// global memory, read through the scalar/vector caches (a few KB, shared by every env).
+#pragma once
+#include <stdint.h>
+
+#include "../../include/mjx355.h"
+
+namespace mjl {
+
+struct ModelF {
+  int nq, nv, nu, nbody, njnt, ngeom, nsite, ntendon, npair, nsensor, nsensordata;
+  int iterations, ls_iterations, solver, integrator, eulerdamp, maxlevel, nlimited, any_damping;
+  float timestep, gravity[3], impratio, tolerance, ls_tolerance, meaninertia, scale;
+
+  int body_parentid[MJL_MAXBODY], body_rootid[MJL_MAXBODY], body_jntadr[MJL_MAXBODY];
+  int body_jntnum[MJL_MAXBODY], body_dofadr[MJL_MAXBODY], body_dofnum[MJL_MAXBODY];
+  int body_subtree_end[MJL_MAXBODY], body_level[MJL_MAXBODY];
+  uint32_t body_dofmask[MJL_MAXBODY];  // bit d set <=> dof d moves body b (ancestor chain)
+  float body_pos[MJL_MAXBODY][3], body_quat[MJL_MAXBODY][4], body_ipos[MJL_MAXBODY][3];
+  float body_inertia[MJL_MAXBODY][6], body_mass[MJL_MAXBODY], body_invweight0[MJL_MAXBODY][2];
+
+  int jnt_type[MJL_MAXJNT], jnt_qposadr[MJL_MAXJNT], jnt_dofadr[MJL_MAXJNT], jnt_limited[MJL_MAXJNT];
+  float jnt_pos[MJL_MAXJNT][3], jnt_axis[MJL_MAXJNT][3], jnt_range[MJL_MAXJNT][2];
+  float jnt_stiffness[MJL_MAXJNT], jnt_margin[MJL_MAXJNT], jnt_solref[MJL_MAXJNT][2];
+  float jnt_solimp[MJL_MAXJNT][5];
+
+  int dof_bodyid[MJL_MAXV], dof_jntid[MJL_MAXV], dof_parentid[MJL_MAXV];
+  float dof_damping[MJL_MAXV], dof_armature[MJL_MAXV], dof_invweight0[MJL_MAXV];
+  float qpos0[MJL_MAXQ], qpos_spring[MJL_MAXQ];
+
+  int geom_type[MJL_MAXGEOM], geom_bodyid[MJL_MAXGEOM];
+  float geom_pos[MJL_MAXGEOM][3], geom_zaxis[MJL_MAXGEOM][3], geom_size[MJL_MAXGEOM][3];
+
+  int pair_geom1[MJL_MAXPAIR], pair_geom2[MJL_MAXPAIR], pair_kind[MJL_MAXPAIR], pair_condim[MJL_MAXPAIR];
+  float pair_mu[MJL_MAXPAIR], pair_solref[MJL_MAXPAIR][2], pair_solimp[MJL_MAXPAIR][5];
+  float pair_includemargin[MJL_MAXPAIR], pair_invweight[MJL_MAXPAIR];  // invweight incl. pyramid factor
+
+  int site_bodyid[MJL_MAXSITE];
+  float site_pos[MJL_MAXSITE][3], site_mat[MJL_MAXSITE][9], site_size[MJL_MAXSITE][3];
+
+  int actuator_dof[MJL_MAXU], actuator_ctrllimited[MJL_MAXU];
+  float actuator_gear[MJL_MAXU], actuator_ctrlrange[MJL_MAXU][2];
+
+  int tendon_num[MJL_MAXTENDON], tendon_qadr[MJL_MAXTENDON][MJL_MAXTENWRAP];
+  int tendon_dof[MJL_MAXTENDON][MJL_MAXTENWRAP], tendon_limited[MJL_MAXTENDON];
+  float tendon_coef[MJL_MAXTENDON][MJL_MAXTENWRAP], tendon_range[MJL_MAXTENDON][2];
+  float tendon_margin[MJL_MAXTENDON], tendon_solref[MJL_MAXTENDON][2], tendon_solimp[MJL_MAXTENDON][5];
+  float tendon_invweight0[MJL_MAXTENDON];
+
+  int sensor_type[MJL_MAXSENSOR], sensor_objid[MJL_MAXSENSOR], sensor_adr[MJL_MAXSENSOR];
+};
+
+enum Mode { MODE_FORWARD = 0, MODE_STEP = 1, MODE_SPEEDTEST = 2, MODE_ENV_STEP = 3, MODE_ENV_RESET = 4 };
+
+// per-env state rows, [nenv, dim] each
+struct StateBuf {
+  float *qpos, *qvel, *qacc_warmstart, *time, *ctrl, *aux;
+  // derived (outputs of the last forward pass)
+  float *qacc, *xpos, *xquat, *qfrc_actuator, *sensordata, *stats;
+  float *qfrc_bias, *qfrc_passive, *qfrc_constraint, *qacc_smooth;
+};
+
+struct KParams {
+  const ModelF* m;
+  const mjlEnvConfig* env;
+  StateBuf s;
+  int nenv;
+  int store_derived;
+  int auto_reset;
+  const float* in_ctrl;   // [nenv, nu] or null
+  const float* mask;      // [nenv] or null
+  const float* noise;     // [nenv, nq-7+nv+2] or null
+  const float* vel;       // speed test input
+  float* out_speed;       // speed test output
+  float *obs, *rew, *term, *trunc;
+  float* scratch;         // global overflow rows, [nenv, scratch_stride]
+  int scratch_stride;    // floats per env
+  int gmax_efc, gmax_con; // row / contact capacity of one scratch slab
+  uint32_t seed_lo, seed_hi, ctr_lo, ctr_hi;
+};
+
+}  // namespace mjl

@@ -1,0 +1,74 @@
+"""Loader for the native library libmjx355.so (C ABI declared in include/mjx355.h).
+
+The library is built in-tree (`mujoco-mjx-lab_amd/csrc/Makefile`, or `__graft_entry__.build()`).
+There is no fallback: every entry point of the product path goes through this library, and a
+missing library or GPU raises.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import subprocess
+
+from . import abi
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libmjx355.so")
+CSRC = os.path.join(os.path.dirname(_HERE), "csrc")
+
+# every symbol include/mjx355.h declares
+EXPORTS = [
+    "mjl_last_error", "mjl_version", "mjl_model_create", "mjl_model_destroy", "mjl_model_nefc_max",
+    "mjl_batch_create", "mjl_batch_destroy", "mjl_batch_nenv", "mjl_batch_set_option", "mjl_get", "mjl_set",
+    "mjl_forward", "mjl_step", "mjl_speedtest_step", "mjl_env_config", "mjl_env_step", "mjl_env_reset",
+]
+
+_lib = None
+
+
+class MjlError(RuntimeError):
+    pass
+
+
+def build(force: bool = False):
+    args = ["make", "-s", "-C", CSRC]
+    if force:
+        args.append("-B")
+    subprocess.run(args, check=True)
+
+
+def lib() -> C.CDLL:
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise MjlError(f"native library missing: {LIB_PATH} (run `make -C {CSRC}` or __graft_entry__.build())")
+    L = C.CDLL(LIB_PATH)
+    P, vp, f32p, i32 = C.POINTER, C.c_void_p, C.c_void_p, C.c_int
+    u64 = C.c_uint64
+    L.mjl_last_error.restype = C.c_char_p
+    L.mjl_version.restype = C.c_char_p
+    L.mjl_model_create.argtypes = [P(abi.ModelDesc), P(vp)]
+    L.mjl_model_destroy.argtypes = [vp]
+    L.mjl_model_destroy.restype = None
+    L.mjl_model_nefc_max.argtypes = [vp]
+    L.mjl_batch_create.argtypes = [vp, i32, i32, P(vp)]
+    L.mjl_batch_destroy.argtypes = [vp]
+    L.mjl_batch_destroy.restype = None
+    L.mjl_batch_nenv.argtypes = [vp]
+    L.mjl_batch_set_option.argtypes = [vp, i32, i32]
+    L.mjl_get.argtypes = [vp, i32, f32p, vp]
+    L.mjl_set.argtypes = [vp, i32, f32p, f32p, vp]
+    L.mjl_forward.argtypes = [vp, f32p, vp]
+    L.mjl_step.argtypes = [vp, f32p, vp]
+    L.mjl_speedtest_step.argtypes = [vp, f32p, f32p, vp]
+    L.mjl_env_config.argtypes = [vp, P(abi.EnvConfigC)]
+    L.mjl_env_step.argtypes = [vp, f32p, f32p, f32p, f32p, f32p, i32, u64, u64, vp]
+    L.mjl_env_reset.argtypes = [vp, f32p, u64, u64, f32p, f32p, vp]
+    _lib = L
+    return L
+
+
+def check(rc: int):
+    if rc != 0:
+        raise MjlError(f"mjx355 error {rc}: {lib().mjl_last_error().decode()}")

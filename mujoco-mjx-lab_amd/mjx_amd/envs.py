@@ -1,0 +1,95 @@
+"""Batched humanoid walker env on the device (reference src/envs.py, train_ppo.py auto-reset).
+
+The reference builds pure functions `single_reset`/`single_step` and vmaps them
+(`create_env_functions`, src/envs.py:26-497); PPO then computes a reset for *every* env on
+*every* step and merges it with `where(done, reset, step)` over the whole mjx.Data pytree
+(train_ppo.py:149-161). Here one native launch does step + reward + obs and, for the envs that
+finished, the reset, in place (`mjl_env_step(auto_reset=1)`); the merged state, obs, reward and
+done flags are exactly those of the reference's merge.
+"""
+from __future__ import annotations
+
+import ctypes as C
+from typing import Optional, Tuple
+
+import torch
+
+from . import abi
+from ._lib import MjlError, check, lib
+from .config import EnvConfig
+from .mjx import Data, Model, _ptr, _stream, make_data
+
+
+def obs_size(nq: int, nv: int) -> int:
+    """1 (height) + 3 (rpy) + (nq-7) joints + nv velocities + 2 target features (src/envs.py:54-56)."""
+    return 1 + 3 + (nq - 7) + nv + 2
+
+
+def resolve_ids(m, cfg: EnvConfig) -> EnvConfig:
+    """Body / sensor id lookup done by reference load_model_and_create_env (training_utils.py:84-89)."""
+    cfg.pelvis_body_id = m.name2id("body", "pelvis")
+    cfg.head_body_id = m.name2id("body", "head")
+    cfg.touch_sensor_right_id = m.name2id("sensor", "touch_foot_right")
+    cfg.touch_sensor_left_id = m.name2id("sensor", "touch_foot_left")
+    if min(cfg.pelvis_body_id, cfg.head_body_id, cfg.touch_sensor_right_id, cfg.touch_sensor_left_id) < 0:
+        raise MjlError("model lacks pelvis/head bodies or touch_foot_* sensors")
+    return cfg
+
+
+class HumanoidEnv:
+    """`num_envs` walker envs resident on one GPU. State lives in `self.data` (native batch)."""
+
+    def __init__(self, sys: Model, cfg: EnvConfig, num_envs: int, device: int = 0, seed: int = 0,
+                 store_derived: bool = False):
+        self.sys = sys
+        self.cfg = cfg
+        self.num_envs = int(num_envs)
+        self.obs_dim = obs_size(sys.nq, sys.nv)
+        self.act_dim = sys.nu
+        self.data: Data = make_data(sys, self.num_envs, device)
+        self.data.set_option(abi.OPT_STORE_DERIVED, int(store_derived))
+        self._cfg_c = abi.env_config_c(cfg, sys.m, self.obs_dim)
+        check(lib().mjl_env_config(self.data.handle, C.byref(self._cfg_c)))
+        dev = self.data.device
+        self.obs = torch.zeros((self.num_envs, self.obs_dim), dtype=torch.float32, device=dev)
+        self.rew = torch.zeros(self.num_envs, dtype=torch.float32, device=dev)
+        self.term = torch.zeros(self.num_envs, dtype=torch.float32, device=dev)
+        self.trunc = torch.zeros(self.num_envs, dtype=torch.float32, device=dev)
+        self.seed = int(seed) & 0xFFFFFFFFFFFFFFFF
+        self.counter = 0
+
+    def _next_counter(self) -> int:
+        self.counter += 1
+        return self.counter
+
+    def reset(self, mask: Optional[torch.Tensor] = None, noise: Optional[torch.Tensor] = None) -> torch.Tensor:
+        """v_reset (src/envs.py:115-202,494) on all envs, or on envs with mask > 0.5.
+        `noise` [num_envs, nq-7+nv+2] of uniforms replaces the on-device RNG (parity tests)."""
+        mk = None if mask is None else mask.to(self.obs.device, torch.float32).contiguous()
+        nz = None if noise is None else noise.to(self.obs.device, torch.float32).contiguous()
+        check(lib().mjl_env_reset(self.data.handle, _ptr(mk), self.seed, self._next_counter(), _ptr(nz),
+                                  _ptr(self.obs), _stream()))
+        return self.obs
+
+    def step(self, act: torch.Tensor, auto_reset: bool = True,
+             out: Optional[Tuple[torch.Tensor, ...]] = None) -> Tuple[torch.Tensor, ...]:
+        """v_step (src/envs.py:333-495) fused with merge_if_done (train_ppo.py:147-161).
+        Returns (obs, reward, terminated, truncated); obs is post-reset for finished envs."""
+        act = act.to(self.obs.device, torch.float32).contiguous()
+        if act.shape != (self.num_envs, self.act_dim):
+            raise MjlError(f"action must have shape {(self.num_envs, self.act_dim)}")
+        obs, rew, term, trunc = out if out is not None else (self.obs, self.rew, self.term, self.trunc)
+        check(lib().mjl_env_step(self.data.handle, _ptr(act), _ptr(obs), _ptr(rew), _ptr(term), _ptr(trunc),
+                                 int(auto_reset), self.seed, self._next_counter(), _stream()))
+        return obs, rew, term, trunc
+
+    @property
+    def aux(self) -> torch.Tensor:
+        return self.data.get("aux")
+
+
+def create_env_functions(sys: Model, cfg: EnvConfig, num_envs: int, device: int = 0, seed: int = 0):
+    """Reference `create_env_functions` (src/envs.py:26) returns (single_reset, single_step,
+    v_reset, v_step); the batched pair is what the trainers use. Here: (env, v_reset, v_step)."""
+    env = HumanoidEnv(sys, cfg, num_envs, device=device, seed=seed)
+    return env, env.reset, env.step
