@@ -166,8 +166,9 @@ int mjl_batch_nenv(const mjlBatch* batch);
 
 /* Batch options. MJL_OPT_STORE_DERIVED (default 1): step/env kernels also write the derived
  * per-env outputs (xpos, xquat, qacc, forces, sensordata, stats) readable with mjl_get; set 0 to
- * keep only the state + env outputs in the hot loop. */
-enum { MJL_OPT_STORE_DERIVED = 0 };
+ * keep only the state + env outputs in the hot loop. MJL_OPT_FORCE_GLOBAL_ROWS (default 0, test
+ * hook): keep constraint rows in the global-memory scratch even when they fit in LDS. */
+enum { MJL_OPT_STORE_DERIVED = 0, MJL_OPT_FORCE_GLOBAL_ROWS = 1 };
 int mjl_batch_set_option(mjlBatch* batch, int option, int value);
 
 /* Copy a per-env field to / from a device buffer [nenv, dim] (async on stream). `mask` (device,

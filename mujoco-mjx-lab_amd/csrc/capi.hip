@@ -44,7 +44,7 @@ struct mjlModel {
 
 struct mjlBatch {
   const mjlModel* model;
-  int device, nenv, store_derived;
+  int device, nenv, store_derived, force_global_rows;
   ModelF* d_model;
   mjlEnvConfig* d_env;
   int has_env, obs_dim;
@@ -301,6 +301,7 @@ int mjl_batch_nenv(const mjlBatch* B) { return B ? B->nenv : -1; }
 int mjl_batch_set_option(mjlBatch* B, int option, int value) {
   if (!B) return fail(MJL_ERR_ARG, "null batch");
   if (option == MJL_OPT_STORE_DERIVED) { B->store_derived = value != 0; return MJL_OK; }
+  if (option == MJL_OPT_FORCE_GLOBAL_ROWS) { B->force_global_rows = value != 0; return MJL_OK; }
   return fail(MJL_ERR_ARG, "unknown option %d", option);
 }
 
@@ -346,6 +347,7 @@ static KParams make_params(mjlBatch* B) {
   P.s = B->s;
   P.nenv = B->nenv;
   P.store_derived = B->store_derived;
+  P.force_global_rows = B->force_global_rows;
   P.scratch = B->d_scratch;
   P.scratch_stride = B->scratch_stride;
   P.gmax_efc = B->gmax_efc;

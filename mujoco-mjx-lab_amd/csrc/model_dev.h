@@ -67,6 +67,7 @@ struct KParams {
   StateBuf s;
   int nenv;
   int store_derived;
+  int force_global_rows;  // test hook: always use the global-scratch row storage
   int auto_reset;
   const float* in_ctrl;   // [nenv, nu] or null
   const float* mask;      // [nenv] or null

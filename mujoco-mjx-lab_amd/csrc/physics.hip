@@ -175,13 +175,13 @@ __device__ __forceinline__ void inert_vec(float* r, const float* i, const float*
 template <int NVC> struct Chol {
   static constexpr int LD = WS<NVC>::LD;
   // lane i < n loads row i of A; rows/cols >= n are padded with the identity
-  __device__ static void load(const float* A, int n, int lane, float (&a)[NVC]) {
+  __device__ __forceinline__ static void load(const float* A, int n, int lane, float (&a)[NVC]) {
 #pragma unroll
     for (int j = 0; j < NVC; j++) a[j] = (lane < n && j < n) ? A[lane * LD + j] : (lane == j ? 1.f : 0.f);
   }
   // in-register right-looking Cholesky: afterwards lane i holds row i of L (a[j], j <= i),
   // invd = 1 / L[i][i]
-  __device__ static void factor(float (&a)[NVC], int lane, float& invd) {
+  __device__ __forceinline__ static void factor(float (&a)[NVC], int lane, float& invd) {
     invd = 1.f;
 #pragma unroll
     for (int k = 0; k < NVC; k++) {
@@ -194,7 +194,7 @@ template <int NVC> struct Chol {
       for (int j = k + 1; j < NVC; j++) a[j] = fmaf(-a[k], rdlane(a[k], j), a[j]);
     }
   }
-  __device__ static void store(float* F, const float (&a)[NVC], int lane, int n) {
+  __device__ __forceinline__ static void store(float* F, const float (&a)[NVC], int lane, int n) {
     if (lane < NVC) {
 #pragma unroll
       for (int j = 0; j < NVC; j++)
@@ -203,7 +203,7 @@ template <int NVC> struct Chol {
   }
   // x distributed (lane i holds b_i, b_i = 0 for i >= n): returns (L L^T)^-1 b in the same layout.
   // forward substitution uses the row in VGPRs, backward substitution reads columns of L from F.
-  __device__ static float solve(const float (&a)[NVC], float invd, const float* F, float x, int lane) {
+  __device__ __forceinline__ static float solve(const float (&a)[NVC], float invd, const float* F, float x, int lane) {
 #pragma unroll
     for (int k = 0; k < NVC; k++) {
       float yk = rdlane(x, k) * rdlane(invd, k);
@@ -222,7 +222,7 @@ template <int NVC> struct Chol {
 // ---------------------------------------------------------------------------------------------
 // position stage
 // ---------------------------------------------------------------------------------------------
-template <int NVC> __device__ void kinematics(const ModelF& m, WS<NVC>& W, int lane) {
+template <int NVC> __device__ __forceinline__ void kinematics(const ModelF& m, WS<NVC>& W, int lane) {
   if (lane == 0) {
     W.xpos[0][0] = W.xpos[0][1] = W.xpos[0][2] = 0.f;
     W.xquat[0][0] = 1.f; W.xquat[0][1] = W.xquat[0][2] = W.xquat[0][3] = 0.f;
@@ -323,7 +323,7 @@ template <int NVC> __device__ void kinematics(const ModelF& m, WS<NVC>& W, int l
 }
 
 // cinert (lane = body) and cdof (lane 32 + dof); then crb (lane = body)   [smooth.com_pos, crb]
-template <int NVC> __device__ void com_pos_crb(const ModelF& m, WS<NVC>& W, int lane) {
+template <int NVC> __device__ __forceinline__ void com_pos_crb(const ModelF& m, WS<NVC>& W, int lane) {
   if (lane < m.nbody) {
     int b = lane;
     float* ci = W.cinert[b];
@@ -430,7 +430,7 @@ __device__ __forceinline__ float sph_sph(float* pos, float* n, const float* p1, 
 }
 
 // candidate contact k (0/1) of pair p: returns false if the pair has no k-th contact
-template <int NVC> __device__ bool collide(const ModelF& m, const WS<NVC>& W, int p, int k, float& dist,
+template <int NVC> __device__ __forceinline__ bool collide(const ModelF& m, const WS<NVC>& W, int p, int k, float& dist,
                                            float* pos, float* fr) {
   int kind = m.pair_kind[p];
   if (k == 1 && kind != MJL_COL_PLANE_CAPSULE) return false;
@@ -519,7 +519,7 @@ template <int NVC> __device__ bool collide(const ModelF& m, const WS<NVC>& W, in
 }
 
 // count active contacts and constraint rows (uniform result in every lane)
-template <int NVC> __device__ void count_rows(const ModelF& m, const WS<NVC>& W, int lane, int& ncon, int& nrows,
+template <int NVC> __device__ __forceinline__ void count_rows(const ModelF& m, const WS<NVC>& W, int lane, int& ncon, int& nrows,
                                               int& nlim) {
   int nc = 0, nr = 0;
   for (int base = 0; base < m.npair; base += 64) {
@@ -732,7 +732,7 @@ template <int NVC> __device__ __forceinline__ void build_rows(const ModelF& m, W
 // ---------------------------------------------------------------------------------------------
 // velocity stage: com_vel + rne forward pass by levels, backward by subtree ranges  [smooth.rne]
 // ---------------------------------------------------------------------------------------------
-template <int NVC> __device__ void velocity_stage(const ModelF& m, WS<NVC>& W, int lane) {
+template <int NVC> __device__ __forceinline__ void velocity_stage(const ModelF& m, WS<NVC>& W, int lane) {
   if (lane == 0) {
     for (int i = 0; i < 6; i++) W.cvel[0][i] = 0.f;
     W.cacc[0][0] = W.cacc[0][1] = W.cacc[0][2] = 0.f;
@@ -1019,7 +1019,7 @@ template <int NVC> __device__ __forceinline__ void solver(const ModelF& m, WS<NV
 }
 
 // touch sensors (lane = sensor)   [sensor.sensor_acc, MuJoCo mjSENS_TOUCH]
-template <int NVC> __device__ void sensors(const ModelF& m, WS<NVC>& W, const Rows& R, int lane) {
+template <int NVC> __device__ __forceinline__ void sensors(const ModelF& m, WS<NVC>& W, const Rows& R, int lane) {
   if (lane < m.nsensor) {
     int site = m.sensor_objid[lane], body = m.site_bodyid[site];
     float val = 0.f;
@@ -1085,7 +1085,7 @@ template <int NVC> __device__ __forceinline__ Rows global_rows(float* base, int 
 }
 
 // full forward pass (mjx.forward)
-template <int NVC> __device__ void forward(const ModelF& m, WS<NVC>& W, const KParams& P, int env, int lane) {
+template <int NVC> __device__ __forceinline__ void forward(const ModelF& m, WS<NVC>& W, const KParams& P, int env, int lane) {
   constexpr int LD = WS<NVC>::LD;
   kinematics<NVC>(m, W, lane);
   com_pos_crb<NVC>(m, W, lane);
@@ -1102,7 +1102,7 @@ template <int NVC> __device__ void forward(const ModelF& m, WS<NVC>& W, const KP
   int ncon, nrows, nlim;
   count_rows<NVC>(m, W, lane, ncon, nrows, nlim);
   SYNC();
-  if (nrows <= CAP && ncon <= CAPC) {
+  if (!P.force_global_rows && nrows <= CAP && ncon <= CAPC) {
     Rows R = lds_rows<NVC>(W);
     build_rows<NVC>(m, W, R, lane);
     solver<NVC>(m, W, R, lane);
@@ -1118,7 +1118,7 @@ template <int NVC> __device__ void forward(const ModelF& m, WS<NVC>& W, const KP
 // ---------------------------------------------------------------------------------------------
 // integration (Euler with eulerdamp / implicitfast)   [forward.euler / forward.implicit]
 // ---------------------------------------------------------------------------------------------
-template <int NVC> __device__ void integrate(const ModelF& m, WS<NVC>& W, int lane) {
+template <int NVC> __device__ __forceinline__ void integrate(const ModelF& m, WS<NVC>& W, int lane) {
   constexpr int LD = WS<NVC>::LD;
   const int nv = m.nv;
   const float dt = m.timestep;
@@ -1184,7 +1184,7 @@ __device__ __forceinline__ float stance_of(const mjlEnvConfig& c, const float* s
 }
 
 // obs entry i of compute_obs (envs.py:317-331): raw obs at index perm[i] (flipped) or i
-template <int NVC> __device__ float raw_obs(const ModelF& m, const WS<NVC>& W, const mjlEnvConfig& c, int idx) {
+template <int NVC> __device__ __forceinline__ float raw_obs(const ModelF& m, const WS<NVC>& W, const mjlEnvConfig& c, int idx) {
   int nj = m.nq - 7;
   if (idx < 4) return W.sc[SC_HEIGHT + idx];  // height, roll, pitch, yaw
   idx -= 4;
@@ -1203,7 +1203,7 @@ template <int NVC> __device__ float raw_obs(const ModelF& m, const WS<NVC>& W, c
   return W.sc[SC_TF0 + idx];
 }
 
-template <int NVC> __device__ void write_obs(const ModelF& m, const WS<NVC>& W, const mjlEnvConfig& c, float* obs,
+template <int NVC> __device__ __forceinline__ void write_obs(const ModelF& m, const WS<NVC>& W, const mjlEnvConfig& c, float* obs,
                                              int lane) {
   if (lane < c.obs_dim) {
     bool flip = W.sc[SC_FLIP] > 0.5f;
@@ -1239,7 +1239,7 @@ __device__ __forceinline__ float uniform01(const KParams& P, int env, int i) {
 }
 
 // single_reset (envs.py:115-202): random pose/velocity, forward, target, aux, obs
-template <int NVC> __device__ void env_reset(const ModelF& m, WS<NVC>& W, const KParams& P, int env, int lane,
+template <int NVC> __device__ __forceinline__ void env_reset(const ModelF& m, WS<NVC>& W, const KParams& P, int env, int lane,
                                              float* aux_out, float* obs_out) {
   const mjlEnvConfig& c = *P.env;
   int nj = m.nq - 7, nd = nj + m.nv + 2;
@@ -1292,7 +1292,7 @@ template <int NVC> __device__ void env_reset(const ModelF& m, WS<NVC>& W, const 
 }
 
 // post-step part of single_step (envs.py:347-492); writes obs, aux and the SC_REW/TERM/TRUNC slots
-template <int NVC> __device__ void env_post(const ModelF& m, WS<NVC>& W, const mjlEnvConfig& c, float* aux,
+template <int NVC> __device__ __forceinline__ void env_post(const ModelF& m, WS<NVC>& W, const mjlEnvConfig& c, float* aux,
                                             float* obs, int lane) {
   // energy terms over actuated hinge dofs (mean over nv-6)
   float pw = 0.f, st = 0.f;

@@ -14,6 +14,7 @@ MAXTENDON, MAXTENWRAP, MAXPAIR, MAXSENSOR, MAXOBS = 4, 4, 256, 4, 64
 AUX_DIM = 9
 
 OPT_STORE_DERIVED = 0
+OPT_FORCE_GLOBAL_ROWS = 1
 
 FIELD = {
     "qpos": 0, "qvel": 1, "qacc_warmstart": 2, "time": 3, "ctrl": 4, "qacc": 5, "xpos": 6,

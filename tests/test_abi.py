@@ -1,0 +1,55 @@
+"""C ABI: struct layouts agree across Python/ctypes, the oracle build and the product library;
+the product library loads without a GPU and exports every symbol include/mjx355.h declares."""
+import ctypes as C
+import os
+import re
+
+import numpy as np
+import pytest
+
+import mjx_amd
+from mjx_amd import _lib, abi
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def test_header_symbols_exported():
+    hdr = open(os.path.join(ROOT, "include", "mjx355.h")).read()
+    declared = set(re.findall(r"^\s*(?:const char\*|int|void)\s+(mjl_\w+)\(", hdr, re.M))
+    assert declared == set(_lib.EXPORTS)
+    L = _lib.lib()
+    for name in declared:
+        assert hasattr(L, name), name
+    assert b"gfx950" in L.mjl_version()
+
+
+def test_struct_layouts_match_oracle_build():
+    import oracle as orc
+    L = orc.lib()  # asserts sizeof(OrcState/ModelDesc/EnvConfig) against the C compiler
+    assert L.orc_desc_size() == C.sizeof(abi.ModelDesc)
+    assert L.orc_envcfg_size() == C.sizeof(abi.EnvConfigC)
+
+
+def test_model_create_validates_without_gpu():
+    L = _lib.lib()
+    m = mjx_amd.load_model("humanoid_mjx")
+    d = abi.model_desc(m)
+    h = C.c_void_p()
+    assert L.mjl_model_create(C.byref(d), C.byref(h)) == 0
+    assert L.mjl_model_nefc_max(h) == 16 * 4 + 100 + 21 + 2  # nefc <= 187
+    L.mjl_model_destroy(h)
+    bad = abi.model_desc(m)
+    bad.integrator = 1  # RK4
+    assert L.mjl_model_create(C.byref(bad), C.byref(h)) == 2
+    assert b"integrator" in L.mjl_last_error()
+
+
+def test_no_silent_cpu_fallback():
+    """Without a GPU the product path fails loudly instead of falling back to the CPU."""
+    import torch
+    if torch.cuda.is_available():
+        pytest.skip("GPU present")
+    from mjx_amd import mjx
+    sys_ = mjx.put_model(mjx_amd.load_model("humanoid_mjx"))
+    with pytest.raises(_lib.MjlError):
+        mjx.make_data(sys_, 4)

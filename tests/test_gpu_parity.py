@@ -1,0 +1,273 @@
+"""HIP path (libmjx355.so on the MI355X) vs the CPU oracle on identical qpos/qvel/ctrl.
+
+Tolerances (fp32 kernel vs fp64 oracle), stated per field, relative to the field's scale
+s = 1 + max|ref| of that env:
+  xpos, qpos after one step           atol 2e-5
+  qfrc_bias / passive / actuator      2e-5 * s
+  qacc_smooth, qacc, qfrc_constraint  2e-3 * s   (measured ~3e-5; stiff contacts amplify fp32 noise)
+  sensordata (touch)                  2e-3 * s
+  contact / constraint-row counts     exact
+"""
+import numpy as np
+import pytest
+import torch
+
+import mjx_amd
+from mjx_amd import abi, mjx
+from mjx_amd.config import reference_ppo_config
+from mjx_amd.envs import HumanoidEnv, resolve_ids
+from oracle import Oracle, state_arrays
+from rng_ref import reset_noise
+
+pytestmark = pytest.mark.gpu
+
+
+def _states(m, n_random=24, seed=0):
+    rng = np.random.default_rng(seed)
+    od = Oracle(m)
+    out = [(m.key_qpos[k].copy(), np.zeros(m.nv), np.zeros(m.nv), rng.uniform(-1, 1, m.nu)) for k in range(m.nkey)]
+    for _ in range(n_random):
+        q = m.qpos0.copy()
+        q[7:] += rng.uniform(-0.3, 0.3, m.nq - 7)
+        q[2] += rng.uniform(-0.25, 0.05)
+        s = od.new_state(q, rng.uniform(-1, 1, m.nv), ctrl=rng.uniform(-1, 1, m.nu))
+        nst = int(rng.integers(0, 60))
+        if nst:
+            od.rollout(s, rng.uniform(-1, 1, (nst, m.nu)))
+        a = state_arrays(m, s)
+        out.append((a["qpos"], a["qvel"], a["qacc_warmstart"], rng.uniform(-1, 1, m.nu)))
+    return [tuple(np.float32(x).astype(np.float64) for x in st) for st in out]
+
+
+def _load(sys_, states):
+    d = mjx.make_data(sys_, len(states))
+    t = lambda i: torch.tensor(np.array([s[i] for s in states]), dtype=torch.float32)
+    d.set("qpos", t(0))
+    d.set("qvel", t(1))
+    d.set("qacc_warmstart", t(2))
+    d.set("ctrl", t(3))
+    return d
+
+
+@pytest.fixture(scope="module", params=["humanoid_mjx", "humanoid"])
+def setup(request):
+    m = mjx_amd.load_model(request.param)
+    return m, mjx.put_model(m), _states(m)
+
+
+def _close(got, ref, rel, what):
+    s = 1.0 + np.abs(ref).max()
+    err = np.abs(np.asarray(got, np.float64) - ref).max()
+    assert err <= rel * s, f"{what}: err {err:.3e} > {rel:.1e} * {s:.3g}"
+
+
+def test_forward_parity(setup):
+    m, sys_, states = setup
+    d = _load(sys_, states)
+    mjx.forward(sys_, d)
+    G = {f: d.get(f).cpu().numpy() for f in ("qacc", "qacc_smooth", "qfrc_bias", "qfrc_passive", "qfrc_actuator",
+                                             "qfrc_constraint", "xpos", "xquat", "sensordata", "stats")}
+    orc = Oracle(m)
+    for i, (q, v, w, c) in enumerate(states):
+        a = state_arrays(m, orc.forward(orc.new_state(q, v, w, c)))
+        assert (G["stats"][i][0], G["stats"][i][1]) == (a["ncon"], a["nefc"]), f"state {i}: contact/row counts"
+        np.testing.assert_allclose(G["xpos"][i], a["xpos"], atol=2e-5)
+        np.testing.assert_allclose(np.abs(G["xquat"][i]), np.abs(a["xquat"]), atol=2e-5)
+        for f in ("qfrc_bias", "qfrc_passive", "qfrc_actuator"):
+            _close(G[f][i], a[f], 2e-5, f"state {i} {f}")
+        for f in ("qacc_smooth", "qacc", "qfrc_constraint", "sensordata"):
+            _close(G[f][i], a[f], 2e-3, f"state {i} {f}")
+
+
+def test_step_parity(setup):
+    m, sys_, states = setup
+    d = _load(sys_, states)
+    mjx.step(sys_, d)
+    q1, v1, w1, t1 = (d.get(f).cpu().numpy() for f in ("qpos", "qvel", "qacc_warmstart", "time"))
+    orc = Oracle(m)
+    for i, (q, v, w, c) in enumerate(states):
+        a = state_arrays(m, orc.step(orc.new_state(q, v, w, c)))
+        np.testing.assert_allclose(q1[i], a["qpos"], atol=2e-5)
+        _close(v1[i], a["qvel"], 2e-3, f"state {i} qvel")
+        _close(w1[i], a["qacc_warmstart"], 2e-3, f"state {i} qacc_warmstart")
+        assert t1[i] == pytest.approx(m.timestep, abs=1e-9)
+
+
+def test_trajectory_parity():
+    """20 chained steps from the standing keyframe with random controls: the fp32 trajectory
+    stays within 1e-3 of the fp64 one (contact-rich, warm-started)."""
+    m = mjx_amd.load_model("humanoid_mjx")
+    sys_ = mjx.put_model(m)
+    rng = np.random.default_rng(5)
+    B, T = 8, 20
+    ctrl = rng.uniform(-1, 1, (T, B, m.nu)).astype(np.float32)
+    d = mjx.make_data(sys_, B)
+    for t in range(T):
+        mjx.step(sys_, d, torch.tensor(ctrl[t], device="cuda"))
+    q = d.get("qpos").cpu().numpy()
+    orc = Oracle(m)
+    for i in range(B):
+        s = orc.rollout(orc.new_state(), ctrl[:, i].astype(np.float64))
+        np.testing.assert_allclose(q[i], state_arrays(m, s)["qpos"], atol=1e-3)
+
+
+def test_speedtest_parity():
+    m = mjx_amd.load_model("humanoid_mjx")
+    sys_ = mjx.put_model(m)
+    vel = torch.linspace(0, 1, 64, device="cuda")
+    out = mjx.speedtest_step(sys_, mjx.make_data(sys_, 64), vel).cpu().numpy()
+    ref = Oracle(m).speedtest(vel.cpu().numpy().astype(np.float64))
+    np.testing.assert_allclose(out, ref, atol=1e-6)
+
+
+def test_global_row_storage_matches_lds(setup):
+    """The global-memory row path (used when rows exceed the LDS capacity) is bit-identical."""
+    m, sys_, states = setup
+    res = []
+    for force in (0, 1):
+        d = _load(sys_, states)
+        d.set_option(abi.OPT_FORCE_GLOBAL_ROWS, force)
+        mjx.step(sys_, d)
+        res.append([d.get(f).cpu().numpy() for f in ("qpos", "qvel", "qacc", "sensordata")])
+    for a, b in zip(*res):
+        np.testing.assert_array_equal(a, b)
+
+
+def test_overflow_state_parity():
+    """A pose with every hinge past its upper limit and the limbs in the floor (89 active rows,
+    more than the 64 the LDS holds) takes the global-memory row path. The pose is so stiff that
+    fp32 and fp64 minimisers differ by percent (the fp32 oracle differs from the fp64 one by up to
+    25% here), so the check is the row count and the optimality condition of the GPU's own
+    solution: M (qacc - qacc_smooth) = qfrc_constraint (solver.py's zero-gradient condition)."""
+    m = mjx_amd.load_model("humanoid_mjx")
+    sys_ = mjx.put_model(m)
+    q = m.key_qpos[m.names["key"].index("supine")].copy()
+    for j in range(1, m.njnt):
+        q[m.jnt_qposadr[j]] = m.jnt_range[j][1] + 0.05
+    d = _load(sys_, [(q, np.zeros(m.nv), np.zeros(m.nv), np.zeros(m.nu))])
+    mjx.forward(sys_, d)
+    st = d.get("stats").cpu().numpy()[0]
+    a = state_arrays(m, Oracle(m).forward(Oracle(m).new_state(q)))
+    assert st[1] == a["nefc"] and a["nefc"] > 64
+    qacc, qsm, fcon = (d.get(f).cpu().numpy()[0].astype(np.float64) for f in ("qacc", "qacc_smooth", "qfrc_constraint"))
+    resid = a["M"] @ (qacc - qsm) - fcon
+    assert np.abs(resid).max() <= 2e-3 * (1 + np.abs(fcon).max())
+
+
+# ------------------------------------------------------------------------------------------------
+def _env(B, seed=3):
+    m = mjx_amd.load_model("humanoid_mjx")
+    sys_ = mjx.put_model(m)
+    cfg = resolve_ids(m, reference_ppo_config().env_config)
+    env = HumanoidEnv(sys_, cfg, B, seed=seed, store_derived=True)
+    return m, env, abi.env_config_c(cfg, m, env.obs_dim)
+
+
+def test_env_reset_parity():
+    B = 16
+    m, env, cfg_c = _env(B)
+    nd = m.nq - 7 + m.nv + 2
+    noise = np.random.default_rng(6).uniform(0, 1, (B, nd)).astype(np.float32)
+    obs = env.reset(noise=torch.tensor(noise)).cpu().numpy()
+    aux = env.aux.cpu().numpy()
+    qpos, qvel = env.data.get("qpos").cpu().numpy(), env.data.get("qvel").cpu().numpy()
+    orc = Oracle(m)
+    for i in range(B):
+        s, oa, oo = orc.env_reset(cfg_c, noise[i].astype(np.float64))
+        a = state_arrays(m, s)
+        np.testing.assert_allclose(qpos[i], a["qpos"], atol=1e-6)
+        np.testing.assert_allclose(qvel[i], a["qvel"], atol=1e-6)
+        np.testing.assert_allclose(aux[i], oa, atol=2e-4, rtol=1e-5)
+        np.testing.assert_allclose(obs[i], oo, atol=2e-4, rtol=1e-4)
+
+
+def test_env_device_rng_matches_reference_stream():
+    B = 32
+    m, env, _ = _env(B, seed=0x1234ABCD5678)
+    obs_rng = env.reset().cpu().numpy().copy()
+    counter = env.counter
+    noise = reset_noise(env.seed, counter, B, m.nq - 7 + m.nv + 2)
+    obs_noise = env.reset(noise=torch.tensor(noise)).cpu().numpy()
+    np.testing.assert_array_equal(obs_rng, obs_noise)
+
+
+def test_env_step_parity():
+    B, T = 8, 12
+    m, env, cfg_c = _env(B)
+    nd = m.nq - 7 + m.nv + 2
+    rng = np.random.default_rng(8)
+    noise = rng.uniform(0, 1, (B, nd)).astype(np.float32)
+    env.reset(noise=torch.tensor(noise))
+    orc = Oracle(m)
+    ost = [orc.env_reset(cfg_c, noise[i].astype(np.float64))[:2] for i in range(B)]
+    ost = [[s, aux] for s, aux in ost]
+    for t in range(T):
+        act = rng.uniform(-1.2, 1.2, (B, m.nu)).astype(np.float32)
+        obs, rew, term, trunc = (x.cpu().numpy() for x in env.step(torch.tensor(act), auto_reset=False))
+        aux = env.aux.cpu().numpy()
+        for i in range(B):
+            s, oa, oo, r, te, tr = orc.env_step(cfg_c, ost[i][0], ost[i][1], act[i].astype(np.float64))
+            ost[i][1] = oa
+            assert (te, tr) == (term[i], trunc[i])
+            assert rew[i] == pytest.approx(r, abs=5e-3 * (1 + abs(r)))
+            np.testing.assert_allclose(obs[i], oo, atol=5e-3 * (1 + np.abs(oo).max()))
+            np.testing.assert_allclose(aux[i][[0, 4, 5, 8]], oa[[0, 4, 5, 8]], atol=0)
+
+
+def test_auto_reset_merge():
+    """merge_if_done semantics (train_ppo.py:147-161): a truncated env comes back reset, its obs
+    is the reset obs, and rew/term/trunc are the finishing step's."""
+    B = 8
+    m, env, cfg_c = _env(B)
+    env.reset()
+    aux = env.aux.clone()
+    aux[::2, 8] = 999.0  # episode_step -> the next step truncates (max_episode_steps = 1000)
+    env.data.set("aux", aux)
+    act = torch.zeros((B, m.nu), device="cuda")
+    counter_next = env.counter + 1
+    obs, rew, term, trunc = (x.cpu().numpy() for x in env.step(act, auto_reset=True))
+    assert np.all(trunc[::2] == 1) and np.all(trunc[1::2] == 0)
+    aux_after = env.aux.cpu().numpy()
+    assert np.all(aux_after[::2, 8] == 0) and np.all(aux_after[1::2, 8] == 1)
+    noise = reset_noise(env.seed, counter_next, B, m.nq - 7 + m.nv + 2)
+    orc = Oracle(m)
+    for i in range(0, B, 2):
+        _, oa, oo = orc.env_reset(cfg_c, noise[i].astype(np.float64))
+        np.testing.assert_allclose(obs[i], oo, atol=2e-4, rtol=1e-4)
+
+
+def test_masked_forward_and_reset():
+    B = 8
+    m, env, _ = _env(B)
+    env.reset()
+    before = env.data.get("qpos").cpu().numpy()
+    mask = torch.tensor([1, 0] * (B // 2), dtype=torch.float32, device="cuda")
+    env.reset(mask=mask)
+    after = env.data.get("qpos").cpu().numpy()
+    np.testing.assert_array_equal(after[1::2], before[1::2])
+    assert not np.array_equal(after[0::2], before[0::2])
+
+
+def test_full_size_properties():
+    """BASELINE sizes (B = 2048, 4096): determinism, env independence, finiteness."""
+    m = mjx_amd.load_model("humanoid_mjx")
+    sys_ = mjx.put_model(m)
+    for B in (2048, 4096):
+        d = mjx.make_data(sys_, B)
+        vel = torch.linspace(0, 1, B, device="cuda")
+        a = mjx.speedtest_step(sys_, d, vel).clone()
+        b = mjx.speedtest_step(sys_, d, vel).clone()
+        c = mjx.speedtest_step(sys_, d, vel.flip(0)).flip(0)
+        assert torch.equal(a, b) and torch.equal(a, c) and torch.isfinite(a).all()
+    B = 4096
+    m, env, _ = _env(B)
+    env.reset()
+    g = torch.Generator(device="cuda").manual_seed(0)
+    for _ in range(50):
+        obs, rew, term, trunc = env.step(torch.rand((B, m.nu), generator=g, device="cuda") * 2 - 1)
+    q = env.data.get("qpos")
+    assert torch.isfinite(q).all() and torch.isfinite(obs).all() and torch.isfinite(rew).all()
+    qn = q[:, 3:7].norm(dim=1)
+    assert torch.allclose(qn, torch.ones_like(qn), atol=1e-5)
+    st = env.data.get("stats")
+    assert (st[:, 3] == 0).all()
