@@ -1,5 +1,5 @@
 // mjx355 C ABI (include/mjx355.h): model upload, batch state ownership, kernel launches.
-// Host side only; the kernels live in physics.hip (same translation unit).
+// Host side only; the kernels live in step_kernels.hip (same translation unit).
 #include <hip/hip_runtime.h>
 
 #include <cmath>
@@ -9,7 +9,7 @@
 #include <new>
 #include <string>
 
-#include "physics.hip"
+#include "step_kernels.hip"
 
 using namespace mjl;
 
@@ -39,7 +39,7 @@ int fail(int code, const char* fmt, ...) {
 struct mjlModel {
   mjlModelDesc desc;
   ModelF mf;
-  int nefc_max, ncon_max, nvc;
+  int nefc_max, ncon_max, nvc;  // nvc: 0 = DHum kernels, 1 = DGen kernels
 };
 
 struct mjlBatch {
@@ -60,6 +60,14 @@ extern "C" {
 
 const char* mjl_last_error(void) { return g_err.c_str(); }
 const char* mjl_version(void) { return "mjx355 0.1 (gfx950)"; }
+
+#ifdef MJL_TIMING
+// diagnostic build only: install a device buffer [nenv, 16] of per-phase s_memtime stamps
+int mjl_debug_set_stamps(unsigned long long* dev_buf) {
+  HIPCHK(hipMemcpyToSymbol(HIP_SYMBOL(mjl::g_stamps), &dev_buf, sizeof(dev_buf)));
+  return MJL_OK;
+}
+#endif
 
 static void q2m_host(const double* q, double* m) {
   double w = q[0], x = q[1], y = q[2], z = q[3];
@@ -218,8 +226,8 @@ int mjl_model_create(const mjlModelDesc* d, mjlModel** out) {
   }
   M->nefc_max = nefc_max;
   M->ncon_max = ncon_max;
-  M->nvc = d->nv <= 27 ? 27 : 32;
-  if (d->nv < 27 && M->nvc == 27) M->nvc = 27;  // padded path handles nv < NVC
+  // compact kernel instantiation when the model fits the humanoid capacities, generic otherwise
+  M->nvc = (d->nv <= DHum::NV && d->nbody <= DHum::NB && d->njnt <= DHum::NJ && d->ngeom <= DHum::NG) ? 0 : 1;
   *out = M;
   return MJL_OK;
 }
@@ -274,7 +282,7 @@ int mjl_batch_create(const mjlModel* model, int nenv, int device, mjlBatch** out
   if (e == hipSuccess) e = hipMemcpy(B->d_model, &model->mf, sizeof(ModelF), hipMemcpyHostToDevice);
   if (e == hipSuccess) e = hipMalloc(&B->d_env, sizeof(mjlEnvConfig));
   // global overflow rows for envs whose active constraints exceed the LDS capacity
-  int LD = model->nvc <= 28 ? 28 : 36;
+  int LD = model->nvc == 0 ? DHum::LD : DGen::LD;
   B->gmax_efc = model->nefc_max > 0 ? model->nefc_max : 1;
   B->gmax_con = model->ncon_max > 0 ? model->ncon_max : 1;
   B->scratch_stride = B->gmax_efc * (LD + 8) + B->gmax_con * (CONW + 2);
@@ -358,10 +366,10 @@ static KParams make_params(mjlBatch* B) {
 template <int MODE> static int launch(mjlBatch* B, const KParams& P, void* stream) {
   HIPCHK(hipSetDevice(B->device));
   dim3 grid(B->nenv), block(64);
-  if (B->model->nvc == 27)
-    hipLaunchKernelGGL((step_kernel<27, MODE>), grid, block, 0, (hipStream_t)stream, P);
+  if (B->model->nvc == 0)
+    hipLaunchKernelGGL((step_kernel<DHum, MODE>), grid, block, 0, (hipStream_t)stream, P);
   else
-    hipLaunchKernelGGL((step_kernel<32, MODE>), grid, block, 0, (hipStream_t)stream, P);
+    hipLaunchKernelGGL((step_kernel<DGen, MODE>), grid, block, 0, (hipStream_t)stream, P);
   HIPCHK(hipGetLastError());
   return MJL_OK;
 }

@@ -1,0 +1,1529 @@
+// mjx355 physics kernels for gfx950 (MI355X / CDNA4).
+//
+// One 64-lane wavefront (= one 64-thread workgroup) owns one environment for the whole step:
+// every stage of mjx.step (reference src/envs.py:345; upstream mujoco-mjx 3.3.6) runs inside a
+// single launch with per-env scratch in LDS, so state crosses HBM once per step (read qpos/qvel/
+// qacc_warmstart/ctrl/aux, write them back plus obs/reward/done). Inside the wave the work is
+// spread over lanes by the natural parallel axis of each stage:
+//   kinematics / com_vel+rne forward pass  lane = body, tree levels serialised   (smooth.py)
+//   subtree sums (com, crb, rne backward)  lane = body, DFS-contiguous ranges    (smooth.py)
+//   cdof, mass-matrix columns, tendons     lane = dof / tendon                   (smooth.py)
+//   collision                              lane = candidate geom pair            (collision_*.py)
+//   constraint rows (J, D, aref)           lane = dof (J entries) / row (params) (constraint.py)
+//   Newton: H = M + J'DJ                   lane = (column, half of rows of H)    (solver.py)
+//           Cholesky / triangular solves   lane = matrix row in VGPRs, v_readlane broadcasts
+//           exact line search              lane = constraint row + DPP wave reductions
+//   integrate                              lane = dof / joint                    (forward.py)
+//   env reward / obs / reset               lane 0 scalars + lane = obs entry     (src/envs.py)
+// Divergence between envs costs nothing: each wave runs its own number of Newton / line-search
+// iterations (unlike vmap's lockstep while_loop).
+//
+// Code layout: every stage is a __noinline__ function taking address-space-qualified pointers
+// (LDS workspace, constant-memory model), so each routine exists once in the code object and the
+// hot loop (H build, factor, solve, line search) stays resident in the instruction cache.
+#include <hip/hip_runtime.h>
+
+#include "model_dev.h"
+
+namespace mjl {
+
+#define LDSA __attribute__((address_space(3)))
+#define CSTA __attribute__((address_space(4)))
+#define GLBA __attribute__((address_space(1)))
+#define NOINL __device__ __noinline__
+#define INL __device__ __forceinline__
+#define SYNC() __syncthreads()
+
+#ifdef MJL_TIMING  // diagnostic build only: per-phase s_memtime stamps to a side buffer
+__device__ unsigned long long* g_stamps;
+#define STAMP(slot, lane)                                                                        \
+  do {                                                                                           \
+    unsigned long long t_ = __builtin_amdgcn_s_memtime();                                        \
+    if ((lane) == 0 && g_stamps) g_stamps[(size_t)blockIdx.x * 16 + (slot)] = t_;               \
+  } while (0)
+#else
+#define STAMP(slot, lane) do { } while (0)
+#endif
+
+typedef const CSTA ModelF* MP;
+
+#ifndef MJL_CAP
+#define MJL_CAP 64
+#endif
+#ifndef MJL_CAPC
+#define MJL_CAPC 32
+#endif
+#ifndef MJL_MINWAVES
+#define MJL_MINWAVES 1
+#endif
+constexpr int CAP = MJL_CAP;    // constraint rows kept in LDS; more go to the env's global scratch slab
+constexpr int CAPC = MJL_CAPC;  // contacts kept in LDS
+constexpr int CONW = 12;  // floats per contact record: pos[3], frame[9]
+constexpr float kMinVal = 1e-15f;
+constexpr float kMinImp = 0.0001f;
+constexpr float kMaxImp = 0.9999f;
+
+// compile-time capacities of one kernel instantiation (model sizes must fit)
+template <int NV_, int NB_, int NJ_, int NG_> struct Dims {
+  static constexpr int NV = NV_, NB = NB_, NJ = NJ_, NG = NG_;
+  static constexpr int LD = (NV_ <= 28) ? 28 : 36;  // dense row stride, LD/4 odd -> conflict-free b128
+};
+using DHum = Dims<27, 17, 22, 20>;  // both reference humanoids (nv 27, 17 bodies, 22 joints, 20 geoms)
+using DGen = Dims<32, 32, 32, 32>;  // any model within the MJL_MAX* capacities
+
+// ---------------------------------------------------------------------------------------------
+// wave primitives
+// ---------------------------------------------------------------------------------------------
+INL float rdlane(float x, int k) { return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(x), k)); }
+INL MP uniform_ptr(MP p) {
+  unsigned long long v = (unsigned long long)p;
+  unsigned lo = __builtin_amdgcn_readfirstlane((unsigned)v), hi = __builtin_amdgcn_readfirstlane((unsigned)(v >> 32));
+  return (MP)(((unsigned long long)hi << 32) | lo);
+}
+template <int CTRL, int ROWMASK> INL float dpp0(float v) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, ROWMASK, 0xF, false));
+}
+template <int CTRL> INL float dppm(float v) {
+  return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), CTRL, 0xF, 0xF, true));
+}
+// sum over the 64 lanes, result in every lane (DPP within rows, row broadcasts, readlane 63)
+INL float wsum(float v) {
+  v += dppm<0xB1>(v);        // quad_perm 1,0,3,2
+  v += dppm<0x4E>(v);        // quad_perm 2,3,0,1
+  v += dppm<0x141>(v);       // row_half_mirror
+  v += dppm<0x140>(v);       // row_mirror
+  v += dpp0<0x142, 0xA>(v);  // row_bcast15
+  v += dpp0<0x143, 0xC>(v);  // row_bcast31
+  return rdlane(v, 63);
+}
+INL unsigned long long lanes_below(int lane) { return (1ull << lane) - 1ull; }
+
+// ---------------------------------------------------------------------------------------------
+// per-env LDS workspace
+// ---------------------------------------------------------------------------------------------
+template <class DM> struct WS {
+  static constexpr int NV = DM::NV, LD = DM::LD, NB = DM::NB, NJ = DM::NJ, NG = DM::NG;
+  alignas(16) float qpos[MJL_MAXQ];
+  alignas(16) float qvel[LD];
+  alignas(16) float qacc_ws[LD];
+  float ctrl[MJL_MAXU];
+  float xpos[NB][3], xquat[NB][4], xmat[NB][9], xipos[NB][3];
+  float xanchor[NJ][3], xaxis[NJ][3];
+  float gpos[NG][3], gaxis[NG][3];
+  float spos[MJL_MAXSITE][3], smat[MJL_MAXSITE][9];
+  float scom[NB][3];
+  float cinert[NB][10], crb[NB][10];
+  float cdof[NV][6], cvel[NB][6], cacc[NB][6];
+  float tenJ[MJL_MAXTENDON][LD], tenlen[MJL_MAXTENDON];
+  alignas(16) float M[NV * LD];
+  alignas(16) float H[NV * LD];  // factor of M, Newton Hessian + factor, or implicit-integration factor
+  float invd[32];                // 1 / diag of the factor in H
+  alignas(16) float frc_bias[LD];
+  alignas(16) float frc_passive[LD];
+  alignas(16) float frc_act[LD];
+  alignas(16) float frc_smooth[LD];
+  alignas(16) float qacc_smooth[LD];
+  alignas(16) float qacc[LD];
+  alignas(16) float frc_con[LD];
+  alignas(16) float grad[LD];
+  alignas(16) float Mgrad[LD];
+  alignas(16) float search[LD];
+  alignas(16) float Ma[LD];
+  alignas(16) float Mv[LD];
+  alignas(16) float gradold[LD];
+  alignas(16) float Mgradold[LD];
+  float sens[MJL_MAXSENSOR];
+  float sc[32];
+  int ncon, nefc, nlim, niter;
+  // constraint rows that fit in LDS
+  alignas(16) float J[CAP * LD];
+  float D[CAP], aref[CAP], jar[CAP], force[CAP], Jv[CAP], epos[CAP], einvw[CAP];
+  int emeta[CAP];
+  float con[CAPC * CONW];
+  int con_pair[CAPC], con_efc[CAPC];
+};
+
+// scalar slots in WS::sc
+enum { SC_FLIP = 0, SC_HEIGHT, SC_ROLL, SC_PITCH, SC_YAW, SC_TF0, SC_TF1, SC_REW, SC_TERM, SC_TRUNC, SC_DONE,
+       SC_NAN, SC_TIME };
+
+// constraint-row storage: the LDS arrays of WS, or the env's slab of global scratch
+template <bool G> struct RowAS;
+template <> struct RowAS<false> { typedef LDSA float F; typedef LDSA int I; };
+template <> struct RowAS<true> { typedef GLBA float F; typedef GLBA int I; };
+template <bool G> struct Rows {
+  typedef typename RowAS<G>::F F;
+  typedef typename RowAS<G>::I I;
+  F *J, *D, *aref, *jar, *force, *Jv, *epos, *einvw, *con;
+  I *emeta, *con_pair, *con_efc;
+  int cap, capc;
+};
+template <class D> INL Rows<false> lds_rows(LDSA WS<D>* W) {
+  Rows<false> R;
+  R.J = W->J; R.D = W->D; R.aref = W->aref; R.jar = W->jar; R.force = W->force; R.Jv = W->Jv;
+  R.epos = W->epos; R.einvw = W->einvw; R.emeta = W->emeta; R.con = W->con; R.con_pair = W->con_pair;
+  R.con_efc = W->con_efc; R.cap = CAP; R.capc = CAPC;
+  return R;
+}
+template <class D> INL Rows<true> global_rows(float* base_generic, int nefc_max, int ncon_max) {
+  constexpr int LD = D::LD;
+  GLBA float* p = (GLBA float*)base_generic;
+  Rows<true> R;
+  R.J = p; p += nefc_max * LD;
+  R.D = p; p += nefc_max;
+  R.aref = p; p += nefc_max;
+  R.jar = p; p += nefc_max;
+  R.force = p; p += nefc_max;
+  R.Jv = p; p += nefc_max;
+  R.epos = p; p += nefc_max;
+  R.einvw = p; p += nefc_max;
+  R.emeta = (GLBA int*)p; p += nefc_max;
+  R.con = p; p += ncon_max * CONW;
+  R.con_pair = (GLBA int*)p; p += ncon_max;
+  R.con_efc = (GLBA int*)p;
+  R.cap = nefc_max; R.capc = ncon_max;
+  return R;
+}
+
+// ---------------------------------------------------------------------------------------------
+// small math (MuJoCo conventions: quat [w x y z], spatial vectors [ang; lin], row-major 3x3)
+// pointer arguments are templates so LDS / constant / private pointers all inline cleanly
+// ---------------------------------------------------------------------------------------------
+template <class A, class B> INL void qmul(float* r, A a, B b) {
+  float t0 = a[0] * b[0] - a[1] * b[1] - a[2] * b[2] - a[3] * b[3];
+  float t1 = a[0] * b[1] + a[1] * b[0] + a[2] * b[3] - a[3] * b[2];
+  float t2 = a[0] * b[2] - a[1] * b[3] + a[2] * b[0] + a[3] * b[1];
+  float t3 = a[0] * b[3] + a[1] * b[2] - a[2] * b[1] + a[3] * b[0];
+  r[0] = t0; r[1] = t1; r[2] = t2; r[3] = t3;
+}
+template <class Q> INL void q2m(float* m, Q q) {
+  float w = q[0], x = q[1], y = q[2], z = q[3];
+  m[0] = 1 - 2 * (y * y + z * z); m[1] = 2 * (x * y - w * z); m[2] = 2 * (x * z + w * y);
+  m[3] = 2 * (x * y + w * z); m[4] = 1 - 2 * (x * x + z * z); m[5] = 2 * (y * z - w * x);
+  m[6] = 2 * (x * z - w * y); m[7] = 2 * (y * z + w * x); m[8] = 1 - 2 * (x * x + y * y);
+}
+INL void qnorm(float* q) {
+  float n = sqrtf(q[0] * q[0] + q[1] * q[1] + q[2] * q[2] + q[3] * q[3]);
+  if (n < kMinVal) { q[0] = 1; q[1] = q[2] = q[3] = 0; return; }
+  float inv = 1.f / n;
+  q[0] *= inv; q[1] *= inv; q[2] *= inv; q[3] *= inv;
+}
+template <class M, class V> INL void mv3(float* r, M m, V v) {
+  float a = m[0] * v[0] + m[1] * v[1] + m[2] * v[2];
+  float b = m[3] * v[0] + m[4] * v[1] + m[5] * v[2];
+  float c = m[6] * v[0] + m[7] * v[1] + m[8] * v[2];
+  r[0] = a; r[1] = b; r[2] = c;
+}
+template <class M, class V> INL void mtv3(float* r, M m, V v) {
+  float a = m[0] * v[0] + m[3] * v[1] + m[6] * v[2];
+  float b = m[1] * v[0] + m[4] * v[1] + m[7] * v[2];
+  float c = m[2] * v[0] + m[5] * v[1] + m[8] * v[2];
+  r[0] = a; r[1] = b; r[2] = c;
+}
+template <class A, class B> INL void cross3(float* r, A a, B b) {
+  float x = a[1] * b[2] - a[2] * b[1], y = a[2] * b[0] - a[0] * b[2], z = a[0] * b[1] - a[1] * b[0];
+  r[0] = x; r[1] = y; r[2] = z;
+}
+template <class A, class B> INL float dot3(A a, B b) { return a[0] * b[0] + a[1] * b[1] + a[2] * b[2]; }
+INL float norm3(float* v) {  // math.normalize_with_norm
+  float n = sqrtf(dot3(v, v));
+  float inv = 1.f / (n + (n == 0.f ? 1e-6f : 0.f));
+  v[0] *= inv; v[1] *= inv; v[2] *= inv;
+  return n;
+}
+template <class V, class U> INL void cross_motion(float* r, V v, U u) {
+  float a[3], b[3], c[3];
+  cross3(a, v, u); cross3(b, v, u + 3); cross3(c, v + 3, u);
+  r[0] = a[0]; r[1] = a[1]; r[2] = a[2]; r[3] = b[0] + c[0]; r[4] = b[1] + c[1]; r[5] = b[2] + c[2];
+}
+template <class V, class F> INL void cross_force(float* r, V v, F f) {
+  float a[3], b[3], c[3];
+  cross3(a, v, f); cross3(b, v + 3, f + 3); cross3(c, v, f + 3);
+  r[0] = a[0] + b[0]; r[1] = a[1] + b[1]; r[2] = a[2] + b[2]; r[3] = c[0]; r[4] = c[1]; r[5] = c[2];
+}
+template <class I, class V> INL void inert_vec(float* r, I i, V v) {
+  r[0] = i[0] * v[0] + i[3] * v[1] + i[4] * v[2] - i[8] * v[4] + i[7] * v[5];
+  r[1] = i[3] * v[0] + i[1] * v[1] + i[5] * v[2] + i[8] * v[3] - i[6] * v[5];
+  r[2] = i[4] * v[0] + i[5] * v[1] + i[2] * v[2] - i[7] * v[3] + i[6] * v[4];
+  r[3] = i[8] * v[1] - i[7] * v[2] + i[9] * v[3];
+  r[4] = i[6] * v[2] - i[8] * v[0] + i[9] * v[4];
+  r[5] = i[7] * v[0] - i[6] * v[1] + i[9] * v[5];
+}
+
+// ---------------------------------------------------------------------------------------------
+// dense SPD factor / solve, one matrix row per lane in VGPRs (v_readlane broadcasts)
+// ---------------------------------------------------------------------------------------------
+// Factor the n x n SPD matrix A (LDS, stride LD) in place: A <- L (lower, upper zeroed),
+// invd_out[i] = 1 / L[i][i]. Rows / cols >= n act as the identity.
+template <class D> INL void chol_factor(LDSA float* A, LDSA float* invd_out, int n, int lane) {
+  constexpr int NV = D::NV, LD = D::LD;
+  float a[NV];
+#pragma unroll
+  for (int j = 0; j < NV; j++) a[j] = (lane < n && j < n) ? A[lane * LD + j] : (lane == j ? 1.f : 0.f);
+  float invd = 1.f;
+#pragma unroll
+  for (int k = 0; k < NV; k++) {
+    float lkk = sqrtf(fmaxf(rdlane(a[k], k), 1e-30f));
+    float inv = 1.f / lkk;
+    a[k] = (lane == k) ? lkk : a[k] * inv;
+    invd = (lane == k) ? inv : invd;
+#pragma unroll
+    for (int j = k + 1; j < NV; j++) a[j] = fmaf(-a[k], rdlane(a[k], j), a[j]);
+  }
+  if (lane < NV) {
+#pragma unroll
+    for (int j = 0; j < NV; j++) A[lane * LD + j] = (lane < n) ? ((j <= lane) ? a[j] : 0.f) : (j == lane ? 1.f : 0.f);
+    invd_out[lane] = invd;
+  }
+  SYNC();
+}
+
+// x distributed (lane i holds b_i, zero for i >= n) -> (L L^T)^-1 b, L from chol_factor
+template <class D> INL float chol_solve(const LDSA float* L, const LDSA float* invd_in, float x, int lane) {
+  constexpr int NV = D::NV, LD = D::LD;
+  float row[NV];
+#pragma unroll
+  for (int j = 0; j < NV; j++) row[j] = (lane < NV) ? L[lane * LD + j] : 0.f;
+  float invd = (lane < NV) ? invd_in[lane] : 1.f;
+#pragma unroll
+  for (int k = 0; k < NV; k++) {
+    float yk = rdlane(x, k) * rdlane(invd, k);
+    x = (lane == k) ? yk : ((lane > k) ? fmaf(-row[k], yk, x) : x);
+  }
+#pragma unroll
+  for (int k = NV - 1; k >= 0; k--) {
+    float zk = rdlane(x, k) * rdlane(invd, k);
+    float lki = (lane < k) ? L[k * LD + lane] : 0.f;
+    x = (lane == k) ? zk : ((lane < k) ? fmaf(-lki, zk, x) : x);
+  }
+  return x;
+}
+
+// ---------------------------------------------------------------------------------------------
+// position stage: kinematics, tendons, geom/site frames, subtree com   [smooth.kinematics]
+// ---------------------------------------------------------------------------------------------
+template <class D> NOINL void kinematics(MP m_, LDSA WS<D>* W, int lane) {
+  MP m = uniform_ptr(m_);
+  if (lane == 0) {
+    W->xpos[0][0] = W->xpos[0][1] = W->xpos[0][2] = 0.f;
+    W->xquat[0][0] = 1.f; W->xquat[0][1] = W->xquat[0][2] = W->xquat[0][3] = 0.f;
+    for (int i = 0; i < 9; i++) W->xmat[0][i] = (i % 4 == 0) ? 1.f : 0.f;
+    W->xipos[0][0] = W->xipos[0][1] = W->xipos[0][2] = 0.f;
+  }
+  if (lane >= 32 && lane - 32 < m->ntendon) {  // fixed tendons  [smooth.tendon]
+    int t = lane - 32;
+    float len = 0.f;
+    for (int k = 0; k < D::LD; k++) W->tenJ[t][k] = 0.f;
+    for (int w = 0; w < m->tendon_num[t]; w++) {
+      len += m->tendon_coef[t][w] * W->qpos[m->tendon_qadr[t][w]];
+      W->tenJ[t][m->tendon_dof[t][w]] += m->tendon_coef[t][w];
+    }
+    W->tenlen[t] = len;
+  }
+  SYNC();
+  const int maxlevel = m->maxlevel, nbody = m->nbody;
+  for (int L = 1; L <= maxlevel; L++) {
+    int b = lane;
+    if (b < nbody && m->body_level[b] == L) {
+      float pos[3], quat[4], mat[9];
+      int ja = m->body_jntadr[b], jn = m->body_jntnum[b];
+      if (jn > 0 && m->jnt_type[ja] == MJL_JNT_FREE) {
+        int qa = m->jnt_qposadr[ja];
+        pos[0] = W->qpos[qa]; pos[1] = W->qpos[qa + 1]; pos[2] = W->qpos[qa + 2];
+        quat[0] = W->qpos[qa + 3]; quat[1] = W->qpos[qa + 4]; quat[2] = W->qpos[qa + 5]; quat[3] = W->qpos[qa + 6];
+        qnorm(quat);
+        q2m(mat, quat);
+        W->xanchor[ja][0] = pos[0]; W->xanchor[ja][1] = pos[1]; W->xanchor[ja][2] = pos[2];
+        W->xaxis[ja][0] = mat[2]; W->xaxis[ja][1] = mat[5]; W->xaxis[ja][2] = mat[8];
+      } else {
+        int p = m->body_parentid[b];
+        mv3(pos, W->xmat[p], m->body_pos[b]);
+        pos[0] += W->xpos[p][0]; pos[1] += W->xpos[p][1]; pos[2] += W->xpos[p][2];
+        qmul(quat, W->xquat[p], m->body_quat[b]);
+        for (int j = ja; j < ja + jn; j++) {
+          q2m(mat, quat);
+          float anc[3], ax[3];
+          mv3(anc, mat, m->jnt_pos[j]);
+          anc[0] += pos[0]; anc[1] += pos[1]; anc[2] += pos[2];
+          mv3(ax, mat, m->jnt_axis[j]);
+          W->xanchor[j][0] = anc[0]; W->xanchor[j][1] = anc[1]; W->xanchor[j][2] = anc[2];
+          W->xaxis[j][0] = ax[0]; W->xaxis[j][1] = ax[1]; W->xaxis[j][2] = ax[2];
+          int qa = m->jnt_qposadr[j];
+          float s, c;
+          sincosf(0.5f * (W->qpos[qa] - m->qpos0[qa]), &s, &c);
+          float ql[4] = {c, m->jnt_axis[j][0] * s, m->jnt_axis[j][1] * s, m->jnt_axis[j][2] * s};
+          qmul(quat, quat, ql);
+          q2m(mat, quat);
+          float off[3];
+          mv3(off, mat, m->jnt_pos[j]);
+          pos[0] = anc[0] - off[0]; pos[1] = anc[1] - off[1]; pos[2] = anc[2] - off[2];
+        }
+        qnorm(quat);
+        q2m(mat, quat);
+      }
+      for (int i = 0; i < 3; i++) W->xpos[b][i] = pos[i];
+      for (int i = 0; i < 4; i++) W->xquat[b][i] = quat[i];
+      for (int i = 0; i < 9; i++) W->xmat[b][i] = mat[i];
+      float ip[3];
+      mv3(ip, mat, m->body_ipos[b]);
+      W->xipos[b][0] = pos[0] + ip[0]; W->xipos[b][1] = pos[1] + ip[1]; W->xipos[b][2] = pos[2] + ip[2];
+    }
+    SYNC();
+  }
+  if (lane < m->ngeom) {  // geom frames (lanes 0..31): centre + z axis is all collision needs
+    int g = lane, b = m->geom_bodyid[g];
+    float p[3], z[3];
+    mv3(p, W->xmat[b], m->geom_pos[g]);
+    mv3(z, W->xmat[b], m->geom_zaxis[g]);
+    W->gpos[g][0] = W->xpos[b][0] + p[0]; W->gpos[g][1] = W->xpos[b][1] + p[1]; W->gpos[g][2] = W->xpos[b][2] + p[2];
+    W->gaxis[g][0] = z[0]; W->gaxis[g][1] = z[1]; W->gaxis[g][2] = z[2];
+  }
+  if (lane >= 32 && lane - 32 < m->nsite) {  // site frames (lanes 32..)
+    int s = lane - 32, b = m->site_bodyid[s];
+    float p[3];
+    mv3(p, W->xmat[b], m->site_pos[s]);
+    W->spos[s][0] = W->xpos[b][0] + p[0]; W->spos[s][1] = W->xpos[b][1] + p[1]; W->spos[s][2] = W->xpos[b][2] + p[2];
+    for (int i = 0; i < 3; i++)
+      for (int j = 0; j < 3; j++)
+        W->smat[s][3 * i + j] = W->xmat[b][3 * i] * m->site_mat[s][j] + W->xmat[b][3 * i + 1] * m->site_mat[s][3 + j] +
+                                W->xmat[b][3 * i + 2] * m->site_mat[s][6 + j];
+  }
+  if (lane < nbody) {  // subtree com over the DFS-contiguous subtree [b, subtree_end)
+    int b = lane;
+    float ms = 0.f, a0 = 0.f, a1 = 0.f, a2 = 0.f;
+    for (int c = b; c < m->body_subtree_end[b]; c++) {
+      float mc = m->body_mass[c];
+      ms += mc; a0 += mc * W->xipos[c][0]; a1 += mc * W->xipos[c][1]; a2 += mc * W->xipos[c][2];
+    }
+    if (ms < kMinVal) { W->scom[b][0] = W->xipos[b][0]; W->scom[b][1] = W->xipos[b][1]; W->scom[b][2] = W->xipos[b][2]; }
+    else { float inv = 1.f / ms; W->scom[b][0] = a0 * inv; W->scom[b][1] = a1 * inv; W->scom[b][2] = a2 * inv; }
+  }
+  SYNC();
+}
+
+// cinert (lane = body) and cdof (lane 32 + dof); crb (lane = body); M columns (lane = dof)
+template <class D> NOINL void com_pos_crb(MP m_, LDSA WS<D>* W, int lane) {
+  MP m = uniform_ptr(m_);
+  constexpr int LD = D::LD;
+  if (lane < m->nbody) {
+    int b = lane;
+    LDSA float* ci = W->cinert[b];
+    float mass = m->body_mass[b];
+    if (b == 0 || mass == 0.f) {
+      for (int i = 0; i < 10; i++) ci[i] = 0.f;
+    } else {
+      const CSTA float* t = m->body_inertia[b];
+      float X[9];
+      for (int i = 0; i < 9; i++) X[i] = W->xmat[b][i];
+      float Ib[9] = {t[0], t[3], t[4], t[3], t[1], t[5], t[4], t[5], t[2]};
+      float T[9], Iw[9];
+      for (int i = 0; i < 3; i++)
+        for (int j = 0; j < 3; j++) T[3 * i + j] = X[3 * i] * Ib[j] + X[3 * i + 1] * Ib[3 + j] + X[3 * i + 2] * Ib[6 + j];
+      for (int i = 0; i < 3; i++)
+        for (int j = 0; j < 3; j++) Iw[3 * i + j] = T[3 * i] * X[3 * j] + T[3 * i + 1] * X[3 * j + 1] + T[3 * i + 2] * X[3 * j + 2];
+      int root = m->body_rootid[b];
+      float c[3] = {W->xipos[b][0] - W->scom[root][0], W->xipos[b][1] - W->scom[root][1], W->xipos[b][2] - W->scom[root][2]};
+      float cc = dot3(c, c);
+      ci[0] = Iw[0] + mass * (cc - c[0] * c[0]);
+      ci[1] = Iw[4] + mass * (cc - c[1] * c[1]);
+      ci[2] = Iw[8] + mass * (cc - c[2] * c[2]);
+      ci[3] = Iw[1] - mass * c[0] * c[1];
+      ci[4] = Iw[2] - mass * c[0] * c[2];
+      ci[5] = Iw[5] - mass * c[1] * c[2];
+      ci[6] = mass * c[0]; ci[7] = mass * c[1]; ci[8] = mass * c[2]; ci[9] = mass;
+    }
+  }
+  if (lane >= 32 && lane - 32 < m->nv) {
+    int d = lane - 32, j = m->dof_jntid[d], b = m->dof_bodyid[d];
+    LDSA float* cd = W->cdof[d];
+    int root = m->body_rootid[b];
+    float off[3] = {W->scom[root][0] - W->xanchor[j][0], W->scom[root][1] - W->xanchor[j][1],
+                    W->scom[root][2] - W->xanchor[j][2]};
+    int k = d - m->jnt_dofadr[j];
+    if (m->jnt_type[j] == MJL_JNT_FREE && k < 3) {
+      for (int i = 0; i < 6; i++) cd[i] = 0.f;
+      cd[3 + k] = 1.f;
+    } else {
+      float ax[3];
+      if (m->jnt_type[j] == MJL_JNT_FREE) {
+        ax[0] = W->xmat[b][k - 3]; ax[1] = W->xmat[b][3 + k - 3]; ax[2] = W->xmat[b][6 + k - 3];
+      } else {
+        ax[0] = W->xaxis[j][0]; ax[1] = W->xaxis[j][1]; ax[2] = W->xaxis[j][2];
+      }
+      float l[3];
+      cross3(l, ax, off);
+      cd[0] = ax[0]; cd[1] = ax[1]; cd[2] = ax[2]; cd[3] = l[0]; cd[4] = l[1]; cd[5] = l[2];
+    }
+  }
+  SYNC();
+  if (lane < m->nbody) {
+    int b = lane;
+    float s[10];
+    for (int i = 0; i < 10; i++) s[i] = 0.f;
+    for (int c = b; c < m->body_subtree_end[b]; c++)
+      for (int i = 0; i < 10; i++) s[i] += W->cinert[c][i];
+    for (int i = 0; i < 10; i++) W->crb[b][i] = s[i];
+  }
+  for (int i = lane; i < D::NV * LD; i += 64) W->M[i] = 0.f;
+  SYNC();
+  if (lane < m->nv) {  // column `lane` of M along the ancestor chain  [smooth.crb / make_m]
+    int i = lane;
+    float f[6], c6[6], cr[10];
+    for (int k = 0; k < 6; k++) c6[k] = W->cdof[i][k];
+    for (int k = 0; k < 10; k++) cr[k] = W->crb[m->dof_bodyid[i]][k];
+    inert_vec(f, cr, c6);
+    for (int j = i; j >= 0; j = m->dof_parentid[j]) {
+      LDSA float* c = W->cdof[j];
+      float v = c[0] * f[0] + c[1] * f[1] + c[2] * f[2] + c[3] * f[3] + c[4] * f[4] + c[5] * f[5];
+      if (j == i) v += m->dof_armature[i];
+      W->M[i * LD + j] = v;
+      W->M[j * LD + i] = v;
+    }
+  }
+  SYNC();
+}
+
+// ---------------------------------------------------------------------------------------------
+// velocity stage: com_vel + rne forward pass by levels, backward by subtree ranges; passive
+// forces and actuation   [smooth.com_vel / smooth.rne / passive.passive / forward.fwd_actuation]
+// ---------------------------------------------------------------------------------------------
+template <class D> NOINL void velocity_stage(MP m_, LDSA WS<D>* W, int lane) {
+  MP m = uniform_ptr(m_);
+  if (lane == 0) {
+    for (int i = 0; i < 6; i++) W->cvel[0][i] = 0.f;
+    W->cacc[0][0] = W->cacc[0][1] = W->cacc[0][2] = 0.f;
+    W->cacc[0][3] = -m->gravity[0]; W->cacc[0][4] = -m->gravity[1]; W->cacc[0][5] = -m->gravity[2];
+  }
+  SYNC();
+  const int maxlevel = m->maxlevel, nbody = m->nbody;
+  for (int L = 1; L <= maxlevel; L++) {
+    int b = lane;
+    if (b < nbody && m->body_level[b] == L) {
+      int p = m->body_parentid[b];
+      float cv[6], ca[6];
+      for (int i = 0; i < 6; i++) { cv[i] = W->cvel[p][i]; ca[i] = W->cacc[p][i]; }
+      int ja = m->body_jntadr[b], jn = m->body_jntnum[b];
+      for (int j = ja; j < ja + jn; j++) {
+        int da = m->jnt_dofadr[j];
+        if (m->jnt_type[j] == MJL_JNT_FREE) {
+          for (int k = 0; k < 3; k++)
+            for (int i = 0; i < 6; i++) cv[i] += W->cdof[da + k][i] * W->qvel[da + k];
+          float cd[3][6];
+          for (int k = 0; k < 3; k++) {
+            float c6[6];
+            for (int i = 0; i < 6; i++) c6[i] = W->cdof[da + 3 + k][i];
+            cross_motion(cd[k], cv, c6);
+          }
+          for (int k = 0; k < 3; k++) {
+            float qd = W->qvel[da + 3 + k];
+            for (int i = 0; i < 6; i++) ca[i] += cd[k][i] * qd;
+          }
+          for (int k = 0; k < 3; k++)
+            for (int i = 0; i < 6; i++) cv[i] += W->cdof[da + 3 + k][i] * W->qvel[da + 3 + k];
+        } else {
+          float cd[6], c6[6];
+          for (int i = 0; i < 6; i++) c6[i] = W->cdof[da][i];
+          cross_motion(cd, cv, c6);
+          float qd = W->qvel[da];
+          for (int i = 0; i < 6; i++) { ca[i] += cd[i] * qd; cv[i] += c6[i] * qd; }
+        }
+      }
+      for (int i = 0; i < 6; i++) { W->cvel[b][i] = cv[i]; W->cacc[b][i] = ca[i]; }
+    }
+    SYNC();
+  }
+  // body forces cfrc = I*a + v x* (I*v), written over cacc
+  float f[6];
+  bool hasb = lane > 0 && lane < nbody;
+  if (hasb) {
+    float f1[6], iv[6], f2[6], cv[6], ca[6], ci[10];
+    for (int i = 0; i < 6; i++) { cv[i] = W->cvel[lane][i]; ca[i] = W->cacc[lane][i]; }
+    for (int i = 0; i < 10; i++) ci[i] = W->cinert[lane][i];
+    inert_vec(f1, ci, ca);
+    inert_vec(iv, ci, cv);
+    cross_force(f2, cv, iv);
+    for (int i = 0; i < 6; i++) f[i] = f1[i] + f2[i];
+  }
+  SYNC();
+  if (hasb) for (int i = 0; i < 6; i++) W->cacc[lane][i] = f[i];
+  SYNC();
+  if (hasb) {  // subtree sums of cfrc into cvel (cvel is no longer needed)
+    float s[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    for (int c = lane; c < m->body_subtree_end[lane]; c++)
+      for (int i = 0; i < 6; i++) s[i] += W->cacc[c][i];
+    for (int i = 0; i < 6; i++) W->cvel[lane][i] = s[i];
+  }
+  SYNC();
+  if (lane < m->nv) {
+    LDSA float* c = W->cdof[lane];
+    LDSA float* fb = W->cvel[m->dof_bodyid[lane]];
+    W->frc_bias[lane] = c[0] * fb[0] + c[1] * fb[1] + c[2] * fb[2] + c[3] * fb[3] + c[4] * fb[4] + c[5] * fb[5];
+    int j = m->dof_jntid[lane];
+    float pf = -m->dof_damping[lane] * W->qvel[lane];
+    if (m->jnt_type[j] == MJL_JNT_HINGE) {
+      int qa = m->jnt_qposadr[j];
+      pf -= m->jnt_stiffness[j] * (W->qpos[qa] - m->qpos_spring[qa]);
+    }
+    W->frc_passive[lane] = pf;
+    W->frc_act[lane] = 0.f;
+  }
+  SYNC();
+  if (lane < m->nu) {  // motors with joint transmission
+    float c = W->ctrl[lane];
+    if (m->actuator_ctrllimited[lane]) c = fminf(fmaxf(c, m->actuator_ctrlrange[lane][0]), m->actuator_ctrlrange[lane][1]);
+    atomicAdd((float*)&W->frc_act[m->actuator_dof[lane]], m->actuator_gear[lane] * c);
+  }
+  SYNC();
+  if (lane < m->nv) W->frc_smooth[lane] = W->frc_passive[lane] - W->frc_bias[lane] + W->frc_act[lane];
+  SYNC();
+}
+
+// ---------------------------------------------------------------------------------------------
+// collision (MJX collision_primitive semantics)
+// ---------------------------------------------------------------------------------------------
+INL void make_frame(float* fr, const float* a_in) {  // math.make_frame
+  float a[3] = {a_in[0], a_in[1], a_in[2]};
+  norm3(a);
+  float b[3] = {0.f, 0.f, 0.f};
+  if (a[1] > -0.5f && a[1] < 0.5f) b[1] = 1.f; else b[2] = 1.f;
+  float ab = dot3(a, b);
+  b[0] -= a[0] * ab; b[1] -= a[1] * ab; b[2] -= a[2] * ab;
+  norm3(b);
+  float c[3];
+  cross3(c, a, b);
+  for (int i = 0; i < 3; i++) { fr[i] = a[i]; fr[3 + i] = b[i]; fr[6 + i] = c[i]; }
+}
+INL void seg_point(float* r, const float* a, const float* b, const float* pt) {  // math.closest_segment_point
+  float ab[3] = {b[0] - a[0], b[1] - a[1], b[2] - a[2]};
+  float ap[3] = {pt[0] - a[0], pt[1] - a[1], pt[2] - a[2]};
+  float t = dot3(ap, ab) / (dot3(ab, ab) + 1e-6f);
+  t = fminf(fmaxf(t, 0.f), 1.f);
+  r[0] = a[0] + t * ab[0]; r[1] = a[1] + t * ab[1]; r[2] = a[2] + t * ab[2];
+}
+INL float sph_sph(float* pos, float* n, const float* p1, float r1, const float* p2, float r2) {
+  n[0] = p2[0] - p1[0]; n[1] = p2[1] - p1[1]; n[2] = p2[2] - p1[2];
+  float dist = norm3(n) - (r1 + r2);
+  float s = r1 + dist * 0.5f;
+  pos[0] = p1[0] + n[0] * s; pos[1] = p1[1] + n[1] * s; pos[2] = p1[2] + n[2] * s;
+  return dist;
+}
+
+// candidate contact k (0/1) of pair p; returns false if the pair has no k-th contact
+template <class D> INL bool collide(MP m, LDSA WS<D>* W, int p, int k, float& dist, float* pos, float* fr) {
+  int kind = m->pair_kind[p];
+  if (k == 1 && kind != MJL_COL_PLANE_CAPSULE) return false;
+  int g1 = m->pair_geom1[p], g2 = m->pair_geom2[p];
+  float x1[3] = {W->gpos[g1][0], W->gpos[g1][1], W->gpos[g1][2]};
+  float x2[3] = {W->gpos[g2][0], W->gpos[g2][1], W->gpos[g2][2]};
+  float z1[3] = {W->gaxis[g1][0], W->gaxis[g1][1], W->gaxis[g1][2]};
+  float z2[3] = {W->gaxis[g2][0], W->gaxis[g2][1], W->gaxis[g2][2]};
+  float r1 = m->geom_size[g1][0], r2 = m->geom_size[g2][0];
+  float h1 = m->geom_size[g1][1], h2 = m->geom_size[g2][1];
+  if (kind == MJL_COL_PLANE_SPHERE) {
+    float d[3] = {x2[0] - x1[0], x2[1] - x1[1], x2[2] - x1[2]};
+    dist = dot3(d, z1) - r2;
+    float s = r2 + 0.5f * dist;
+    pos[0] = x2[0] - z1[0] * s; pos[1] = x2[1] - z1[1] * s; pos[2] = x2[2] - z1[2] * s;
+    make_frame(fr, z1);
+    return true;
+  }
+  if (kind == MJL_COL_PLANE_CAPSULE) {
+    const float* n = z1;
+    float nd = dot3(n, z2);
+    float b[3] = {z2[0] - n[0] * nd, z2[1] - n[1] * nd, z2[2] - n[2] * nd};
+    float bn = norm3(b);
+    if (bn < 0.5f) {
+      b[0] = 0.f; b[1] = 0.f; b[2] = 0.f;
+      if (n[1] > -0.5f && n[1] < 0.5f) b[1] = 1.f; else b[2] = 1.f;
+    }
+    float c[3];
+    cross3(c, n, b);
+    float sg = (k == 0) ? 1.f : -1.f;
+    float sp[3] = {x2[0] + sg * z2[0] * h2, x2[1] + sg * z2[1] * h2, x2[2] + sg * z2[2] * h2};
+    float d[3] = {sp[0] - x1[0], sp[1] - x1[1], sp[2] - x1[2]};
+    dist = dot3(d, n) - r2;
+    float s = r2 + 0.5f * dist;
+    pos[0] = sp[0] - n[0] * s; pos[1] = sp[1] - n[1] * s; pos[2] = sp[2] - n[2] * s;
+    for (int i = 0; i < 3; i++) { fr[i] = n[i]; fr[3 + i] = b[i]; fr[6 + i] = c[i]; }
+    return true;
+  }
+  float pa[3], pb[3];
+  if (kind == MJL_COL_SPHERE_SPHERE) {
+    for (int i = 0; i < 3; i++) { pa[i] = x1[i]; pb[i] = x2[i]; }
+  } else if (kind == MJL_COL_SPHERE_CAPSULE) {
+    float a[3] = {x2[0] - z2[0] * h2, x2[1] - z2[1] * h2, x2[2] - z2[2] * h2};
+    float bb[3] = {x2[0] + z2[0] * h2, x2[1] + z2[1] * h2, x2[2] + z2[2] * h2};
+    for (int i = 0; i < 3; i++) pa[i] = x1[i];
+    seg_point(pb, a, bb, x1);
+  } else {  // capsule-capsule (math.closest_segment_to_segment_points)
+    float a0[3], a1[3], b0[3], b1[3];
+    for (int i = 0; i < 3; i++) {
+      a0[i] = x1[i] - z1[i] * h1; a1[i] = x1[i] + z1[i] * h1;
+      b0[i] = x2[i] - z2[i] * h2; b1[i] = x2[i] + z2[i] * h2;
+    }
+    float da[3] = {a1[0] - a0[0], a1[1] - a0[1], a1[2] - a0[2]};
+    float db[3] = {b1[0] - b0[0], b1[1] - b0[1], b1[2] - b0[2]};
+    float la = norm3(da), lb = norm3(db);
+    float ha = la * 0.5f, hb = lb * 0.5f;
+    float am[3], bm[3], tr[3];
+    for (int i = 0; i < 3; i++) { am[i] = a0[i] + da[i] * ha; bm[i] = b0[i] + db[i] * hb; tr[i] = am[i] - bm[i]; }
+    float dadb = dot3(da, db), datr = dot3(da, tr), dbtr = dot3(db, tr);
+    float den = 1.f - dadb * dadb;
+    float ta0 = (-datr + dadb * dbtr) / (den + 1e-6f);
+    float tb0 = dbtr + ta0 * dadb;
+    float ta = fminf(fmaxf(ta0, -ha), ha), tb = fminf(fmaxf(tb0, -hb), hb);
+    float na[3], nb[3];
+    for (int i = 0; i < 3; i++) { pa[i] = am[i] + da[i] * ta; pb[i] = bm[i] + db[i] * tb; }
+    seg_point(na, a0, a1, pb);
+    seg_point(nb, b0, b1, pa);
+    float d1 = 0.f, d2 = 0.f;
+    for (int i = 0; i < 3; i++) { d1 += (pb[i] - na[i]) * (pb[i] - na[i]); d2 += (pa[i] - nb[i]) * (pa[i] - nb[i]); }
+    if (d1 < d2) { pa[0] = na[0]; pa[1] = na[1]; pa[2] = na[2]; }
+    else { pb[0] = nb[0]; pb[1] = nb[1]; pb[2] = nb[2]; }
+  }
+  float n[3];
+  dist = sph_sph(pos, n, pa, r1, pb, r2);
+  make_frame(fr, n);
+  return true;
+}
+
+// ---------------------------------------------------------------------------------------------
+// constraint rows: limits, contacts; then per-row D / aref   [constraint.make_constraint]
+// ---------------------------------------------------------------------------------------------
+INL void kbi(float tstep, const CSTA float* solref, const CSTA float* solimp, float pos, float& k, float& b,
+             float& imp) {
+  float timeconst = fmaxf(solref[0], 2.f * tstep), dampratio = solref[1];
+  float dmin = fminf(fmaxf(solimp[0], kMinImp), kMaxImp);
+  float dmax = fminf(fmaxf(solimp[1], kMinImp), kMaxImp);
+  float width = fmaxf(kMinVal, solimp[2]);
+  float mid = fminf(fmaxf(solimp[3], kMinImp), kMaxImp);
+  float power = fmaxf(1.f, solimp[4]);
+  k = 1.f / (dmax * dmax * timeconst * timeconst * dampratio * dampratio);
+  b = 2.f / (dmax * timeconst);
+  if (solref[0] <= 0.f) k = -solref[0] / (dmax * dmax);
+  if (solref[1] <= 0.f) b = -solref[1] / dmax;
+  float x = fabsf(pos) / width;
+  float y;
+  if (power == 2.f) {  // the default power: exact squares instead of powf
+    y = (x < mid) ? (1.f / mid) * x * x : 1.f - (1.f / (1.f - mid)) * (1.f - x) * (1.f - x);
+  } else {
+    y = (x < mid) ? (1.f / powf(mid, power - 1.f)) * powf(x, power)
+                  : 1.f - (1.f / powf(1.f - mid, power - 1.f)) * powf(1.f - x, power);
+  }
+  imp = dmin + y * (dmax - dmin);
+  imp = fminf(fmaxf(imp, dmin), dmax);
+  if (x > 1.f) imp = dmax;
+}
+
+// Builds limit and contact rows into R (capacity R.cap / R.capc). Returns false, without writing
+// past capacity, when they do not fit; W->ncon / nefc always hold the true counts.
+template <class D, bool G> NOINL bool build_rows(MP m_, LDSA WS<D>* W, Rows<G> R, int lane) {
+  MP m = uniform_ptr(m_);
+  constexpr int LD = D::LD;
+  typedef typename Rows<G>::F RF;
+  const int nv = m->nv, cap = R.cap, capc = R.capc;
+  int nl = 0;
+  {  // joint limits (lane = joint), then tendon limits (lane = tendon), ballot-compacted
+    bool act = false;
+    float dist = 0.f, sgn = 0.f;
+    if (lane < m->njnt && m->jnt_limited[lane] && m->jnt_type[lane] == MJL_JNT_HINGE) {
+      float q = W->qpos[m->jnt_qposadr[lane]];
+      float dmin = q - m->jnt_range[lane][0], dmax = m->jnt_range[lane][1] - q;
+      dist = fminf(dmin, dmax);
+      sgn = dmin < dmax ? 1.f : -1.f;
+      act = dist - m->jnt_margin[lane] < 0.f;
+    }
+    unsigned long long bal = __ballot(act);
+    int r = __popcll(bal & lanes_below(lane));
+    if (act && r < cap) {
+      RF* Jr = R.J + r * LD;
+      for (int k = 0; k < LD; k++) Jr[k] = 0.f;
+      Jr[m->jnt_dofadr[lane]] = sgn;
+      R.epos[r] = dist - m->jnt_margin[lane];
+      R.einvw[r] = m->dof_invweight0[m->jnt_dofadr[lane]];
+      R.emeta[r] = (0 << 16) | lane;
+    }
+    nl = __popcll(bal);
+    act = false;
+    if (lane < m->ntendon && m->tendon_limited[lane]) {
+      float len = W->tenlen[lane];
+      float dmin = len - m->tendon_range[lane][0], dmax = m->tendon_range[lane][1] - len;
+      dist = fminf(dmin, dmax);
+      sgn = dmin < dmax ? 1.f : -1.f;
+      act = dist - m->tendon_margin[lane] < 0.f;
+    }
+    bal = __ballot(act);
+    r = nl + __popcll(bal & lanes_below(lane));
+    if (act && r < cap) {
+      RF* Jr = R.J + r * LD;
+      for (int k = 0; k < LD; k++) Jr[k] = (k < nv) ? sgn * W->tenJ[lane][k] : 0.f;
+      R.epos[r] = dist - m->tendon_margin[lane];
+      R.einvw[r] = m->tendon_invweight0[lane];
+      R.emeta[r] = (1 << 16) | lane;
+    }
+    nl += __popcll(bal);
+  }
+  // contacts: one pass over candidate pairs (lane = pair), active ones compacted in pair order
+  int nc = 0, nr = nl;
+  const int npair = m->npair;
+  for (int base = 0; base < npair; base += 64) {
+    int p = base + lane;
+    for (int k = 0; k < 2; k++) {
+      bool act = false;
+      float dist = 0.f, pos[3], fr[9];
+      int condim = 1;
+      if (p < npair && collide(m, W, p, k, dist, pos, fr)) {
+        act = dist - m->pair_includemargin[p] < 0.f;
+        condim = m->pair_condim[p];
+      }
+      // rows per contact are 1 (condim 1) or 4 (condim 3, pyramidal): prefix sums from ballots
+      unsigned long long b1 = __ballot(act && condim == 1), b4 = __ballot(act && condim != 1);
+      unsigned long long below = lanes_below(lane);
+      int slot = __popcll((b1 | b4) & below);
+      int rbefore = __popcll(b1 & below) + 4 * __popcll(b4 & below);
+      int rows = condim == 1 ? 1 : 4;
+      int c = nc + slot, r0 = nr + rbefore;
+      if (act && c < capc && r0 + rows <= cap) {
+        RF* cr = R.con + c * CONW;
+        cr[0] = pos[0]; cr[1] = pos[1]; cr[2] = pos[2];
+        for (int i = 0; i < 9; i++) cr[3 + i] = fr[i];
+        R.con_pair[c] = p;
+        R.con_efc[c] = r0;
+        float ep = dist - m->pair_includemargin[p], iw = m->pair_invweight[p];
+        for (int q = 0; q < rows; q++) {
+          R.epos[r0 + q] = ep;
+          R.einvw[r0 + q] = iw;
+          R.emeta[r0 + q] = (2 << 16) | p;
+        }
+      }
+      nc += __popcll(b1 | b4);
+      nr += __popcll(b1) + 4 * __popcll(b4);
+    }
+  }
+  if (lane == 0) { W->ncon = nc; W->nefc = nr; W->nlim = nl; }
+  SYNC();
+  if (nr > cap || nc > capc) return false;
+  // contact Jacobian rows: lanes 0..31 -> contact c, lanes 32..63 -> contact c+1; lane%32 = dof
+  const int d = lane & 31;
+  for (int c0 = 0; c0 < nc; c0 += 2) {
+    int c = c0 + (lane >> 5);
+    if (c < nc && d < LD) {
+      RF* cr = R.con + c * CONW;
+      int p = R.con_pair[c];
+      int b1 = m->geom_bodyid[m->pair_geom1[p]], b2 = m->geom_bodyid[m->pair_geom2[p]];
+      int dim = m->pair_condim[p];
+      int r0 = R.con_efc[c];
+      float vn = 0.f, vt1 = 0.f, vt2 = 0.f;
+      if (d < nv) {
+        float s = (float)((m->body_dofmask[b2] >> d) & 1u) - (float)((m->body_dofmask[b1] >> d) & 1u);
+        if (s != 0.f) {
+          float cd[6];
+          for (int i = 0; i < 6; i++) cd[i] = W->cdof[d][i];
+          int root = m->body_rootid[m->dof_bodyid[d]];
+          float off[3] = {cr[0] - W->scom[root][0], cr[1] - W->scom[root][1], cr[2] - W->scom[root][2]};
+          float cx[3];
+          cross3(cx, cd, off);
+          float jp[3] = {s * (cd[3] + cx[0]), s * (cd[4] + cx[1]), s * (cd[5] + cx[2])};
+          vn = cr[3] * jp[0] + cr[4] * jp[1] + cr[5] * jp[2];
+          vt1 = cr[6] * jp[0] + cr[7] * jp[1] + cr[8] * jp[2];
+          vt2 = cr[9] * jp[0] + cr[10] * jp[1] + cr[11] * jp[2];
+        }
+      }
+      if (dim == 1) {
+        R.J[r0 * LD + d] = vn;
+      } else {
+        float mu = m->pair_mu[p];
+        R.J[(r0 + 0) * LD + d] = vn + mu * vt1;
+        R.J[(r0 + 1) * LD + d] = vn - mu * vt1;
+        R.J[(r0 + 2) * LD + d] = vn + mu * vt2;
+        R.J[(r0 + 3) * LD + d] = vn - mu * vt2;
+      }
+    }
+  }
+  SYNC();
+  // per-row impedance, D and reference acceleration (lane = row)
+  for (int r = lane; r < nr; r += 64) {
+    int meta = R.emeta[r], type = meta >> 16, id = meta & 0xffff;
+    const CSTA float *sr, *si;
+    if (type == 0) { sr = m->jnt_solref[id]; si = m->jnt_solimp[id]; }
+    else if (type == 1) { sr = m->tendon_solref[id]; si = m->tendon_solimp[id]; }
+    else { sr = m->pair_solref[id]; si = m->pair_solimp[id]; }
+    float k, b, imp, pos = R.epos[r];
+    kbi(m->timestep, sr, si, pos, k, b, imp);
+    float rr = fmaxf(R.einvw[r] * (1.f - imp) / imp, kMinVal);
+    R.D[r] = 1.f / rr;
+    float vel = 0.f;
+#pragma unroll
+    for (int kk = 0; kk < LD; kk++) vel += R.J[r * LD + kk] * W->qvel[kk];
+    R.aref[r] = -b * vel - k * imp * pos;
+  }
+  SYNC();
+  return true;
+}
+
+// ---------------------------------------------------------------------------------------------
+// primal solver (Newton with exact line search; CG with Polak-Ribiere)   [solver.solve]
+// ---------------------------------------------------------------------------------------------
+template <class D> INL float mrow(LDSA WS<D>* W, LDSA float* v, int lane) {  // (M v)[lane]
+  constexpr int LD = D::LD;
+  float s = 0.f;
+#pragma unroll
+  for (int k = 0; k < LD; k++) s += W->M[lane * LD + k] * v[k];
+  return s;
+}
+template <class D, class RowF> INL float jrow(RowF* J, LDSA float* v, int r) {  // (J v)[r]
+  constexpr int LD = D::LD;
+  float s = 0.f;
+#pragma unroll
+  for (int k = 0; k < LD; k++) s += J[r * LD + k] * v[k];
+  return s;
+}
+
+// forces, cost, qfrc_constraint and gradient at the current qacc / Ma / jar; returns the cost
+template <class D, bool G> INL float solver_update(MP m_, LDSA WS<D>* W, Rows<G> R, int lane) {
+  MP m = uniform_ptr(m_);
+  constexpr int LD = D::LD;
+  const int nv = m->nv, nefc = W->nefc;
+  float c = 0.f;
+  for (int r = lane; r < nefc; r += 64) {
+    float j = R.jar[r];
+    float f = j < 0.f ? -R.D[r] * j : 0.f;
+    R.force[r] = f;
+    if (j < 0.f) c += 0.5f * R.D[r] * j * j;
+  }
+  SYNC();
+  int d = lane & 31, h = lane >> 5;  // J' f : lane%32 = dof, lane/32 = row parity
+  float s = 0.f;
+  if (d < nv)
+    for (int r = h; r < nefc; r += 2) s += R.J[r * LD + d] * R.force[r];
+  s += __shfl_xor(s, 32);
+  float g = 0.f;
+  if (lane < nv) {
+    W->frc_con[lane] = s;
+    float ma = W->Ma[lane];
+    g = 0.5f * (ma - W->frc_smooth[lane]) * (W->qacc[lane] - W->qacc_smooth[lane]);
+    W->grad[lane] = ma - W->frc_smooth[lane] - s;
+  }
+  float cost = wsum(g + c);
+  SYNC();
+  return cost;
+}
+
+// Newton direction: Mgrad = H^-1 grad with H = M + J' D_active J
+template <class D, bool G> INL void solver_newton_dir(MP m_, LDSA WS<D>* W, Rows<G> R, int lane) {
+  MP m = uniform_ptr(m_);
+  constexpr int LD = D::LD;
+  const int nv = m->nv, nefc = W->nefc;
+  const int l = lane & 31, kh = lane >> 5;  // lane = (column l, half kh of the rows of H)
+  float acc[16];
+#pragma unroll
+  for (int kk = 0; kk < 16; kk++) {
+    int k = 16 * kh + kk;
+    acc[kk] = (l < nv && k < nv) ? W->M[k * LD + l] : 0.f;
+  }
+  for (int r = 0; r < nefc; r++) {
+    if (R.jar[r] < 0.f) {
+      float w = (l < LD) ? R.D[r] * R.J[r * LD + l] : 0.f;
+#pragma unroll
+      for (int kk = 0; kk < 16; kk++) {
+        int k = 16 * kh + kk;
+        if (k < LD) acc[kk] = fmaf(w, R.J[r * LD + k], acc[kk]);
+      }
+    }
+  }
+  if (l < nv) {
+#pragma unroll
+    for (int kk = 0; kk < 16; kk++) {
+      int k = 16 * kh + kk;
+      if (k < nv) W->H[k * LD + l] = acc[kk];
+    }
+  }
+  SYNC();
+  chol_factor<D>(W->H, W->invd, nv, lane);
+  float x = chol_solve<D>(W->H, W->invd, lane < nv ? W->grad[lane] : 0.f, lane);
+  if (lane < nv) W->Mgrad[lane] = x;
+  SYNC();
+}
+
+// exact line search along `search`: safeguarded Newton on the piecewise-linear f'(alpha)
+template <class D, bool G> INL float solver_linesearch(MP m_, LDSA WS<D>* W, Rows<G> R, int lane) {
+  MP m = uniform_ptr(m_);
+  const int nv = m->nv, nefc = W->nefc;
+  float sn = (lane < nv) ? W->search[lane] * W->search[lane] : 0.f;
+  float snorm = sqrtf(wsum(sn));
+  if (!(snorm >= kMinVal)) return 0.f;
+  float gtol = m->tolerance * m->ls_tolerance * snorm / m->scale;
+  float mvl = 0.f;
+  if (lane < nv) { mvl = mrow<D>(W, W->search, lane); W->Mv[lane] = mvl; }
+  for (int r = lane; r < nefc; r += 64) R.Jv[r] = jrow<D>(R.J, W->search, r);
+  float c1p = 0.f, c2p = 0.f;
+  if (lane < nv) { c1p = W->search[lane] * (W->Ma[lane] - W->frc_smooth[lane]); c2p = W->search[lane] * mvl; }
+  float c1 = wsum(c1p), c2 = wsum(c2p);
+  SYNC();
+  // the first 128 rows stay in registers across the line-search iterations
+  float jv0 = 0.f, ja0 = 0.f, dd0 = 0.f, jv1 = 0.f, ja1 = 0.f, dd1 = 0.f;
+  if (lane < nefc) { jv0 = R.Jv[lane]; ja0 = R.jar[lane]; dd0 = R.D[lane]; }
+  if (lane + 64 < nefc) { jv1 = R.Jv[lane + 64]; ja1 = R.jar[lane + 64]; dd1 = R.D[lane + 64]; }
+  auto eval = [&](float al, float& der, float& hes) {
+    float dp = 0.f, hp = 0.f;
+    float j = ja0 + al * jv0;
+    if (j < 0.f) { float dj = dd0 * jv0; dp += dj * j; hp += dj * jv0; }
+    j = ja1 + al * jv1;
+    if (j < 0.f) { float dj = dd1 * jv1; dp += dj * j; hp += dj * jv1; }
+    for (int r = lane + 128; r < nefc; r += 64) {
+      float jv = R.Jv[r];
+      float jj = R.jar[r] + al * jv;
+      if (jj < 0.f) { float dj = R.D[r] * jv; dp += dj * jj; hp += dj * jv; }
+    }
+    der = c1 + al * c2 + wsum(dp);
+    hes = c2 + wsum(hp);
+  };
+  float der, hes;
+  eval(0.f, der, hes);
+  if (!(der < 0.f)) return 0.f;
+  float lo = 0.f, hi = -1.f;
+  float alpha = -der / hes;
+  const int lsit = m->ls_iterations;
+  for (int it = 0; it < lsit; it++) {
+    eval(alpha, der, hes);
+    if (fabsf(der) < gtol) break;
+    if (der < 0.f) lo = alpha; else hi = alpha;
+    float nxt = alpha - der / hes;
+    bool inside = nxt > lo && (hi < 0.f || nxt < hi);
+    if (!inside) nxt = hi < 0.f ? 2.f * alpha : 0.5f * (lo + hi);
+    if (nxt == alpha) break;
+    alpha = nxt;
+  }
+  return alpha;
+}
+
+template <class D, bool G> NOINL void solver(MP m_, LDSA WS<D>* W, Rows<G> R, int lane) {
+  MP m = uniform_ptr(m_);
+  constexpr int LD = D::LD;
+  const int nv = m->nv, nefc = W->nefc;
+  const bool newton = m->solver == MJL_SOLVER_NEWTON;
+  if (nefc == 0) {
+    if (lane < LD) { W->qacc[lane] = W->qacc_smooth[lane]; W->frc_con[lane] = 0.f; }
+    if (lane == 0) W->niter = 0;
+    SYNC();
+    return;
+  }
+  const float scale = m->scale;
+  // warm start: the cheaper of qacc_warmstart and qacc_smooth
+  float cost2[2];
+  for (int w = 0; w < 2; w++) {
+    LDSA float* q = w == 0 ? W->qacc_ws : W->qacc_smooth;
+    float g = 0.f;
+    if (lane < nv) g = 0.5f * (mrow<D>(W, q, lane) - W->frc_smooth[lane]) * (q[lane] - W->qacc_smooth[lane]);
+    float c = 0.f;
+    for (int r = lane; r < nefc; r += 64) {
+      float j = jrow<D>(R.J, q, r) - R.aref[r];
+      if (j < 0.f) c += 0.5f * R.D[r] * j * j;
+    }
+    cost2[w] = wsum(g + c);
+  }
+  LDSA float* q0 = cost2[0] < cost2[1] ? W->qacc_ws : W->qacc_smooth;
+  if (lane < LD) W->qacc[lane] = q0[lane];
+  SYNC();
+  if (lane < nv) W->Ma[lane] = mrow<D>(W, W->qacc, lane);
+  for (int r = lane; r < nefc; r += 64) R.jar[r] = jrow<D>(R.J, W->qacc, r) - R.aref[r];
+  SYNC();
+  // Newton / CG iterations, written so that each helper appears once in the loop body.
+  // Exact early exit (Newton): rows are affine in alpha, so if the active set at the new point
+  // equals the set the Hessian was built from, no row switched along the step, the cost was one
+  // quadratic there and the exact line search landed on its minimiser, where the gradient is
+  // zero: the global optimum MuJoCo's tolerance test converges to. In fp32 that test only fires
+  // once rounding noise turns the improvement non-positive, which costs extra iterations.
+  float cost = 0.f;
+  int iter = 0;
+  const int maxit = m->iterations;
+  const bool exact_exit = newton && nefc <= 256;
+  unsigned long long hm[4] = {0ull, 0ull, 0ull, 0ull};
+  auto active_masks = [&](unsigned long long* out) {
+#pragma unroll
+    for (int c = 0; c < 4; c++) {
+      int r = lane + 64 * c;
+      out[c] = __ballot(r < nefc && R.jar[r] < 0.f);
+    }
+  };
+  for (bool first = true;; first = false) {
+    if (!first) {
+      float alpha = solver_linesearch<D, G>(m, W, R, lane);
+      if (!(alpha != 0.f)) break;  // also stops on NaN
+      if (lane < nv) {
+        W->qacc[lane] += alpha * W->search[lane];
+        W->Ma[lane] += alpha * W->Mv[lane];
+        if (!newton) { W->gradold[lane] = W->grad[lane]; W->Mgradold[lane] = W->Mgrad[lane]; }
+      }
+      for (int r = lane; r < nefc; r += 64) R.jar[r] += alpha * R.Jv[r];
+      SYNC();
+    }
+    float oldcost = cost;
+    cost = solver_update<D, G>(m, W, R, lane);
+    if (!first) {
+      iter++;
+      float gp = (lane < nv) ? W->grad[lane] * W->grad[lane] : 0.f;
+      float gnorm = scale * sqrtf(wsum(gp));
+      float improvement = scale * (oldcost - cost);
+      if (improvement < m->tolerance || gnorm < m->tolerance || iter >= maxit) break;
+      if (exact_exit) {
+        unsigned long long am[4];
+        active_masks(am);
+        if (am[0] == hm[0] && am[1] == hm[1] && am[2] == hm[2] && am[3] == hm[3]) break;
+      }
+    }
+    if (newton) {
+      if (exact_exit) active_masks(hm);
+      solver_newton_dir<D, G>(m, W, R, lane);
+      if (lane < LD) W->search[lane] = (lane < nv) ? -W->Mgrad[lane] : 0.f;
+    } else {
+      float x = chol_solve<D>(W->H, W->invd, lane < nv ? W->grad[lane] : 0.f, lane);  // H holds L(M)
+      if (lane < nv) W->Mgrad[lane] = x;
+      float num = 0.f, den = 0.f;
+      if (!first && lane < nv) {
+        num = W->grad[lane] * (x - W->Mgradold[lane]);
+        den = W->gradold[lane] * W->Mgradold[lane];
+      }
+      num = wsum(num);
+      den = wsum(den);
+      float beta = (!first && den > kMinVal) ? fmaxf(0.f, num / den) : 0.f;
+      if (lane < LD) W->search[lane] = (lane < nv) ? -x + beta * W->search[lane] : 0.f;
+    }
+    SYNC();
+  }
+  if (lane == 0) W->niter = iter;
+  SYNC();
+}
+
+// touch sensors (lane = sensor)   [sensor.sensor_acc, MuJoCo mjSENS_TOUCH]
+template <class D, bool G> NOINL void sensors(MP m_, LDSA WS<D>* W, Rows<G> R, int lane) {
+  MP m = uniform_ptr(m_);
+  if (lane < m->nsensor) {
+    int site = m->sensor_objid[lane], body = m->site_bodyid[site];
+    float val = 0.f;
+    const int ncon = W->ncon;
+    for (int c = 0; c < ncon; c++) {
+      int p = R.con_pair[c];
+      int b1 = m->geom_bodyid[m->pair_geom1[p]], b2 = m->geom_bodyid[m->pair_geom2[p]];
+      if (b1 != body && b2 != body) continue;
+      int dim = m->pair_condim[p], nrow = dim == 1 ? 1 : 2 * (dim - 1), r0 = R.con_efc[c];
+      float fn = 0.f;
+      for (int r = 0; r < nrow; r++) fn += R.force[r0 + r];
+      if (fn <= 0.f) continue;
+      typename Rows<G>::F* cr = R.con + c * CONW;
+      float dir[3] = {cr[3], cr[4], cr[5]};
+      if (b2 == body) { dir[0] = -dir[0]; dir[1] = -dir[1]; dir[2] = -dir[2]; }
+      float dp[3] = {cr[0] - W->spos[site][0], cr[1] - W->spos[site][1], cr[2] - W->spos[site][2]};
+      float S[9];
+      for (int i = 0; i < 9; i++) S[i] = W->smat[site][i];
+      float lp[3], lv[3];
+      mtv3(lp, S, dp);
+      mtv3(lv, S, dir);
+      float sz[3] = {m->site_size[site][0], m->site_size[site][1], m->site_size[site][2]};
+      float best = -1.f;
+      for (int i = 0; i < 3; i++) {  // ray-box test in the site frame (mju_rayGeom, box)
+        if (fabsf(lv[i]) <= kMinVal) continue;
+        for (int side = -1; side <= 1; side += 2) {
+          float sol = ((float)side * sz[i] - lp[i]) / lv[i];
+          if (sol < 0.f) continue;
+          int i1 = (i + 1) % 3, i2 = (i + 2) % 3;
+          float a = lp[i1] + sol * lv[i1], b = lp[i2] + sol * lv[i2];
+          if (fabsf(a) <= sz[i1] && fabsf(b) <= sz[i2] && (best < 0.f || sol < best)) best = sol;
+        }
+      }
+      if (best >= 0.f) val += fn;
+    }
+    W->sens[m->sensor_adr[lane]] = val;
+  }
+  SYNC();
+}
+
+// full forward pass (mjx.forward)
+template <class D> NOINL void forward(MP m_, LDSA WS<D>* W, float* scratch_env, int gmax_efc, int gmax_con,
+                                      int force_global, int lane) {
+  MP m = uniform_ptr(m_);
+  constexpr int LD = D::LD;
+  STAMP(0, lane);
+  kinematics<D>(m, W, lane);
+  STAMP(1, lane);
+  com_pos_crb<D>(m, W, lane);
+  STAMP(2, lane);
+  velocity_stage<D>(m, W, lane);
+  STAMP(3, lane);
+  // factor M into H: qacc_smooth now, warm start / CG preconditioner later
+  for (int i = lane; i < D::NV * LD; i += 64) W->H[i] = W->M[i];
+  SYNC();
+  chol_factor<D>(W->H, W->invd, m->nv, lane);
+  float x = chol_solve<D>(W->H, W->invd, lane < m->nv ? W->frc_smooth[lane] : 0.f, lane);
+  if (lane < LD) W->qacc_smooth[lane] = (lane < m->nv) ? x : 0.f;
+  SYNC();
+  STAMP(4, lane);
+  bool ok = false;
+  if (!force_global) ok = build_rows<D, false>(m, W, lds_rows<D>(W), lane);
+  STAMP(5, lane);
+  if (ok) {
+    Rows<false> R = lds_rows<D>(W);
+    solver<D, false>(m, W, R, lane);
+    STAMP(6, lane);
+    sensors<D, false>(m, W, R, lane);
+    STAMP(7, lane);
+  } else {  // more rows than fit in LDS (or forced): this env's slab of global scratch
+    Rows<true> R = global_rows<D>(scratch_env, gmax_efc, gmax_con);
+    build_rows<D, true>(m, W, R, lane);
+    solver<D, true>(m, W, R, lane);
+    sensors<D, true>(m, W, R, lane);
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
+// integration (Euler with eulerdamp / implicitfast)   [forward.euler / forward.implicit]
+// ---------------------------------------------------------------------------------------------
+template <class D> NOINL void integrate(MP m_, LDSA WS<D>* W, int lane) {
+  MP m = uniform_ptr(m_);
+  constexpr int LD = D::LD;
+  const int nv = m->nv;
+  const float dt = m->timestep;
+  float qa = (lane < nv) ? W->qacc[lane] : 0.f;
+  bool damp = (m->integrator == MJL_INT_IMPLICITFAST || m->eulerdamp) && m->any_damping;
+  if (damp) {  // (M + dt*diag(damping)) qacc' = qfrc_smooth + qfrc_constraint
+    for (int i = lane; i < D::NV * LD; i += 64) W->H[i] = W->M[i];
+    SYNC();
+    if (lane < nv) W->H[lane * LD + lane] += dt * m->dof_damping[lane];
+    SYNC();
+    chol_factor<D>(W->H, W->invd, nv, lane);
+    float rhs = (lane < nv) ? W->frc_smooth[lane] + W->frc_con[lane] : 0.f;
+    qa = chol_solve<D>(W->H, W->invd, rhs, lane);
+  }
+  if (lane < nv) {
+    W->qacc_ws[lane] = W->qacc[lane];
+    W->qvel[lane] += dt * qa;
+  }
+  SYNC();
+  if (lane < m->njnt) {
+    int j = lane, q = m->jnt_qposadr[j], d = m->jnt_dofadr[j];
+    if (m->jnt_type[j] == MJL_JNT_FREE) {
+      W->qpos[q] += dt * W->qvel[d];
+      W->qpos[q + 1] += dt * W->qvel[d + 1];
+      W->qpos[q + 2] += dt * W->qvel[d + 2];
+      float w[3] = {W->qvel[d + 3], W->qvel[d + 4], W->qvel[d + 5]};
+      float nrm = norm3(w);
+      float s, c;
+      sincosf(0.5f * nrm * dt, &s, &c);
+      float qr[4] = {c, w[0] * s, w[1] * s, w[2] * s};
+      float qq[4] = {W->qpos[q + 3], W->qpos[q + 4], W->qpos[q + 5], W->qpos[q + 6]};
+      qmul(qq, qq, qr);
+      qnorm(qq);
+      W->qpos[q + 3] = qq[0]; W->qpos[q + 4] = qq[1]; W->qpos[q + 5] = qq[2]; W->qpos[q + 6] = qq[3];
+    } else {
+      W->qpos[q] += dt * W->qvel[d];
+    }
+  }
+  if (lane == 0) W->sc[SC_TIME] += dt;
+  SYNC();
+}
+
+// ---------------------------------------------------------------------------------------------
+// env wrapper (reference src/envs.py)
+// ---------------------------------------------------------------------------------------------
+template <class Q> INL void rpy(Q q, float& roll, float& pitch, float& yaw) {  // envs.py:357-365
+  float w = q[0], x = q[1], y = q[2], z = q[3];
+  roll = atan2f(2.f * (w * x + y * z), 1.f - 2.f * (x * x + y * y));
+  pitch = asinf(fminf(fmaxf(2.f * (w * y - z * x), -1.f), 1.f));
+  yaw = atan2f(2.f * (w * z + x * y), 1.f - 2.f * (y * y + z * z));
+}
+template <class P> INL float xydist(float tx, float ty, P p) {
+  float dx = tx - p[0], dy = ty - p[1];
+  return sqrtf(dx * dx + dy * dy);
+}
+typedef const CSTA mjlEnvConfig* CP;
+template <class S> INL float stance_of(CP c, S sens) {  // envs.py:89-106
+  bool r = sens[c->touch_sensor_right_id] > 0.f, l = sens[c->touch_sensor_left_id] > 0.f;
+  return (r && l) ? 0.f : ((r && !l) ? 1.f : ((!r && l) ? 2.f : 3.f));
+}
+
+// obs entry i of compute_obs (envs.py:317-331): raw obs at index perm[i] (flipped) or i
+template <class D> INL float raw_obs(MP m, LDSA WS<D>* W, CP c, int idx) {
+  int nj = m->nq - 7;
+  if (idx < 4) return W->sc[SC_HEIGHT + idx];  // height, roll, pitch, yaw
+  idx -= 4;
+  if (idx < nj) return W->qpos[7 + idx];
+  idx -= nj;
+  if (idx < 6) {  // pelvis-rotation^T applied to the root free-joint linear / angular qvel (envs.py:274-315)
+    float R[9];
+    q2m(R, W->xquat[c->pelvis_body_id]);
+    int h = idx / 3, k = idx % 3;
+    return R[k] * W->qvel[3 * h] + R[3 + k] * W->qvel[3 * h + 1] + R[6 + k] * W->qvel[3 * h + 2];
+  }
+  idx -= 6;
+  if (idx < m->nv - 6) return W->qvel[6 + idx];
+  idx -= m->nv - 6;
+  return W->sc[SC_TF0 + idx];
+}
+template <class D> INL void write_obs(MP m, LDSA WS<D>* W, CP c, float* obs, int lane) {
+  if (lane < c->obs_dim) {
+    bool flip = W->sc[SC_FLIP] > 0.5f;
+    obs[lane] = flip ? raw_obs<D>(m, W, c, c->obs_perm[lane]) * c->obs_sign[lane] : raw_obs<D>(m, W, c, lane);
+  }
+}
+
+// threefry2x32-20 (Random123; the generator behind jax.random)
+INL uint32_t rotl32(uint32_t x, int r) { return (x << r) | (x >> (32 - r)); }
+INL void threefry2x32(uint32_t k0, uint32_t k1, uint32_t& x0, uint32_t& x1) {
+  const uint32_t k2 = k0 ^ k1 ^ 0x1BD11BDAu;
+  const uint32_t ks[3] = {k0, k1, k2};
+  const int rot[8] = {13, 15, 26, 6, 17, 29, 16, 24};
+  x0 += k0; x1 += k1;
+#pragma unroll
+  for (int i = 0; i < 5; i++) {
+#pragma unroll
+    for (int j = 0; j < 4; j++) { x0 += x1; x1 = rotl32(x1, rot[(i & 1) * 4 + j]); x1 ^= x0; }
+    x0 += ks[(i + 1) % 3];
+    x1 += ks[(i + 2) % 3] + (uint32_t)(i + 1);
+  }
+}
+// uniform [0,1) for draw i of env e: key = threefry(seed, counter), bits = threefry(key, (e, i))
+INL float uniform01(uint32_t s0, uint32_t s1, uint32_t c0, uint32_t c1, int env, int i) {
+  uint32_t k0 = c0, k1 = c1;
+  threefry2x32(s0, s1, k0, k1);
+  uint32_t x0 = (uint32_t)env, x1 = (uint32_t)i;
+  threefry2x32(k0, k1, x0, x1);
+  return __uint_as_float((x0 >> 9) | 0x3f800000u) - 1.f;  // jax.random.uniform bit mapping
+}
+
+struct EnvArgs {  // per-launch env arguments
+  const mjlEnvConfig* cfg;
+  const float* noise;
+  float* scratch_env;
+  int gmax_efc, gmax_con, force_global;
+  uint32_t s0, s1, c0, c1;
+};
+
+// single_reset (envs.py:115-202): random pose / velocity, forward, target, aux, obs
+template <class D> NOINL void env_reset(MP m_, LDSA WS<D>* W, const EnvArgs* Ap, int env, int lane,
+                                        LDSA float* aux_out, float* obs_out) {
+  MP m = uniform_ptr(m_);
+  EnvArgs A = *Ap;
+  CP c = (CP)A.cfg;
+  const int nj = m->nq - 7, nv = m->nv, nd = nj + nv + 2;
+  float u = 0.f;
+  if (lane < nd) u = A.noise ? A.noise[(size_t)env * nd + lane] : uniform01(A.s0, A.s1, A.c0, A.c1, env, lane);
+  if (lane < m->nq) W->qpos[lane] = m->qpos0[lane];
+  if (lane < 32) W->ctrl[lane] = 0.f;
+  if (lane < D::LD) { W->qacc_ws[lane] = 0.f; W->qvel[lane] = 0.f; }
+  SYNC();
+  if (lane < nj) W->qpos[7 + lane] += c->random_joint_noise * (u * 2.f - 1.f);
+  if (lane >= nj && lane < nj + nv) W->qvel[lane - nj] = c->random_vel_noise * (u * 2.f - 1.f);
+  float uflip = rdlane(u, nj + nv), uspeed = rdlane(u, nj + nv + 1);
+  if (lane == 0) {
+    W->sc[SC_FLIP] = c->random_flip ? (uflip < 0.5f ? 1.f : 0.f) : 0.f;
+    W->sc[SC_TIME] = 0.f;
+  }
+  SYNC();
+  if (c->initial_velocity_max > 0.f) {
+    kinematics<D>(m, W, lane);  // the first forward's pelvis position (positions depend on qpos only)
+    LDSA float* bp = W->xpos[c->pelvis_body_id];
+    float tx = bp[0] + c->target_dist, ty = bp[1];
+    float dx = tx - bp[0], dy = ty - bp[1];
+    float dxy = sqrtf(dx * dx + dy * dy);
+    float vmag = uspeed * c->initial_velocity_max;
+    float vx = dxy > 1e-6f ? vmag * dx / dxy : 0.f;
+    float vy = dxy > 1e-6f ? vmag * dy / dxy : 0.f;
+    SYNC();
+    if (lane == 0) { W->qvel[0] = vx; W->qvel[1] = vy; }
+    SYNC();
+  }
+  forward<D>(m, W, A.scratch_env, A.gmax_efc, A.gmax_con, A.force_global, lane);
+  if (lane == 0) {
+    LDSA float* bp = W->xpos[c->pelvis_body_id];
+    float tx = bp[0] + c->target_dist, ty = bp[1], tz = bp[2];
+    float dxp = tx - bp[0], dyp = ty - bp[1];
+    float dist = fmaxf(xydist(tx, ty, bp), xydist(tx, ty, W->xpos[c->head_body_id]));
+    float roll, pitch, yaw;
+    rpy(W->xquat[c->pelvis_body_id], roll, pitch, yaw);
+    float angle = atan2f(dyp, dxp) - yaw;
+    float soft = dist / (1.f + fabsf(dist));
+    float sa, ca;
+    sincosf(angle, &sa, &ca);
+    W->sc[SC_HEIGHT] = bp[2]; W->sc[SC_ROLL] = roll; W->sc[SC_PITCH] = pitch; W->sc[SC_YAW] = yaw;
+    W->sc[SC_TF0] = soft * sa; W->sc[SC_TF1] = soft * ca;
+    float a[MJL_AUX_DIM] = {W->sc[SC_FLIP], tx, ty, tz, 0.f, stance_of(c, W->sens), 0.f, -dist / m->timestep, 0.f};
+    for (int i = 0; i < MJL_AUX_DIM; i++) aux_out[i] = a[i];
+  }
+  SYNC();
+  if (obs_out) write_obs<D>(m, W, c, obs_out, lane);
+}
+
+// post-step part of single_step (envs.py:347-492): reward, termination, aux, obs
+template <class D> NOINL void env_post(MP m_, LDSA WS<D>* W, const mjlEnvConfig* cfg, LDSA float* aux, float* obs,
+                                       int lane) {
+  MP m = uniform_ptr(m_);
+  CP c = (CP)cfg;
+  float pw = 0.f, st = 0.f;  // energy terms over the actuated hinge dofs (mean over nv - 6)
+  if (lane >= 6 && lane < m->nv) {
+    float fa = W->frc_act[lane];
+    pw = fabsf(fa * W->qvel[lane]);
+    st = fa * fa;
+  }
+  pw = wsum(pw);
+  st = wsum(st);
+  if (lane == 0) {
+    const float dt = m->timestep;
+    LDSA float* hp = W->xpos[c->head_body_id];
+    LDSA float* bp = W->xpos[c->pelvis_body_id];
+    float height = bp[2];
+    float roll, pitch, yaw;
+    rpy(W->xquat[c->pelvis_body_id], roll, pitch, yaw);
+    float tx = aux[1], ty = aux[2], tz = aux[3];
+    float dist = fmaxf(xydist(tx, ty, bp), xydist(tx, ty, hp));
+    float progress = (-dist / dt - aux[7]) * c->progress_weight;
+    float nj = (float)(m->nv - 6);
+    float energy = c->electricity_cost * (pw / nj) + c->stall_torque_cost * (st / nj);
+    float posture = ((pitch > -0.087f) && (pitch < 0.174f)) ? 0.f : fabsf(pitch);
+    posture += ((roll > -0.174f) && (roll < 0.174f)) ? 0.f : fabsf(roll);
+    posture *= c->posture_penalty_weight;
+    float tall = c->tall_bonus_weight * (height > c->tall_height_threshold ? 1.f : -1.f);
+    float time = W->sc[SC_TIME];
+    float old_st = aux[5], st_time = aux[6];
+    float new_st = stance_of(c, W->sens);
+    bool changed = new_st != old_st;
+    float dur = time - st_time;
+    float stance_rew = (changed && dur > 0.1f) ? c->stance_time_reward_weight * dur / dt : 0.f;
+    float st_upd = changed ? new_st : old_st;
+    float st_time_upd = changed ? time : st_time;
+    bool close = dist < c->target_threshold;
+    float close_count = close ? aux[4] + 1.f : 0.f;
+    float bonus = close ? 2.f : 0.f;
+    if (close_count >= (float)c->stop_frames) { tx = bp[0] + c->target_dist; ty = bp[1]; tz = bp[2]; close_count = 0.f; }
+    float dxp = tx - bp[0], dyp = ty - bp[1];
+    float dist2 = fmaxf(xydist(tx, ty, bp), xydist(tx, ty, hp));
+    float angle = atan2f(dyp, dxp) - yaw;
+    float soft = dist2 / (1.f + fabsf(dist2));
+    float sa, ca;
+    sincosf(angle, &sa, &ca);
+    float reward = progress + bonus + stance_rew - energy + tall - posture;
+    float ep = aux[8] + 1.f;
+    bool fallen = height < c->terminate_height;
+    float term = fallen ? 1.f : 0.f;
+    float trunc = (c->max_episode_steps > 0 && ep >= (float)c->max_episode_steps) ? 1.f : 0.f;
+    if (fallen) reward += c->terminate_reward;
+    W->sc[SC_REW] = reward; W->sc[SC_TERM] = term; W->sc[SC_TRUNC] = trunc; W->sc[SC_DONE] = fmaxf(term, trunc);
+    W->sc[SC_HEIGHT] = height; W->sc[SC_ROLL] = roll; W->sc[SC_PITCH] = pitch; W->sc[SC_YAW] = yaw;
+    W->sc[SC_TF0] = soft * sa; W->sc[SC_TF1] = soft * ca;
+    float a[MJL_AUX_DIM] = {aux[0], tx, ty, tz, close_count, st_upd, st_time_upd, -dist2 / dt, ep};
+    for (int i = 0; i < MJL_AUX_DIM; i++) aux[i] = a[i];
+  }
+  SYNC();
+  write_obs<D>(m, W, c, obs, lane);
+}
+
+// ---------------------------------------------------------------------------------------------
+// the kernel: one workgroup (= one wavefront) per env
+// ---------------------------------------------------------------------------------------------
+template <class D, int MODE> __global__ __launch_bounds__(64, MJL_MINWAVES) void step_kernel(KParams P) {
+  __shared__ WS<D> Ws;
+  __shared__ float aux_s[MJL_AUX_DIM + 3];
+  LDSA WS<D>* W = (LDSA WS<D>*)&Ws;
+  LDSA float* aux = (LDSA float*)aux_s;
+  constexpr int LD = D::LD;
+  MP m = (MP)P.m;
+  const int env = blockIdx.x;
+  const int lane = threadIdx.x;
+  if (env >= P.nenv) return;
+  if ((MODE == MODE_FORWARD || MODE == MODE_ENV_RESET) && P.mask && !(P.mask[env] > 0.5f)) return;
+  const int nq = m->nq, nv = m->nv, nu = m->nu;
+  const StateBuf& S = P.s;
+  EnvArgs A;
+  A.cfg = P.env; A.noise = P.noise; A.scratch_env = P.scratch + (size_t)env * (size_t)P.scratch_stride;
+  A.gmax_efc = P.gmax_efc; A.gmax_con = P.gmax_con; A.force_global = P.force_global_rows;
+  A.s0 = P.seed_lo; A.s1 = P.seed_hi; A.c0 = P.ctr_lo; A.c1 = P.ctr_hi;
+
+  // vectors beyond nv must read as zero in the LD-wide row kernels
+  for (int i = lane; i < LD; i += 64) {
+    W->qvel[i] = 0.f; W->qacc_ws[i] = 0.f;
+    W->frc_bias[i] = W->frc_passive[i] = W->frc_act[i] = W->frc_smooth[i] = W->qacc_smooth[i] = 0.f;
+    W->qacc[i] = W->frc_con[i] = W->grad[i] = W->Mgrad[i] = W->search[i] = W->Ma[i] = W->Mv[i] = 0.f;
+    W->gradold[i] = W->Mgradold[i] = 0.f;
+  }
+  SYNC();
+
+  if (MODE == MODE_ENV_RESET) {
+    env_reset<D>(m, W, &A, env, lane, aux, P.obs ? P.obs + (size_t)env * P.env->obs_dim : nullptr);
+  } else {
+    if (MODE == MODE_SPEEDTEST) {  // fresh make_data, qvel[0] = vel (mjx_humanoid_speed_test.py:50-55)
+      if (lane < nq) W->qpos[lane] = m->qpos0[lane];
+      if (lane < nv) W->qvel[lane] = (lane == 0) ? P.vel[env] : 0.f;
+      if (lane < nu) W->ctrl[lane] = 0.f;
+      if (lane == 0) W->sc[SC_TIME] = 0.f;
+    } else {
+      if (lane < nq) W->qpos[lane] = S.qpos[(size_t)env * nq + lane];
+      if (lane < nv) { W->qvel[lane] = S.qvel[(size_t)env * nv + lane]; W->qacc_ws[lane] = S.qacc_warmstart[(size_t)env * nv + lane]; }
+      if (lane < nu) W->ctrl[lane] = (MODE == MODE_STEP && P.in_ctrl) ? P.in_ctrl[(size_t)env * nu + lane]
+                                                                       : S.ctrl[(size_t)env * nu + lane];
+      if (lane == 0) W->sc[SC_TIME] = S.time[env];
+      if (MODE == MODE_ENV_STEP && lane < MJL_AUX_DIM) aux[lane] = S.aux[(size_t)env * MJL_AUX_DIM + lane];
+    }
+    SYNC();
+    if (MODE == MODE_ENV_STEP) {  // flip + clip the action (envs.py:335-344)
+      const mjlEnvConfig* c = P.env;
+      bool flip = aux[0] > 0.5f;
+      if (lane < nu) {
+        float a = flip ? P.in_ctrl[(size_t)env * nu + c->act_perm[lane]] * c->act_sign[lane]
+                       : P.in_ctrl[(size_t)env * nu + lane];
+        W->ctrl[lane] = fminf(fmaxf(a, -1.f), 1.f);
+      }
+      if (lane == 0) W->sc[SC_FLIP] = aux[0];
+      SYNC();
+    }
+    forward<D>(m, W, A.scratch_env, A.gmax_efc, A.gmax_con, A.force_global, lane);
+    if (MODE != MODE_FORWARD) integrate<D>(m, W, lane);
+    STAMP(8, lane);
+    if (MODE == MODE_ENV_STEP) {
+      float* obs = P.obs + (size_t)env * P.env->obs_dim;
+      env_post<D>(m, W, P.env, aux, obs, lane);
+      if (lane == 0) { P.rew[env] = W->sc[SC_REW]; P.term[env] = W->sc[SC_TERM]; P.trunc[env] = W->sc[SC_TRUNC]; }
+      bool bad = (lane < nq && !isfinite(W->qpos[lane])) || (lane < nv && !isfinite(W->qvel[lane]));
+      bool anybad = __ballot(bad) != 0ull;
+      if (lane == 0) W->sc[SC_NAN] = anybad ? 1.f : 0.f;
+      SYNC();
+      if (P.auto_reset && W->sc[SC_DONE] > 0.5f)  // merge_if_done (train_ppo.py:154-161)
+        env_reset<D>(m, W, &A, env, lane, aux, obs);
+    }
+  }
+  SYNC();
+  // ---- write back
+  if (MODE == MODE_SPEEDTEST) {
+    if (lane == 0) P.out_speed[env] = W->qpos[0];
+    return;
+  }
+  if (MODE != MODE_FORWARD) {
+    if (lane < nq) S.qpos[(size_t)env * nq + lane] = W->qpos[lane];
+    if (lane < nv) {
+      S.qvel[(size_t)env * nv + lane] = W->qvel[lane];
+      S.qacc_warmstart[(size_t)env * nv + lane] = W->qacc_ws[lane];
+    }
+    if (lane < nu) S.ctrl[(size_t)env * nu + lane] = W->ctrl[lane];
+    if (lane == 0) S.time[env] = W->sc[SC_TIME];
+    if ((MODE == MODE_ENV_STEP || MODE == MODE_ENV_RESET) && lane < MJL_AUX_DIM)
+      S.aux[(size_t)env * MJL_AUX_DIM + lane] = aux[lane];
+  }
+  if (MODE == MODE_FORWARD || P.store_derived) {
+    if (lane < nv) {
+      size_t o = (size_t)env * nv + lane;
+      S.qacc[o] = W->qacc[lane]; S.qfrc_actuator[o] = W->frc_act[lane]; S.qfrc_bias[o] = W->frc_bias[lane];
+      S.qfrc_passive[o] = W->frc_passive[lane]; S.qfrc_constraint[o] = W->frc_con[lane];
+      S.qacc_smooth[o] = W->qacc_smooth[lane];
+    }
+    const int nb = m->nbody;
+    for (int i = lane; i < nb * 3; i += 64) S.xpos[(size_t)env * nb * 3 + i] = W->xpos[i / 3][i % 3];
+    for (int i = lane; i < nb * 4; i += 64) S.xquat[(size_t)env * nb * 4 + i] = W->xquat[i / 4][i % 4];
+    if (lane < m->nsensordata) S.sensordata[(size_t)env * m->nsensordata + lane] = W->sens[lane];
+    if (lane == 0) {
+      S.stats[(size_t)env * 4 + 0] = (float)W->ncon;
+      S.stats[(size_t)env * 4 + 1] = (float)W->nefc;
+      S.stats[(size_t)env * 4 + 2] = (float)W->niter;
+      S.stats[(size_t)env * 4 + 3] = (MODE == MODE_ENV_STEP) ? W->sc[SC_NAN] : 0.f;
+    }
+  }
+}
+
+}  // namespace mjl

@@ -13,7 +13,7 @@ import subprocess
 from . import abi
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libmjx355.so")
+LIB_PATH = os.environ.get("MJX355_LIB", os.path.join(_HERE, "libmjx355.so"))  # override: A/B builds
 CSRC = os.path.join(os.path.dirname(_HERE), "csrc")
 
 # every symbol include/mjx355.h declares

@@ -1,0 +1,43 @@
+"""Diagnostic: per-phase cycle shares from the MJL_TIMING build (s_memtime stamps, lane 0).
+Run with MJX355_LIB pointing at a library built with -DMJL_TIMING. Read the shares, not the
+absolute time (the stamps perturb what they measure)."""
+import ctypes as C
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "mujoco-mjx-lab_amd"))
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+import mjx_amd  # noqa: E402
+from mjx_amd import _lib, mjx  # noqa: E402
+
+names = ["kinematics", "com_pos+crb+M", "velocity(rne,passive,act)", "factor M + qacc_smooth", "collision+rows",
+         "solver", "sensors", "integrate"]
+L = _lib.lib()
+L.mjl_debug_set_stamps.argtypes = [C.c_void_p]
+m = mjx_amd.load_model("humanoid_mjx")
+sys_ = mjx.put_model(m)
+B = 2048
+buf = torch.zeros((B, 16), dtype=torch.int64, device="cuda")
+L.mjl_debug_set_stamps(C.c_void_p(buf.data_ptr()))
+for mode in ("speedtest", "trajectory"):
+    d = mjx.make_data(sys_, B)
+    if mode == "speedtest":
+        vel = torch.linspace(0, 1, B, device="cuda")
+        for _ in range(3):
+            mjx.speedtest_step(sys_, d, vel)
+    else:
+        g = torch.Generator(device="cuda").manual_seed(0)
+        for _ in range(30):
+            mjx.step(sys_, d, torch.rand((B, m.nu), generator=g, device="cuda") * 2 - 1)
+    torch.cuda.synchronize()
+    s = buf.cpu().numpy().astype(np.float64)
+    ok = s[:, 8] > 0
+    d8 = np.diff(s[ok][:, [0, 1, 2, 3, 4, 5, 6, 7, 8]], axis=1)
+    tot = d8.sum(1).mean()
+    print(f"{mode}: envs with LDS rows {ok.mean():.2f}; mean cycles/env-step {tot:.0f}")
+    for i, n in enumerate(names):
+        print(f"   {n:28s} {d8[:, i].mean():9.0f}  {100 * d8[:, i].mean() / tot:5.1f}%")
+    buf.zero_()
