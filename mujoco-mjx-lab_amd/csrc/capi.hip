@@ -224,6 +224,53 @@ int mjl_model_create(const mjlModelDesc* d, mjlModel** out) {
     if (d->sensor_type[s] != MJL_SENS_TOUCH) { delete M; return fail(MJL_ERR_UNSUPPORTED, "sensor type"); }
     f.sensor_type[s] = d->sensor_type[s]; f.sensor_objid[s] = d->sensor_objid[s]; f.sensor_adr[s] = d->sensor_adr[s];
   }
+  // packed per-lane records
+  for (int b = 0; b < d->nbody; b++) {
+    BodyRec& r = f.brec[b];
+    r.parent = d->body_parentid[b]; r.level = d->body_level[b];
+    r.jntadr = d->body_jntadr[b]; r.jntnum = d->body_jntnum[b];
+    r.dofadr = d->body_dofadr[b]; r.dofnum = d->body_dofnum[b];
+    r.subtree_end = d->body_subtree_end[b]; r.rootid = d->body_rootid[b];
+    r.isfree = d->body_jntnum[b] > 0 && d->jnt_type[d->body_jntadr[b]] == MJL_JNT_FREE;
+    r.qadr = r.isfree ? d->jnt_qposadr[d->body_jntadr[b]] : 0;
+    if (r.isfree && d->body_jntnum[b] != 1) {
+      delete M; return fail(MJL_ERR_UNSUPPORTED, "a body with a free joint must have no other joint");
+    }
+    for (int i = 0; i < 3; i++) { r.pos[i] = f.body_pos[b][i]; r.ipos[i] = f.body_ipos[b][i]; }
+    for (int i = 0; i < 4; i++) r.quat[i] = f.body_quat[b][i];
+    r.mass = f.body_mass[b];
+  }
+  for (int j = 0; j < d->njnt; j++) {
+    JntRec& r = f.jrec[j];
+    for (int i = 0; i < 3; i++) { r.pos[i] = f.jnt_pos[j][i]; r.axis[i] = f.jnt_axis[j][i]; }
+    r.qadr = d->jnt_qposadr[j];
+    r.qpos0 = f.qpos0[r.qadr];
+    r.body = d->jnt_bodyid[j]; r.parent = d->body_parentid[r.body];
+    r.isfree = d->jnt_type[j] == MJL_JNT_FREE; r.dofadr = d->jnt_dofadr[j];
+  }
+  for (int k = 0; k < d->nv; k++) {
+    DofRec& r = f.drec[k];
+    int j = d->dof_jntid[k];
+    r.bodyid = d->dof_bodyid[k]; r.jntid = j; r.rootid = d->body_rootid[r.bodyid];
+    r.kfree = d->jnt_type[j] == MJL_JNT_FREE ? k - d->jnt_dofadr[j] : -1;
+    uint32_t am = 0;
+    for (int a = k; a >= 0; a = d->dof_parentid[a]) am |= 1u << a;
+    r.ancmask = am;
+    r.qadr_spring = d->jnt_type[j] == MJL_JNT_HINGE ? d->jnt_qposadr[j] : -1;
+    r.damping = f.dof_damping[k]; r.armature = f.dof_armature[k];
+    r.stiffness = f.jnt_stiffness[j];
+    r.qpos_spring = r.qadr_spring >= 0 ? f.qpos_spring[r.qadr_spring] : 0.f;
+    r.invweight0 = f.dof_invweight0[k];
+  }
+  for (int p = 0; p < d->npair; p++) {
+    PairRec& r = f.prec[p];
+    r.g1 = f.pair_geom1[p]; r.g2 = f.pair_geom2[p]; r.kind = f.pair_kind[p]; r.condim = f.pair_condim[p];
+    r.r1 = f.geom_size[r.g1][0]; r.h1 = f.geom_size[r.g1][1];
+    r.r2 = f.geom_size[r.g2][0]; r.h2 = f.geom_size[r.g2][1];
+    r.includemargin = f.pair_includemargin[p]; r.mu = f.pair_mu[p]; r.invweight = f.pair_invweight[p];
+    r.b1 = d->geom_bodyid[r.g1]; r.b2 = d->geom_bodyid[r.g2];
+    r.mask1 = f.body_dofmask[r.b1]; r.mask2 = f.body_dofmask[r.b2];
+  }
   M->nefc_max = nefc_max;
   M->ncon_max = ncon_max;
   // compact kernel instantiation when the model fits the humanoid capacities, generic otherwise

@@ -8,6 +8,37 @@
 
 namespace mjl {
 
+// Packed per-lane records (16-byte rows -> one b128 load each): a phase loads the records of
+// its lane once, up front, instead of walking dependent index chains inside its level loops.
+struct alignas(16) BodyRec {
+  int parent, level, jntadr, jntnum;
+  int dofadr, dofnum, subtree_end, rootid;
+  int isfree, qadr, pad0, pad1;  // isfree: the body's only joint is free (qadr: its qpos address)
+  float pos[3], mass;
+  float quat[4];
+  float ipos[3], pad2;
+};
+struct alignas(16) JntRec {  // hinge joints (local frame of the body)
+  float pos[3], qpos0;
+  float axis[3];
+  int qadr;
+  int body, parent, isfree, dofadr;
+};
+struct alignas(16) DofRec {
+  int bodyid, jntid, rootid, kfree;  // kfree: index 0..5 inside a free joint, -1 otherwise
+  uint32_t ancmask;                  // bit j set <=> dof j is this dof or one of its ancestors
+  int qadr_spring;                   // qpos address of a hinge spring, -1 when none
+  float damping, armature;
+  float stiffness, qpos_spring, invweight0, pad;
+};
+struct alignas(16) PairRec {
+  int g1, g2, kind, condim;
+  float r1, h1, r2, h2;  // geom_size[:, 0:2] of both geoms
+  float includemargin, mu, invweight, pad;
+  uint32_t mask1, mask2;  // body_dofmask of both bodies
+  int b1, b2;
+};
+
 struct ModelF {
   int nq, nv, nu, nbody, njnt, ngeom, nsite, ntendon, npair, nsensor, nsensordata;
   int iterations, ls_iterations, solver, integrator, eulerdamp, maxlevel, nlimited, any_damping;
@@ -49,6 +80,11 @@ struct ModelF {
   float tendon_invweight0[MJL_MAXTENDON];
 
   int sensor_type[MJL_MAXSENSOR], sensor_objid[MJL_MAXSENSOR], sensor_adr[MJL_MAXSENSOR];
+
+  BodyRec brec[MJL_MAXBODY];
+  JntRec jrec[MJL_MAXJNT];
+  DofRec drec[MJL_MAXV];
+  PairRec prec[MJL_MAXPAIR];
 };
 
 enum Mode { MODE_FORWARD = 0, MODE_STEP = 1, MODE_SPEEDTEST = 2, MODE_ENV_STEP = 3, MODE_ENV_RESET = 4 };

@@ -47,29 +47,32 @@ __device__ unsigned long long* g_stamps;
 
 typedef const CSTA ModelF* MP;
 
+// LDS budget: 160 KB per CU / 8 waves (the VGPR limit at 2 waves per SIMD) = 20 KB per one-wave
+// workgroup, so 2048 envs are resident on 256 CUs at once. Rows beyond CAP (contacts beyond CAPC)
+// go to the env's global scratch slab.
 #ifndef MJL_CAP
-#define MJL_CAP 64
+#define MJL_CAP 48
 #endif
 #ifndef MJL_CAPC
-#define MJL_CAPC 32
+#define MJL_CAPC 16
 #endif
 #ifndef MJL_MINWAVES
-#define MJL_MINWAVES 1
+#define MJL_MINWAVES 2
 #endif
-constexpr int CAP = MJL_CAP;    // constraint rows kept in LDS; more go to the env's global scratch slab
-constexpr int CAPC = MJL_CAPC;  // contacts kept in LDS
-constexpr int CONW = 12;  // floats per contact record: pos[3], frame[9]
+constexpr int kLdsBudget = 20480;
+constexpr int CONW = 16;  // floats per contact record: pos[3], frame[9], then the pair's
+                          // dof masks of both bodies, mu, and b1 | b2 << 8 | condim << 16 (int bits)
 constexpr float kMinVal = 1e-15f;
 constexpr float kMinImp = 0.0001f;
 constexpr float kMaxImp = 0.9999f;
 
 // compile-time capacities of one kernel instantiation (model sizes must fit)
-template <int NV_, int NB_, int NJ_, int NG_> struct Dims {
-  static constexpr int NV = NV_, NB = NB_, NJ = NJ_, NG = NG_;
+template <int NV_, int NB_, int NJ_, int NG_, int CAP_, int CAPC_> struct Dims {
+  static constexpr int NV = NV_, NB = NB_, NJ = NJ_, NG = NG_, CAP = CAP_, CAPC = CAPC_;
   static constexpr int LD = (NV_ <= 28) ? 28 : 36;  // dense row stride, LD/4 odd -> conflict-free b128
 };
-using DHum = Dims<27, 17, 22, 20>;  // both reference humanoids (nv 27, 17 bodies, 22 joints, 20 geoms)
-using DGen = Dims<32, 32, 32, 32>;  // any model within the MJL_MAX* capacities
+using DHum = Dims<27, 17, 22, 20, MJL_CAP, MJL_CAPC>;  // both reference humanoids (nv 27, 17 bodies, 22 joints, 20 geoms)
+using DGen = Dims<32, 32, 32, 32, 32, 16>;               // any model within the MJL_MAX* capacities
 
 // ---------------------------------------------------------------------------------------------
 // wave primitives
@@ -98,6 +101,17 @@ INL float wsum(float v) {
 }
 INL unsigned long long lanes_below(int lane) { return (1ull << lane) - 1ull; }
 
+// a packed model record as whole b128 loads from the constant model block
+typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+template <class T> INL T ldrec(const CSTA T* p) {
+  static_assert(sizeof(T) % 16 == 0, "records are 16-byte rows");
+  union { u32x4 v[sizeof(T) / 16]; T t; } u;
+  const CSTA u32x4* s = (const CSTA u32x4*)p;
+#pragma unroll
+  for (int i = 0; i < (int)(sizeof(T) / 16); i++) u.v[i] = s[i];
+  return u.t;
+}
+
 // ---------------------------------------------------------------------------------------------
 // per-env LDS workspace
 // ---------------------------------------------------------------------------------------------
@@ -112,12 +126,11 @@ template <class DM> struct WS {
   float gpos[NG][3], gaxis[NG][3];
   float spos[MJL_MAXSITE][3], smat[MJL_MAXSITE][9];
   float scom[NB][3];
-  float cinert[NB][10], crb[NB][10];
-  float cdof[NV][6], cvel[NB][6], cacc[NB][6];
+  float cdof[NV][6];
   float tenJ[MJL_MAXTENDON][LD], tenlen[MJL_MAXTENDON];
   alignas(16) float M[NV * LD];
   alignas(16) float H[NV * LD];  // factor of M, Newton Hessian + factor, or implicit-integration factor
-  float invd[32];                // 1 / diag of the factor in H
+  float invd[LD];                // 1 / diag of the factor in H
   alignas(16) float frc_bias[LD];
   alignas(16) float frc_passive[LD];
   alignas(16) float frc_act[LD];
@@ -133,15 +146,23 @@ template <class DM> struct WS {
   alignas(16) float gradold[LD];
   alignas(16) float Mgradold[LD];
   float sens[MJL_MAXSENSOR];
-  float sc[32];
+  float sc[16];
   int ncon, nefc, nlim, niter;
-  // constraint rows that fit in LDS
-  alignas(16) float J[CAP * LD];
-  float D[CAP], aref[CAP], jar[CAP], force[CAP], Jv[CAP], epos[CAP], einvw[CAP];
-  int emeta[CAP];
-  float con[CAPC * CONW];
-  int con_pair[CAPC], con_efc[CAPC];
+  static constexpr int CAP = DM::CAP, CAPC = DM::CAPC;
+  union {
+    // smooth-dynamics scratch: dead once the constraint rows are built
+    struct { float cinert[NB][10], crb[NB][10], cvel[NB][6], cacc[NB][6]; };
+    // constraint rows that fit in LDS
+    struct {
+      alignas(16) float J[CAP * LD];
+      float D[CAP], aref[CAP], jar[CAP], force[CAP], Jv[CAP], epos[CAP], einvw[CAP];
+      int emeta[CAP];
+      float con[CAPC * CONW];
+      int con_pair[CAPC], con_efc[CAPC];
+    };
+  };
 };
+static_assert(sizeof(WS<DHum>) <= kLdsBudget, "humanoid workspace exceeds the 8-waves-per-CU LDS budget");
 
 // scalar slots in WS::sc
 enum { SC_FLIP = 0, SC_HEIGHT, SC_ROLL, SC_PITCH, SC_YAW, SC_TF0, SC_TF1, SC_REW, SC_TERM, SC_TRUNC, SC_DONE,
@@ -162,7 +183,7 @@ template <class D> INL Rows<false> lds_rows(LDSA WS<D>* W) {
   Rows<false> R;
   R.J = W->J; R.D = W->D; R.aref = W->aref; R.jar = W->jar; R.force = W->force; R.Jv = W->Jv;
   R.epos = W->epos; R.einvw = W->einvw; R.emeta = W->emeta; R.con = W->con; R.con_pair = W->con_pair;
-  R.con_efc = W->con_efc; R.cap = CAP; R.capc = CAPC;
+  R.con_efc = W->con_efc; R.cap = D::CAP; R.capc = D::CAPC;
   return R;
 }
 template <class D> INL Rows<true> global_rows(float* base_generic, int nefc_max, int ncon_max) {
@@ -304,11 +325,26 @@ template <class D> INL float chol_solve(const LDSA float* L, const LDSA float* i
 // ---------------------------------------------------------------------------------------------
 template <class D> NOINL void kinematics(MP m_, LDSA WS<D>* W, int lane) {
   MP m = uniform_ptr(m_);
+  const int maxlevel = m->maxlevel, nbody = m->nbody, ngeom = m->ngeom, nsite = m->nsite, njnt = m->njnt;
+  // model records of this lane, loaded once: body `lane`, geom `lane`, site `lane - 32`, joint `lane`
+  const bool isb = lane > 0 && lane < nbody;
+  BodyRec br = ldrec(&m->brec[isb ? lane : 0]);
+  const bool isg = lane < ngeom, iss = lane >= 32 && lane - 32 < nsite, isj = lane < njnt;
+  const int gb = isg ? m->geom_bodyid[lane] : 0, sb = iss ? m->site_bodyid[lane - 32] : 0;
+  float gp[3] = {0.f, 0.f, 0.f}, gz[3] = {0.f, 0.f, 0.f}, sp[3] = {0.f, 0.f, 0.f}, sm[9];
+  if (isg) for (int i = 0; i < 3; i++) { gp[i] = m->geom_pos[lane][i]; gz[i] = m->geom_zaxis[lane][i]; }
+  if (iss) {
+    for (int i = 0; i < 3; i++) sp[i] = m->site_pos[lane - 32][i];
+    for (int i = 0; i < 9; i++) sm[i] = m->site_mat[lane - 32][i];
+  }
+  const JntRec jown = ldrec(&m->jrec[isj ? lane : 0]);
+  const int jpar = jown.parent, jfree = isj ? jown.isfree : 1;
   if (lane == 0) {
     W->xpos[0][0] = W->xpos[0][1] = W->xpos[0][2] = 0.f;
     W->xquat[0][0] = 1.f; W->xquat[0][1] = W->xquat[0][2] = W->xquat[0][3] = 0.f;
     for (int i = 0; i < 9; i++) W->xmat[0][i] = (i % 4 == 0) ? 1.f : 0.f;
     W->xipos[0][0] = W->xipos[0][1] = W->xipos[0][2] = 0.f;
+    W->cacc[0][0] = W->cacc[0][1] = W->cacc[0][2] = W->cacc[0][3] = 0.f;
   }
   if (lane >= 32 && lane - 32 < m->ntendon) {  // fixed tendons  [smooth.tendon]
     int t = lane - 32;
@@ -320,80 +356,103 @@ template <class D> NOINL void kinematics(MP m_, LDSA WS<D>* W, int lane) {
     }
     W->tenlen[t] = len;
   }
-  SYNC();
-  const int maxlevel = m->maxlevel, nbody = m->nbody;
-  for (int L = 1; L <= maxlevel; L++) {
-    int b = lane;
-    if (b < nbody && m->body_level[b] == L) {
-      float pos[3], quat[4], mat[9];
-      int ja = m->body_jntadr[b], jn = m->body_jntnum[b];
-      if (jn > 0 && m->jnt_type[ja] == MJL_JNT_FREE) {
-        int qa = m->jnt_qposadr[ja];
-        pos[0] = W->qpos[qa]; pos[1] = W->qpos[qa + 1]; pos[2] = W->qpos[qa + 2];
-        quat[0] = W->qpos[qa + 3]; quat[1] = W->qpos[qa + 4]; quat[2] = W->qpos[qa + 5]; quat[3] = W->qpos[qa + 6];
-        qnorm(quat);
-        q2m(mat, quat);
-        W->xanchor[ja][0] = pos[0]; W->xanchor[ja][1] = pos[1]; W->xanchor[ja][2] = pos[2];
-        W->xaxis[ja][0] = mat[2]; W->xaxis[ja][1] = mat[5]; W->xaxis[ja][2] = mat[8];
-      } else {
-        int p = m->body_parentid[b];
-        mv3(pos, W->xmat[p], m->body_pos[b]);
-        pos[0] += W->xpos[p][0]; pos[1] += W->xpos[p][1]; pos[2] += W->xpos[p][2];
-        qmul(quat, W->xquat[p], m->body_quat[b]);
-        for (int j = ja; j < ja + jn; j++) {
-          q2m(mat, quat);
-          float anc[3], ax[3];
-          mv3(anc, mat, m->jnt_pos[j]);
-          anc[0] += pos[0]; anc[1] += pos[1]; anc[2] += pos[2];
-          mv3(ax, mat, m->jnt_axis[j]);
-          W->xanchor[j][0] = anc[0]; W->xanchor[j][1] = anc[1]; W->xanchor[j][2] = anc[2];
-          W->xaxis[j][0] = ax[0]; W->xaxis[j][1] = ax[1]; W->xaxis[j][2] = ax[2];
-          int qa = m->jnt_qposadr[j];
-          float s, c;
-          sincosf(0.5f * (W->qpos[qa] - m->qpos0[qa]), &s, &c);
-          float ql[4] = {c, m->jnt_axis[j][0] * s, m->jnt_axis[j][1] * s, m->jnt_axis[j][2] * s};
-          qmul(quat, quat, ql);
-          q2m(mat, quat);
-          float off[3];
-          mv3(off, mat, m->jnt_pos[j]);
-          pos[0] = anc[0] - off[0]; pos[1] = anc[1] - off[1]; pos[2] = anc[2] - off[2];
-        }
-        qnorm(quat);
-        q2m(mat, quat);
+  // body transform relative to its parent (lane = body, all bodies at once); hinge anchors and
+  // axes are left in the parent frame in xanchor / xaxis and moved to world after the tree pass
+  float lp[3], lq[4];
+  if (isb) {
+    if (br.isfree) {  // free joint: qpos is the world pose
+      const int qa = br.qadr;
+      lp[0] = W->qpos[qa]; lp[1] = W->qpos[qa + 1]; lp[2] = W->qpos[qa + 2];
+      lq[0] = W->qpos[qa + 3]; lq[1] = W->qpos[qa + 4]; lq[2] = W->qpos[qa + 5]; lq[3] = W->qpos[qa + 6];
+      qnorm(lq);
+    } else {
+      lp[0] = br.pos[0]; lp[1] = br.pos[1]; lp[2] = br.pos[2];
+      lq[0] = br.quat[0]; lq[1] = br.quat[1]; lq[2] = br.quat[2]; lq[3] = br.quat[3];
+      for (int j = br.jntadr; j < br.jntadr + br.jntnum; j++) {
+        const JntRec jr = ldrec(&m->jrec[j]);
+        float mat[9], anc[3], ax[3];
+        q2m(mat, lq);
+        mv3(anc, mat, jr.pos);
+        anc[0] += lp[0]; anc[1] += lp[1]; anc[2] += lp[2];
+        mv3(ax, mat, jr.axis);
+        W->xanchor[j][0] = anc[0]; W->xanchor[j][1] = anc[1]; W->xanchor[j][2] = anc[2];
+        W->xaxis[j][0] = ax[0]; W->xaxis[j][1] = ax[1]; W->xaxis[j][2] = ax[2];
+        float s, c;
+        sincosf(0.5f * (W->qpos[jr.qadr] - jr.qpos0), &s, &c);
+        const float ql[4] = {c, jr.axis[0] * s, jr.axis[1] * s, jr.axis[2] * s};
+        qmul(lq, lq, ql);
+        float off[3];
+        q2m(mat, lq);
+        mv3(off, mat, jr.pos);
+        lp[0] = anc[0] - off[0]; lp[1] = anc[1] - off[1]; lp[2] = anc[2] - off[2];
       }
+    }
+  }
+  SYNC();
+  // tree pass: compose with the parent's world frame, one level at a time  [smooth.kinematics]
+  for (int L = 1; L <= maxlevel; L++) {
+    if (isb && br.level == L) {
+      float pos[3], quat[4], mat[9];
+      if (br.isfree) {
+        pos[0] = lp[0]; pos[1] = lp[1]; pos[2] = lp[2];
+        quat[0] = lq[0]; quat[1] = lq[1]; quat[2] = lq[2]; quat[3] = lq[3];
+      } else {
+        const int p = br.parent;
+        mv3(pos, W->xmat[p], lp);
+        pos[0] += W->xpos[p][0]; pos[1] += W->xpos[p][1]; pos[2] += W->xpos[p][2];
+        qmul(quat, W->xquat[p], lq);
+        qnorm(quat);
+      }
+      q2m(mat, quat);
+      const int b = lane;
       for (int i = 0; i < 3; i++) W->xpos[b][i] = pos[i];
       for (int i = 0; i < 4; i++) W->xquat[b][i] = quat[i];
       for (int i = 0; i < 9; i++) W->xmat[b][i] = mat[i];
       float ip[3];
-      mv3(ip, mat, m->body_ipos[b]);
+      mv3(ip, mat, br.ipos);
       W->xipos[b][0] = pos[0] + ip[0]; W->xipos[b][1] = pos[1] + ip[1]; W->xipos[b][2] = pos[2] + ip[2];
+      // body mass moment for the subtree com (cacc is free until the velocity stage)
+      W->cacc[b][0] = br.mass * W->xipos[b][0]; W->cacc[b][1] = br.mass * W->xipos[b][1];
+      W->cacc[b][2] = br.mass * W->xipos[b][2]; W->cacc[b][3] = br.mass;
     }
     SYNC();
   }
-  if (lane < m->ngeom) {  // geom frames (lanes 0..31): centre + z axis is all collision needs
-    int g = lane, b = m->geom_bodyid[g];
-    float p[3], z[3];
-    mv3(p, W->xmat[b], m->geom_pos[g]);
-    mv3(z, W->xmat[b], m->geom_zaxis[g]);
-    W->gpos[g][0] = W->xpos[b][0] + p[0]; W->gpos[g][1] = W->xpos[b][1] + p[1]; W->gpos[g][2] = W->xpos[b][2] + p[2];
-    W->gaxis[g][0] = z[0]; W->gaxis[g][1] = z[1]; W->gaxis[g][2] = z[2];
+  if (isj) {  // joint anchors / axes to world (lane = joint)
+    float anc[3], ax[3];
+    if (jfree) {  // free joint: anchor = body position, axis = body z
+      const int b = jown.body;
+      for (int i = 0; i < 3; i++) { anc[i] = W->xpos[b][i]; ax[i] = W->xmat[b][3 * i + 2]; }
+    } else {
+      const float la[3] = {W->xanchor[lane][0], W->xanchor[lane][1], W->xanchor[lane][2]};
+      const float lx[3] = {W->xaxis[lane][0], W->xaxis[lane][1], W->xaxis[lane][2]};
+      mv3(anc, W->xmat[jpar], la);
+      anc[0] += W->xpos[jpar][0]; anc[1] += W->xpos[jpar][1]; anc[2] += W->xpos[jpar][2];
+      mv3(ax, W->xmat[jpar], lx);
+    }
+    for (int i = 0; i < 3; i++) { W->xanchor[lane][i] = anc[i]; W->xaxis[lane][i] = ax[i]; }
   }
-  if (lane >= 32 && lane - 32 < m->nsite) {  // site frames (lanes 32..)
-    int s = lane - 32, b = m->site_bodyid[s];
+  if (isg) {  // geom frames (lanes 0..31): centre + z axis is all collision needs
+    float p[3], z[3];
+    mv3(p, W->xmat[gb], gp);
+    mv3(z, W->xmat[gb], gz);
+    W->gpos[lane][0] = W->xpos[gb][0] + p[0]; W->gpos[lane][1] = W->xpos[gb][1] + p[1];
+    W->gpos[lane][2] = W->xpos[gb][2] + p[2];
+    W->gaxis[lane][0] = z[0]; W->gaxis[lane][1] = z[1]; W->gaxis[lane][2] = z[2];
+  }
+  if (iss) {  // site frames (lanes 32..)
+    const int s = lane - 32;
     float p[3];
-    mv3(p, W->xmat[b], m->site_pos[s]);
-    W->spos[s][0] = W->xpos[b][0] + p[0]; W->spos[s][1] = W->xpos[b][1] + p[1]; W->spos[s][2] = W->xpos[b][2] + p[2];
+    mv3(p, W->xmat[sb], sp);
+    W->spos[s][0] = W->xpos[sb][0] + p[0]; W->spos[s][1] = W->xpos[sb][1] + p[1]; W->spos[s][2] = W->xpos[sb][2] + p[2];
     for (int i = 0; i < 3; i++)
       for (int j = 0; j < 3; j++)
-        W->smat[s][3 * i + j] = W->xmat[b][3 * i] * m->site_mat[s][j] + W->xmat[b][3 * i + 1] * m->site_mat[s][3 + j] +
-                                W->xmat[b][3 * i + 2] * m->site_mat[s][6 + j];
+        W->smat[s][3 * i + j] = W->xmat[sb][3 * i] * sm[j] + W->xmat[sb][3 * i + 1] * sm[3 + j] + W->xmat[sb][3 * i + 2] * sm[6 + j];
   }
   if (lane < nbody) {  // subtree com over the DFS-contiguous subtree [b, subtree_end)
-    int b = lane;
+    const int b = lane;
     float ms = 0.f, a0 = 0.f, a1 = 0.f, a2 = 0.f;
-    for (int c = b; c < m->body_subtree_end[b]; c++) {
-      float mc = m->body_mass[c];
-      ms += mc; a0 += mc * W->xipos[c][0]; a1 += mc * W->xipos[c][1]; a2 += mc * W->xipos[c][2];
+    for (int c = b; c < br.subtree_end; c++) {
+      a0 += W->cacc[c][0]; a1 += W->cacc[c][1]; a2 += W->cacc[c][2]; ms += W->cacc[c][3];
     }
     if (ms < kMinVal) { W->scom[b][0] = W->xipos[b][0]; W->scom[b][1] = W->xipos[b][1]; W->scom[b][2] = W->xipos[b][2]; }
     else { float inv = 1.f / ms; W->scom[b][0] = a0 * inv; W->scom[b][1] = a1 * inv; W->scom[b][2] = a2 * inv; }
@@ -405,14 +464,19 @@ template <class D> NOINL void kinematics(MP m_, LDSA WS<D>* W, int lane) {
 template <class D> NOINL void com_pos_crb(MP m_, LDSA WS<D>* W, int lane) {
   MP m = uniform_ptr(m_);
   constexpr int LD = D::LD;
-  if (lane < m->nbody) {
-    int b = lane;
+  const int nbody = m->nbody, nv = m->nv;
+  const bool isb = lane < nbody, iscd = lane >= 32 && lane - 32 < nv, iscol = lane < nv;
+  const BodyRec br = ldrec(&m->brec[isb ? lane : 0]);
+  const DofRec dcd = ldrec(&m->drec[iscd ? lane - 32 : 0]), dcol = ldrec(&m->drec[iscol ? lane : 0]);
+  float t[6];
+  for (int i = 0; i < 6; i++) t[i] = isb ? m->body_inertia[lane][i] : 0.f;
+  if (isb) {
+    const int b = lane;
     LDSA float* ci = W->cinert[b];
-    float mass = m->body_mass[b];
+    const float mass = br.mass;
     if (b == 0 || mass == 0.f) {
       for (int i = 0; i < 10; i++) ci[i] = 0.f;
     } else {
-      const CSTA float* t = m->body_inertia[b];
       float X[9];
       for (int i = 0; i < 9; i++) X[i] = W->xmat[b][i];
       float Ib[9] = {t[0], t[3], t[4], t[3], t[1], t[5], t[4], t[5], t[2]};
@@ -421,7 +485,7 @@ template <class D> NOINL void com_pos_crb(MP m_, LDSA WS<D>* W, int lane) {
         for (int j = 0; j < 3; j++) T[3 * i + j] = X[3 * i] * Ib[j] + X[3 * i + 1] * Ib[3 + j] + X[3 * i + 2] * Ib[6 + j];
       for (int i = 0; i < 3; i++)
         for (int j = 0; j < 3; j++) Iw[3 * i + j] = T[3 * i] * X[3 * j] + T[3 * i + 1] * X[3 * j + 1] + T[3 * i + 2] * X[3 * j + 2];
-      int root = m->body_rootid[b];
+      const int root = br.rootid;
       float c[3] = {W->xipos[b][0] - W->scom[root][0], W->xipos[b][1] - W->scom[root][1], W->xipos[b][2] - W->scom[root][2]};
       float cc = dot3(c, c);
       ci[0] = Iw[0] + mass * (cc - c[0] * c[0]);
@@ -433,19 +497,17 @@ template <class D> NOINL void com_pos_crb(MP m_, LDSA WS<D>* W, int lane) {
       ci[6] = mass * c[0]; ci[7] = mass * c[1]; ci[8] = mass * c[2]; ci[9] = mass;
     }
   }
-  if (lane >= 32 && lane - 32 < m->nv) {
-    int d = lane - 32, j = m->dof_jntid[d], b = m->dof_bodyid[d];
+  if (iscd) {
+    const int d = lane - 32, j = dcd.jntid, b = dcd.bodyid, root = dcd.rootid, k = dcd.kfree;
     LDSA float* cd = W->cdof[d];
-    int root = m->body_rootid[b];
     float off[3] = {W->scom[root][0] - W->xanchor[j][0], W->scom[root][1] - W->xanchor[j][1],
                     W->scom[root][2] - W->xanchor[j][2]};
-    int k = d - m->jnt_dofadr[j];
-    if (m->jnt_type[j] == MJL_JNT_FREE && k < 3) {
+    if (k >= 0 && k < 3) {
       for (int i = 0; i < 6; i++) cd[i] = 0.f;
       cd[3 + k] = 1.f;
     } else {
       float ax[3];
-      if (m->jnt_type[j] == MJL_JNT_FREE) {
+      if (k >= 3) {
         ax[0] = W->xmat[b][k - 3]; ax[1] = W->xmat[b][3 + k - 3]; ax[2] = W->xmat[b][6 + k - 3];
       } else {
         ax[0] = W->xaxis[j][0]; ax[1] = W->xaxis[j][1]; ax[2] = W->xaxis[j][2];
@@ -456,26 +518,29 @@ template <class D> NOINL void com_pos_crb(MP m_, LDSA WS<D>* W, int lane) {
     }
   }
   SYNC();
-  if (lane < m->nbody) {
-    int b = lane;
+  if (isb) {
+    const int b = lane;
     float s[10];
     for (int i = 0; i < 10; i++) s[i] = 0.f;
-    for (int c = b; c < m->body_subtree_end[b]; c++)
+    for (int c = b; c < br.subtree_end; c++)
       for (int i = 0; i < 10; i++) s[i] += W->cinert[c][i];
     for (int i = 0; i < 10; i++) W->crb[b][i] = s[i];
   }
   for (int i = lane; i < D::NV * LD; i += 64) W->M[i] = 0.f;
   SYNC();
-  if (lane < m->nv) {  // column `lane` of M along the ancestor chain  [smooth.crb / make_m]
-    int i = lane;
+  if (iscol) {  // column `lane` of M along the ancestor chain  [smooth.crb / make_m]
+    const int i = lane;
     float f[6], c6[6], cr[10];
     for (int k = 0; k < 6; k++) c6[k] = W->cdof[i][k];
-    for (int k = 0; k < 10; k++) cr[k] = W->crb[m->dof_bodyid[i]][k];
+    for (int k = 0; k < 10; k++) cr[k] = W->crb[dcol.bodyid][k];
     inert_vec(f, cr, c6);
-    for (int j = i; j >= 0; j = m->dof_parentid[j]) {
+    uint32_t anc = dcol.ancmask;
+    while (anc) {
+      const int j = 31 - __builtin_clz(anc);
+      anc &= ~(1u << j);
       LDSA float* c = W->cdof[j];
       float v = c[0] * f[0] + c[1] * f[1] + c[2] * f[2] + c[3] * f[3] + c[4] * f[4] + c[5] * f[5];
-      if (j == i) v += m->dof_armature[i];
+      if (j == i) v += dcol.armature;
       W->M[i * LD + j] = v;
       W->M[j * LD + i] = v;
     }
@@ -489,53 +554,58 @@ template <class D> NOINL void com_pos_crb(MP m_, LDSA WS<D>* W, int lane) {
 // ---------------------------------------------------------------------------------------------
 template <class D> NOINL void velocity_stage(MP m_, LDSA WS<D>* W, int lane) {
   MP m = uniform_ptr(m_);
+  const int maxlevel = m->maxlevel, nbody = m->nbody, nv = m->nv, nu = m->nu;
+  const bool isb = lane > 0 && lane < nbody, isd = lane < nv, isu = lane < nu;
+  const BodyRec br = ldrec(&m->brec[isb ? lane : 0]);
+  const DofRec dr = ldrec(&m->drec[isd ? lane : 0]);
+  int udof = 0, ulim = 0;
+  float ugear = 0.f, ulo = 0.f, uhi = 0.f;
+  if (isu) {
+    udof = m->actuator_dof[lane]; ulim = m->actuator_ctrllimited[lane]; ugear = m->actuator_gear[lane];
+    ulo = m->actuator_ctrlrange[lane][0]; uhi = m->actuator_ctrlrange[lane][1];
+  }
   if (lane == 0) {
     for (int i = 0; i < 6; i++) W->cvel[0][i] = 0.f;
     W->cacc[0][0] = W->cacc[0][1] = W->cacc[0][2] = 0.f;
     W->cacc[0][3] = -m->gravity[0]; W->cacc[0][4] = -m->gravity[1]; W->cacc[0][5] = -m->gravity[2];
   }
-  SYNC();
-  const int maxlevel = m->maxlevel, nbody = m->nbody;
-  for (int L = 1; L <= maxlevel; L++) {
-    int b = lane;
-    if (b < nbody && m->body_level[b] == L) {
-      int p = m->body_parentid[b];
-      float cv[6], ca[6];
-      for (int i = 0; i < 6; i++) { cv[i] = W->cvel[p][i]; ca[i] = W->cacc[p][i]; }
-      int ja = m->body_jntadr[b], jn = m->body_jntnum[b];
-      for (int j = ja; j < ja + jn; j++) {
-        int da = m->jnt_dofadr[j];
-        if (m->jnt_type[j] == MJL_JNT_FREE) {
-          for (int k = 0; k < 3; k++)
-            for (int i = 0; i < 6; i++) cv[i] += W->cdof[da + k][i] * W->qvel[da + k];
-          float cd[3][6];
-          for (int k = 0; k < 3; k++) {
-            float c6[6];
-            for (int i = 0; i < 6; i++) c6[i] = W->cdof[da + 3 + k][i];
-            cross_motion(cd[k], cv, c6);
-          }
-          for (int k = 0; k < 3; k++) {
-            float qd = W->qvel[da + 3 + k];
-            for (int i = 0; i < 6; i++) ca[i] += cd[k][i] * qd;
-          }
-          for (int k = 0; k < 3; k++)
-            for (int i = 0; i < 6; i++) cv[i] += W->cdof[da + 3 + k][i] * W->qvel[da + 3 + k];
-        } else {
-          float cd[6], c6[6];
-          for (int i = 0; i < 6; i++) c6[i] = W->cdof[da][i];
-          cross_motion(cd, cv, c6);
-          float qd = W->qvel[da];
-          for (int i = 0; i < 6; i++) { ca[i] += cd[i] * qd; cv[i] += c6[i] * qd; }
-        }
+  // this body's joint terms (lane = body): cvel_b = cvel_p + S, cacc_b = cacc_p + cvel_p x U + T
+  // with S = sum cdof qd, U = the part of S that gets a cdof_dot term, T = the in-body cross terms
+  float S[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f}, U[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  float T[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  if (isb) {
+    const int da = br.dofadr, dn = br.dofnum;
+    if (br.isfree) {  // translation first; the rotational cdof_dot use cvel after translation
+      for (int k = 0; k < 3; k++)
+        for (int i = 0; i < 6; i++) S[i] += W->cdof[da + k][i] * W->qvel[da + k];
+      for (int k = 3; k < 6; k++)
+        for (int i = 0; i < 6; i++) U[i] += W->cdof[da + k][i] * W->qvel[da + k];
+      cross_motion(T, S, U);
+      for (int i = 0; i < 6; i++) S[i] += U[i];
+    } else {
+      for (int k = 0; k < dn; k++) {
+        float v[6], x[6];
+        const float qd = W->qvel[da + k];
+        for (int i = 0; i < 6; i++) v[i] = W->cdof[da + k][i] * qd;
+        cross_motion(x, S, v);
+        for (int i = 0; i < 6; i++) { T[i] += x[i]; U[i] += v[i]; S[i] += v[i]; }
       }
-      for (int i = 0; i < 6; i++) { W->cvel[b][i] = cv[i]; W->cacc[b][i] = ca[i]; }
+    }
+  }
+  SYNC();
+  for (int L = 1; L <= maxlevel; L++) {
+    if (isb && br.level == L) {
+      const int p = br.parent;
+      float cv[6], ca[6], x[6];
+      for (int i = 0; i < 6; i++) { cv[i] = W->cvel[p][i]; ca[i] = W->cacc[p][i]; }
+      cross_motion(x, cv, U);
+      for (int i = 0; i < 6; i++) { W->cvel[lane][i] = cv[i] + S[i]; W->cacc[lane][i] = ca[i] + x[i] + T[i]; }
     }
     SYNC();
   }
   // body forces cfrc = I*a + v x* (I*v), written over cacc
   float f[6];
-  bool hasb = lane > 0 && lane < nbody;
-  if (hasb) {
+  if (isb) {
     float f1[6], iv[6], f2[6], cv[6], ca[6], ci[10];
     for (int i = 0; i < 6; i++) { cv[i] = W->cvel[lane][i]; ca[i] = W->cacc[lane][i]; }
     for (int i = 0; i < 10; i++) ci[i] = W->cinert[lane][i];
@@ -545,36 +615,31 @@ template <class D> NOINL void velocity_stage(MP m_, LDSA WS<D>* W, int lane) {
     for (int i = 0; i < 6; i++) f[i] = f1[i] + f2[i];
   }
   SYNC();
-  if (hasb) for (int i = 0; i < 6; i++) W->cacc[lane][i] = f[i];
+  if (isb) for (int i = 0; i < 6; i++) W->cacc[lane][i] = f[i];
   SYNC();
-  if (hasb) {  // subtree sums of cfrc into cvel (cvel is no longer needed)
+  if (isb) {  // subtree sums of cfrc into cvel (cvel is no longer needed)
     float s[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-    for (int c = lane; c < m->body_subtree_end[lane]; c++)
+    for (int c = lane; c < br.subtree_end; c++)
       for (int i = 0; i < 6; i++) s[i] += W->cacc[c][i];
     for (int i = 0; i < 6; i++) W->cvel[lane][i] = s[i];
   }
+  if (lane < D::LD) W->frc_act[lane] = 0.f;
   SYNC();
-  if (lane < m->nv) {
-    LDSA float* c = W->cdof[lane];
-    LDSA float* fb = W->cvel[m->dof_bodyid[lane]];
-    W->frc_bias[lane] = c[0] * fb[0] + c[1] * fb[1] + c[2] * fb[2] + c[3] * fb[3] + c[4] * fb[4] + c[5] * fb[5];
-    int j = m->dof_jntid[lane];
-    float pf = -m->dof_damping[lane] * W->qvel[lane];
-    if (m->jnt_type[j] == MJL_JNT_HINGE) {
-      int qa = m->jnt_qposadr[j];
-      pf -= m->jnt_stiffness[j] * (W->qpos[qa] - m->qpos_spring[qa]);
-    }
-    W->frc_passive[lane] = pf;
-    W->frc_act[lane] = 0.f;
-  }
-  SYNC();
-  if (lane < m->nu) {  // motors with joint transmission
+  if (isu) {  // motors with joint transmission
     float c = W->ctrl[lane];
-    if (m->actuator_ctrllimited[lane]) c = fminf(fmaxf(c, m->actuator_ctrlrange[lane][0]), m->actuator_ctrlrange[lane][1]);
-    atomicAdd((float*)&W->frc_act[m->actuator_dof[lane]], m->actuator_gear[lane] * c);
+    if (ulim) c = fminf(fmaxf(c, ulo), uhi);
+    atomicAdd((float*)&W->frc_act[udof], ugear * c);
+  }
+  if (isd) {
+    LDSA float* c = W->cdof[lane];
+    LDSA float* fb = W->cvel[dr.bodyid];
+    W->frc_bias[lane] = c[0] * fb[0] + c[1] * fb[1] + c[2] * fb[2] + c[3] * fb[3] + c[4] * fb[4] + c[5] * fb[5];
+    float pf = -dr.damping * W->qvel[lane];
+    if (dr.qadr_spring >= 0) pf -= dr.stiffness * (W->qpos[dr.qadr_spring] - dr.qpos_spring);
+    W->frc_passive[lane] = pf;
   }
   SYNC();
-  if (lane < m->nv) W->frc_smooth[lane] = W->frc_passive[lane] - W->frc_bias[lane] + W->frc_act[lane];
+  if (isd) W->frc_smooth[lane] = W->frc_passive[lane] - W->frc_bias[lane] + W->frc_act[lane];
   SYNC();
 }
 
@@ -609,16 +674,15 @@ INL float sph_sph(float* pos, float* n, const float* p1, float r1, const float* 
 }
 
 // candidate contact k (0/1) of pair p; returns false if the pair has no k-th contact
-template <class D> INL bool collide(MP m, LDSA WS<D>* W, int p, int k, float& dist, float* pos, float* fr) {
-  int kind = m->pair_kind[p];
+template <class D> INL bool collide(const PairRec& pr, LDSA WS<D>* W, int k, float& dist, float* pos, float* fr) {
+  const int kind = pr.kind;
   if (k == 1 && kind != MJL_COL_PLANE_CAPSULE) return false;
-  int g1 = m->pair_geom1[p], g2 = m->pair_geom2[p];
+  const int g1 = pr.g1, g2 = pr.g2;
   float x1[3] = {W->gpos[g1][0], W->gpos[g1][1], W->gpos[g1][2]};
   float x2[3] = {W->gpos[g2][0], W->gpos[g2][1], W->gpos[g2][2]};
   float z1[3] = {W->gaxis[g1][0], W->gaxis[g1][1], W->gaxis[g1][2]};
   float z2[3] = {W->gaxis[g2][0], W->gaxis[g2][1], W->gaxis[g2][2]};
-  float r1 = m->geom_size[g1][0], r2 = m->geom_size[g2][0];
-  float h1 = m->geom_size[g1][1], h2 = m->geom_size[g2][1];
+  const float r1 = pr.r1, r2 = pr.r2, h1 = pr.h1, h2 = pr.h2;
   if (kind == MJL_COL_PLANE_SPHERE) {
     float d[3] = {x2[0] - x1[0], x2[1] - x1[1], x2[2] - x1[2]};
     dist = dot3(d, z1) - r2;
@@ -767,29 +831,29 @@ template <class D, bool G> NOINL bool build_rows(MP m_, LDSA WS<D>* W, Rows<G> R
   int nc = 0, nr = nl;
   const int npair = m->npair;
   for (int base = 0; base < npair; base += 64) {
-    int p = base + lane;
+    const int p = base + lane;
+    const bool isp = p < npair;
+    const PairRec pr = ldrec(&m->prec[isp ? p : 0]);
     for (int k = 0; k < 2; k++) {
       bool act = false;
       float dist = 0.f, pos[3], fr[9];
-      int condim = 1;
-      if (p < npair && collide(m, W, p, k, dist, pos, fr)) {
-        act = dist - m->pair_includemargin[p] < 0.f;
-        condim = m->pair_condim[p];
-      }
+      if (isp && collide(pr, W, k, dist, pos, fr)) act = dist - pr.includemargin < 0.f;
       // rows per contact are 1 (condim 1) or 4 (condim 3, pyramidal): prefix sums from ballots
-      unsigned long long b1 = __ballot(act && condim == 1), b4 = __ballot(act && condim != 1);
+      unsigned long long b1 = __ballot(act && pr.condim == 1), b4 = __ballot(act && pr.condim != 1);
       unsigned long long below = lanes_below(lane);
       int slot = __popcll((b1 | b4) & below);
       int rbefore = __popcll(b1 & below) + 4 * __popcll(b4 & below);
-      int rows = condim == 1 ? 1 : 4;
+      int rows = pr.condim == 1 ? 1 : 4;
       int c = nc + slot, r0 = nr + rbefore;
       if (act && c < capc && r0 + rows <= cap) {
         RF* cr = R.con + c * CONW;
         cr[0] = pos[0]; cr[1] = pos[1]; cr[2] = pos[2];
         for (int i = 0; i < 9; i++) cr[3 + i] = fr[i];
+        cr[12] = __uint_as_float(pr.mask1); cr[13] = __uint_as_float(pr.mask2); cr[14] = pr.mu;
+        cr[15] = __int_as_float(pr.b1 | (pr.b2 << 8) | (pr.condim << 16));
         R.con_pair[c] = p;
         R.con_efc[c] = r0;
-        float ep = dist - m->pair_includemargin[p], iw = m->pair_invweight[p];
+        float ep = dist - pr.includemargin, iw = pr.invweight;
         for (int q = 0; q < rows; q++) {
           R.epos[r0 + q] = ep;
           R.einvw[r0 + q] = iw;
@@ -805,22 +869,21 @@ template <class D, bool G> NOINL bool build_rows(MP m_, LDSA WS<D>* W, Rows<G> R
   if (nr > cap || nc > capc) return false;
   // contact Jacobian rows: lanes 0..31 -> contact c, lanes 32..63 -> contact c+1; lane%32 = dof
   const int d = lane & 31;
+  const int droot = ldrec(&m->drec[d < nv ? d : 0]).rootid;
   for (int c0 = 0; c0 < nc; c0 += 2) {
     int c = c0 + (lane >> 5);
     if (c < nc && d < LD) {
       RF* cr = R.con + c * CONW;
-      int p = R.con_pair[c];
-      int b1 = m->geom_bodyid[m->pair_geom1[p]], b2 = m->geom_bodyid[m->pair_geom2[p]];
-      int dim = m->pair_condim[p];
+      const uint32_t mask1 = __float_as_uint(cr[12]), mask2 = __float_as_uint(cr[13]);
+      const int dim = (__float_as_int(cr[15]) >> 16) & 0xff;
       int r0 = R.con_efc[c];
       float vn = 0.f, vt1 = 0.f, vt2 = 0.f;
       if (d < nv) {
-        float s = (float)((m->body_dofmask[b2] >> d) & 1u) - (float)((m->body_dofmask[b1] >> d) & 1u);
+        float s = (float)((mask2 >> d) & 1u) - (float)((mask1 >> d) & 1u);
         if (s != 0.f) {
           float cd[6];
           for (int i = 0; i < 6; i++) cd[i] = W->cdof[d][i];
-          int root = m->body_rootid[m->dof_bodyid[d]];
-          float off[3] = {cr[0] - W->scom[root][0], cr[1] - W->scom[root][1], cr[2] - W->scom[root][2]};
+          float off[3] = {cr[0] - W->scom[droot][0], cr[1] - W->scom[droot][1], cr[2] - W->scom[droot][2]};
           float cx[3];
           cross3(cx, cd, off);
           float jp[3] = {s * (cd[3] + cx[0]), s * (cd[4] + cx[1]), s * (cd[5] + cx[2])};
@@ -832,7 +895,7 @@ template <class D, bool G> NOINL bool build_rows(MP m_, LDSA WS<D>* W, Rows<G> R
       if (dim == 1) {
         R.J[r0 * LD + d] = vn;
       } else {
-        float mu = m->pair_mu[p];
+        const float mu = cr[14];
         R.J[(r0 + 0) * LD + d] = vn + mu * vt1;
         R.J[(r0 + 1) * LD + d] = vn - mu * vt1;
         R.J[(r0 + 2) * LD + d] = vn + mu * vt2;
@@ -1096,45 +1159,55 @@ template <class D, bool G> NOINL void solver(MP m_, LDSA WS<D>* W, Rows<G> R, in
 }
 
 // touch sensors (lane = sensor)   [sensor.sensor_acc, MuJoCo mjSENS_TOUCH]
+// Lane = contact: every contact's normal force and ray-box test run in parallel, one wave sum per
+// sensor (the sensor loop is uniform, so its constants come through the scalar cache).
 template <class D, bool G> NOINL void sensors(MP m_, LDSA WS<D>* W, Rows<G> R, int lane) {
   MP m = uniform_ptr(m_);
-  if (lane < m->nsensor) {
-    int site = m->sensor_objid[lane], body = m->site_bodyid[site];
-    float val = 0.f;
-    const int ncon = W->ncon;
-    for (int c = 0; c < ncon; c++) {
-      int p = R.con_pair[c];
-      int b1 = m->geom_bodyid[m->pair_geom1[p]], b2 = m->geom_bodyid[m->pair_geom2[p]];
-      if (b1 != body && b2 != body) continue;
-      int dim = m->pair_condim[p], nrow = dim == 1 ? 1 : 2 * (dim - 1), r0 = R.con_efc[c];
-      float fn = 0.f;
-      for (int r = 0; r < nrow; r++) fn += R.force[r0 + r];
-      if (fn <= 0.f) continue;
+  const int ncon = W->ncon, nsensor = m->nsensor;
+  for (int c0 = 0; c0 < ncon; c0 += 64) {
+    const int c = c0 + lane;
+    const bool has = c < ncon;
+    int b1 = -1, b2 = -1;
+    float fn = 0.f, cp[3] = {0.f, 0.f, 0.f}, cn[3] = {0.f, 0.f, 0.f};
+    if (has) {
       typename Rows<G>::F* cr = R.con + c * CONW;
-      float dir[3] = {cr[3], cr[4], cr[5]};
-      if (b2 == body) { dir[0] = -dir[0]; dir[1] = -dir[1]; dir[2] = -dir[2]; }
-      float dp[3] = {cr[0] - W->spos[site][0], cr[1] - W->spos[site][1], cr[2] - W->spos[site][2]};
-      float S[9];
-      for (int i = 0; i < 9; i++) S[i] = W->smat[site][i];
-      float lp[3], lv[3];
-      mtv3(lp, S, dp);
-      mtv3(lv, S, dir);
-      float sz[3] = {m->site_size[site][0], m->site_size[site][1], m->site_size[site][2]};
-      float best = -1.f;
-      for (int i = 0; i < 3; i++) {  // ray-box test in the site frame (mju_rayGeom, box)
-        if (fabsf(lv[i]) <= kMinVal) continue;
-        for (int side = -1; side <= 1; side += 2) {
-          float sol = ((float)side * sz[i] - lp[i]) / lv[i];
-          if (sol < 0.f) continue;
-          int i1 = (i + 1) % 3, i2 = (i + 2) % 3;
-          float a = lp[i1] + sol * lv[i1], b = lp[i2] + sol * lv[i2];
-          if (fabsf(a) <= sz[i1] && fabsf(b) <= sz[i2] && (best < 0.f || sol < best)) best = sol;
-        }
-      }
-      if (best >= 0.f) val += fn;
+      const int packed = __float_as_int(cr[15]), dim = (packed >> 16) & 0xff;
+      b1 = packed & 0xff; b2 = (packed >> 8) & 0xff;
+      int nrow = dim == 1 ? 1 : 2 * (dim - 1), r0 = R.con_efc[c];
+      for (int r = 0; r < nrow; r++) fn += R.force[r0 + r];
+      cp[0] = cr[0]; cp[1] = cr[1]; cp[2] = cr[2];
+      cn[0] = cr[3]; cn[1] = cr[4]; cn[2] = cr[5];
     }
-    W->sens[m->sensor_adr[lane]] = val;
+    for (int s = 0; s < nsensor; s++) {
+      const int site = m->sensor_objid[s], body = m->site_bodyid[site];
+      float val = 0.f;
+      if (has && fn > 0.f && (b1 == body || b2 == body)) {
+        float sg = (b2 == body) ? -1.f : 1.f;
+        float dir[3] = {sg * cn[0], sg * cn[1], sg * cn[2]};
+        float dp[3] = {cp[0] - W->spos[site][0], cp[1] - W->spos[site][1], cp[2] - W->spos[site][2]};
+        float S[9];
+        for (int i = 0; i < 9; i++) S[i] = W->smat[site][i];
+        float lp[3], lv[3];
+        mtv3(lp, S, dp);
+        mtv3(lv, S, dir);
+        const float sz[3] = {m->site_size[site][0], m->site_size[site][1], m->site_size[site][2]};
+        bool hit = false;
+        for (int i = 0; i < 3; i++) {  // ray-box test in the site frame (mju_rayGeom, box)
+          if (fabsf(lv[i]) <= kMinVal) continue;
+          const int i1 = (i + 1) % 3, i2 = (i + 2) % 3;
+          for (int side = -1; side <= 1; side += 2) {
+            float sol = ((float)side * sz[i] - lp[i]) / lv[i];
+            float a = lp[i1] + sol * lv[i1], b = lp[i2] + sol * lv[i2];
+            hit |= sol >= 0.f && fabsf(a) <= sz[i1] && fabsf(b) <= sz[i2];
+          }
+        }
+        val = hit ? fn : 0.f;
+      }
+      val = wsum(val);
+      if (lane == 0) W->sens[m->sensor_adr[s]] = (c0 == 0 ? 0.f : W->sens[m->sensor_adr[s]]) + val;
+    }
   }
+  if (ncon == 0 && lane < nsensor) W->sens[m->sensor_adr[lane]] = 0.f;
   SYNC();
 }
 
