@@ -41,8 +41,18 @@ __device__ unsigned long long* g_stamps;
     unsigned long long t_ = __builtin_amdgcn_s_memtime();                                        \
     if ((lane) == 0 && g_stamps) g_stamps[(size_t)blockIdx.x * 16 + (slot)] = t_;               \
   } while (0)
+// accumulate the cycles since `var` into slot (solver sub-phases), restart `var`
+#define TSTART(var) unsigned long long var = __builtin_amdgcn_s_memtime()
+#define TACC(slot, var, lane)                                                                    \
+  do {                                                                                           \
+    unsigned long long t_ = __builtin_amdgcn_s_memtime();                                        \
+    if ((lane) == 0 && g_stamps) g_stamps[(size_t)blockIdx.x * 16 + (slot)] += t_ - (var);      \
+    (var) = t_;                                                                                  \
+  } while (0)
 #else
 #define STAMP(slot, lane) do { } while (0)
+#define TSTART(var) do { } while (0)
+#define TACC(slot, var, lane) do { } while (0)
 #endif
 
 typedef const CSTA ModelF* MP;
@@ -284,8 +294,8 @@ template <class D> INL void chol_factor(LDSA float* A, LDSA float* invd_out, int
   float invd = 1.f;
 #pragma unroll
   for (int k = 0; k < NV; k++) {
-    float lkk = sqrtf(fmaxf(rdlane(a[k], k), 1e-30f));
-    float inv = 1.f / lkk;
+    const float piv = fmaxf(rdlane(a[k], k), 1e-30f);
+    const float inv = __builtin_amdgcn_rsqf(piv), lkk = piv * inv;
     a[k] = (lane == k) ? lkk : a[k] * inv;
     invd = (lane == k) ? inv : invd;
 #pragma unroll
@@ -957,8 +967,13 @@ template <class D, bool G> INL float solver_update(MP m_, LDSA WS<D>* W, Rows<G>
   SYNC();
   int d = lane & 31, h = lane >> 5;  // J' f : lane%32 = dof, lane/32 = row parity
   float s = 0.f;
-  if (d < nv)
-    for (int r = h; r < nefc; r += 2) s += R.J[r * LD + d] * R.force[r];
+  if (d < nv) {
+    int r = h;
+    for (; r + 6 < nefc; r += 8)  // 4 rows per trip: the loads issue together
+      s += R.J[r * LD + d] * R.force[r] + R.J[(r + 2) * LD + d] * R.force[r + 2] +
+           R.J[(r + 4) * LD + d] * R.force[r + 4] + R.J[(r + 6) * LD + d] * R.force[r + 6];
+    for (; r < nefc; r += 2) s += R.J[r * LD + d] * R.force[r];
+  }
   s += __shfl_xor(s, 32);
   float g = 0.f;
   if (lane < nv) {
@@ -972,39 +987,39 @@ template <class D, bool G> INL float solver_update(MP m_, LDSA WS<D>* W, Rows<G>
   return cost;
 }
 
-// Newton direction: Mgrad = H^-1 grad with H = M + J' D_active J
-template <class D, bool G> INL void solver_newton_dir(MP m_, LDSA WS<D>* W, Rows<G> R, int lane) {
+// Newton Hessian H = M + J' D_active J (factored by the caller), on the matrix cores:
+// v_mfma_f32_32x32x2_f32 takes two constraint rows per instruction, lane l supplying
+// A[i][k] = D_r J[r][i] (active rows only) and B[k][j] = J[r][j] with i = j = l & 31, r = r0 + (l >> 5);
+// the 32x32 accumulator (nv <= 32) is H - M in the C layout row = (v&3) + 8(v>>2) + 4(l>>5), col = l&31.
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+template <class D, bool G> INL void solver_hessian(MP m_, LDSA WS<D>* W, Rows<G> R, int lane) {
   MP m = uniform_ptr(m_);
   constexpr int LD = D::LD;
   const int nv = m->nv, nefc = W->nefc;
-  const int l = lane & 31, kh = lane >> 5;  // lane = (column l, half kh of the rows of H)
-  float acc[16];
+  const int col = lane & 31, kh = lane >> 5;
+  f32x16 acc;
 #pragma unroll
-  for (int kk = 0; kk < 16; kk++) {
-    int k = 16 * kh + kk;
-    acc[kk] = (l < nv && k < nv) ? W->M[k * LD + l] : 0.f;
-  }
-  for (int r = 0; r < nefc; r++) {
-    if (R.jar[r] < 0.f) {
-      float w = (l < LD) ? R.D[r] * R.J[r * LD + l] : 0.f;
+  for (int v = 0; v < 16; v++) acc[v] = 0.f;
+  for (int r0 = 0; r0 < nefc; r0 += 8) {
+    float a[4], b[4];
 #pragma unroll
-      for (int kk = 0; kk < 16; kk++) {
-        int k = 16 * kh + kk;
-        if (k < LD) acc[kk] = fmaf(w, R.J[r * LD + k], acc[kk]);
+    for (int u = 0; u < 4; u++) {  // loads of 4 row pairs first, then 4 MFMAs
+      const int r = r0 + 2 * u + kh;
+      a[u] = 0.f; b[u] = 0.f;
+      if (r < nefc && col < LD) {
+        const float j = R.J[r * LD + col];
+        b[u] = j;
+        a[u] = R.jar[r] < 0.f ? R.D[r] * j : 0.f;
       }
     }
-  }
-  if (l < nv) {
 #pragma unroll
-    for (int kk = 0; kk < 16; kk++) {
-      int k = 16 * kh + kk;
-      if (k < nv) W->H[k * LD + l] = acc[kk];
-    }
+    for (int u = 0; u < 4; u++) acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a[u], b[u], acc, 0, 0, 0);
   }
-  SYNC();
-  chol_factor<D>(W->H, W->invd, nv, lane);
-  float x = chol_solve<D>(W->H, W->invd, lane < nv ? W->grad[lane] : 0.f, lane);
-  if (lane < nv) W->Mgrad[lane] = x;
+#pragma unroll
+  for (int v = 0; v < 16; v++) {
+    const int row = (v & 3) + 8 * (v >> 2) + 4 * kh;
+    if (row < nv && col < nv) W->H[row * LD + col] = W->M[row * LD + col] + acc[v];
+  }
   SYNC();
 }
 
@@ -1072,6 +1087,7 @@ template <class D, bool G> NOINL void solver(MP m_, LDSA WS<D>* W, Rows<G> R, in
     return;
   }
   const float scale = m->scale;
+  TSTART(ts);
   // warm start: the cheaper of qacc_warmstart and qacc_smooth
   float cost2[2];
   for (int w = 0; w < 2; w++) {
@@ -1091,6 +1107,7 @@ template <class D, bool G> NOINL void solver(MP m_, LDSA WS<D>* W, Rows<G> R, in
   if (lane < nv) W->Ma[lane] = mrow<D>(W, W->qacc, lane);
   for (int r = lane; r < nefc; r += 64) R.jar[r] = jrow<D>(R.J, W->qacc, r) - R.aref[r];
   SYNC();
+  TACC(9, ts, lane);
   // Newton / CG iterations, written so that each helper appears once in the loop body.
   // Exact early exit (Newton): rows are affine in alpha, so if the active set at the new point
   // equals the set the Hessian was built from, no row switched along the step, the cost was one
@@ -1120,6 +1137,7 @@ template <class D, bool G> NOINL void solver(MP m_, LDSA WS<D>* W, Rows<G> R, in
       }
       for (int r = lane; r < nefc; r += 64) R.jar[r] += alpha * R.Jv[r];
       SYNC();
+      TACC(10, ts, lane);
     }
     float oldcost = cost;
     cost = solver_update<D, G>(m, W, R, lane);
@@ -1135,10 +1153,17 @@ template <class D, bool G> NOINL void solver(MP m_, LDSA WS<D>* W, Rows<G> R, in
         if (am[0] == hm[0] && am[1] == hm[1] && am[2] == hm[2] && am[3] == hm[3]) break;
       }
     }
+    TACC(11, ts, lane);
     if (newton) {
       if (exact_exit) active_masks(hm);
-      solver_newton_dir<D, G>(m, W, R, lane);
-      if (lane < LD) W->search[lane] = (lane < nv) ? -W->Mgrad[lane] : 0.f;
+      solver_hessian<D, G>(m, W, R, lane);
+      TACC(12, ts, lane);
+      chol_factor<D>(W->H, W->invd, nv, lane);
+      float x = chol_solve<D>(W->H, W->invd, lane < nv ? W->grad[lane] : 0.f, lane);
+      if (lane < nv) W->Mgrad[lane] = x;
+      SYNC();
+      TACC(13, ts, lane);
+      if (lane < LD) W->search[lane] = (lane < nv) ? -x : 0.f;
     } else {
       float x = chol_solve<D>(W->H, W->invd, lane < nv ? W->grad[lane] : 0.f, lane);  // H holds L(M)
       if (lane < nv) W->Mgrad[lane] = x;

@@ -11,6 +11,7 @@ import numpy as np  # noqa: E402
 import torch  # noqa: E402
 
 import mjx_amd  # noqa: E402
+import mjx_amd.abi  # noqa: E402
 from mjx_amd import _lib, mjx  # noqa: E402
 
 names = ["kinematics", "com_pos+crb+M", "velocity(rne,passive,act)", "factor M + qacc_smooth", "collision+rows",
@@ -24,15 +25,23 @@ buf = torch.zeros((B, 16), dtype=torch.int64, device="cuda")
 L.mjl_debug_set_stamps(C.c_void_p(buf.data_ptr()))
 for mode in ("speedtest", "trajectory"):
     d = mjx.make_data(sys_, B)
+    d.set_option(mjx_amd.abi.OPT_STORE_DERIVED, 1)
     if mode == "speedtest":
         vel = torch.linspace(0, 1, B, device="cuda")
-        for _ in range(3):
+        for _ in range(2):
             mjx.speedtest_step(sys_, d, vel)
+        torch.cuda.synchronize()
+        buf.zero_()
+        mjx.speedtest_step(sys_, d, vel)
     else:
         g = torch.Generator(device="cuda").manual_seed(0)
-        for _ in range(30):
+        for _ in range(29):
             mjx.step(sys_, d, torch.rand((B, m.nu), generator=g, device="cuda") * 2 - 1)
+        torch.cuda.synchronize()
+        buf.zero_()
+        mjx.step(sys_, d, torch.rand((B, m.nu), generator=g, device="cuda") * 2 - 1)
     torch.cuda.synchronize()
+    st = d.get("stats").cpu().numpy()
     s = buf.cpu().numpy().astype(np.float64)
     ok = s[:, 8] > 0
     d8 = np.diff(s[ok][:, [0, 1, 2, 3, 4, 5, 6, 7, 8]], axis=1)
@@ -40,4 +49,10 @@ for mode in ("speedtest", "trajectory"):
     print(f"{mode}: envs with LDS rows {ok.mean():.2f}; mean cycles/env-step {tot:.0f}")
     for i, n in enumerate(names):
         print(f"   {n:28s} {d8[:, i].mean():9.0f}  {100 * d8[:, i].mean() / tot:5.1f}%")
+    it = st[:, 2].mean()
+    print(f"   solver: mean ncon {st[:, 0].mean():.2f} nefc {st[:, 1].mean():.2f} iterations {it:.2f}")
+    for i, n in zip(range(9, 14), ["warm start", "line search (+step)", "update + convergence", "hessian J'DJ",
+                                   "cholesky factor+solve"]):
+        v = s[ok][:, i].mean()
+        print(f"      {n:26s} {v:9.0f}  per iteration {v / max(it, 1e-9):8.0f}")
     buf.zero_()
