@@ -117,6 +117,8 @@ int mjl_model_create(const mjlModelDesc* d, mjlModel** out) {
     if (b > 0 && d->body_parentid[b] >= b) { delete M; return fail(MJL_ERR_ARG, "bodies must be in DFS order"); }
   }
   f.maxlevel = maxlevel;
+  for (int b = 1; b < d->nbody; b++)
+    if (d->body_parentid[b] == 0) f.root[f.nroot++] = b;
   // dof masks along ancestor chains
   for (int b = 1; b < d->nbody; b++) {
     uint32_t mask = 0;

@@ -42,6 +42,7 @@ struct alignas(16) PairRec {
 struct ModelF {
   int nq, nv, nu, nbody, njnt, ngeom, nsite, ntendon, npair, nsensor, nsensordata;
   int iterations, ls_iterations, solver, integrator, eulerdamp, maxlevel, nlimited, any_damping;
+  int nroot, root[MJL_MAXBODY];  // kinematic roots: bodies whose parent is the world
   float timestep, gravity[3], impratio, tolerance, ls_tolerance, meaninertia, scale;
 
   int body_parentid[MJL_MAXBODY], body_rootid[MJL_MAXBODY], body_jntadr[MJL_MAXBODY];

@@ -113,6 +113,7 @@ INL unsigned long long lanes_below(int lane) { return (1ull << lane) - 1ull; }
 
 // a packed model record as whole b128 loads from the constant model block
 typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+typedef float f32x16 __attribute__((ext_vector_type(16)));
 template <class T> INL T ldrec(const CSTA T* p) {
   static_assert(sizeof(T) % 16 == 0, "records are 16-byte rows");
   union { u32x4 v[sizeof(T) / 16]; T t; } u;
@@ -309,6 +310,88 @@ template <class D> INL void chol_factor(LDSA float* A, LDSA float* invd_out, int
   SYNC();
 }
 
+// Factor + solve in one pass, for the hot callers (M in forward / integrate, the Newton Hessian):
+// L L^T = S (S: n x n SPD in LDS at src, stride LD), L written to dst (upper zeroed) with
+// invd_out[i] = 1 / L[i][i]; returns (L L^T)^-1 rhs with row i's value in lanes i and i + 32.
+// Lanes l and l + 32 both hold row l & 31, so the trailing update of the two-block right-looking
+// factorisation, S22 -= L21 L21^T over the first 16 columns, is 8 fp32 MFMAs whose A and B
+// operands are the lane's own registers. The MFMA result C has row r of C in column r of the
+// C layout, i.e. C[i][j] sits in lane i (half (j >> 2) & 1) register (j & 3) + 4 (j >> 3);
+// v_permlane32_swap of a register with itself hands each lane both halves' values.
+template <class D> INL float chol_factor_solve(const LDSA float* src, LDSA float* dst, LDSA float* invd_out,
+                                               int n, const LDSA float* rhs, int lane) {
+  constexpr int NV = D::NV, LD = D::LD;
+  constexpr int B1 = NV > 16 ? 16 : NV;
+  const int i = lane & 31, kh = lane >> 5;
+  float a[NV];
+#pragma unroll
+  for (int j = 0; j < NV; j++) a[j] = (i < n && j < n) ? src[i * LD + j] : (i == j ? 1.f : 0.f);
+  float x = (i < n) ? rhs[i] : 0.f;
+  float invd = 1.f;
+#pragma unroll
+  for (int k = 0; k < B1; k++) {
+    const float piv = fmaxf(rdlane(a[k], k), 1e-30f);
+    const float inv = __builtin_amdgcn_rsqf(piv), lkk = piv * inv;
+    a[k] = (i == k) ? lkk : a[k] * inv;
+    invd = (i == k) ? inv : invd;
+#pragma unroll
+    for (int j = k + 1; j < B1; j++) a[j] = fmaf(-a[k], rdlane(a[k], j), a[j]);
+  }
+  if constexpr (NV > B1) {
+    f32x16 acc;
+#pragma unroll
+    for (int v = 0; v < 16; v++) acc[v] = 0.f;
+#pragma unroll
+    for (int t = 0; t < B1 / 2; t++) {
+      const float op = kh ? a[2 * t + 1] : a[2 * t];
+      acc = __builtin_amdgcn_mfma_f32_32x32x2f32(op, op, acc, 0, 0, 0);
+    }
+    float lo[16], hi[16];  // lo[v]: register v of the kh = 0 half, hi[v]: of the kh = 1 half
+#pragma unroll
+    for (int v = B1 / 2; v < 16; v++) {
+      auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(acc[v]), __float_as_uint(acc[v]), false, false);
+      lo[v] = __uint_as_float(r[0]);
+      hi[v] = __uint_as_float(r[1]);
+    }
+#pragma unroll
+    for (int j = B1; j < NV; j++) {
+      const int v = (j & 3) + 4 * (j >> 3);
+      a[j] -= ((j >> 2) & 1) ? hi[v] : lo[v];
+    }
+#pragma unroll
+    for (int k = B1; k < NV; k++) {
+      const float piv = fmaxf(rdlane(a[k], k), 1e-30f);
+      const float inv = __builtin_amdgcn_rsqf(piv), lkk = piv * inv;
+      a[k] = (i == k) ? lkk : a[k] * inv;
+      invd = (i == k) ? inv : invd;
+#pragma unroll
+      for (int j = k + 1; j < NV; j++) a[j] = fmaf(-a[k], rdlane(a[k], j), a[j]);
+    }
+  }
+  if (lane < NV) {
+#pragma unroll
+    for (int j = 0; j < NV; j++) dst[i * LD + j] = (i < n) ? ((j <= i) ? a[j] : 0.f) : (j == i ? 1.f : 0.f);
+    invd_out[i] = invd;
+  }
+  // forward substitution L y = rhs, from the rows in registers
+#pragma unroll
+  for (int k = 0; k < NV; k++) {
+    const float yk = rdlane(x * invd, k);
+    x = (i == k) ? yk : ((i > k) ? fmaf(-a[k], yk, x) : x);
+  }
+  SYNC();
+  // back substitution L^T z = y: column i of L from the rows just written
+  float lc[NV];
+#pragma unroll
+  for (int k = 0; k < NV; k++) lc[k] = (i < k) ? dst[k * LD + i] : 0.f;
+#pragma unroll
+  for (int k = NV - 1; k >= 0; k--) {
+    const float zk = rdlane(x * invd, k);
+    x = (i == k) ? zk : ((i < k) ? fmaf(-lc[k], zk, x) : x);
+  }
+  return x;
+}
+
 // x distributed (lane i holds b_i, zero for i >= n) -> (L L^T)^-1 b, L from chol_factor
 template <class D> INL float chol_solve(const LDSA float* L, const LDSA float* invd_in, float x, int lane) {
   constexpr int NV = D::NV, LD = D::LD;
@@ -354,7 +437,6 @@ template <class D> NOINL void kinematics(MP m_, LDSA WS<D>* W, int lane) {
     W->xquat[0][0] = 1.f; W->xquat[0][1] = W->xquat[0][2] = W->xquat[0][3] = 0.f;
     for (int i = 0; i < 9; i++) W->xmat[0][i] = (i % 4 == 0) ? 1.f : 0.f;
     W->xipos[0][0] = W->xipos[0][1] = W->xipos[0][2] = 0.f;
-    W->cacc[0][0] = W->cacc[0][1] = W->cacc[0][2] = W->cacc[0][3] = 0.f;
   }
   if (lane >= 32 && lane - 32 < m->ntendon) {  // fixed tendons  [smooth.tendon]
     int t = lane - 32;
@@ -400,6 +482,7 @@ template <class D> NOINL void kinematics(MP m_, LDSA WS<D>* W, int lane) {
   }
   SYNC();
   // tree pass: compose with the parent's world frame, one level at a time  [smooth.kinematics]
+  float bm[4] = {0.f, 0.f, 0.f, 0.f};  // this body's mass moment and mass
   for (int L = 1; L <= maxlevel; L++) {
     if (isb && br.level == L) {
       float pos[3], quat[4], mat[9];
@@ -421,9 +504,8 @@ template <class D> NOINL void kinematics(MP m_, LDSA WS<D>* W, int lane) {
       float ip[3];
       mv3(ip, mat, br.ipos);
       W->xipos[b][0] = pos[0] + ip[0]; W->xipos[b][1] = pos[1] + ip[1]; W->xipos[b][2] = pos[2] + ip[2];
-      // body mass moment for the subtree com (cacc is free until the velocity stage)
-      W->cacc[b][0] = br.mass * W->xipos[b][0]; W->cacc[b][1] = br.mass * W->xipos[b][1];
-      W->cacc[b][2] = br.mass * W->xipos[b][2]; W->cacc[b][3] = br.mass;
+      bm[0] = br.mass * W->xipos[b][0]; bm[1] = br.mass * W->xipos[b][1]; bm[2] = br.mass * W->xipos[b][2];
+      bm[3] = br.mass;
     }
     SYNC();
   }
@@ -458,14 +540,17 @@ template <class D> NOINL void kinematics(MP m_, LDSA WS<D>* W, int lane) {
       for (int j = 0; j < 3; j++)
         W->smat[s][3 * i + j] = W->xmat[sb][3 * i] * sm[j] + W->xmat[sb][3 * i + 1] * sm[3 + j] + W->xmat[sb][3 * i + 2] * sm[6 + j];
   }
-  if (lane < nbody) {  // subtree com over the DFS-contiguous subtree [b, subtree_end)
-    const int b = lane;
-    float ms = 0.f, a0 = 0.f, a1 = 0.f, a2 = 0.f;
-    for (int c = b; c < br.subtree_end; c++) {
-      a0 += W->cacc[c][0]; a1 += W->cacc[c][1]; a2 += W->cacc[c][2]; ms += W->cacc[c][3];
+  // subtree com of the kinematic roots, the only subtree com the dynamics reads (cinert, cdof and
+  // contact Jacobians are taken about scom[rootid]); a root's subtree is lanes [r, subtree_end)
+  for (int q = 0; q < m->nroot; q++) {
+    const int r = m->root[q], e = m->body_subtree_end[r];
+    const bool in = lane >= r && lane < e;
+    const float s0 = wsum(in ? bm[0] : 0.f), s1 = wsum(in ? bm[1] : 0.f), s2 = wsum(in ? bm[2] : 0.f);
+    const float ms = wsum(in ? bm[3] : 0.f);
+    if (lane == 0) {
+      if (ms < kMinVal) { W->scom[r][0] = W->xipos[r][0]; W->scom[r][1] = W->xipos[r][1]; W->scom[r][2] = W->xipos[r][2]; }
+      else { const float inv = 1.f / ms; W->scom[r][0] = s0 * inv; W->scom[r][1] = s1 * inv; W->scom[r][2] = s2 * inv; }
     }
-    if (ms < kMinVal) { W->scom[b][0] = W->xipos[b][0]; W->scom[b][1] = W->xipos[b][1]; W->scom[b][2] = W->xipos[b][2]; }
-    else { float inv = 1.f / ms; W->scom[b][0] = a0 * inv; W->scom[b][1] = a1 * inv; W->scom[b][2] = a2 * inv; }
   }
   SYNC();
 }
@@ -991,7 +1076,6 @@ template <class D, bool G> INL float solver_update(MP m_, LDSA WS<D>* W, Rows<G>
 // v_mfma_f32_32x32x2_f32 takes two constraint rows per instruction, lane l supplying
 // A[i][k] = D_r J[r][i] (active rows only) and B[k][j] = J[r][j] with i = j = l & 31, r = r0 + (l >> 5);
 // the 32x32 accumulator (nv <= 32) is H - M in the C layout row = (v&3) + 8(v>>2) + 4(l>>5), col = l&31.
-typedef float f32x16 __attribute__((ext_vector_type(16)));
 template <class D, bool G> INL void solver_hessian(MP m_, LDSA WS<D>* W, Rows<G> R, int lane) {
   MP m = uniform_ptr(m_);
   constexpr int LD = D::LD;
@@ -1158,8 +1242,7 @@ template <class D, bool G> NOINL void solver(MP m_, LDSA WS<D>* W, Rows<G> R, in
       if (exact_exit) active_masks(hm);
       solver_hessian<D, G>(m, W, R, lane);
       TACC(12, ts, lane);
-      chol_factor<D>(W->H, W->invd, nv, lane);
-      float x = chol_solve<D>(W->H, W->invd, lane < nv ? W->grad[lane] : 0.f, lane);
+      float x = chol_factor_solve<D>(W->H, W->H, W->invd, nv, W->grad, lane);
       if (lane < nv) W->Mgrad[lane] = x;
       SYNC();
       TACC(13, ts, lane);
@@ -1248,11 +1331,8 @@ template <class D> NOINL void forward(MP m_, LDSA WS<D>* W, float* scratch_env, 
   STAMP(2, lane);
   velocity_stage<D>(m, W, lane);
   STAMP(3, lane);
-  // factor M into H: qacc_smooth now, warm start / CG preconditioner later
-  for (int i = lane; i < D::NV * LD; i += 64) W->H[i] = W->M[i];
-  SYNC();
-  chol_factor<D>(W->H, W->invd, m->nv, lane);
-  float x = chol_solve<D>(W->H, W->invd, lane < m->nv ? W->frc_smooth[lane] : 0.f, lane);
+  // factor M into H: qacc_smooth now, CG preconditioner later
+  float x = chol_factor_solve<D>(W->M, W->H, W->invd, m->nv, W->frc_smooth, lane);
   if (lane < LD) W->qacc_smooth[lane] = (lane < m->nv) ? x : 0.f;
   SYNC();
   STAMP(4, lane);
@@ -1286,11 +1366,12 @@ template <class D> NOINL void integrate(MP m_, LDSA WS<D>* W, int lane) {
   if (damp) {  // (M + dt*diag(damping)) qacc' = qfrc_smooth + qfrc_constraint
     for (int i = lane; i < D::NV * LD; i += 64) W->H[i] = W->M[i];
     SYNC();
-    if (lane < nv) W->H[lane * LD + lane] += dt * m->dof_damping[lane];
+    if (lane < nv) {
+      W->H[lane * LD + lane] += dt * m->dof_damping[lane];
+      W->Mv[lane] = W->frc_smooth[lane] + W->frc_con[lane];  // Mv: solver scratch, free now
+    }
     SYNC();
-    chol_factor<D>(W->H, W->invd, nv, lane);
-    float rhs = (lane < nv) ? W->frc_smooth[lane] + W->frc_con[lane] : 0.f;
-    qa = chol_solve<D>(W->H, W->invd, rhs, lane);
+    qa = chol_factor_solve<D>(W->H, W->H, W->invd, nv, W->Mv, lane);
   }
   if (lane < nv) {
     W->qacc_ws[lane] = W->qacc[lane];
