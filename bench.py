@@ -27,7 +27,8 @@ import torch  # noqa: E402
 
 REF_DEVICE_STEPS_PER_S = 72618.0  # HUMANOID_MJX device steps/s (README.md:77), batch 4096
 HBM_PEAK_GBS = 8000.0             # MI355X_MICROARCH.md: HBM3E peak 8.0 TB/s (spec)
-VALU_PEAK_TFLOPS = 157.3          # MI355X_MICROARCH.md: peak FP32 vector
+F32_PEAK_TFLOPS = 157.3           # MI355X_MICROARCH.md: peak FP32 matrix (dense) = FP32 vector
+SPEEDTEST_KERNEL = "step_kernel<mjl::Dims<27, 17, 22, 20, 48, 16>, 2>"  # rocprofv3 kernel name
 
 
 def parse():
@@ -91,6 +92,21 @@ def max_over_ranks(x, dist, local):
     return float(t.item())
 
 
+def pmc_traffic(B: int):
+    """HBM bytes per speed-test launch from the committed rocprofv3 PMC passes (tools/profile_round.sh),
+    used only when they were taken on the current kernel sources and this batch size."""
+    from mjx_amd import _lib
+    path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    try:
+        with open(path) as f:
+            t = json.load(f)
+    except (OSError, ValueError):
+        return None
+    if t.get("src_hash") != _lib.source_hash() or int(t.get("envs", -1)) != B:
+        return None
+    return t.get("bytes_per_launch")
+
+
 def cpu_baseline(model, budget_s: float):
     """Oracle (CPU restatement, fp64) on the same speed-test workload, one env per host thread."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
@@ -135,9 +151,20 @@ def main():
     value = B * args.steps * world / wall
     ms_per_step = wall / args.steps * 1e3
 
-    # per-env solver statistics of this workload (for the FLOP estimate and the record)
-    bytes_per_env = 8  # speed test: 4 B vel in + 4 B qpos[0] out
+    # solver statistics of exactly these states (a forward pass from the same fresh state), for the
+    # algorithmic FLOP count of one env-step (mjx_amd/flops.py, DESIGN.md "Roofline")
+    from mjx_amd import flops as flops_mod
+    ds = mjx.make_data(sys_, B, device=local)
+    qv = torch.zeros((B, sys_.nv), device=f"cuda:{local}")
+    qv[:, 0] = vel
+    ds.set("qvel", qv)
+    mjx.forward(sys_, ds)
+    wst = ds.get("stats").double().mean(0).cpu().numpy()
+    fl = flops_mod.step_flops(model, float(wst[0]), float(wst[1]), float(wst[2]))
+    achieved_tflops = fl["total"] * B / (kern_ms * 1e-3) / 1e12
+    bytes_per_env = 8  # speed test: 4 B vel in + 4 B qpos[0] out; the state never leaves LDS
     achieved_gbs = bytes_per_env * B / (kern_ms * 1e-3) / 1e9
+    traffic = pmc_traffic(B)
 
     extras = {}
     if not args.no_extras and rank == 0:
@@ -191,11 +218,16 @@ def main():
             "config": {"workload": f"{args.model}.xml speed-test step (fresh state per step), {B} envs per GPU",
                        "envs_per_gpu": B, "parallelism": f"env-sharded x{world}, no collective",
                        "baseline_note": "vs_baseline divides by the README HUMANOID_MJX row (72,618 steps/s, batch 4096)"},
-            "roofline": {"bound": "hbm", "achieved": achieved_gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": achieved_gbs / HBM_PEAK_GBS, "traffic": None,
-                         "kernel_ms": kern_ms,
-                         "note": "algorithmic bytes = 8 B/env-step (vel in, qpos[0] out); the kernel is bound by "
-                                 "in-wave VALU/LDS latency, not HBM (DESIGN.md)"},
+            "roofline": {"bound": "mfma", "achieved": achieved_tflops, "peak": F32_PEAK_TFLOPS, "unit": "TFLOP/s",
+                         "frac": achieved_tflops / F32_PEAK_TFLOPS, "traffic": traffic,
+                         "kernel": SPEEDTEST_KERNEL, "kernel_ms": kern_ms,
+                         "flops_per_env_step": fl["total"],
+                         "workload_mean_ncon_nefc_iter": [float(x) for x in wst[:3]],
+                         "hbm_algorithmic_bytes_per_launch": bytes_per_env * B,
+                         "hbm_achieved_gbs": achieved_gbs, "hbm_frac": achieved_gbs / HBM_PEAK_GBS,
+                         "note": "FP32 roof (dense MFMA = vector peak); achieved = algorithmic FP32 FLOPs "
+                                 "(mjx_amd/flops.py) / kernel time; traffic = HBM bytes per launch from the "
+                                 "committed FETCH_SIZE/WRITE_SIZE passes (profiles/, DESIGN.md)"},
             "cpu_baseline": cpu,
         }
         line.update(extras)

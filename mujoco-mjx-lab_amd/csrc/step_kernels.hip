@@ -31,6 +31,14 @@ namespace mjl {
 #define CSTA __attribute__((address_space(4)))
 #define GLBA __attribute__((address_space(1)))
 #define NOINL __device__ __noinline__
+// The hot phases are inlined into the kernel entry: a kernel has no callee-saved registers, while a
+// called phase function saves every callee-saved VGPR block it touches (v40-47, v56-63, ...) to
+// scratch on entry; at 130-250 VGPRs per phase that was ~35 KB of scratch traffic per env-step.
+#ifndef MJL_NOINLINE_PHASES
+#define PHASE __device__ __forceinline__
+#else
+#define PHASE NOINL
+#endif
 #define INL __device__ __forceinline__
 #define SYNC() __syncthreads()
 
@@ -416,7 +424,7 @@ template <class D> INL float chol_solve(const LDSA float* L, const LDSA float* i
 // ---------------------------------------------------------------------------------------------
 // position stage: kinematics, tendons, geom/site frames, subtree com   [smooth.kinematics]
 // ---------------------------------------------------------------------------------------------
-template <class D> NOINL void kinematics(MP m_, LDSA WS<D>* W, int lane) {
+template <class D> PHASE void kinematics(MP m_, LDSA WS<D>* W, int lane) {
   MP m = uniform_ptr(m_);
   const int maxlevel = m->maxlevel, nbody = m->nbody, ngeom = m->ngeom, nsite = m->nsite, njnt = m->njnt;
   // model records of this lane, loaded once: body `lane`, geom `lane`, site `lane - 32`, joint `lane`
@@ -556,7 +564,7 @@ template <class D> NOINL void kinematics(MP m_, LDSA WS<D>* W, int lane) {
 }
 
 // cinert (lane = body) and cdof (lane 32 + dof); crb (lane = body); M columns (lane = dof)
-template <class D> NOINL void com_pos_crb(MP m_, LDSA WS<D>* W, int lane) {
+template <class D> PHASE void com_pos_crb(MP m_, LDSA WS<D>* W, int lane) {
   MP m = uniform_ptr(m_);
   constexpr int LD = D::LD;
   const int nbody = m->nbody, nv = m->nv;
@@ -647,7 +655,7 @@ template <class D> NOINL void com_pos_crb(MP m_, LDSA WS<D>* W, int lane) {
 // velocity stage: com_vel + rne forward pass by levels, backward by subtree ranges; passive
 // forces and actuation   [smooth.com_vel / smooth.rne / passive.passive / forward.fwd_actuation]
 // ---------------------------------------------------------------------------------------------
-template <class D> NOINL void velocity_stage(MP m_, LDSA WS<D>* W, int lane) {
+template <class D> PHASE void velocity_stage(MP m_, LDSA WS<D>* W, int lane) {
   MP m = uniform_ptr(m_);
   const int maxlevel = m->maxlevel, nbody = m->nbody, nv = m->nv, nu = m->nu;
   const bool isb = lane > 0 && lane < nbody, isd = lane < nv, isu = lane < nu;
@@ -876,7 +884,7 @@ INL void kbi(float tstep, const CSTA float* solref, const CSTA float* solimp, fl
 
 // Builds limit and contact rows into R (capacity R.cap / R.capc). Returns false, without writing
 // past capacity, when they do not fit; W->ncon / nefc always hold the true counts.
-template <class D, bool G> NOINL bool build_rows(MP m_, LDSA WS<D>* W, Rows<G> R, int lane) {
+template <class D, bool G> PHASE bool build_rows(MP m_, LDSA WS<D>* W, Rows<G> R, int lane) {
   MP m = uniform_ptr(m_);
   constexpr int LD = D::LD;
   typedef typename Rows<G>::F RF;
@@ -1159,7 +1167,7 @@ template <class D, bool G> INL float solver_linesearch(MP m_, LDSA WS<D>* W, Row
   return alpha;
 }
 
-template <class D, bool G> NOINL void solver(MP m_, LDSA WS<D>* W, Rows<G> R, int lane) {
+template <class D, bool G> PHASE void solver(MP m_, LDSA WS<D>* W, Rows<G> R, int lane) {
   MP m = uniform_ptr(m_);
   constexpr int LD = D::LD;
   const int nv = m->nv, nefc = W->nefc;
@@ -1269,7 +1277,7 @@ template <class D, bool G> NOINL void solver(MP m_, LDSA WS<D>* W, Rows<G> R, in
 // touch sensors (lane = sensor)   [sensor.sensor_acc, MuJoCo mjSENS_TOUCH]
 // Lane = contact: every contact's normal force and ray-box test run in parallel, one wave sum per
 // sensor (the sensor loop is uniform, so its constants come through the scalar cache).
-template <class D, bool G> NOINL void sensors(MP m_, LDSA WS<D>* W, Rows<G> R, int lane) {
+template <class D, bool G> PHASE void sensors(MP m_, LDSA WS<D>* W, Rows<G> R, int lane) {
   MP m = uniform_ptr(m_);
   const int ncon = W->ncon, nsensor = m->nsensor;
   for (int c0 = 0; c0 < ncon; c0 += 64) {
@@ -1319,8 +1327,17 @@ template <class D, bool G> NOINL void sensors(MP m_, LDSA WS<D>* W, Rows<G> R, i
   SYNC();
 }
 
+// rows that do not fit in LDS: the cold path, kept out of line
+template <class D> NOINL void global_rows_path(MP m, LDSA WS<D>* W, float* scratch_env, int gmax_efc, int gmax_con,
+                                               int lane) {
+  Rows<true> R = global_rows<D>(scratch_env, gmax_efc, gmax_con);
+  build_rows<D, true>(m, W, R, lane);
+  solver<D, true>(m, W, R, lane);
+  sensors<D, true>(m, W, R, lane);
+}
+
 // full forward pass (mjx.forward)
-template <class D> NOINL void forward(MP m_, LDSA WS<D>* W, float* scratch_env, int gmax_efc, int gmax_con,
+template <class D> PHASE void forward(MP m_, LDSA WS<D>* W, float* scratch_env, int gmax_efc, int gmax_con,
                                       int force_global, int lane) {
   MP m = uniform_ptr(m_);
   constexpr int LD = D::LD;
@@ -1346,17 +1363,14 @@ template <class D> NOINL void forward(MP m_, LDSA WS<D>* W, float* scratch_env, 
     sensors<D, false>(m, W, R, lane);
     STAMP(7, lane);
   } else {  // more rows than fit in LDS (or forced): this env's slab of global scratch
-    Rows<true> R = global_rows<D>(scratch_env, gmax_efc, gmax_con);
-    build_rows<D, true>(m, W, R, lane);
-    solver<D, true>(m, W, R, lane);
-    sensors<D, true>(m, W, R, lane);
+    global_rows_path<D>(m, W, scratch_env, gmax_efc, gmax_con, lane);
   }
 }
 
 // ---------------------------------------------------------------------------------------------
 // integration (Euler with eulerdamp / implicitfast)   [forward.euler / forward.implicit]
 // ---------------------------------------------------------------------------------------------
-template <class D> NOINL void integrate(MP m_, LDSA WS<D>* W, int lane) {
+template <class D> PHASE void integrate(MP m_, LDSA WS<D>* W, int lane) {
   MP m = uniform_ptr(m_);
   constexpr int LD = D::LD;
   const int nv = m->nv;
@@ -1533,7 +1547,7 @@ template <class D> NOINL void env_reset(MP m_, LDSA WS<D>* W, const EnvArgs* Ap,
 }
 
 // post-step part of single_step (envs.py:347-492): reward, termination, aux, obs
-template <class D> NOINL void env_post(MP m_, LDSA WS<D>* W, const mjlEnvConfig* cfg, LDSA float* aux, float* obs,
+template <class D> PHASE void env_post(MP m_, LDSA WS<D>* W, const mjlEnvConfig* cfg, LDSA float* aux, float* obs,
                                        int lane) {
   MP m = uniform_ptr(m_);
   CP c = (CP)cfg;

@@ -30,6 +30,19 @@ class MjlError(RuntimeError):
     pass
 
 
+def source_hash() -> str:
+    """sha256 over the native sources (kernel + C ABI), to tie recorded profiles to a kernel build."""
+    import hashlib
+    h = hashlib.sha256()
+    inc = os.path.join(os.path.dirname(os.path.dirname(_HERE)), "include", "mjx355.h")
+    for p in sorted(os.listdir(CSRC)) + [inc]:
+        fp = p if os.path.isabs(p) else os.path.join(CSRC, p)
+        if fp.endswith((".hip", ".h")):
+            with open(fp, "rb") as f:
+                h.update(os.path.basename(fp).encode() + b"\0" + f.read())
+    return h.hexdigest()[:16]
+
+
 def build(force: bool = False):
     args = ["make", "-s", "-C", CSRC]
     if force:

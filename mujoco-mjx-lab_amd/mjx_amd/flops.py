@@ -1,0 +1,44 @@
+"""Algorithmic FP32 FLOP model of one humanoid step (mjx.step), for bench.py's roofline.
+
+Counts the arithmetic the algorithm needs (an FMA is 2 FLOPs), not what the kernel issues: the
+kernel runs one env per 64-lane wave and most of its VALU instructions have few active lanes, so
+issued lane-FLOPs are many times this. Each term follows the stage of the reference pipeline it
+models (mujoco/mjx/_src: smooth.py, collision_driver.py, constraint.py, solver.py, forward.py);
+DESIGN.md lists the derivation. Sizes come from the compiled model, the solver statistics (active
+contacts, rows, Newton iterations) from a forward pass over the benchmarked states.
+"""
+from __future__ import annotations
+
+
+def cholesky(n: int) -> float:
+    """Dense LL^T factor (n^3/3 FMAs) + forward and back substitution (2 n^2 FMAs)."""
+    return 2.0 * (n ** 3 / 3.0 + 2.0 * n * n)
+
+
+def step_flops(m, ncon: float, nefc: float, iters: float, ls_evals: float = 3.0) -> dict:
+    """FP32 FLOPs of one env-step, by stage. `m` is a CompiledModel (sizes only)."""
+    nv, nb, nj, npair = m.nv, m.nbody, m.njnt, m.npair
+    f = {}
+    # kinematics: per joint local quaternion (sincos, qmul, 2 quat->mat, 2 mat-vec),
+    # per body compose with the parent (qmul, quat->mat, 2 mat-vec), geom and site frames
+    f["kinematics"] = 2.0 * (nj * 70 + nb * 60 + m.ngeom * 18 + m.nsite * 36)
+    # com_pos / crb: cinert (two 3x3 products + parallel axis), cdof, subtree crb, M columns
+    depth = 0.5 * nv  # mean ancestor-chain length of a dof (humanoid: 6 free + limb chains)
+    f["crb_M"] = 2.0 * (nb * 70 + nv * 9 + nb * 10 * 4 + nv * (36 + 6 * depth))
+    # rne (cvel, cacc by levels; body forces; subtree sums; dof projection), passive, actuation
+    f["rne"] = 2.0 * (nb * (2 * 18 + 2 * 36 + 18 + 6 * 4) + nv * 8)
+    # collision: every candidate pair (capsule-capsule dominates: ~120 FMAs)
+    f["collision"] = 2.0 * npair * 120
+    # constraint rows: contact Jacobians (4 pyramid rows x nv) + impedance + reference accel
+    f["rows"] = 2.0 * (ncon * nv * 20 + nefc * (nv + 30))
+    # smooth acceleration M^-1 qfrc_smooth and the implicit-integration solve
+    f["factor_M"] = cholesky(nv)
+    f["integrate"] = cholesky(nv) + 2.0 * nv * 4
+    # Newton solver: warm-start costs (M q, J q for two candidates), then per iteration:
+    # Hessian J'DJ (full nv x nv over the rows), factor + solve, line search (M s, J s,
+    # ls_evals evaluations of the rows), update (J'f, gradient)
+    per_it = (2.0 * nv * nv * nefc + cholesky(nv) + 2.0 * (nv * nv + nv * nefc + ls_evals * 4 * nefc)
+              + 2.0 * (nv * nefc + 4 * nv))
+    f["solver"] = 2.0 * 2 * (nv * nv + nv * nefc) + iters * per_it
+    f["total"] = sum(f.values())
+    return f
