@@ -271,3 +271,23 @@ def test_full_size_properties():
     assert torch.allclose(qn, torch.ones_like(qn), atol=1e-5)
     st = env.data.get("stats")
     assert (st[:, 3] == 0).all()
+
+
+def test_sphere_speedtest_kat_on_gpu():
+    """SPHERE row of mjx_humanoid_speed_test.py:29-40,50-55 on the HIP path: a free sphere, no floor,
+    Euler, dt 0.002: one step from qvel[0] = v gives qpos[0] = v dt, qpos[2] = -g dt^2 (fp32)."""
+    from mjx_amd import mjcf
+    m = mjcf.compile_xml_string(
+        "<mujoco><worldbody><body><freejoint/><geom size='.15' type='sphere'/></body></worldbody></mujoco>")
+    sys_ = mjx.put_model(m)
+    B = 64
+    vel = torch.linspace(0, 1, B, device="cuda")
+    d = mjx.make_data(sys_, B)
+    out = mjx.speedtest_step(sys_, d, vel).cpu().numpy()
+    np.testing.assert_allclose(out, np.linspace(0, 1, B) * 0.002, rtol=1e-6, atol=1e-9)
+    qv = torch.zeros((B, 6))
+    qv[:, 0] = vel.cpu()
+    d.set("qvel", qv)
+    mjx.step(sys_, d)
+    q = d.get("qpos").cpu().numpy()
+    np.testing.assert_allclose(q[:, 2], -9.81 * 0.002 ** 2, rtol=1e-5)
