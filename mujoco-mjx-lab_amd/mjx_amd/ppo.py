@@ -1,0 +1,379 @@
+"""PPO trainer over the native env step (reference train_ppo.py, src/networks.py, src/training_utils.py).
+
+Host-side PyTorch: the MLPs are rocBLAS/hipBLASLt GEMMs on the same stream as the env kernels; the
+env step (physics + reward + obs + auto-reset) is one `mjl_env_step` launch per rollout step.
+Formulas follow the reference line by line (cited per function); data-parallel training over
+`torch.distributed` (RCCL on GPUs, gloo on CPU) adds exactly the exchanges SURVEY.md §8e lists:
+parameter broadcast at start, one all-reduce of the flattened policy+value gradients per
+minibatch, the advantage-normalisation sums per minibatch, and the observation statistics per
+iteration. Each rank steps its own envs; nothing in the physics path communicates.
+"""
+from __future__ import annotations
+
+import json
+import math
+import os
+import time
+from dataclasses import asdict, is_dataclass
+from typing import List, Optional, Sequence, Tuple
+
+import torch
+import torch.nn as nn
+
+ACTIVATIONS = {
+    "tanh": torch.tanh, "relu": torch.relu, "elu": nn.functional.elu, "swish": nn.functional.silu,
+    "silu": nn.functional.silu, "gelu": nn.functional.gelu, "linear": lambda x: x, "none": lambda x: x,
+}
+
+
+# ----------------------------------------------------------------------------------------- networks
+class MLP(nn.Module):
+    """src/networks.py:22-61: layers of (features, activation); Glorot-normal weights
+    N(0, 2/(in+out)), zero biases (networks.py:32-53). Unknown activations fall back to tanh."""
+
+    def __init__(self, in_dim: int, layer_specs: Sequence[Tuple[int, str]], generator: Optional[torch.Generator] = None):
+        super().__init__()
+        self.acts = [str(a).lower() for _, a in layer_specs]
+        layers, d = [], in_dim
+        for feat, _ in layer_specs:
+            lin = nn.Linear(d, int(feat))
+            with torch.no_grad():
+                lin.weight.normal_(0.0, math.sqrt(2.0 / (d + int(feat))), generator=generator)
+                lin.bias.zero_()
+            layers.append(lin)
+            d = int(feat)
+        self.layers = nn.ModuleList(layers)
+
+    def forward(self, x):
+        for lin, a in zip(self.layers, self.acts):
+            x = ACTIVATIONS.get(a, torch.tanh)(lin(x))
+        return x
+
+
+class GaussianPolicy(nn.Module):
+    """networks.py:82-112: mean = tanh(MLP(x)), learnable log_std (init log_std_init), clipped to [-20, 2]."""
+
+    def __init__(self, obs_dim, act_dim, hidden_layer_specs, log_std_init=0.0, generator=None):
+        super().__init__()
+        self.mlp = MLP(obs_dim, list(hidden_layer_specs) + [(act_dim, "linear")], generator)
+        self.log_std = nn.Parameter(torch.full((act_dim,), float(log_std_init)))
+
+    def forward(self, x):
+        return torch.tanh(self.mlp(x)), torch.clamp(self.log_std, -20.0, 2.0)
+
+
+class ValueNet(nn.Module):
+    """networks.py:114-131: MLP -> scalar."""
+
+    def __init__(self, obs_dim, hidden_layer_specs, generator=None):
+        super().__init__()
+        self.mlp = MLP(obs_dim, list(hidden_layer_specs) + [(1, "linear")], generator)
+
+    def forward(self, x):
+        return self.mlp(x).squeeze(-1)
+
+
+class APGPolicy(nn.Module):
+    """networks.py:63-80: tanh-squashed MLP (hidden_dim x hidden_depth tanh layers)."""
+
+    def __init__(self, obs_dim, act_dim, hidden_dim=64, hidden_depth=2, hidden_layer_specs=None, generator=None):
+        super().__init__()
+        specs = list(hidden_layer_specs) if hidden_layer_specs is not None else [(hidden_dim, "tanh")] * hidden_depth
+        self.mlp = MLP(obs_dim, specs + [(act_dim, "linear")], generator)
+
+    def forward(self, x):
+        return torch.tanh(self.mlp(x))
+
+
+# ------------------------------------------------------------------------------------- statistics
+class RunningMeanStd:
+    """training_utils.py:20-56 (RMSState / update_rms / normalize_obs): mean 0, var 1, count 1e-4;
+    parallel-variance merge with population batch variance; var floored at 1e-4."""
+
+    def __init__(self, dim: int, device="cpu"):
+        self.mean = torch.zeros(dim, device=device)
+        self.var = torch.ones(dim, device=device)
+        self.count = torch.tensor(1e-4, device=device)
+
+    def update(self, x: torch.Tensor, dist=None):
+        x = x.reshape(-1, x.shape[-1]).float()
+        n = torch.tensor(float(x.shape[0]), device=x.device)
+        s1, s2 = x.sum(0), (x * x).sum(0)
+        if dist is not None:  # global batch statistics: sum, sum of squares, count over ranks
+            buf = torch.cat([s1, s2, n.reshape(1)])
+            dist.all_reduce(buf)
+            s1, s2, n = buf[: x.shape[1]], buf[x.shape[1]: 2 * x.shape[1]], buf[-1]
+            bmean = s1 / n
+            bvar = torch.clamp(s2 / n - bmean * bmean, min=0.0)
+        else:
+            bmean = x.mean(0)
+            bvar = x.var(0, unbiased=False)
+        delta = bmean - self.mean
+        tot = self.count + n
+        new_mean = self.mean + delta * n / tot
+        m2 = self.var * self.count + bvar * n + delta * delta * self.count * n / tot
+        self.mean, self.var, self.count = new_mean, torch.clamp(m2 / tot, min=1e-4), tot
+
+    def normalize(self, x, clip: float = 10.0):
+        """normalize_obs + the clip to [-10, 10] the trainers apply (train_ppo.py:134-135)."""
+        return torch.clamp((x - self.mean) / torch.sqrt(self.var + 1e-8), -clip, clip)
+
+    def state_dict(self):
+        return {"mean": self.mean, "var": self.var, "count": self.count}
+
+    def load_state_dict(self, d):
+        self.mean, self.var, self.count = d["mean"], d["var"], d["count"]
+
+
+# ---------------------------------------------------------------------------------- PPO formulas
+LOG2PI = math.log(2.0 * math.pi)
+
+
+def gaussian_logprob(mean, log_std, action):
+    """train_ppo.py:121-126: diagonal Gaussian log-density summed over action dims."""
+    var = torch.exp(2.0 * log_std)
+    return -0.5 * torch.sum((action - mean) ** 2 / var + 2.0 * log_std + LOG2PI, dim=-1)
+
+
+def gaussian_entropy(log_std, act_dim):
+    """train_ppo.py:215: 0.5 * sum(1 + log 2pi + 2 log_std) / act_dim."""
+    return 0.5 * torch.sum(1.0 + LOG2PI + 2.0 * log_std) / act_dim
+
+
+def compute_gae(rewards, values, terminated, truncated, gamma: float, lam: float):
+    """train_ppo.py:171-202: values [T+1, B]; only termination stops the bootstrap, either
+    termination or truncation stops the advantage accumulation. Returns (adv, ret) [T, B]."""
+    T = rewards.shape[0]
+    adv = torch.empty_like(rewards)
+    carry = torch.zeros_like(rewards[0])
+    for t in range(T - 1, -1, -1):
+        delta = rewards[t] + gamma * values[t + 1] * (1.0 - terminated[t]) - values[t]
+        carry = delta + gamma * lam * (1.0 - torch.maximum(terminated[t], truncated[t])) * carry
+        adv[t] = carry
+    return adv, adv + values[:-1]
+
+
+def normalize_adv(adv, dist=None):
+    """(adv - mean) / (std + 1e-8) over the minibatch (train_ppo.py:209; jnp.std is the population
+    std); over the global minibatch when data-parallel."""
+    if dist is None:
+        return (adv - adv.mean()) / (adv.std(unbiased=False) + 1e-8)
+    buf = torch.stack([adv.sum(), (adv * adv).sum(), torch.tensor(float(adv.numel()), device=adv.device)])
+    dist.all_reduce(buf)
+    mu = buf[0] / buf[2]
+    sd = torch.sqrt(torch.clamp(buf[1] / buf[2] - mu * mu, min=0.0))
+    return (adv - mu) / (sd + 1e-8)
+
+
+def ppo_policy_loss(policy, obs, acts, old_logp, adv, clip_eps, ent_coef, dist=None):
+    """train_ppo.py:204-216."""
+    mean, log_std = policy(obs)
+    ratio = torch.exp(gaussian_logprob(mean, log_std, acts) - old_logp)
+    adv_n = normalize_adv(adv, dist)
+    surr = torch.minimum(ratio * adv_n, torch.clamp(ratio, 1.0 - clip_eps, 1.0 + clip_eps) * adv_n)
+    return -surr.mean() - ent_coef * gaussian_entropy(log_std, acts.shape[-1])
+
+
+def value_loss(value, obs, returns):
+    """train_ppo.py:218-220 (vf_coef is unused by the reference)."""
+    return torch.mean((value(obs) - returns) ** 2)
+
+
+def make_index_batches(total: int, minibatch: int, epochs: int, generator: torch.Generator, device):
+    """train_ppo.py:222-231: a fresh permutation per epoch, the last partial minibatch dropped."""
+    per = total // minibatch
+    out = [torch.randperm(total, generator=generator, device="cpu")[: per * minibatch].view(per, minibatch)
+           for _ in range(epochs)]
+    return torch.cat(out, 0).to(device)
+
+
+def _flat_grads(params: List[torch.Tensor]) -> torch.Tensor:
+    return torch.cat([(p.grad if p.grad is not None else torch.zeros_like(p)).reshape(-1) for p in params])
+
+
+def _set_grads(params: List[torch.Tensor], flat: torch.Tensor):
+    o = 0
+    for p in params:
+        n = p.numel()
+        p.grad = flat[o:o + n].view_as(p).clone()
+        o += n
+
+
+def ppo_update(policy, value, opt_p, opt_v, obs, acts, logp, ret, adv, index_batches, cfg, dist=None, world=1):
+    """train_ppo.py:233-252: per minibatch, a policy Adam step then a value Adam step. Data-parallel:
+    each rank takes its share of every minibatch; gradients of both nets travel in one all-reduce."""
+    pp, vp = list(policy.parameters()), list(value.parameters())
+    for idx in index_batches:
+        o, a, ol, r, ad = obs[idx], acts[idx], logp[idx], ret[idx], adv[idx]
+        opt_p.zero_grad(set_to_none=True)
+        opt_v.zero_grad(set_to_none=True)
+        ppo_policy_loss(policy, o, a, ol, ad, cfg.clip_eps, cfg.ent_coef, dist).backward()
+        value_loss(value, o, r).backward()
+        if dist is not None:
+            g = _flat_grads(pp + vp)
+            dist.all_reduce(g)
+            g /= world
+            _set_grads(pp + vp, g)
+        opt_p.step()
+        opt_v.step()
+
+
+# ----------------------------------------------------------------------------------------- trainer
+def _jsonable(cfg):
+    d = asdict(cfg) if is_dataclass(cfg) else dict(cfg)
+    return json.loads(json.dumps(d, default=str))
+
+
+class PPOTrainer:
+    """train_ppo.py:64-441 over any env exposing reset() -> obs, step(act) -> (obs, rew, term, trunc)
+    with auto-reset (HumanoidEnv, or a stand-in in CPU tests), obs_dim, act_dim, num_envs."""
+
+    def __init__(self, cfg, env, eval_env=None, device="cuda", dist=None, out_dir: Optional[str] = None):
+        self.cfg, self.env, self.eval_env, self.dist = cfg, env, eval_env, dist
+        self.rank = dist.get_rank() if dist is not None else 0
+        self.world = dist.get_world_size() if dist is not None else 1
+        self.device = torch.device(device)
+        g = torch.Generator().manual_seed(int(cfg.seed))  # identical initial params on every rank
+        self.policy = GaussianPolicy(env.obs_dim, env.act_dim, cfg.policy_hidden_layer_specs, cfg.log_std_init,
+                                     g).to(self.device)
+        self.value = ValueNet(env.obs_dim, cfg.value_hidden_layer_specs, g).to(self.device)
+        if dist is not None:
+            for p in list(self.policy.parameters()) + list(self.value.parameters()):
+                dist.broadcast(p.data, 0)
+        # optax.adam defaults (b1 .9, b2 .999, eps 1e-8) = torch.optim.Adam defaults
+        self.opt_p = torch.optim.Adam(self.policy.parameters(), lr=cfg.lr_policy, betas=(0.9, 0.999), eps=1e-8)
+        self.opt_v = torch.optim.Adam(self.value.parameters(), lr=cfg.lr_value, betas=(0.9, 0.999), eps=1e-8)
+        self.rms = RunningMeanStd(env.obs_dim, self.device)
+        self.gen = torch.Generator(device=self.device).manual_seed(int(cfg.seed) * 1000 + self.rank)
+        self.idx_gen = torch.Generator().manual_seed(int(cfg.seed) + 7919 * (self.rank + 1))
+        self.obs = env.reset().clone()
+        self.total_env_steps = 0.0
+        self.start = time.time()
+        self.out_dir = out_dir if self.rank == 0 else None
+        if self.out_dir:
+            for sub in ("checkpoints", "logs"):
+                os.makedirs(os.path.join(self.out_dir, sub), exist_ok=True)
+            with open(os.path.join(self.out_dir, "config.json"), "w") as f:
+                json.dump(_jsonable(cfg), f, indent=2)
+
+    # train_ppo.py:128-169
+    @torch.no_grad()
+    def collect_rollout(self):
+        T, B, env = self.cfg.rollout_length, self.env.num_envs, self.env
+        dev = self.device
+        obs_t = torch.empty((T, B, env.obs_dim), device=dev)
+        act_t = torch.empty((T, B, env.act_dim), device=dev)
+        logp_t = torch.empty((T, B), device=dev)
+        r_t, te_t, tr_t = (torch.empty((T, B), device=dev) for _ in range(3))
+        obs = self.obs
+        for t in range(T):
+            obs_t[t] = obs
+            mean, log_std = self.policy(self.rms.normalize(obs))
+            eps = torch.randn(mean.shape, generator=self.gen, device=dev)
+            act = mean + torch.exp(log_std) * eps
+            act_t[t] = act
+            logp_t[t] = gaussian_logprob(mean, log_std, act)
+            o2, r, te, tr = env.step(act)  # physics + reward + obs + merge_if_done, one launch
+            r_t[t], te_t[t], tr_t[t] = r, te, tr
+            obs = o2
+        self.obs = obs.clone()
+        return obs_t, act_t, logp_t, r_t, te_t, tr_t
+
+    def iteration(self, it: int) -> dict:
+        cfg, dev = self.cfg, self.device
+        if dev.type == "cuda":
+            torch.cuda.synchronize(dev)
+        t0 = time.time()
+        obs_t, act_t, logp_t, r_t, te_t, tr_t = self.collect_rollout()
+        T, B = r_t.shape
+        self.rms.update(obs_t, self.dist)
+        with torch.no_grad():
+            obs_n = self.rms.normalize(obs_t)
+            last_n = self.rms.normalize(self.obs)
+            v = self.value(torch.cat([obs_n, last_n[None]], 0).reshape((T + 1) * B, -1)).reshape(T + 1, B)
+            adv, ret = compute_gae(r_t, v, te_t, tr_t, cfg.gamma, cfg.lam)
+        mb = cfg.minibatch_size // self.world
+        idx = make_index_batches(T * B, mb, cfg.epochs, self.idx_gen, dev)
+        ppo_update(self.policy, self.value, self.opt_p, self.opt_v, obs_n.reshape(T * B, -1),
+                   act_t.reshape(T * B, -1), logp_t.reshape(-1), ret.reshape(-1), adv.reshape(-1), idx, cfg,
+                   self.dist, self.world)
+        if dev.type == "cuda":
+            torch.cuda.synchronize(dev)
+        dt = max(time.time() - t0, 1e-9)
+        ep_ret = r_t.sum(0)
+        stats = torch.stack([ep_ret.sum(), torch.maximum(te_t, tr_t).sum(), torch.tensor(float(B), device=dev)])
+        mx = ep_ret.max().reshape(1)
+        if self.dist is not None:
+            self.dist.all_reduce(stats)
+            self.dist.all_reduce(mx, op=self.dist.ReduceOp.MAX)
+        env_steps = float(T) * float(stats[2])
+        self.total_env_steps += env_steps
+        dones = float(stats[1])
+        return {"train_return_avg": float(stats[0] / stats[2]), "train_return_max": float(mx[0]),
+                "train_eplen_avg": env_steps / dones if dones > 0 else float(T),
+                "env_steps_per_sec": env_steps / dt}
+
+    @torch.no_grad()
+    def evaluate(self, it: int = 0, steps: int = 500) -> float:
+        """train_ppo.py:261-313: deterministic mean action, auto-reset, mean summed reward; the eval
+        envs are reseeded with seed + 10000 + iteration each time (train_ppo.py:268-270)."""
+        env = self.eval_env
+        if hasattr(env, "seed"):
+            env.seed, env.counter = int(self.cfg.seed) + 10000 + it, 0
+        obs = env.reset().clone()
+        acc = torch.zeros(env.num_envs, device=self.device)
+        for _ in range(steps):
+            mean, _ = self.policy(self.rms.normalize(obs))
+            obs, r, _, _ = env.step(mean)
+            acc += r
+        return float(acc.mean())
+
+    def save_checkpoint(self, it: int, metrics: dict):
+        """checkpoint_utils.py:38-61 layout (results/<ts>_ppo/checkpoints/), torch state dicts."""
+        if not self.out_dir:
+            return None
+        path = os.path.join(self.out_dir, "checkpoints", f"checkpoint_{it:06d}.pt")
+        torch.save({"step": it, "policy": self.policy.state_dict(), "value": self.value.state_dict(),
+                    "rms": self.rms.state_dict(), "opt_policy": self.opt_p.state_dict(),
+                    "opt_value": self.opt_v.state_dict(), "metrics": metrics}, path)
+        return path
+
+    def load_checkpoint(self, path: str):
+        ck = torch.load(path, map_location=self.device, weights_only=True)
+        self.policy.load_state_dict(ck["policy"])
+        self.value.load_state_dict(ck["value"])
+        self.rms.load_state_dict(ck["rms"])
+        self.opt_p.load_state_dict(ck["opt_policy"])
+        self.opt_v.load_state_dict(ck["opt_value"])
+        return ck["step"]
+
+    def log(self, it: int, metrics: dict):
+        """checkpoint_utils.py:93-100 + training_utils.py:146-152: metrics.jsonl lines."""
+        metrics["total_env_steps"] = self.total_env_steps
+        metrics["elapsed_time"] = time.time() - self.start
+        if self.out_dir:
+            with open(os.path.join(self.out_dir, "logs", "metrics.jsonl"), "a") as f:
+                f.write(json.dumps({"step": it, **metrics}) + "\n")
+
+    def train(self, iterations: Optional[int] = None, verbose: bool = True) -> List[dict]:
+        cfg = self.cfg
+        n = cfg.total_iterations if iterations is None else iterations
+        hist = []
+        for it in range(n):
+            m = self.iteration(it)
+            should_eval = (it % cfg.eval_interval == 0) and self.eval_env is not None
+            should_ckpt = it % cfg.checkpoint_every == 0
+            if should_eval and self.rank == 0:
+                m["eval_return"] = self.evaluate(it)
+            if (it % cfg.log_interval == 0) or should_eval or should_ckpt or it == n - 1:
+                self.log(it, m)
+                if verbose and self.rank == 0:
+                    s = (f"Iter {it:4d} | S/s: {m['env_steps_per_sec']:10.0f} | Train_Ret(Avg): "
+                         f"{m['train_return_avg']:8.2f} | Train_Len(Avg): {m['train_eplen_avg']:6.0f}")
+                    if "eval_return" in m:
+                        s += f" | Eval_Ret(Avg): {m['eval_return']:8.2f}"
+                    print(s, flush=True)
+            if should_ckpt:
+                self.save_checkpoint(it, m)
+            hist.append(m)
+        return hist

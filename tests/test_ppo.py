@@ -1,0 +1,232 @@
+"""PPO trainer (mjx_amd/ppo.py) against the reference formulas (train_ppo.py, src/networks.py,
+src/training_utils.py) and its data-parallel path (world size 2, gloo, CPU).
+
+No reference outputs can be captured (jax is absent), so the formulas are pinned by
+closed forms and hand-computed recurrences; the distributed path is pinned by equality with the
+single-process computation over the union of the ranks' data.
+"""
+import json
+import math
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as tdist
+import torch.multiprocessing as mp
+
+from mjx_amd import ppo
+from mjx_amd.config import reference_ppo_config
+
+
+class PointEnv:
+    """CPU stand-in with the HumanoidEnv interface (reset / step with auto-reset): a damped 3-D
+    point pushed by a 2-D action; reward -|x|; terminates outside |x| < 2, truncates at 20 steps."""
+
+    def __init__(self, num_envs, seed=0):
+        self.num_envs, self.obs_dim, self.act_dim = num_envs, 6, 2
+        self.g = torch.Generator().manual_seed(seed)
+        self.x = torch.zeros(num_envs, 3)
+        self.v = torch.zeros(num_envs, 3)
+        self.t = torch.zeros(num_envs)
+
+    def _obs(self):
+        return torch.cat([self.x, self.v], 1)
+
+    def reset(self, mask=None):
+        m = torch.ones(self.num_envs, dtype=torch.bool) if mask is None else mask > 0.5
+        self.x[m] = torch.rand((int(m.sum()), 3), generator=self.g) - 0.5
+        self.v[m] = 0.0
+        self.t[m] = 0.0
+        return self._obs()
+
+    def step(self, act):
+        a = torch.clamp(act, -1, 1)
+        self.v = 0.9 * self.v + 0.1 * torch.cat([a, -a[:, :1]], 1)
+        self.x = self.x + 0.1 * self.v
+        self.t += 1
+        r = -self.x.norm(dim=1)
+        term = (self.x.abs().max(1).values > 2.0).float()
+        trunc = (self.t >= 20).float() * (1 - term)
+        done = torch.maximum(term, trunc)
+        if done.any():
+            self.reset(done)
+        return self._obs(), r, term, trunc
+
+
+def small_cfg(**kw):
+    cfg = reference_ppo_config()
+    cfg.policy_hidden_layer_specs = [(32, "tanh"), (32, "tanh")]
+    cfg.value_hidden_layer_specs = [(32, "tanh"), (32, "tanh")]
+    cfg.rollout_length, cfg.minibatch_size, cfg.epochs = 8, 32, 2
+    cfg.eval_interval, cfg.checkpoint_every, cfg.log_interval = 1, 1, 1
+    for k, v in kw.items():
+        setattr(cfg, k, v)
+    return cfg
+
+
+# --------------------------------------------------------------------------------- formulas
+def test_param_counts_and_glorot_init():
+    cfg = reference_ppo_config()
+    pol = ppo.GaussianPolicy(54, 21, cfg.policy_hidden_layer_specs, cfg.log_std_init, torch.Generator().manual_seed(0))
+    val = ppo.ValueNet(54, cfg.value_hidden_layer_specs, torch.Generator().manual_seed(1))
+    assert sum(p.numel() for p in pol.parameters()) == 151082
+    assert sum(p.numel() for p in val.parameters()) == 145921
+    w = pol.mlp.layers[1].weight.detach()
+    assert abs(w.std().item() - math.sqrt(2.0 / 512)) < 0.003
+    assert all(float(l.bias.detach().abs().max()) == 0.0 for l in pol.mlp.layers)
+    assert float(pol.log_std.detach().abs().max()) == 0.0
+
+
+def test_logprob_and_entropy_closed_forms():
+    g = torch.Generator().manual_seed(3)
+    mean, act = torch.randn(5, 21, generator=g), torch.randn(5, 21, generator=g)
+    log_std = torch.randn(21, generator=g) * 0.3
+    ref = torch.distributions.Normal(mean, torch.exp(log_std)).log_prob(act).sum(-1)
+    torch.testing.assert_close(ppo.gaussian_logprob(mean, log_std, act), ref, rtol=1e-5, atol=1e-5)
+    ent = torch.distributions.Normal(torch.zeros(21), torch.exp(log_std)).entropy().sum() / 21
+    torch.testing.assert_close(ppo.gaussian_entropy(log_std, 21), ent, rtol=1e-6, atol=1e-6)
+
+
+def test_gae_matches_hand_recurrence():
+    rng = np.random.default_rng(0)
+    T, B, gam, lam = 7, 3, 0.99, 0.95
+    r, v = rng.normal(size=(T, B)), rng.normal(size=(T + 1, B))
+    te = (rng.uniform(size=(T, B)) < 0.2).astype(float)
+    tr = (rng.uniform(size=(T, B)) < 0.2).astype(float) * (1 - te)
+    adv = np.zeros((T, B))
+    for b in range(B):
+        nxt = 0.0
+        for t in reversed(range(T)):
+            delta = r[t, b] + gam * v[t + 1, b] * (1 - te[t, b]) - v[t, b]
+            nxt = delta + gam * lam * (1 - max(te[t, b], tr[t, b])) * nxt
+            adv[t, b] = nxt
+    a, ret = ppo.compute_gae(*(torch.tensor(x) for x in (r, v, te, tr)), gam, lam)
+    np.testing.assert_allclose(a.numpy(), adv, atol=1e-12)
+    np.testing.assert_allclose(ret.numpy(), adv + v[:-1], atol=1e-12)
+
+
+def test_rms_merge_formula():
+    rng = np.random.default_rng(1)
+    rms = ppo.RunningMeanStd(4)
+    mean, var, count = np.zeros(4), np.ones(4), 1e-4
+    for _ in range(3):
+        x = rng.normal(2.0, 3.0, size=(50, 4))
+        rms.update(torch.tensor(x, dtype=torch.float32))
+        bm, bv, n = x.mean(0), x.var(0), x.shape[0]
+        d, tot = bm - mean, count + n
+        mean, var, count = mean + d * n / tot, np.maximum((var * count + bv * n + d * d * count * n / tot) / tot, 1e-4), tot
+    np.testing.assert_allclose(rms.mean.numpy(), mean, rtol=1e-5)
+    np.testing.assert_allclose(rms.var.numpy(), var, rtol=1e-4)
+    x = torch.tensor(rng.normal(size=(3, 4)), dtype=torch.float32)
+    torch.testing.assert_close(rms.normalize(x), torch.clamp((x - rms.mean) / torch.sqrt(rms.var + 1e-8), -10, 10))
+
+
+def test_adam_matches_optax_formula():
+    """optax.adam (b1 .9, b2 .999, eps 1e-8, eps_root 0): u = -lr m_hat / (sqrt(v_hat) + eps)."""
+    p = torch.nn.Parameter(torch.tensor([1.0, -2.0, 0.5]))
+    opt = torch.optim.Adam([p], lr=3e-4, betas=(0.9, 0.999), eps=1e-8)
+    x = p.detach().clone().double()
+    m = torch.zeros(3, dtype=torch.float64)
+    v = torch.zeros(3, dtype=torch.float64)
+    for t in range(1, 6):
+        g = torch.tensor([0.3, -1.0, 2.0]) * t
+        p.grad = g.clone()
+        opt.step()
+        m = 0.9 * m + 0.1 * g.double()
+        v = 0.999 * v + 0.001 * g.double() ** 2
+        x = x - 3e-4 * (m / (1 - 0.9 ** t)) / (torch.sqrt(v / (1 - 0.999 ** t)) + 1e-8)
+    np.testing.assert_allclose(p.detach().numpy(), x.numpy(), rtol=1e-6)
+
+
+def test_index_batches_drop_partial():
+    idx = ppo.make_index_batches(100, 32, 2, torch.Generator().manual_seed(0), "cpu")
+    assert idx.shape == (6, 32)
+    for e in range(2):
+        assert len(set(idx[3 * e:3 * e + 3].reshape(-1).tolist())) == 96
+
+
+# ------------------------------------------------------------------------ trainer end to end
+def test_trainer_end_to_end_cpu(tmp_path):
+    cfg = small_cfg(total_iterations=3)
+    tr = ppo.PPOTrainer(cfg, PointEnv(16, 0), PointEnv(8, 1), device="cpu", out_dir=str(tmp_path))
+    tr.evaluate = lambda it=0, steps=500: ppo.PPOTrainer.evaluate(tr, it, 20)
+    hist = tr.train(verbose=False)
+    assert len(hist) == 3 and all(np.isfinite(h["train_return_avg"]) for h in hist)
+    lines = [json.loads(l) for l in open(tmp_path / "logs" / "metrics.jsonl")]
+    keys = {"step", "train_return_avg", "train_return_max", "train_eplen_avg", "env_steps_per_sec",
+            "total_env_steps", "elapsed_time", "eval_return"}
+    assert keys <= set(lines[0]) and lines[-1]["total_env_steps"] == 3 * 16 * 8
+    assert json.load(open(tmp_path / "config.json"))["rollout_length"] == 8
+    ck = sorted(os.listdir(tmp_path / "checkpoints"))
+    assert ck[-1] == "checkpoint_000002.pt"
+    tr2 = ppo.PPOTrainer(cfg, PointEnv(16, 0), None, device="cpu")
+    assert tr2.load_checkpoint(str(tmp_path / "checkpoints" / ck[-1])) == 2
+    for a, b in zip(tr.policy.parameters(), tr2.policy.parameters()):
+        torch.testing.assert_close(a, b)
+
+
+# ------------------------------------------------------------------- data parallel (gloo, ws 2)
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _synthetic(n, seed):
+    g = torch.Generator().manual_seed(seed)
+    return (torch.randn(n, 6, generator=g), torch.randn(n, 2, generator=g), torch.randn(n, generator=g) - 3,
+            torch.randn(n, generator=g), torch.randn(n, generator=g))
+
+
+def _dp_worker(rank, port, out):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    tdist.init_process_group("gloo", rank=rank, world_size=2)
+    torch.manual_seed(0)
+    cfg = small_cfg()
+    pol = ppo.GaussianPolicy(6, 2, cfg.policy_hidden_layer_specs, 0.0, torch.Generator().manual_seed(5))
+    val = ppo.ValueNet(6, cfg.value_hidden_layer_specs, torch.Generator().manual_seed(6))
+    op = torch.optim.Adam(pol.parameters(), lr=1e-3)
+    ov = torch.optim.Adam(val.parameters(), lr=1e-3)
+    data = _synthetic(64, 10 + rank)
+    idx = torch.arange(64).view(4, 16)  # 4 minibatches, 16 local rows each
+    ppo.ppo_update(pol, val, op, ov, *data, idx, cfg, tdist, 2)
+    rms = ppo.RunningMeanStd(6)
+    rms.update(data[0], tdist)
+    # trainer on two ranks: identical parameters after training
+    tr = ppo.PPOTrainer(small_cfg(total_iterations=2), PointEnv(8, 100 + rank), None, device="cpu", dist=tdist)
+    tr.train(verbose=False)
+    flat = torch.cat([p.detach().reshape(-1) for p in tr.policy.parameters()])
+    if rank == 0:
+        torch.save({"pol": pol.state_dict(), "val": val.state_dict(), "rms": rms.state_dict(), "trainer": flat}, out[0])
+    else:
+        torch.save({"trainer": flat}, out[1])
+    tdist.destroy_process_group()
+
+
+def test_data_parallel_update_equals_single_process(tmp_path):
+    out = [str(tmp_path / "r0.pt"), str(tmp_path / "r1.pt")]
+    mp.spawn(_dp_worker, args=(_free_port(), out), nprocs=2, join=True)
+    got = torch.load(out[0], weights_only=True)
+    cfg = small_cfg()
+    pol = ppo.GaussianPolicy(6, 2, cfg.policy_hidden_layer_specs, 0.0, torch.Generator().manual_seed(5))
+    val = ppo.ValueNet(6, cfg.value_hidden_layer_specs, torch.Generator().manual_seed(6))
+    op = torch.optim.Adam(pol.parameters(), lr=1e-3)
+    ov = torch.optim.Adam(val.parameters(), lr=1e-3)
+    d0, d1 = _synthetic(64, 10), _synthetic(64, 11)
+    data = tuple(torch.cat([a, b]) for a, b in zip(d0, d1))
+    idx = torch.cat([torch.arange(64).view(4, 16), torch.arange(64, 128).view(4, 16)], 1)  # union minibatches
+    ppo.ppo_update(pol, val, op, ov, *data, idx, cfg)
+    for k, v in pol.state_dict().items():
+        torch.testing.assert_close(got["pol"][k], v, rtol=2e-5, atol=2e-6)
+    for k, v in val.state_dict().items():
+        torch.testing.assert_close(got["val"][k], v, rtol=2e-5, atol=2e-6)
+    rms = ppo.RunningMeanStd(6)
+    rms.update(data[0])
+    torch.testing.assert_close(got["rms"]["mean"], rms.mean, rtol=1e-5, atol=1e-6)
+    torch.testing.assert_close(got["rms"]["var"], rms.var, rtol=1e-4, atol=1e-5)
+    t1 = torch.load(out[1], weights_only=True)["trainer"]
+    torch.testing.assert_close(got["trainer"], t1, rtol=0, atol=0)
