@@ -207,6 +207,22 @@ int mjl_env_step(mjlBatch* batch, const float* act, float* obs, float* rew, floa
 int mjl_env_reset(mjlBatch* batch, const float* mask, uint64_t seed, uint64_t counter,
                   const float* noise, float* obs, void* stream);
 
+/* Reverse-mode derivative of one mjl_step (APG backward; reference train_apg.py:161-209 takes
+ * jax.value_and_grad through mjx.step, src/envs.py:345). The pre-step state is the batch state
+ * (qpos, qvel, qacc_warmstart, ctrl), which is not modified. Given the cotangents of the step
+ * outputs g_qpos [nenv,nq], g_qvel [nenv,nv], writes the cotangents of the inputs out_qpos
+ * [nenv,nq], out_qvel [nenv,nv], out_ctrl [nenv,nu]. The constraint solve is differentiated at
+ * its converged active set; qacc_warmstart gets no cotangent (DESIGN.md "APG"). */
+int mjl_step_vjp(mjlBatch* batch, const float* g_qpos, const float* g_qvel, float* out_qpos,
+                 float* out_qvel, float* out_ctrl, void* stream);
+
+/* VJP of one env step (src/envs.py:333-492 single_step, without the reset merge) at the batch
+ * state and aux with action act [nenv,nu]: cotangents of (qpos', qvel', reward, aux') ->
+ * (qpos, qvel, action, aux). g_rew [nenv], g_aux / out_aux [nenv, MJL_AUX_DIM]. */
+int mjl_env_step_vjp(mjlBatch* batch, const float* act, const float* g_qpos, const float* g_qvel,
+                     const float* g_rew, const float* g_aux, float* out_qpos, float* out_qvel,
+                     float* out_act, float* out_aux, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -1,0 +1,1258 @@
+// Reverse-mode derivative (VJP) of one mjx.step and of one env step, for APG
+// (reference train_apg.py:161-209 differentiates the discounted return through mjx.step).
+//
+// One wave per env, like the forward kernel: the step is recomputed in LDS (per-step remat, as
+// train_apg.py:187-189 checkpoints every step), then the reverse passes run phase by phase.
+// Derivative conventions (DESIGN.md "APG"):
+//  * the constraint solve is differentiated at its converged active set A (implicit function):
+//    qacc = Hc^-1 (qfrc_smooth + J_A' D_A aref_A), Hc = M + J_A' D_A J_A; and the total force that
+//    enters the integrator, qfrc_smooth + J' f, equals M qacc there;
+//  * qacc_warmstart only seeds the solver and gets no cotangent;
+//  * piecewise-constant quantities (contact/limit activity, target jumps, flags) follow the branch
+//    the primal takes, as reverse-mode autodiff of the reference does.
+// Checked against the exact Jacobian of the fp64 oracle (oracle/dual.hpp) in tests/test_adjoint.py.
+
+namespace mjl {
+
+// ------------------------------------------------------------------- derivative helpers
+INL void add3(float* a, const float* b) { a[0] += b[0]; a[1] += b[1]; a[2] += b[2]; }
+// r = a x b  ->  abar += b x rbar, bbar += rbar x a
+template <class A, class B> INL void cross3_adj(A a, B b, const float* rb, float* ab, float* bb) {
+  float t[3];
+  cross3(t, b, rb); add3(ab, t);
+  cross3(t, rb, a); add3(bb, t);
+}
+// r = a (x) b (quaternion product)
+template <class A, class B> INL void qmul_adj(A a, B b, const float* r, float* ab, float* bb) {
+  bb[0] += a[0] * r[0] + a[1] * r[1] + a[2] * r[2] + a[3] * r[3];
+  bb[1] += -a[1] * r[0] + a[0] * r[1] + a[3] * r[2] - a[2] * r[3];
+  bb[2] += -a[2] * r[0] - a[3] * r[1] + a[0] * r[2] + a[1] * r[3];
+  bb[3] += -a[3] * r[0] + a[2] * r[1] - a[1] * r[2] + a[0] * r[3];
+  ab[0] += b[0] * r[0] + b[1] * r[1] + b[2] * r[2] + b[3] * r[3];
+  ab[1] += -b[1] * r[0] + b[0] * r[1] - b[3] * r[2] + b[2] * r[3];
+  ab[2] += -b[2] * r[0] + b[3] * r[1] + b[0] * r[2] - b[1] * r[3];
+  ab[3] += -b[3] * r[0] - b[2] * r[1] + b[1] * r[2] + b[0] * r[3];
+}
+// m = q2m(q)
+template <class Q, class MB> INL void q2m_adj(Q q, MB mb, float* qb) {
+  const float w = q[0], x = q[1], y = q[2], z = q[3];
+  qb[0] += 2.f * (-z * mb[1] + y * mb[2] + z * mb[3] - x * mb[5] - y * mb[6] + x * mb[7]);
+  qb[1] += 2.f * (y * mb[1] + z * mb[2] + y * mb[3] - 2.f * x * mb[4] - w * mb[5] + z * mb[6] + w * mb[7] - 2.f * x * mb[8]);
+  qb[2] += 2.f * (-2.f * y * mb[0] + x * mb[1] + w * mb[2] + x * mb[3] + z * mb[5] - w * mb[6] + z * mb[7] - 2.f * y * mb[8]);
+  qb[3] += 2.f * (-2.f * z * mb[0] - w * mb[1] + x * mb[2] + w * mb[3] - 2.f * z * mb[4] + y * mb[5] + x * mb[6] + y * mb[7]);
+}
+// q = p / |p| (qnorm): pbar += (qbar - q (q . qbar)) / |p|
+INL void qnorm_adj(const float* p, const float* qb, float* pb) {
+  float n = sqrtf(p[0] * p[0] + p[1] * p[1] + p[2] * p[2] + p[3] * p[3]);
+  if (n < kMinVal) return;
+  float inv = 1.f / n, q[4] = {p[0] * inv, p[1] * inv, p[2] * inv, p[3] * inv};
+  float d = q[0] * qb[0] + q[1] * qb[1] + q[2] * qb[2] + q[3] * qb[3];
+  for (int i = 0; i < 4; i++) pb[i] += (qb[i] - q[i] * d) * inv;
+}
+// r = m v (row-major 3x3)
+template <class M, class V> INL void mv3_adj(M m, V v, const float* rb, float* mb, float* vb) {
+  for (int i = 0; i < 3; i++)
+    for (int j = 0; j < 3; j++) { mb[3 * i + j] += rb[i] * v[j]; vb[j] += m[3 * i + j] * rb[i]; }
+}
+// u = v / |v| with the forward's norm3 (normalize_with_norm)
+INL void norm3_adj(const float* v, const float* ub, float* vb) {
+  float n = sqrtf(dot3(v, v));
+  float inv = 1.f / (n + (n == 0.f ? 1e-6f : 0.f));
+  float u[3] = {v[0] * inv, v[1] * inv, v[2] * inv};
+  float d = dot3(u, ub);
+  for (int i = 0; i < 3; i++) vb[i] += (ub[i] - u[i] * d) * inv;
+}
+template <class V, class U> INL void cross_motion_adj(V v, U u, const float* rb, float* vb, float* ub) {
+  cross3_adj(v, u, rb, vb, ub);              // r_ang = v_a x u_a
+  cross3_adj(v, u + 3, rb + 3, vb, ub + 3);  // r_lin += v_a x u_l
+  cross3_adj(v + 3, u, rb + 3, vb + 3, ub);  // r_lin += v_l x u_a
+}
+template <class V, class F> INL void cross_force_adj(V v, F f, const float* rb, float* vb, float* fb) {
+  cross3_adj(v, f, rb, vb, fb);                  // r_ang = v_a x f_a
+  cross3_adj(v + 3, f + 3, rb, vb + 3, fb + 3);  //       + v_l x f_l
+  cross3_adj(v, f + 3, rb + 3, vb, fb + 3);      // r_lin = v_a x f_l
+}
+// r = I(i) v (inert_vec): vbar += I rbar (I symmetric), ibar += dr/di . rbar
+template <class I, class V> INL void inert_vec_adj(I i, V v, const float* rb, float* ib, float* vb) {
+  if (vb) {
+    float t[6];
+    inert_vec(t, i, rb);
+    for (int k = 0; k < 6; k++) vb[k] += t[k];
+  }
+  if (ib) {
+    ib[0] += rb[0] * v[0]; ib[1] += rb[1] * v[1]; ib[2] += rb[2] * v[2];
+    ib[3] += rb[0] * v[1] + rb[1] * v[0]; ib[4] += rb[0] * v[2] + rb[2] * v[0]; ib[5] += rb[1] * v[2] + rb[2] * v[1];
+    ib[6] += -rb[1] * v[5] + rb[2] * v[4] + rb[4] * v[2] - rb[5] * v[1];
+    ib[7] += rb[0] * v[5] - rb[2] * v[3] - rb[3] * v[2] + rb[5] * v[0];
+    ib[8] += -rb[0] * v[4] + rb[1] * v[3] + rb[3] * v[1] - rb[4] * v[0];
+    ib[9] += rb[3] * v[3] + rb[4] * v[4] + rb[5] * v[5];
+  }
+}
+// impedance with its derivative d imp / d pos (kbi; power 2 and general power)
+INL float imp_dpos(const CSTA float* solimp, float pos) {
+  float dmin = fminf(fmaxf(solimp[0], kMinImp), kMaxImp);
+  float dmax = fminf(fmaxf(solimp[1], kMinImp), kMaxImp);
+  float width = fmaxf(kMinVal, solimp[2]);
+  float mid = fminf(fmaxf(solimp[3], kMinImp), kMaxImp);
+  float power = fmaxf(1.f, solimp[4]);
+  float x = fabsf(pos) / width;
+  if (x > 1.f) return 0.f;
+  float y, dy;
+  if (power == 2.f) {
+    y = (x < mid) ? (1.f / mid) * x * x : 1.f - (1.f / (1.f - mid)) * (1.f - x) * (1.f - x);
+    dy = (x < mid) ? 2.f * x / mid : 2.f * (1.f - x) / (1.f - mid);
+  } else {
+    y = (x < mid) ? (1.f / powf(mid, power - 1.f)) * powf(x, power)
+                  : 1.f - (1.f / powf(1.f - mid, power - 1.f)) * powf(1.f - x, power);
+    dy = (x < mid) ? power / powf(mid, power - 1.f) * powf(x, power - 1.f)
+                   : power / powf(1.f - mid, power - 1.f) * powf(1.f - x, power - 1.f);
+  }
+  float imp = dmin + y * (dmax - dmin);
+  if (imp < dmin || imp > dmax) return 0.f;
+  return (dmax - dmin) * dy * (pos < 0.f ? -1.f : 1.f) / width;
+}
+
+// ------------------------------------------------------------------- adjoint workspace (LDS)
+template <class DM> struct WSA {
+  static constexpr int NV = DM::NV, LD = DM::LD, NB = DM::NB, NJ = DM::NJ, NG = DM::NG;
+  // forward values kept for the reverse passes
+  float qpos0[MJL_MAXQ], qvel0[LD];    // pre-step state
+  float cvel[NB][6], cacc[NB][6];      // recomputed in the RNE reverse
+  alignas(16) float Lc[NV * LD];       // factor of Hc at the converged active set
+  float invdc[LD];
+  float ap[LD];                        // integrator acceleration a'
+  float lp[NB][3], lq[NB][4];          // body transform in the parent frame
+  float ftmp[NV][6];                   // scratch: f_i = I(crb) cdof_i, then its cotangent
+  // cotangents
+  float qposb[MJL_MAXQ], qvelb[LD], ctrlb[MJL_MAXU], auxb[MJL_AUX_DIM + 3];
+  float frcsb[LD], qaccb[LD], frcactb[LD], mu[LD], rb[LD], vtmp[LD];
+  float xposb[NB][3], xquatb[NB][4], xmatb[NB][9], xiposb[NB][3], scomb[NB][3];
+  float xanchorb[NJ][3], xaxisb[NJ][3], gposb[NG][3], gaxisb[NG][3];
+  float cdofb[NV][6], cinertb[NB][10], crbb[NB][10], cvelb[NB][6], caccb[NB][6], cfrcb[NB][6], cfsubb[NB][6];
+  float Sb[NB][6], Ub[NB][6], Tb[NB][6];
+  alignas(16) float Mb[NV * LD];
+};
+
+// per-env global scratch of the adjoint (after the env's row slab): per row (alpha, gamma, posbar),
+// per contact kConAdjW floats: pos 3, frame 9, dist 1, geom1 (pos, axis) 6, geom2 (pos, axis) 6
+constexpr int kConAdjW = 25;
+__host__ __device__ inline int adj_scratch_floats(int nefc_max, int ncon_max) { return 3 * nefc_max + kConAdjW * ncon_max; }
+
+// wave sum of a 3-vector contribution into LDS dst (lane 0 writes)
+INL void wsum3_into(LDSA float* dst, const float* v, int lane) {
+  float a = wsum(v[0]), b = wsum(v[1]), c = wsum(v[2]);
+  if (lane == 0) { dst[0] += a; dst[1] += b; dst[2] += c; }
+}
+// per-root reduction of lane-held subtree-com cotangents (only roots' scom are read forward)
+template <class D> INL void scom_reduce(MP m, LDSA WSA<D>* A, int root_of_lane, const float* v, int lane) {
+  for (int q = 0; q < m->nroot; q++) {
+    const int r = m->root[q];
+    float t[3] = {0.f, 0.f, 0.f};
+    if (root_of_lane == r) { t[0] = v[0]; t[1] = v[1]; t[2] = v[2]; }
+    wsum3_into(A->scomb[r], t, lane);
+  }
+}
+
+// ------------------------------------------------------------------- env step (envs.py:333-492)
+// Reward, aux' cotangents -> xpos / xquat of pelvis and head, qfrc_actuator, post-step qvel (in
+// A->vtmp), input aux. Mirrors env_post branch for branch.
+template <class D> INL void adj_env(MP m, LDSA WS<D>* W, LDSA WSA<D>* A, CP c, const float* aux, float rb,
+                                    const float* auxb_o, int lane) {
+  const float dt = m->timestep;
+  const float nj = (float)(m->nv - 6);
+  if (lane >= 6 && lane < m->nv) {  // energy = ec mean|f v| + sc mean f^2 (reward has -energy)
+    const float f = W->frc_act[lane], v = W->qvel[lane], sg = (f * v < 0.f) ? -1.f : 1.f;
+    A->frcactb[lane] += -rb * (c->electricity_cost / nj * sg * v + c->stall_torque_cost / nj * 2.f * f);
+    A->vtmp[lane] += -rb * c->electricity_cost / nj * sg * f;
+  }
+  if (lane == 0) {
+    LDSA float* hp = W->xpos[c->head_body_id];
+    LDSA float* bp = W->xpos[c->pelvis_body_id];
+    LDSA float* bpb = A->xposb[c->pelvis_body_id];
+    LDSA float* hpb = A->xposb[c->head_body_id];
+    float tx = aux[1], ty = aux[2];
+    const float db = xydist(tx, ty, bp), dh = xydist(tx, ty, hp);
+    const float dist = fmaxf(db, dh);
+    const bool close = dist < c->target_threshold;
+    const float cc = close ? aux[4] + 1.f : 0.f;
+    const bool adv = cc >= (float)c->stop_frames;
+    const float tx2 = adv ? bp[0] + c->target_dist : tx, ty2 = adv ? bp[1] : ty;
+    const float time = W->sc[SC_TIME];
+    const float new_st = stance_of(c, W->sens);
+    const bool changed = new_st != aux[5];
+    (void)time;
+    // aux' = {flip, tx2, ty2, tz2, cc', st', st_time', -dist2/dt, ep}
+    A->auxb[0] += auxb_o[0];
+    if (adv) { bpb[0] += auxb_o[1]; bpb[1] += auxb_o[2]; bpb[2] += auxb_o[3]; }
+    else { A->auxb[1] += auxb_o[1]; A->auxb[2] += auxb_o[2]; A->auxb[3] += auxb_o[3]; }
+    if (close && !adv) A->auxb[4] += auxb_o[4];
+    if (!changed) { A->auxb[5] += auxb_o[5]; A->auxb[6] += auxb_o[6]; }
+    A->auxb[8] += auxb_o[8];
+    // d(dist2) from aux'[7] = -dist2 / dt
+    float d2b = -auxb_o[7] / dt;
+    {
+      const float e_b = xydist(tx2, ty2, bp), e_h = xydist(tx2, ty2, hp);
+      const bool pel = e_b >= e_h;
+      LDSA float* p = pel ? bp : hp;
+      LDSA float* pb = pel ? bpb : hpb;
+      const float e = pel ? e_b : e_h;
+      if (e > 0.f) {
+        const float gx = d2b * (p[0] - tx2) / e, gy = d2b * (p[1] - ty2) / e;
+        pb[0] += gx; pb[1] += gy;
+        if (adv) { bpb[0] -= gx; bpb[1] -= gy; }  // tx2 = bp[0] + const, ty2 = bp[1]
+        else { A->auxb[1] -= gx; A->auxb[2] -= gy; }
+      }
+    }
+    // progress = (-dist/dt - aux[7]) * w
+    const float w = c->progress_weight;
+    A->auxb[7] += -w * rb;
+    const float distb = -w / dt * rb;
+    {
+      const bool pel = db >= dh;
+      LDSA float* p = pel ? bp : hp;
+      LDSA float* pb = pel ? bpb : hpb;
+      const float e = pel ? db : dh;
+      if (e > 0.f) {
+        const float gx = distb * (p[0] - tx) / e, gy = distb * (p[1] - ty) / e;
+        pb[0] += gx; pb[1] += gy;
+        A->auxb[1] -= gx; A->auxb[2] -= gy;
+      }
+    }
+    // posture = wp (|pitch| outside (-0.087, 0.174) + |roll| outside (-0.174, 0.174))
+    if (c->posture_penalty_weight != 0.f) {
+      LDSA float* q = W->xquat[c->pelvis_body_id];
+      LDSA float* qb = A->xquatb[c->pelvis_body_id];
+      const float qw = q[0], qx = q[1], qy = q[2], qz = q[3];
+      float roll, pitch, yaw;
+      rpy(q, roll, pitch, yaw);
+      const float wp = -rb * c->posture_penalty_weight;
+      const float pitchb = ((pitch > -0.087f) && (pitch < 0.174f)) ? 0.f : wp * (pitch < 0.f ? -1.f : 1.f);
+      const float rollb = ((roll > -0.174f) && (roll < 0.174f)) ? 0.f : wp * (roll < 0.f ? -1.f : 1.f);
+      const float sp = 2.f * (qw * qy - qz * qx);
+      if (sp > -1.f && sp < 1.f) {
+        const float spb = pitchb / sqrtf(1.f - sp * sp);
+        qb[0] += 2.f * qy * spb; qb[2] += 2.f * qw * spb; qb[3] -= 2.f * qx * spb; qb[1] -= 2.f * qz * spb;
+      }
+      const float ra = 2.f * (qw * qx + qy * qz), rbb = 1.f - 2.f * (qx * qx + qy * qy), den = ra * ra + rbb * rbb;
+      if (den > 0.f) {
+        const float ab = rollb * rbb / den, bb = -rollb * ra / den;
+        qb[0] += 2.f * qx * ab; qb[1] += 2.f * qw * ab; qb[2] += 2.f * qz * ab; qb[3] += 2.f * qy * ab;
+        qb[1] += -4.f * qx * bb; qb[2] += -4.f * qy * bb;
+      }
+    }
+  }
+  SYNC();
+}
+
+// ------------------------------------------------------------------- integration (forward.py)
+// in: A->vtmp = cotangent of qvel', gq = cotangent of qpos' (global). out: A->qposb, A->qvelb,
+// A->qaccb, A->Mb (implicit / eulerdamp matrix path).
+template <class D> INL void adj_integrate(MP m, LDSA WS<D>* W, LDSA WSA<D>* A, const float* gq, int lane) {
+  constexpr int LD = D::LD;
+  const int nv = m->nv;
+  const float dt = m->timestep;
+  if (lane < m->njnt) {
+    const JntRec jr = ldrec(&m->jrec[lane]);
+    const int q = jr.qadr, d = jr.dofadr;
+    if (jr.isfree) {
+      for (int i = 0; i < 3; i++) { A->qposb[q + i] += gq[q + i]; A->vtmp[d + i] += dt * gq[q + i]; }
+      // quat' = normalize(q0 (x) qr), qr = (cos th, w^ sin th), th = |w| dt / 2, w = qvel'[3:6]
+      float w[3] = {W->qvel[d + 3], W->qvel[d + 4], W->qvel[d + 5]};
+      float wn[3] = {w[0], w[1], w[2]};
+      const float nrm = norm3(wn);
+      float s, cth;
+      sincosf(0.5f * nrm * dt, &s, &cth);
+      const float qr[4] = {cth, wn[0] * s, wn[1] * s, wn[2] * s};
+      const float q0[4] = {A->qpos0[q + 3], A->qpos0[q + 4], A->qpos0[q + 5], A->qpos0[q + 6]};
+      float pq[4];
+      qmul(pq, q0, qr);
+      const float qb[4] = {gq[q + 3], gq[q + 4], gq[q + 5], gq[q + 6]};
+      float pb[4] = {0.f, 0.f, 0.f, 0.f}, q0b[4] = {0.f, 0.f, 0.f, 0.f}, qrb[4] = {0.f, 0.f, 0.f, 0.f};
+      qnorm_adj(pq, qb, pb);
+      qmul_adj(q0, qr, pb, q0b, qrb);
+      for (int i = 0; i < 4; i++) A->qposb[q + 3 + i] += q0b[i];
+      const float thb = -s * qrb[0] + cth * (wn[0] * qrb[1] + wn[1] * qrb[2] + wn[2] * qrb[3]);
+      const float wnb[3] = {s * qrb[1], s * qrb[2], s * qrb[3]};
+      float wb[3] = {0.f, 0.f, 0.f};
+      norm3_adj(w, wnb, wb);
+      if (nrm > 0.f) { const float nb = 0.5f * dt * thb / nrm; wb[0] += nb * w[0]; wb[1] += nb * w[1]; wb[2] += nb * w[2]; }
+      for (int i = 0; i < 3; i++) A->vtmp[d + 3 + i] += wb[i];
+    } else {
+      A->qposb[q] += gq[q];
+      A->vtmp[d] += dt * gq[q];
+    }
+  }
+  SYNC();
+  // qvel' = qvel + dt a'
+  float apb = 0.f;
+  if (lane < nv) { A->qvelb[lane] += A->vtmp[lane]; apb = dt * A->vtmp[lane]; }
+  const bool damp = (m->integrator == MJL_INT_IMPLICITFAST || m->eulerdamp) && m->any_damping;
+  if (damp) {  // a' = Hd^-1 (M qacc), Hd = M + dt diag(damping), factor in W->H
+    if (lane < LD) A->rb[lane] = (lane < nv) ? apb : 0.f;
+    SYNC();
+    const float r = chol_solve<D>(W->H, W->invd, lane < nv ? A->rb[lane] : 0.f, lane);
+    SYNC();
+    if (lane < LD) A->rb[lane] = (lane < nv) ? r : 0.f;
+    SYNC();
+    if (lane < nv) {
+      const float rl = A->rb[lane];
+      for (int k = 0; k < nv; k++) A->Mb[lane * LD + k] += rl * (W->qacc[k] - A->ap[k]);
+      A->qaccb[lane] += mrow<D>(W, A->rb, lane);
+    }
+  } else if (lane < nv) {
+    A->qaccb[lane] += apb;
+  }
+  SYNC();
+}
+
+// ------------------------------------------------------------------- constraint solve + rows
+// Implicit derivative at the converged active set; per row alpha (J-bar coefficient of qvel),
+// gamma (of qacc; the coefficient of mu is the row force), posbar -> global scratch.
+template <class D> INL void adj_solver_rows(MP m, LDSA WS<D>* W, LDSA WSA<D>* A, Rows<true> R, GLBA float* scr,
+                                            int nefc_max, int lane) {
+  constexpr int LD = D::LD;
+  const int nv = m->nv, nefc = W->nefc;
+  GLBA float* alpha = scr;
+  GLBA float* gamma = scr + nefc_max;
+  GLBA float* posb = scr + 2 * nefc_max;
+  const float mu = chol_solve<D>(A->Lc, A->invdc, lane < nv ? A->qaccb[lane] : 0.f, lane);
+  if (lane < LD) A->mu[lane] = (lane < nv) ? mu : 0.f;
+  SYNC();
+  if (lane < nv) {
+    A->frcsb[lane] += A->mu[lane];
+    const float ml = A->mu[lane];
+    for (int k = 0; k < nv; k++) A->Mb[lane * LD + k] -= ml * W->qacc[k];
+  }
+  for (int r = lane; r < nefc; r += 64) {
+    const int meta = R.emeta[r], type = meta >> 16, id = meta & 0xffff;
+    const float jar = R.jar[r], Dr = R.D[r];
+    const bool act = jar < 0.f;
+    float jm = 0.f;
+    for (int k = 0; k < LD; k++) jm += R.J[r * LD + k] * A->mu[k];
+    const float arefb = act ? Dr * jm : 0.f;
+    const float Db = act ? -jm * jar : 0.f;
+    const CSTA float *sr, *si;
+    if (type == 0) { sr = m->jnt_solref[id]; si = m->jnt_solimp[id]; }
+    else if (type == 1) { sr = m->tendon_solref[id]; si = m->tendon_solimp[id]; }
+    else { sr = m->pair_solref[id]; si = m->pair_solimp[id]; }
+    float k, b, imp;
+    const float pos = R.epos[r];
+    kbi(m->timestep, sr, si, pos, k, b, imp);
+    const float invw = R.einvw[r];
+    const float rr = invw * (1.f - imp) / imp;
+    const float dDdimp = (rr > kMinVal) ? 1.f / (invw * (1.f - imp) * (1.f - imp)) : 0.f;
+    const float impb = -k * pos * arefb + Db * dDdimp;
+    alpha[r] = -b * arefb;
+    gamma[r] = act ? -Dr * jm : 0.f;
+    posb[r] = -k * imp * arefb + impb * imp_dpos(si, pos);
+  }
+  SYNC();
+  if (lane < nv) {  // qvel-bar += sum_r alpha_r J_r  (aref depends on J qvel)
+    float s = 0.f;
+    for (int r = 0; r < nefc; r++) s += alpha[r] * R.J[r * LD + lane];
+    A->qvelb[lane] += s;
+  }
+  if (lane == 0) {  // limit rows: pos = min(q - lo, hi - q) - margin (serial: tendons may share joints)
+    for (int r = 0; r < W->nlim; r++) {
+      const int meta = R.emeta[r], type = meta >> 16, id = meta & 0xffff;
+      const float pb = posb[r];
+      if (type == 0) {
+        const int qa = m->jnt_qposadr[id];
+        const float q = A->qpos0[qa];
+        const float sg = (q - m->jnt_range[id][0] < m->jnt_range[id][1] - q) ? 1.f : -1.f;
+        A->qposb[qa] += sg * pb;
+      } else {
+        const float len = W->tenlen[id];
+        const float sg = (len - m->tendon_range[id][0] < m->tendon_range[id][1] - len) ? 1.f : -1.f;
+        for (int w = 0; w < m->tendon_num[id]; w++) A->qposb[m->tendon_qadr[id][w]] += sg * m->tendon_coef[id][w] * pb;
+      }
+    }
+  }
+  SYNC();
+}
+
+// ------------------------------------------------------------------- contact Jacobians
+// J rows of contact c from Jp_d = s_d (cdof_lin_d + cdof_ang_d x (pos - scom_root)); lanes 0..31 =
+// dof. Accumulates cdof-bar (lane-owned), scom-bar (per root), and the contact's pos / frame /
+// dist cotangents into the scratch record.
+template <class D> INL void adj_contact_jac(MP m, LDSA WS<D>* W, LDSA WSA<D>* A, Rows<true> R, GLBA float* scr,
+                                            int nefc_max, int lane) {
+  constexpr int LD = D::LD;
+  const int nv = m->nv, ncon = W->ncon;
+  GLBA float* alpha = scr;
+  GLBA float* gamma = scr + nefc_max;
+  GLBA float* posb = scr + 2 * nefc_max;
+  GLBA float* conb = scr + 3 * nefc_max;
+  const int d = lane;
+  const bool isd = lane < nv;
+  const int root = isd ? ldrec(&m->drec[d]).rootid : 0;
+  float scb[3] = {0.f, 0.f, 0.f};
+  for (int c = 0; c < ncon; c++) {
+    GLBA float* cr = R.con + c * CONW;
+    const int packed = __float_as_int(cr[15]), dim = (packed >> 16) & 0xff;
+    const uint32_t mask1 = __float_as_uint(cr[12]), mask2 = __float_as_uint(cr[13]);
+    const float muf = cr[14];
+    const int r0 = R.con_efc[c], nrow = dim == 1 ? 1 : 4;
+    float jn = 0.f, jt1 = 0.f, jt2 = 0.f, pb = 0.f;
+    if (isd) {
+      const float qv = A->qvel0[d], mu = A->mu[d], qa = W->qacc[d];
+      float Jb[4];
+      for (int q = 0; q < nrow; q++) {
+        const int r = r0 + q;
+        Jb[q] = alpha[r] * qv + R.force[r] * mu + gamma[r] * qa;
+      }
+      if (dim == 1) jn = Jb[0];
+      else { jn = Jb[0] + Jb[1] + Jb[2] + Jb[3]; jt1 = muf * (Jb[0] - Jb[1]); jt2 = muf * (Jb[2] - Jb[3]); }
+    }
+    if (lane < nrow) pb = posb[r0 + lane];
+    const float distb = wsum(pb);
+    float nb[3] = {0.f, 0.f, 0.f}, t1b[3] = {0.f, 0.f, 0.f}, t2b[3] = {0.f, 0.f, 0.f}, offb[3] = {0.f, 0.f, 0.f};
+    const float s = isd ? (float)((mask2 >> d) & 1u) - (float)((mask1 >> d) & 1u) : 0.f;
+    if (s != 0.f) {
+      const float cd[6] = {W->cdof[d][0], W->cdof[d][1], W->cdof[d][2], W->cdof[d][3], W->cdof[d][4], W->cdof[d][5]};
+      const float off[3] = {cr[0] - W->scom[root][0], cr[1] - W->scom[root][1], cr[2] - W->scom[root][2]};
+      float cx[3];
+      cross3(cx, cd, off);
+      const float jp[3] = {s * (cd[3] + cx[0]), s * (cd[4] + cx[1]), s * (cd[5] + cx[2])};
+      for (int i = 0; i < 3; i++) { nb[i] = jn * jp[i]; t1b[i] = jt1 * jp[i]; t2b[i] = jt2 * jp[i]; }
+      float jpb[3];
+      for (int i = 0; i < 3; i++) jpb[i] = jn * cr[3 + i] + jt1 * cr[6 + i] + jt2 * cr[9 + i];
+      // jp = s (lin + ang x off)
+      for (int i = 0; i < 3; i++) A->cdofb[d][3 + i] += s * jpb[i];
+      const float sjpb[3] = {s * jpb[0], s * jpb[1], s * jpb[2]};
+      float angb[3] = {0.f, 0.f, 0.f};
+      cross3_adj(cd, off, sjpb, angb, offb);
+      for (int i = 0; i < 3; i++) { A->cdofb[d][i] += angb[i]; scb[i] -= offb[i]; }
+    }
+    float v[13];
+    for (int i = 0; i < 3; i++) { v[i] = wsum(offb[i]); v[3 + i] = wsum(nb[i]); v[6 + i] = wsum(t1b[i]); v[9 + i] = wsum(t2b[i]); }
+    v[12] = distb;
+    if (lane < 13) conb[c * kConAdjW + lane] = v[lane];
+  }
+  scom_reduce<D>(m, A, isd ? root : -1, scb, lane);
+  SYNC();
+}
+
+// ------------------------------------------------------------------- collision (collide())
+// frame rows: n, t1, t2. In: dist / pos / frame cotangents; out: cotangents of the geoms' centre
+// and z axis. Each branch recomputes the forward's intermediate values with the same operations.
+INL void make_frame_adj(const float* a_in, const float* fb, float* a_inb) {
+  float a[3] = {a_in[0], a_in[1], a_in[2]};
+  norm3(a);
+  float b0[3] = {0.f, 0.f, 0.f};
+  if (a[1] > -0.5f && a[1] < 0.5f) b0[1] = 1.f; else b0[2] = 1.f;
+  const float ab = dot3(a, b0);
+  float braw[3] = {b0[0] - a[0] * ab, b0[1] - a[1] * ab, b0[2] - a[2] * ab};
+  float b[3] = {braw[0], braw[1], braw[2]};
+  norm3(b);
+  float abar[3] = {fb[0], fb[1], fb[2]}, bbar[3] = {fb[3], fb[4], fb[5]};
+  cross3_adj(a, b, fb + 6, abar, bbar);
+  float brawb[3] = {0.f, 0.f, 0.f};
+  norm3_adj(braw, bbar, brawb);
+  const float abb = -dot3(a, brawb);
+  for (int i = 0; i < 3; i++) abar[i] += -ab * brawb[i] + abb * b0[i];
+  norm3_adj(a_in, abar, a_inb);
+}
+// seg_point(r, a, b, pt) adjoint
+INL void seg_point_adj(const float* a, const float* b, const float* pt, const float* rb, float* ab_, float* bb_,
+                       float* ptb) {
+  const float ab[3] = {b[0] - a[0], b[1] - a[1], b[2] - a[2]};
+  const float ap[3] = {pt[0] - a[0], pt[1] - a[1], pt[2] - a[2]};
+  const float num = dot3(ap, ab), den = dot3(ab, ab) + 1e-6f;
+  const float t0 = num / den, t = fminf(fmaxf(t0, 0.f), 1.f);
+  float abb[3] = {t * rb[0], t * rb[1], t * rb[2]};
+  for (int i = 0; i < 3; i++) ab_[i] += rb[i];
+  const float tb = dot3(rb, ab);
+  if (t0 > 0.f && t0 < 1.f) {
+    const float numb = tb / den, denb = -tb * num / (den * den);
+    for (int i = 0; i < 3; i++) {
+      const float apb = numb * ab[i];
+      abb[i] += numb * ap[i] + 2.f * denb * ab[i];
+      ptb[i] += apb; ab_[i] -= apb;
+    }
+  }
+  for (int i = 0; i < 3; i++) { bb_[i] += abb[i]; ab_[i] -= abb[i]; }
+}
+template <class D> INL void collide_adj(const PairRec& pr, LDSA WS<D>* W, int k, float distb, const float* posb,
+                                        const float* frb, float* x1b, float* z1b, float* x2b, float* z2b) {
+  const int kind = pr.kind, g1 = pr.g1, g2 = pr.g2;
+  const float x1[3] = {W->gpos[g1][0], W->gpos[g1][1], W->gpos[g1][2]};
+  const float x2[3] = {W->gpos[g2][0], W->gpos[g2][1], W->gpos[g2][2]};
+  const float z1[3] = {W->gaxis[g1][0], W->gaxis[g1][1], W->gaxis[g1][2]};
+  const float z2[3] = {W->gaxis[g2][0], W->gaxis[g2][1], W->gaxis[g2][2]};
+  const float r1 = pr.r1, r2 = pr.r2, h1 = pr.h1, h2 = pr.h2;
+  if (kind == MJL_COL_PLANE_SPHERE) {
+    const float d[3] = {x2[0] - x1[0], x2[1] - x1[1], x2[2] - x1[2]};
+    const float dist = dot3(d, z1) - r2, s = r2 + 0.5f * dist;
+    for (int i = 0; i < 3; i++) { x2b[i] += posb[i]; z1b[i] -= s * posb[i]; }
+    distb += 0.5f * -dot3(z1, posb);
+    for (int i = 0; i < 3; i++) { z1b[i] += distb * d[i]; x2b[i] += distb * z1[i]; x1b[i] -= distb * z1[i]; }
+    make_frame_adj(z1, frb, z1b);
+    return;
+  }
+  if (kind == MJL_COL_PLANE_CAPSULE) {
+    const float* n = z1;
+    const float nd = dot3(n, z2);
+    const float braw[3] = {z2[0] - n[0] * nd, z2[1] - n[1] * nd, z2[2] - n[2] * nd};
+    float b[3] = {braw[0], braw[1], braw[2]};
+    const float bn = norm3(b);
+    if (bn < 0.5f) { b[0] = 0.f; b[1] = 0.f; b[2] = 0.f; if (n[1] > -0.5f && n[1] < 0.5f) b[1] = 1.f; else b[2] = 1.f; }
+    const float sg = (k == 0) ? 1.f : -1.f;
+    const float sp[3] = {x2[0] + sg * z2[0] * h2, x2[1] + sg * z2[1] * h2, x2[2] + sg * z2[2] * h2};
+    const float d[3] = {sp[0] - x1[0], sp[1] - x1[1], sp[2] - x1[2]};
+    const float dist = dot3(d, n) - r2, s = r2 + 0.5f * dist;
+    float nb[3] = {frb[0], frb[1], frb[2]}, bb[3] = {frb[3], frb[4], frb[5]}, spb[3];
+    for (int i = 0; i < 3; i++) { spb[i] = posb[i]; nb[i] -= s * posb[i]; }
+    distb += 0.5f * -dot3(n, posb);
+    for (int i = 0; i < 3; i++) { spb[i] += distb * n[i]; x1b[i] -= distb * n[i]; nb[i] += distb * d[i]; }
+    cross3_adj(n, b, frb + 6, nb, bb);
+    if (bn >= 0.5f) {
+      float brb[3] = {0.f, 0.f, 0.f};
+      norm3_adj(braw, bb, brb);
+      const float ndb = -dot3(n, brb);
+      for (int i = 0; i < 3; i++) { z2b[i] += brb[i] + ndb * n[i]; nb[i] += -nd * brb[i] + ndb * z2[i]; }
+    }
+    for (int i = 0; i < 3; i++) { x2b[i] += spb[i]; z2b[i] += sg * h2 * spb[i]; z1b[i] += nb[i]; }
+    return;
+  }
+  // closest points pa (on geom 1), pb (on geom 2), then sph_sph + make_frame
+  float pa[3], pb[3];
+  // forward intermediates of the capsule-capsule branch (kept for its adjoint)
+  float a0[3], a1[3], b0[3], b1[3], dar[3], dbr[3], da[3], db[3], am[3], bm[3], tr[3];
+  float la = 0.f, lb = 0.f, ha = 0.f, hb = 0.f, dadb = 0.f, datr = 0.f, dbtr = 0.f, den = 0.f, ta0 = 0.f, tb0 = 0.f;
+  float ta = 0.f, tb = 0.f, pa0[3], pb0[3];
+  bool use_na = false;
+  if (kind == MJL_COL_SPHERE_SPHERE) {
+    for (int i = 0; i < 3; i++) { pa[i] = x1[i]; pb[i] = x2[i]; }
+  } else if (kind == MJL_COL_SPHERE_CAPSULE) {
+    const float a[3] = {x2[0] - z2[0] * h2, x2[1] - z2[1] * h2, x2[2] - z2[2] * h2};
+    const float bbv[3] = {x2[0] + z2[0] * h2, x2[1] + z2[1] * h2, x2[2] + z2[2] * h2};
+    for (int i = 0; i < 3; i++) pa[i] = x1[i];
+    seg_point(pb, a, bbv, x1);
+  } else {
+    for (int i = 0; i < 3; i++) {
+      a0[i] = x1[i] - z1[i] * h1; a1[i] = x1[i] + z1[i] * h1;
+      b0[i] = x2[i] - z2[i] * h2; b1[i] = x2[i] + z2[i] * h2;
+      dar[i] = a1[i] - a0[i]; dbr[i] = b1[i] - b0[i]; da[i] = dar[i]; db[i] = dbr[i];
+    }
+    la = norm3(da); lb = norm3(db);
+    ha = la * 0.5f; hb = lb * 0.5f;
+    for (int i = 0; i < 3; i++) { am[i] = a0[i] + da[i] * ha; bm[i] = b0[i] + db[i] * hb; tr[i] = am[i] - bm[i]; }
+    dadb = dot3(da, db); datr = dot3(da, tr); dbtr = dot3(db, tr);
+    den = 1.f - dadb * dadb;
+    ta0 = (-datr + dadb * dbtr) / (den + 1e-6f);
+    tb0 = dbtr + ta0 * dadb;
+    ta = fminf(fmaxf(ta0, -ha), ha); tb = fminf(fmaxf(tb0, -hb), hb);
+    for (int i = 0; i < 3; i++) { pa0[i] = am[i] + da[i] * ta; pb0[i] = bm[i] + db[i] * tb; }
+    float na[3], nb2[3];
+    seg_point(na, a0, a1, pb0);
+    seg_point(nb2, b0, b1, pa0);
+    float d1 = 0.f, d2 = 0.f;
+    for (int i = 0; i < 3; i++) { d1 += (pb0[i] - na[i]) * (pb0[i] - na[i]); d2 += (pa0[i] - nb2[i]) * (pa0[i] - nb2[i]); }
+    use_na = d1 < d2;
+    for (int i = 0; i < 3; i++) { pa[i] = use_na ? na[i] : pa0[i]; pb[i] = use_na ? pb0[i] : nb2[i]; }
+  }
+  // sph_sph + make_frame adjoint -> pa-bar, pb-bar
+  float nraw[3] = {pb[0] - pa[0], pb[1] - pa[1], pb[2] - pa[2]}, n[3] = {nraw[0], nraw[1], nraw[2]};
+  const float nrm = norm3(n);
+  const float dist = nrm - (r1 + r2), s = r1 + dist * 0.5f;
+  (void)dist;
+  float nb[3] = {0.f, 0.f, 0.f}, pab[3] = {0.f, 0.f, 0.f}, pbb[3] = {0.f, 0.f, 0.f};
+  make_frame_adj(n, frb, nb);
+  for (int i = 0; i < 3; i++) { pab[i] += posb[i]; nb[i] += s * posb[i]; }
+  distb += 0.5f * dot3(n, posb);
+  float nrb[3] = {0.f, 0.f, 0.f};
+  norm3_adj(nraw, nb, nrb);
+  for (int i = 0; i < 3; i++) { nrb[i] += distb * n[i]; pbb[i] += nrb[i]; pab[i] -= nrb[i]; }
+  if (kind == MJL_COL_SPHERE_SPHERE) {
+    for (int i = 0; i < 3; i++) { x1b[i] += pab[i]; x2b[i] += pbb[i]; }
+    return;
+  }
+  if (kind == MJL_COL_SPHERE_CAPSULE) {
+    const float a[3] = {x2[0] - z2[0] * h2, x2[1] - z2[1] * h2, x2[2] - z2[2] * h2};
+    const float bbv[3] = {x2[0] + z2[0] * h2, x2[1] + z2[1] * h2, x2[2] + z2[2] * h2};
+    float aB[3] = {0.f, 0.f, 0.f}, bB[3] = {0.f, 0.f, 0.f};
+    for (int i = 0; i < 3; i++) x1b[i] += pab[i];
+    seg_point_adj(a, bbv, x1, pbb, aB, bB, x1b);
+    for (int i = 0; i < 3; i++) { x2b[i] += aB[i] + bB[i]; z2b[i] += h2 * (bB[i] - aB[i]); }
+    return;
+  }
+  // capsule-capsule (math.closest_segment_to_segment_points)
+  float a0b[3] = {0.f, 0.f, 0.f}, a1b[3] = {0.f, 0.f, 0.f}, b0b[3] = {0.f, 0.f, 0.f}, b1b[3] = {0.f, 0.f, 0.f};
+  float pa0b[3] = {0.f, 0.f, 0.f}, pb0b[3] = {0.f, 0.f, 0.f};
+  if (use_na) {  // pa = seg_point(a0, a1, pb0), pb = pb0
+    seg_point_adj(a0, a1, pb0, pab, a0b, a1b, pb0b);
+    for (int i = 0; i < 3; i++) pb0b[i] += pbb[i];
+  } else {       // pb = seg_point(b0, b1, pa0), pa = pa0
+    seg_point_adj(b0, b1, pa0, pbb, b0b, b1b, pa0b);
+    for (int i = 0; i < 3; i++) pa0b[i] += pab[i];
+  }
+  float amb[3], bmb[3], dab[3], dbb[3];
+  for (int i = 0; i < 3; i++) { amb[i] = pa0b[i]; dab[i] = ta * pa0b[i]; bmb[i] = pb0b[i]; dbb[i] = tb * pb0b[i]; }
+  float tab = dot3(da, pa0b), tbb = dot3(db, pb0b), hab = 0.f, hbb = 0.f;
+  float tb0b = 0.f, ta0b = 0.f;
+  if (tb0 > -hb && tb0 < hb) tb0b = tbb; else hbb += (tb0 >= hb ? 1.f : -1.f) * tbb;
+  if (ta0 > -ha && ta0 < ha) ta0b = tab; else hab += (ta0 >= ha ? 1.f : -1.f) * tab;
+  float dbtrb = tb0b, dadbb = tb0b * ta0;
+  ta0b += tb0b * dadb;
+  const float Q = den + 1e-6f, Nb = ta0b / Q, Qb = -ta0b * ta0 / Q;
+  float datrb = -Nb;
+  dadbb += Nb * dbtr;
+  dbtrb += Nb * dadb;
+  dadbb += -2.f * dadb * Qb;
+  float trb[3];
+  for (int i = 0; i < 3; i++) {
+    dab[i] += dadbb * db[i] + datrb * tr[i];
+    dbb[i] += dadbb * da[i] + dbtrb * tr[i];
+    trb[i] = datrb * da[i] + dbtrb * db[i];
+    amb[i] += trb[i]; bmb[i] -= trb[i];
+  }
+  for (int i = 0; i < 3; i++) { a0b[i] += amb[i]; dab[i] += ha * amb[i]; b0b[i] += bmb[i]; dbb[i] += hb * bmb[i]; }
+  hab += dot3(da, amb); hbb += dot3(db, bmb);
+  const float lab = 0.5f * hab, lbb = 0.5f * hbb;
+  float darb[3] = {0.f, 0.f, 0.f}, dbrb[3] = {0.f, 0.f, 0.f};
+  norm3_adj(dar, dab, darb);
+  norm3_adj(dbr, dbb, dbrb);
+  for (int i = 0; i < 3; i++) {
+    darb[i] += lab * da[i]; dbrb[i] += lbb * db[i];
+    a1b[i] += darb[i]; a0b[i] -= darb[i]; b1b[i] += dbrb[i]; b0b[i] -= dbrb[i];
+    x1b[i] += a0b[i] + a1b[i]; z1b[i] += h1 * (a1b[i] - a0b[i]);
+    x2b[i] += b0b[i] + b1b[i]; z2b[i] += h2 * (b1b[i] - b0b[i]);
+  }
+}
+
+// lane = contact: geometry cotangents into the scratch record; then lane = geom gathers them
+template <class D> INL void adj_collision(MP m, LDSA WS<D>* W, LDSA WSA<D>* A, Rows<true> R, GLBA float* scr,
+                                          int nefc_max, int lane) {
+  const int ncon = W->ncon;
+  GLBA float* conb = scr + 3 * nefc_max;
+  for (int c = lane; c < ncon; c += 64) {
+    GLBA float* cb = conb + c * kConAdjW;
+    const int p = R.con_pair[c];
+    const int k = (__float_as_int(R.con[c * CONW + 15]) >> 24) & 0xff;
+    const PairRec pr = ldrec(&m->prec[p]);
+    float posb[3] = {cb[0], cb[1], cb[2]}, frb[9];
+    for (int i = 0; i < 9; i++) frb[i] = cb[3 + i];
+    float x1b[3] = {0.f, 0.f, 0.f}, z1b[3] = {0.f, 0.f, 0.f}, x2b[3] = {0.f, 0.f, 0.f}, z2b[3] = {0.f, 0.f, 0.f};
+    collide_adj<D>(pr, W, k, cb[12], posb, frb, x1b, z1b, x2b, z2b);
+    for (int i = 0; i < 3; i++) { cb[13 + i] = x1b[i]; cb[16 + i] = z1b[i]; cb[19 + i] = x2b[i]; cb[22 + i] = z2b[i]; }
+  }
+  SYNC();
+  if (lane < m->ngeom) {
+    float gp[3] = {0.f, 0.f, 0.f}, ga[3] = {0.f, 0.f, 0.f};
+    for (int c = 0; c < ncon; c++) {
+      const PairRec pr = ldrec(&m->prec[R.con_pair[c]]);
+      GLBA float* cb = conb + c * kConAdjW;
+      if (pr.g1 == lane) for (int i = 0; i < 3; i++) { gp[i] += cb[13 + i]; ga[i] += cb[16 + i]; }
+      if (pr.g2 == lane) for (int i = 0; i < 3; i++) { gp[i] += cb[19 + i]; ga[i] += cb[22 + i]; }
+    }
+    for (int i = 0; i < 3; i++) { A->gposb[lane][i] += gp[i]; A->gaxisb[lane][i] += ga[i]; }
+  }
+  SYNC();
+}
+
+// geom frames (kinematics): gpos = xpos_b + xmat_b geom_pos, gaxis = xmat_b zaxis; lane = body
+template <class D> INL void adj_geom_frames(MP m, LDSA WSA<D>* A, int lane) {
+  if (lane > 0 && lane < m->nbody) {
+    for (int g = 0; g < m->ngeom; g++) {
+      if (m->geom_bodyid[g] != lane) continue;
+      for (int i = 0; i < 3; i++) {
+        const float pb = A->gposb[g][i], ab = A->gaxisb[g][i];
+        A->xposb[lane][i] += pb;
+        for (int j = 0; j < 3; j++) A->xmatb[lane][3 * i + j] += pb * m->geom_pos[g][j] + ab * m->geom_zaxis[g][j];
+      }
+    }
+  }
+  SYNC();
+}
+
+// qfrc_smooth = passive - bias + actuator: passive and actuation adjoints; bias-bar -> A->vtmp
+template <class D> INL void adj_forces(MP m, LDSA WS<D>* W, LDSA WSA<D>* A, int lane) {
+  const int nv = m->nv;
+  if (lane < nv) {
+    const DofRec dr = ldrec(&m->drec[lane]);
+    const float fs = A->frcsb[lane];
+    A->vtmp[lane] = -fs;
+    A->frcactb[lane] += fs;
+    A->qvelb[lane] += -dr.damping * fs;
+    if (dr.qadr_spring >= 0) A->qposb[dr.qadr_spring] += -dr.stiffness * fs;
+  }
+  SYNC();
+  if (lane < m->nu) {
+    const float c = W->ctrl[lane];
+    const bool inside = !m->actuator_ctrllimited[lane] ||
+                        (c > m->actuator_ctrlrange[lane][0] && c < m->actuator_ctrlrange[lane][1]);
+    A->ctrlb[lane] += inside ? m->actuator_gear[lane] * A->frcactb[m->actuator_dof[lane]] : 0.f;
+  }
+  SYNC();
+}
+
+// per-body velocity terms (velocity_stage): S, U, T from cdof and qvel
+template <class D> INL void body_vel_terms(LDSA WS<D>* W, const LDSA float* qvel, const BodyRec& br, float* S,
+                                           float* U, float* T) {
+  for (int i = 0; i < 6; i++) { S[i] = 0.f; U[i] = 0.f; T[i] = 0.f; }
+  const int da = br.dofadr, dn = br.dofnum;
+  if (br.isfree) {
+    for (int k = 0; k < 3; k++)
+      for (int i = 0; i < 6; i++) S[i] += W->cdof[da + k][i] * qvel[da + k];
+    for (int k = 3; k < 6; k++)
+      for (int i = 0; i < 6; i++) U[i] += W->cdof[da + k][i] * qvel[da + k];
+    cross_motion(T, S, U);
+    for (int i = 0; i < 6; i++) S[i] += U[i];
+  } else {
+    for (int k = 0; k < dn; k++) {
+      float v[6], x[6];
+      for (int i = 0; i < 6; i++) v[i] = W->cdof[da + k][i] * qvel[da + k];
+      cross_motion(x, S, v);
+      for (int i = 0; i < 6; i++) { T[i] += x[i]; U[i] += v[i]; S[i] += v[i]; }
+    }
+  }
+}
+
+// recursive Newton-Euler (qfrc_bias) adjoint. In: bias-bar in A->vtmp. W->cvel holds the
+// subtree force sums, W->cacc the body forces (velocity_stage overwrote them).
+template <class D> INL void adj_rne(MP m, LDSA WS<D>* W, LDSA WSA<D>* A, int lane) {
+  const int nv = m->nv, nbody = m->nbody, maxlevel = m->maxlevel;
+  const bool isb = lane > 0 && lane < nbody;
+  const BodyRec br = ldrec(&m->brec[isb ? lane : 0]);
+  if (lane < nv) {  // bias_d = cdof_d . cfsub_body(d)
+    const int b = ldrec(&m->drec[lane]).bodyid;
+    for (int k = 0; k < 6; k++) A->cdofb[lane][k] += A->vtmp[lane] * W->cvel[b][k];
+  }
+  if (isb) {
+    float s[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    for (int d = br.dofadr; d < br.dofadr + br.dofnum; d++)
+      for (int k = 0; k < 6; k++) s[k] += A->vtmp[d] * W->cdof[d][k];
+    for (int k = 0; k < 6; k++) A->cfsubb[lane][k] = s[k];
+  }
+  SYNC();
+  if (isb) {  // cfrc-bar_c = sum over ancestors-or-self b of cfsub-bar_b
+    float s[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    for (int b = lane; b > 0; b = ldrec(&m->brec[b]).parent)
+      for (int k = 0; k < 6; k++) s[k] += A->cfsubb[b][k];
+    for (int k = 0; k < 6; k++) A->cfrcb[lane][k] = s[k];
+  }
+  // recompute cvel / cacc (tree pass of velocity_stage)
+  float S[6], U[6], T[6];
+  if (isb) body_vel_terms<D>(W, A->qvel0, br, S, U, T);
+  if (lane == 0) {
+    for (int i = 0; i < 6; i++) A->cvel[0][i] = 0.f;
+    A->cacc[0][0] = A->cacc[0][1] = A->cacc[0][2] = 0.f;
+    A->cacc[0][3] = -m->gravity[0]; A->cacc[0][4] = -m->gravity[1]; A->cacc[0][5] = -m->gravity[2];
+  }
+  SYNC();
+  for (int L = 1; L <= maxlevel; L++) {
+    if (isb && br.level == L) {
+      const int p = br.parent;
+      float x[6];
+      cross_motion(x, A->cvel[p], U);
+      for (int i = 0; i < 6; i++) { A->cvel[lane][i] = A->cvel[p][i] + S[i]; A->cacc[lane][i] = A->cacc[p][i] + x[i] + T[i]; }
+    }
+    SYNC();
+  }
+  if (isb) {  // cfrc = I cacc + cvel x* (I cvel)
+    float ci[10], cv[6], ca[6], fb[6], iv[6], ivb[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    float cib[10] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f}, cvb[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    float cab[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    for (int i = 0; i < 10; i++) ci[i] = W->cinert[lane][i];
+    for (int i = 0; i < 6; i++) { cv[i] = A->cvel[lane][i]; ca[i] = A->cacc[lane][i]; fb[i] = A->cfrcb[lane][i]; }
+    inert_vec(iv, ci, cv);
+    inert_vec_adj(ci, ca, fb, cib, cab);
+    cross_force_adj(cv, iv, fb, cvb, ivb);
+    inert_vec_adj(ci, cv, ivb, cib, cvb);
+    for (int i = 0; i < 10; i++) A->cinertb[lane][i] += cib[i];
+    for (int i = 0; i < 6; i++) { A->cvelb[lane][i] += cvb[i]; A->caccb[lane][i] += cab[i]; }
+  }
+  SYNC();
+  // tree reverse: cvel_b = cvel_p + S, cacc_b = cacc_p + cvel_p x U + T; children -> parent gather
+  float Sb[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f}, Ubr[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f}, Tbr[6];
+  for (int L = maxlevel; L >= 1; L--) {
+    if (isb && br.level == L) {
+      float pvb[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+      for (int i = 0; i < 6; i++) { Sb[i] = A->cvelb[lane][i]; Tbr[i] = A->caccb[lane][i]; }
+      cross_motion_adj(A->cvel[br.parent], U, Tbr, pvb, Ubr);
+      for (int i = 0; i < 6; i++) { A->cfsubb[lane][i] = Sb[i] + pvb[i]; A->cfrcb[lane][i] = Tbr[i]; }
+    }
+    SYNC();
+    if (isb && br.level == L - 1) {
+      for (int c = lane + 1; c < br.subtree_end; c++) {
+        const BodyRec cb = ldrec(&m->brec[c]);
+        if (cb.parent != lane) continue;
+        for (int i = 0; i < 6; i++) { A->cvelb[lane][i] += A->cfsubb[c][i]; A->caccb[lane][i] += A->cfrcb[c][i]; }
+      }
+    }
+    SYNC();
+  }
+  if (isb) {  // local terms -> cdof-bar, qvel-bar
+    const int da = br.dofadr, dn = br.dofnum;
+    if (br.isfree) {
+      float St[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f}, Uf[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+      for (int k = 0; k < 3; k++)
+        for (int i = 0; i < 6; i++) St[i] += W->cdof[da + k][i] * A->qvel0[da + k];
+      for (int k = 3; k < 6; k++)
+        for (int i = 0; i < 6; i++) Uf[i] += W->cdof[da + k][i] * A->qvel0[da + k];
+      float Stb[6], Utb[6];
+      for (int i = 0; i < 6; i++) { Stb[i] = Sb[i]; Utb[i] = Ubr[i] + Sb[i]; }
+      cross_motion_adj(St, Uf, Tbr, Stb, Utb);
+      for (int k = 0; k < 6; k++) {
+        const int d = da + k;
+        const float* vb = k < 3 ? Stb : Utb;
+        float dot = 0.f;
+        for (int i = 0; i < 6; i++) { A->cdofb[d][i] += A->qvel0[d] * vb[i]; dot += W->cdof[d][i] * vb[i]; }
+        A->qvelb[d] += dot;
+      }
+    } else {
+      float Srun[6];
+      for (int i = 0; i < 6; i++) Srun[i] = Sb[i];
+      for (int k = dn - 1; k >= 0; k--) {
+        float Sk[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f}, v[6];
+        for (int kk = 0; kk < k; kk++)
+          for (int i = 0; i < 6; i++) Sk[i] += W->cdof[da + kk][i] * A->qvel0[da + kk];
+        const int d = da + k;
+        for (int i = 0; i < 6; i++) v[i] = W->cdof[d][i] * A->qvel0[d];
+        float skb[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f}, vb[6];
+        for (int i = 0; i < 6; i++) vb[i] = Srun[i] + Ubr[i];
+        cross_motion_adj(Sk, v, Tbr, skb, vb);
+        for (int i = 0; i < 6; i++) Srun[i] += skb[i];
+        float dot = 0.f;
+        for (int i = 0; i < 6; i++) { A->cdofb[d][i] += A->qvel0[d] * vb[i]; dot += W->cdof[d][i] * vb[i]; }
+        A->qvelb[d] += dot;
+      }
+    }
+  }
+  SYNC();
+}
+
+// mass matrix (crb / make_m): M[i][j] = cdof_j . I(crb_body(i)) cdof_i (+ armature), j in anc(i)
+template <class D> INL void adj_mass(MP m, LDSA WS<D>* W, LDSA WSA<D>* A, int lane) {
+  constexpr int LD = D::LD;
+  const int nv = m->nv;
+  const bool isd = lane < nv;
+  const DofRec dr = ldrec(&m->drec[isd ? lane : 0]);
+  if (isd) {
+    float f6[6];
+    inert_vec(f6, W->crb[dr.bodyid], W->cdof[lane]);
+    for (int k = 0; k < 6; k++) A->ftmp[lane][k] = f6[k];
+  }
+  SYNC();
+  float fb[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  if (isd) {
+    const int i = lane;
+    for (uint32_t anc = dr.ancmask; anc;) {  // f-bar_i = sum_j vbar_ij cdof_j
+      const int j = 31 - __builtin_clz(anc);
+      anc &= ~(1u << j);
+      const float vb = (j == i) ? A->Mb[i * LD + i] : A->Mb[i * LD + j] + A->Mb[j * LD + i];
+      for (int k = 0; k < 6; k++) fb[k] += vb * W->cdof[j][k];
+    }
+    const int j = lane;  // cdof-bar_j += sum over descendants i of vbar_ij f_i
+    float cb[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    for (int ii = j; ii < nv; ii++) {
+      if (!((ldrec(&m->drec[ii]).ancmask >> j) & 1u)) continue;
+      const float vb = (ii == j) ? A->Mb[j * LD + j] : A->Mb[ii * LD + j] + A->Mb[j * LD + ii];
+      for (int k = 0; k < 6; k++) cb[k] += vb * A->ftmp[ii][k];
+    }
+    for (int k = 0; k < 6; k++) A->cdofb[j][k] += cb[k];
+  }
+  SYNC();
+  if (isd) {  // f_i = I(crb) cdof_i
+    float t[6];
+    inert_vec(t, W->crb[dr.bodyid], fb);
+    for (int k = 0; k < 6; k++) { A->cdofb[lane][k] += t[k]; A->ftmp[lane][k] = fb[k]; }
+  }
+  SYNC();
+  if (lane > 0 && lane < m->nbody) {
+    const BodyRec br = ldrec(&m->brec[lane]);
+    float ib[10] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    for (int d = br.dofadr; d < br.dofadr + br.dofnum; d++) {
+      float f6[6], c6[6];
+      for (int k = 0; k < 6; k++) { f6[k] = A->ftmp[d][k]; c6[k] = W->cdof[d][k]; }
+      inert_vec_adj(W->crb[lane], c6, f6, ib, (float*)nullptr);
+    }
+    for (int k = 0; k < 10; k++) A->crbb[lane][k] += ib[k];
+  }
+  SYNC();
+}
+
+// crb_b = sum of cinert over the subtree of b: cinert-bar_c = sum of crb-bar over ancestors-or-self
+template <class D> INL void adj_crb(MP m, LDSA WSA<D>* A, int lane) {
+  if (lane > 0 && lane < m->nbody) {
+    float s[10] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    for (int b = lane; b > 0; b = ldrec(&m->brec[b]).parent)
+      for (int k = 0; k < 10; k++) s[k] += A->crbb[b][k];
+    for (int k = 0; k < 10; k++) A->cinertb[lane][k] += s[k];
+  }
+  SYNC();
+}
+
+// cinert (com_pos): rotated inertia about the root's subtree com -> xmat, xipos, scom
+template <class D> INL void adj_cinert(MP m, LDSA WS<D>* W, LDSA WSA<D>* A, int lane) {
+  const bool isb = lane > 0 && lane < m->nbody;
+  const BodyRec br = ldrec(&m->brec[isb ? lane : 0]);
+  float scb[3] = {0.f, 0.f, 0.f};
+  if (isb && br.mass != 0.f) {
+    const int b = lane, root = br.rootid;
+    const float ms = br.mass;
+    LDSA float* cb = A->cinertb[b];
+    const CSTA float* t = m->body_inertia[b];
+    const float Ib[9] = {t[0], t[3], t[4], t[3], t[1], t[5], t[4], t[5], t[2]};
+    float X[9];
+    for (int i = 0; i < 9; i++) X[i] = W->xmat[b][i];
+    float G[9] = {cb[0], cb[3], cb[4], 0.f, cb[1], cb[5], 0.f, 0.f, cb[2]};
+    float S[9];  // G + G^T
+    for (int i = 0; i < 3; i++)
+      for (int j = 0; j < 3; j++) S[3 * i + j] = G[3 * i + j] + G[3 * j + i];
+    float XI[9];  // X Ib
+    for (int i = 0; i < 3; i++)
+      for (int j = 0; j < 3; j++) XI[3 * i + j] = X[3 * i] * Ib[j] + X[3 * i + 1] * Ib[3 + j] + X[3 * i + 2] * Ib[6 + j];
+    for (int i = 0; i < 3; i++)
+      for (int j = 0; j < 3; j++)
+        A->xmatb[b][3 * i + j] += S[3 * i] * XI[j] + S[3 * i + 1] * XI[3 + j] + S[3 * i + 2] * XI[6 + j];
+    const float c[3] = {W->xipos[b][0] - W->scom[root][0], W->xipos[b][1] - W->scom[root][1],
+                        W->xipos[b][2] - W->scom[root][2]};
+    float cbar[3];
+    for (int i = 0; i < 3; i++) cbar[i] = 2.f * ms * c[i] * (cb[0] + cb[1] + cb[2]) + ms * cb[6 + i];
+    cbar[0] -= 2.f * ms * c[0] * cb[0]; cbar[1] -= 2.f * ms * c[1] * cb[1]; cbar[2] -= 2.f * ms * c[2] * cb[2];
+    cbar[0] -= ms * (cb[3] * c[1] + cb[4] * c[2]);
+    cbar[1] -= ms * (cb[3] * c[0] + cb[5] * c[2]);
+    cbar[2] -= ms * (cb[4] * c[0] + cb[5] * c[1]);
+    for (int i = 0; i < 3; i++) { A->xiposb[b][i] += cbar[i]; scb[i] = -cbar[i]; }
+  }
+  scom_reduce<D>(m, A, isb ? br.rootid : -1, scb, lane);
+  SYNC();
+}
+
+// cdof (com_pos): hinge (axis, axis x (scom_root - anchor)); free rotation uses xmat columns
+template <class D> INL void adj_cdof(MP m, LDSA WS<D>* W, LDSA WSA<D>* A, int lane) {
+  const int nv = m->nv;
+  const bool isd = lane < nv;
+  const DofRec dr = ldrec(&m->drec[isd ? lane : 0]);
+  float scb[3] = {0.f, 0.f, 0.f};
+  if (isd) {
+    const int d = lane, j = dr.jntid, b = dr.bodyid, root = dr.rootid, k = dr.kfree;
+    float axb[3] = {0.f, 0.f, 0.f}, offb[3] = {0.f, 0.f, 0.f};
+    if (!(k >= 0 && k < 3)) {
+      float ax[3];
+      if (k >= 3) { ax[0] = W->xmat[b][k - 3]; ax[1] = W->xmat[b][3 + k - 3]; ax[2] = W->xmat[b][6 + k - 3]; }
+      else { ax[0] = W->xaxis[j][0]; ax[1] = W->xaxis[j][1]; ax[2] = W->xaxis[j][2]; }
+      const float off[3] = {W->scom[root][0] - W->xanchor[j][0], W->scom[root][1] - W->xanchor[j][1],
+                            W->scom[root][2] - W->xanchor[j][2]};
+      float lb[3] = {A->cdofb[d][3], A->cdofb[d][4], A->cdofb[d][5]};
+      axb[0] = A->cdofb[d][0]; axb[1] = A->cdofb[d][1]; axb[2] = A->cdofb[d][2];
+      cross3_adj(ax, off, lb, axb, offb);
+      for (int i = 0; i < 3; i++) scb[i] = offb[i];
+    }
+    for (int i = 0; i < 3; i++) { A->ftmp[d][i] = axb[i]; A->ftmp[d][3 + i] = offb[i]; }
+  }
+  scom_reduce<D>(m, A, isd ? dr.rootid : -1, scb, lane);
+  SYNC();
+  if (lane < m->njnt) {  // gather the joint's dofs
+    const JntRec jr = ldrec(&m->jrec[lane]);
+    const int nd = jr.isfree ? 6 : 1;
+    for (int q = 0; q < nd; q++) {
+      const int d = jr.dofadr + q;
+      for (int i = 0; i < 3; i++) A->xanchorb[lane][i] -= A->ftmp[d][3 + i];
+      if (!jr.isfree) for (int i = 0; i < 3; i++) A->xaxisb[lane][i] += A->ftmp[d][i];
+      else if (q >= 3) for (int i = 0; i < 3; i++) A->xmatb[jr.body][3 * i + (q - 3)] += A->ftmp[d][i];
+    }
+  }
+  SYNC();
+}
+
+// kinematics: root subtree com, joint frames, xipos, the level-by-level tree pass, and the
+// per-body local transforms -> qpos-bar
+template <class D> INL void adj_kinematics(MP m, LDSA WS<D>* W, LDSA WSA<D>* A, int lane) {
+  const int nbody = m->nbody, maxlevel = m->maxlevel, njnt = m->njnt;
+  const bool isb = lane > 0 && lane < nbody;
+  const BodyRec br = ldrec(&m->brec[isb ? lane : 0]);
+  // scom_r = sum_c m_c xipos_c / sum_c m_c over the root's subtree
+  if (isb) {
+    const int r = br.rootid;
+    float mr = 0.f;
+    const BodyRec rr = ldrec(&m->brec[r]);
+    for (int c = r; c < rr.subtree_end; c++) mr += m->body_mass[c];
+    if (mr >= kMinVal) for (int i = 0; i < 3; i++) A->xiposb[lane][i] += br.mass / mr * A->scomb[r][i];
+  }
+  SYNC();
+  // joint anchors / axes (world) -> parent frame cotangents; local anchor / axis cotangents in ftmp
+  if (lane < njnt) {
+    const JntRec jr = ldrec(&m->jrec[lane]);
+    if (!jr.isfree) {
+      const int p = jr.parent;
+      float lab[3], lxb[3];
+      mtv3(lab, W->xmat[p], A->xanchorb[lane]);
+      mtv3(lxb, W->xmat[p], A->xaxisb[lane]);
+      for (int i = 0; i < 3; i++) { A->ftmp[lane][i] = lab[i]; A->ftmp[lane][3 + i] = lxb[i]; }
+    }
+  }
+  SYNC();
+  if (lane < nbody) {  // gather: free joint -> its body; hinge -> its parent frame (la, lx in local)
+    float pb[3] = {0.f, 0.f, 0.f}, mb[9] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    for (int j = 0; j < njnt; j++) {
+      const JntRec jr = ldrec(&m->jrec[j]);
+      if (jr.isfree && jr.body == lane) {
+        for (int i = 0; i < 3; i++) { pb[i] += A->xanchorb[j][i]; mb[3 * i + 2] += A->xaxisb[j][i]; }
+      } else if (!jr.isfree && jr.parent == lane) {
+        // anc = xpos_p + xmat_p la, ax = xmat_p lx with la, lx the local values stored in xanchor/xaxis?
+        // (the forward overwrote them with world values: recover local = xmat_p^T (world - xpos_p))
+        float la[3], lx[3], wa[3] = {W->xanchor[j][0] - W->xpos[lane][0], W->xanchor[j][1] - W->xpos[lane][1],
+                                     W->xanchor[j][2] - W->xpos[lane][2]};
+        mtv3(la, W->xmat[lane], wa);
+        mtv3(lx, W->xmat[lane], W->xaxis[j]);
+        for (int i = 0; i < 3; i++) {
+          pb[i] += A->xanchorb[j][i];
+          for (int k = 0; k < 3; k++) mb[3 * i + k] += A->xanchorb[j][i] * la[k] + A->xaxisb[j][i] * lx[k];
+        }
+      }
+    }
+    for (int i = 0; i < 3; i++) A->xposb[lane][i] += pb[i];
+    for (int i = 0; i < 9; i++) A->xmatb[lane][i] += mb[i];
+  }
+  SYNC();
+  if (isb) {  // xipos = xpos + xmat ipos
+    for (int i = 0; i < 3; i++) {
+      A->xposb[lane][i] += A->xiposb[lane][i];
+      for (int k = 0; k < 3; k++) A->xmatb[lane][3 * i + k] += A->xiposb[lane][i] * br.ipos[k];
+    }
+  }
+  // local transforms (as the forward computes them), kept in A->lp / A->lq
+  if (isb) {
+    float lp[3], lq[4];
+    if (br.isfree) {
+      const int qa = br.qadr;
+      for (int i = 0; i < 3; i++) lp[i] = A->qpos0[qa + i];
+      for (int i = 0; i < 4; i++) lq[i] = A->qpos0[qa + 3 + i];
+      qnorm(lq);
+    } else {
+      for (int i = 0; i < 3; i++) lp[i] = br.pos[i];
+      for (int i = 0; i < 4; i++) lq[i] = br.quat[i];
+      for (int j = br.jntadr; j < br.jntadr + br.jntnum; j++) {
+        const JntRec jr = ldrec(&m->jrec[j]);
+        float mat[9], anc[3], off[3];
+        q2m(mat, lq);
+        mv3(anc, mat, jr.pos);
+        for (int i = 0; i < 3; i++) anc[i] += lp[i];
+        float s, c;
+        sincosf(0.5f * (A->qpos0[jr.qadr] - jr.qpos0), &s, &c);
+        const float ql[4] = {c, jr.axis[0] * s, jr.axis[1] * s, jr.axis[2] * s};
+        qmul(lq, lq, ql);
+        q2m(mat, lq);
+        mv3(off, mat, jr.pos);
+        for (int i = 0; i < 3; i++) lp[i] = anc[i] - off[i];
+      }
+    }
+    for (int i = 0; i < 3; i++) A->lp[lane][i] = lp[i];
+    for (int i = 0; i < 4; i++) A->lq[lane][i] = lq[i];
+  }
+  SYNC();
+  // tree pass reverse; child contributions to the parent go through A->Sb (xquat 4, xpos 3) and
+  // A->Tb (first 6 of xmat) + A->Ub (last 3 of xmat)
+  float lpb[3] = {0.f, 0.f, 0.f}, lqb[4] = {0.f, 0.f, 0.f, 0.f};
+  for (int L = maxlevel; L >= 1; L--) {
+    if (isb && br.level == L) {
+      const int b = lane;
+      float qb[4] = {A->xquatb[b][0], A->xquatb[b][1], A->xquatb[b][2], A->xquatb[b][3]};
+      q2m_adj(W->xquat[b], A->xmatb[b], qb);
+      float cq[4] = {0.f, 0.f, 0.f, 0.f}, cp[3] = {0.f, 0.f, 0.f}, cm[9] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+      if (br.isfree) {
+        for (int i = 0; i < 3; i++) lpb[i] = A->xposb[b][i];
+        for (int i = 0; i < 4; i++) lqb[i] = qb[i];
+      } else {
+        const int p = br.parent;
+        float pre[4];
+        qmul(pre, W->xquat[p], A->lq[b]);
+        float preb[4] = {0.f, 0.f, 0.f, 0.f};
+        qnorm_adj(pre, qb, preb);
+        qmul_adj(W->xquat[p], A->lq[b], preb, cq, lqb);
+        for (int i = 0; i < 3; i++) cp[i] = A->xposb[b][i];
+        const float xpb[3] = {A->xposb[b][0], A->xposb[b][1], A->xposb[b][2]};
+        mv3_adj(W->xmat[p], A->lp[b], xpb, cm, lpb);
+      }
+      for (int i = 0; i < 4; i++) A->Sb[b][i] = cq[i];
+      for (int i = 0; i < 2; i++) A->Sb[b][4 + i] = cp[i];
+      A->Ub[b][0] = cp[2];
+      for (int i = 0; i < 6; i++) A->Tb[b][i] = cm[i];
+      for (int i = 0; i < 3; i++) A->Ub[b][1 + i] = cm[6 + i];
+    }
+    SYNC();
+    if (isb && br.level == L - 1) {
+      for (int c = lane + 1; c < br.subtree_end; c++) {
+        const BodyRec cb = ldrec(&m->brec[c]);
+        if (cb.parent != lane || cb.isfree) continue;
+        for (int i = 0; i < 4; i++) A->xquatb[lane][i] += A->Sb[c][i];
+        A->xposb[lane][0] += A->Sb[c][4]; A->xposb[lane][1] += A->Sb[c][5]; A->xposb[lane][2] += A->Ub[c][0];
+        for (int i = 0; i < 6; i++) A->xmatb[lane][i] += A->Tb[c][i];
+        for (int i = 0; i < 3; i++) A->xmatb[lane][6 + i] += A->Ub[c][1 + i];
+      }
+    }
+    SYNC();
+  }
+  // local transforms reverse -> qpos-bar
+  if (isb) {
+    if (br.isfree) {
+      const int qa = br.qadr;
+      for (int i = 0; i < 3; i++) A->qposb[qa + i] += lpb[i];
+      const float q[4] = {A->qpos0[qa + 3], A->qpos0[qa + 4], A->qpos0[qa + 5], A->qpos0[qa + 6]};
+      float qb[4] = {0.f, 0.f, 0.f, 0.f};
+      qnorm_adj(q, lqb, qb);
+      for (int i = 0; i < 4; i++) A->qposb[qa + 3 + i] += qb[i];
+    } else {
+      constexpr int KJ = 8;  // joints per body kept for the reverse sweep
+      float lqs[KJ][4], lps[KJ][3], sn[KJ], cs[KJ];
+      float lp[3], lq[4];
+      for (int i = 0; i < 3; i++) lp[i] = br.pos[i];
+      for (int i = 0; i < 4; i++) lq[i] = br.quat[i];
+      const int jn = br.jntnum < KJ ? br.jntnum : KJ;
+      for (int q = 0; q < jn; q++) {
+        const JntRec jr = ldrec(&m->jrec[br.jntadr + q]);
+        for (int i = 0; i < 4; i++) lqs[q][i] = lq[i];
+        for (int i = 0; i < 3; i++) lps[q][i] = lp[i];
+        float mat[9], anc[3], off[3];
+        q2m(mat, lq);
+        mv3(anc, mat, jr.pos);
+        for (int i = 0; i < 3; i++) anc[i] += lp[i];
+        sincosf(0.5f * (A->qpos0[jr.qadr] - jr.qpos0), &sn[q], &cs[q]);
+        const float ql[4] = {cs[q], jr.axis[0] * sn[q], jr.axis[1] * sn[q], jr.axis[2] * sn[q]};
+        qmul(lq, lq, ql);
+        q2m(mat, lq);
+        mv3(off, mat, jr.pos);
+        for (int i = 0; i < 3; i++) lp[i] = anc[i] - off[i];
+      }
+      for (int q = jn - 1; q >= 0; q--) {
+        const int j = br.jntadr + q;
+        const JntRec jr = ldrec(&m->jrec[j]);
+        const float ql[4] = {cs[q], jr.axis[0] * sn[q], jr.axis[1] * sn[q], jr.axis[2] * sn[q]};
+        float lqa[4];
+        qmul(lqa, lqs[q], ql);
+        // lp_after = anc - q2m(lq_after) jpos
+        float ancb[3] = {lpb[0], lpb[1], lpb[2]};
+        float m2b[9];
+        for (int i = 0; i < 3; i++)
+          for (int k = 0; k < 3; k++) m2b[3 * i + k] = -lpb[i] * jr.pos[k];
+        q2m_adj(lqa, m2b, lqb);
+        // lq_after = lq_before (x) ql
+        float lqbb[4] = {0.f, 0.f, 0.f, 0.f}, qlb[4] = {0.f, 0.f, 0.f, 0.f};
+        qmul_adj(lqs[q], ql, lqb, lqbb, qlb);
+        const float thb = -sn[q] * qlb[0] + cs[q] * (jr.axis[0] * qlb[1] + jr.axis[1] * qlb[2] + jr.axis[2] * qlb[3]);
+        A->qposb[jr.qadr] += 0.5f * thb;
+        // anc = lp_before + mat_before jpos, ax = mat_before jaxis (+ their world-frame cotangents)
+        for (int i = 0; i < 3; i++) ancb[i] += A->ftmp[j][i];
+        float mb[9];
+        for (int i = 0; i < 3; i++)
+          for (int k = 0; k < 3; k++) mb[3 * i + k] = ancb[i] * jr.pos[k] + A->ftmp[j][3 + i] * jr.axis[k];
+        q2m_adj(lqs[q], mb, lqbb);
+        for (int i = 0; i < 3; i++) lpb[i] = ancb[i];
+        for (int i = 0; i < 4; i++) lqb[i] = lqbb[i];
+      }
+    }
+  }
+  SYNC();
+}
+
+// ------------------------------------------------------------------- VJP kernel
+struct VjpArgs {
+  const float *act, *g_qpos, *g_qvel, *g_rew, *g_aux;  // act / g_rew / g_aux: env mode only
+  float *o_qpos, *o_qvel, *o_ctrl, *o_aux;
+  float* scratch;                                     // per env: row slab, then the adjoint scratch
+  int scratch_stride, row_floats;
+};
+
+// One wave per env: recompute the step from the batch state (not modified), then run the reverse
+// passes. ENV: the env step of envs.py (action flip / clip, reward, aux) without the reset merge.
+template <class D, bool ENV> __global__ __launch_bounds__(64, 1) void vjp_kernel(KParams P, VjpArgs V) {
+  __shared__ WS<D> Ws;
+  __shared__ WSA<D> As;
+  __shared__ float aux_s[MJL_AUX_DIM + 3];
+  LDSA WS<D>* W = (LDSA WS<D>*)&Ws;
+  LDSA WSA<D>* A = (LDSA WSA<D>*)&As;
+  LDSA float* aux = (LDSA float*)aux_s;
+  constexpr int LD = D::LD;
+  MP m = (MP)P.m;
+  const int env = blockIdx.x, lane = threadIdx.x;
+  if (env >= P.nenv) return;
+  const int nq = m->nq, nv = m->nv, nu = m->nu;
+  const StateBuf& S = P.s;
+  float* scr_env = V.scratch + (size_t)env * (size_t)V.scratch_stride;
+  GLBA float* scr_adj = (GLBA float*)(scr_env + V.row_floats);
+  {  // zero the adjoint workspace and the LD-wide vectors of the forward one
+    LDSA float* a = (LDSA float*)A;
+    for (int i = lane; i < (int)(sizeof(WSA<D>) / 4); i += 64) a[i] = 0.f;
+    for (int i = lane; i < LD; i += 64) {
+      W->qvel[i] = 0.f; W->qacc_ws[i] = 0.f;
+      W->frc_bias[i] = W->frc_passive[i] = W->frc_act[i] = W->frc_smooth[i] = W->qacc_smooth[i] = 0.f;
+      W->qacc[i] = W->frc_con[i] = W->grad[i] = W->Mgrad[i] = W->search[i] = W->Ma[i] = W->Mv[i] = 0.f;
+      W->gradold[i] = W->Mgradold[i] = 0.f;
+    }
+  }
+  SYNC();
+  if (lane < nq) { W->qpos[lane] = S.qpos[(size_t)env * nq + lane]; A->qpos0[lane] = W->qpos[lane]; }
+  if (lane < nv) {
+    W->qvel[lane] = S.qvel[(size_t)env * nv + lane]; A->qvel0[lane] = W->qvel[lane];
+    W->qacc_ws[lane] = S.qacc_warmstart[(size_t)env * nv + lane];
+  }
+  if (lane == 0) W->sc[SC_TIME] = S.time[env];
+  if (ENV && lane < MJL_AUX_DIM) aux[lane] = S.aux[(size_t)env * MJL_AUX_DIM + lane];
+  SYNC();
+  if (ENV) {  // flip + clip the action (envs.py:335-344)
+    const mjlEnvConfig* c = P.env;
+    const bool flip = aux[0] > 0.5f;
+    if (lane < nu) {
+      const float a = flip ? V.act[(size_t)env * nu + c->act_perm[lane]] * c->act_sign[lane] : V.act[(size_t)env * nu + lane];
+      W->ctrl[lane] = fminf(fmaxf(a, -1.f), 1.f);
+    }
+  } else if (lane < nu) {
+    W->ctrl[lane] = S.ctrl[(size_t)env * nu + lane];
+  }
+  SYNC();
+  // ---- forward (forward() + integrate(), rows in the env's global slab)
+  kinematics<D>(m, W, lane);
+  com_pos_crb<D>(m, W, lane);
+  velocity_stage<D>(m, W, lane);
+  {
+    const float x = chol_factor_solve<D>(W->M, W->H, W->invd, nv, W->frc_smooth, lane);
+    if (lane < LD) W->qacc_smooth[lane] = (lane < nv) ? x : 0.f;
+    SYNC();
+  }
+  Rows<true> R = global_rows<D>(scr_env, P.gmax_efc, P.gmax_con);
+  build_rows<D, true>(m, W, R, lane);
+  solver<D, true>(m, W, R, lane);
+  sensors<D, true>(m, W, R, lane);
+  solver_hessian<D, true>(m, W, R, lane);  // Hc at the converged active set
+  chol_factor_solve<D>(W->H, A->Lc, A->invdc, nv, W->frc_smooth, lane);
+  SYNC();
+  integrate<D>(m, W, lane, A->ap);
+  // ---- reverse
+  const float* gq = V.g_qpos + (size_t)env * nq;
+  if (lane < nv) A->vtmp[lane] = V.g_qvel[(size_t)env * nv + lane];
+  SYNC();
+  if (ENV) adj_env<D>(m, W, A, (CP)P.env, (const float*)aux, V.g_rew[env], V.g_aux + (size_t)env * MJL_AUX_DIM, lane);
+  adj_integrate<D>(m, W, A, gq, lane);
+  adj_solver_rows<D>(m, W, A, R, scr_adj, P.gmax_efc, lane);
+  adj_contact_jac<D>(m, W, A, R, scr_adj, P.gmax_efc, lane);
+  adj_collision<D>(m, W, A, R, scr_adj, P.gmax_efc, lane);
+  adj_geom_frames<D>(m, A, lane);
+  adj_forces<D>(m, W, A, lane);
+  adj_rne<D>(m, W, A, lane);
+  adj_mass<D>(m, W, A, lane);
+  adj_crb<D>(m, A, lane);
+  adj_cinert<D>(m, W, A, lane);
+  adj_cdof<D>(m, W, A, lane);
+  adj_kinematics<D>(m, W, A, lane);
+  // ---- outputs
+  if (lane < nq) V.o_qpos[(size_t)env * nq + lane] = A->qposb[lane];
+  if (lane < nv) V.o_qvel[(size_t)env * nv + lane] = A->qvelb[lane];
+  if (lane < nu) {
+    if (ENV) {  // ctrl = clip(flip ? act[perm] * sign : act, -1, 1)
+      const mjlEnvConfig* c = P.env;
+      const bool flip = aux[0] > 0.5f;
+      const int src = flip ? c->act_perm[lane] : lane;
+      const float sg = flip ? (float)c->act_sign[lane] : 1.f;
+      const float a = V.act[(size_t)env * nu + src] * sg;
+      V.o_ctrl[(size_t)env * nu + src] = (a > -1.f && a < 1.f) ? sg * A->ctrlb[lane] : 0.f;
+    } else {
+      V.o_ctrl[(size_t)env * nu + lane] = A->ctrlb[lane];
+    }
+  }
+  if (ENV && lane < MJL_AUX_DIM) V.o_aux[(size_t)env * MJL_AUX_DIM + lane] = A->auxb[lane];
+}
+
+}  // namespace mjl

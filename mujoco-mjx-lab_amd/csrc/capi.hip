@@ -10,6 +10,7 @@
 #include <string>
 
 #include "step_kernels.hip"
+#include "adjoint.hip"
 
 using namespace mjl;
 
@@ -54,6 +55,8 @@ struct mjlBatch {
   float* field_ptr[MJL_NFIELD];
   float* d_scratch;
   int scratch_stride, gmax_efc, gmax_con;
+  float* d_adj_scratch;  // step VJP: per env row slab + adjoint scratch (allocated on first use)
+  int adj_stride, adj_row_floats;
 };
 
 extern "C" {
@@ -350,6 +353,7 @@ void mjl_batch_destroy(mjlBatch* B) {
   if (!B) return;
   (void)hipSetDevice(B->device);
   (void)hipFree(B->d_state); (void)hipFree(B->d_model); (void)hipFree(B->d_env); (void)hipFree(B->d_scratch);
+  (void)hipFree(B->d_adj_scratch);
   delete B;
 }
 
@@ -492,6 +496,58 @@ int mjl_env_reset(mjlBatch* B, const float* mask, uint64_t seed, uint64_t counte
   P.seed_lo = (uint32_t)seed; P.seed_hi = (uint32_t)(seed >> 32);
   P.ctr_lo = (uint32_t)counter; P.ctr_hi = (uint32_t)(counter >> 32);
   return launch<MODE_ENV_RESET>(B, P, stream);
+}
+
+}  // extern "C"
+
+// ---------------------------------------------------------------- step VJP (APG backward)
+template <bool ENV> static int launch_vjp(mjlBatch* B, const VjpArgs& V0, void* stream) {
+  HIPCHK(hipSetDevice(B->device));
+  if (!B->d_adj_scratch) {
+    const int LD = B->model->nvc == 0 ? DHum::LD : DGen::LD;
+    B->adj_row_floats = B->gmax_efc * (LD + 8) + B->gmax_con * (CONW + 2);
+    B->adj_row_floats = (B->adj_row_floats + 3) & ~3;
+    B->adj_stride = B->adj_row_floats + adj_scratch_floats(B->gmax_efc, B->gmax_con);
+    B->adj_stride = (B->adj_stride + 3) & ~3;
+    hipError_t e = hipMalloc(&B->d_adj_scratch, (size_t)B->adj_stride * B->nenv * sizeof(float));
+    if (e != hipSuccess) { B->d_adj_scratch = nullptr; return fail(MJL_ERR_HIP, "adjoint scratch: %s", hipGetErrorString(e)); }
+  }
+  KParams P = make_params(B);
+  VjpArgs V = V0;
+  V.scratch = B->d_adj_scratch;
+  V.scratch_stride = B->adj_stride;
+  V.row_floats = B->adj_row_floats;
+  dim3 grid(B->nenv), block(64);
+  if (B->model->nvc == 0)
+    hipLaunchKernelGGL((vjp_kernel<DHum, ENV>), grid, block, 0, (hipStream_t)stream, P, V);
+  else
+    hipLaunchKernelGGL((vjp_kernel<DGen, ENV>), grid, block, 0, (hipStream_t)stream, P, V);
+  HIPCHK(hipGetLastError());
+  return MJL_OK;
+}
+
+extern "C" {
+
+int mjl_step_vjp(mjlBatch* B, const float* g_qpos, const float* g_qvel, float* out_qpos, float* out_qvel,
+                 float* out_ctrl, void* stream) {
+  if (!B || !g_qpos || !g_qvel || !out_qpos || !out_qvel || !out_ctrl) return fail(MJL_ERR_ARG, "bad argument");
+  VjpArgs V;
+  std::memset(&V, 0, sizeof(V));
+  V.g_qpos = g_qpos; V.g_qvel = g_qvel; V.o_qpos = out_qpos; V.o_qvel = out_qvel; V.o_ctrl = out_ctrl;
+  return launch_vjp<false>(B, V, stream);
+}
+
+int mjl_env_step_vjp(mjlBatch* B, const float* act, const float* g_qpos, const float* g_qvel, const float* g_rew,
+                     const float* g_aux, float* out_qpos, float* out_qvel, float* out_act, float* out_aux,
+                     void* stream) {
+  if (!B || !act || !g_qpos || !g_qvel || !g_rew || !g_aux || !out_qpos || !out_qvel || !out_act || !out_aux)
+    return fail(MJL_ERR_ARG, "bad argument");
+  if (!B->has_env) return fail(MJL_ERR_ARG, "mjl_env_config not called");
+  VjpArgs V;
+  std::memset(&V, 0, sizeof(V));
+  V.act = act; V.g_qpos = g_qpos; V.g_qvel = g_qvel; V.g_rew = g_rew; V.g_aux = g_aux;
+  V.o_qpos = out_qpos; V.o_qvel = out_qvel; V.o_ctrl = out_act; V.o_aux = out_aux;
+  return launch_vjp<true>(B, V, stream);
 }
 
 }  // extern "C"

@@ -78,8 +78,9 @@ typedef const CSTA ModelF* MP;
 #define MJL_MINWAVES 2
 #endif
 constexpr int kLdsBudget = 20480;
-constexpr int CONW = 16;  // floats per contact record: pos[3], frame[9], then the pair's
-                          // dof masks of both bodies, mu, and b1 | b2 << 8 | condim << 16 (int bits)
+constexpr int CONW = 16;  // floats per contact record: pos[3], frame[9], then the pair's dof masks
+                          // of both bodies, mu, and b1 | b2 << 8 | condim << 16 | k << 24 (int bits;
+                          // k = which of a plane-capsule pair's two contacts)
 constexpr float kMinVal = 1e-15f;
 constexpr float kMinImp = 0.0001f;
 constexpr float kMaxImp = 0.9999f;
@@ -953,7 +954,7 @@ template <class D, bool G> PHASE bool build_rows(MP m_, LDSA WS<D>* W, Rows<G> R
         cr[0] = pos[0]; cr[1] = pos[1]; cr[2] = pos[2];
         for (int i = 0; i < 9; i++) cr[3 + i] = fr[i];
         cr[12] = __uint_as_float(pr.mask1); cr[13] = __uint_as_float(pr.mask2); cr[14] = pr.mu;
-        cr[15] = __int_as_float(pr.b1 | (pr.b2 << 8) | (pr.condim << 16));
+        cr[15] = __int_as_float(pr.b1 | (pr.b2 << 8) | (pr.condim << 16) | (k << 24));
         R.con_pair[c] = p;
         R.con_efc[c] = r0;
         float ep = dist - pr.includemargin, iw = pr.invweight;
@@ -1370,7 +1371,7 @@ template <class D> PHASE void forward(MP m_, LDSA WS<D>* W, float* scratch_env, 
 // ---------------------------------------------------------------------------------------------
 // integration (Euler with eulerdamp / implicitfast)   [forward.euler / forward.implicit]
 // ---------------------------------------------------------------------------------------------
-template <class D> PHASE void integrate(MP m_, LDSA WS<D>* W, int lane) {
+template <class D> PHASE void integrate(MP m_, LDSA WS<D>* W, int lane, LDSA float* ap_out = nullptr) {
   MP m = uniform_ptr(m_);
   constexpr int LD = D::LD;
   const int nv = m->nv;
@@ -1387,6 +1388,7 @@ template <class D> PHASE void integrate(MP m_, LDSA WS<D>* W, int lane) {
     SYNC();
     qa = chol_factor_solve<D>(W->H, W->H, W->invd, nv, W->Mv, lane);
   }
+  if (ap_out && lane < D::LD) ap_out[lane] = (lane < nv) ? qa : 0.f;  // a' for the step adjoint
   if (lane < nv) {
     W->qacc_ws[lane] = W->qacc[lane];
     W->qvel[lane] += dt * qa;

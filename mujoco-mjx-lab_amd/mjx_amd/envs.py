@@ -83,6 +83,21 @@ class HumanoidEnv:
                                  int(auto_reset), self.seed, self._next_counter(), _stream()))
         return obs, rew, term, trunc
 
+    def step_vjp(self, act: torch.Tensor, g_qpos: torch.Tensor, g_qvel: torch.Tensor, g_rew: torch.Tensor,
+                 g_aux: Optional[torch.Tensor] = None) -> Tuple[torch.Tensor, ...]:
+        """VJP of one env step (src/envs.py:333-492, no reset merge) at the current state and aux:
+        cotangents of (qpos', qvel', reward, aux') -> (qpos, qvel, action, aux). State unchanged."""
+        dev, B = self.obs.device, self.num_envs
+        f = lambda x, *shape: x.to(dev, torch.float32).reshape(B, *shape).contiguous()  # noqa: E731
+        act = f(act, self.act_dim)
+        gq, gv, gr = f(g_qpos, self.sys.nq), f(g_qvel, self.sys.nv), f(g_rew)
+        ga = torch.zeros((B, abi.AUX_DIM), device=dev) if g_aux is None else f(g_aux, abi.AUX_DIM)
+        oq, ov = torch.empty_like(gq), torch.empty_like(gv)
+        oa, oaux = torch.empty_like(act), torch.empty_like(ga)
+        check(lib().mjl_env_step_vjp(self.data.handle, _ptr(act), _ptr(gq), _ptr(gv), _ptr(gr), _ptr(ga), _ptr(oq),
+                                     _ptr(ov), _ptr(oa), _ptr(oaux), _stream()))
+        return oq, ov, oa, oaux
+
     @property
     def aux(self) -> torch.Tensor:
         return self.data.get("aux")

@@ -155,3 +155,16 @@ def speedtest_step(sys: Model, d: Data, vel: torch.Tensor, out: Optional[torch.T
     out = torch.empty_like(vel) if out is None else out
     check(lib().mjl_speedtest_step(d.handle, _ptr(vel), _ptr(out), _stream()))
     return out
+
+
+def step_vjp(sys: Model, d: Data, g_qpos: torch.Tensor, g_qvel: torch.Tensor):
+    """Reverse-mode derivative of one mjx.step at the batch's current state (not modified):
+    cotangents of (qpos', qvel') -> cotangents of (qpos, qvel, ctrl). See include/mjx355.h."""
+    dev = d.device
+    gq = g_qpos.to(dev, torch.float32).reshape(d.nenv, sys.nq).contiguous()
+    gv = g_qvel.to(dev, torch.float32).reshape(d.nenv, sys.nv).contiguous()
+    oq = torch.empty_like(gq)
+    ov = torch.empty_like(gv)
+    oc = torch.empty((d.nenv, sys.nu), dtype=torch.float32, device=dev)
+    check(lib().mjl_step_vjp(d.handle, _ptr(gq), _ptr(gv), _ptr(oq), _ptr(ov), _ptr(oc), _stream()))
+    return oq, ov, oc

@@ -71,6 +71,8 @@ def lib():
                                    C.c_int]
         L.orc_speedtest.argtypes = [P(abi.ModelDesc), P(f64), C.c_int, P(f64), C.c_int]
         L.orc_rollout.argtypes = [P(abi.ModelDesc), P(OrcState), P(f64), C.c_int, C.c_int]
+        L.orc_step_jacobian.argtypes = [P(abi.ModelDesc), P(OrcState), P(f64)]
+        L.orc_env_step_jacobian.argtypes = [P(abi.ModelDesc), P(abi.EnvConfigC), P(OrcState), P(f64), P(f64), P(f64)]
         assert L.orc_state_size() == C.sizeof(OrcState), "OrcState layout mismatch"
         assert L.orc_desc_size() == C.sizeof(abi.ModelDesc), "ModelDesc layout mismatch"
         assert L.orc_envcfg_size() == C.sizeof(abi.EnvConfigC), "EnvConfig layout mismatch"
@@ -141,6 +143,25 @@ class Oracle:
         self.L.orc_env_step(C.byref(self.desc), C.byref(envcfg), C.byref(s), _dp(aux), _dp(act), _dp(obs), _dp(rtt),
                             self.use_float)
         return s, aux, obs[:envcfg.obs_dim].copy(), rtt[0], rtt[1], rtt[2]
+
+
+    def step_jacobian(self, s: OrcState) -> np.ndarray:
+        """Exact d(qpos', qvel')/d(qpos, qvel, ctrl) of one step (forward-mode dual numbers)."""
+        m = self.m
+        jac = np.zeros((m.nq + m.nv, m.nq + m.nv + m.nu))
+        assert self.L.orc_step_jacobian(C.byref(self.desc), C.byref(s), _dp(jac)) == 0
+        return jac
+
+    def env_step_jacobian(self, envcfg, s: OrcState, aux: np.ndarray, action: np.ndarray) -> np.ndarray:
+        """Exact d(qpos', qvel', reward, aux')/d(qpos, qvel, action, aux) of one env step."""
+        m = self.m
+        rows, cols = m.nq + m.nv + 1 + abi.AUX_DIM, m.nq + m.nv + m.nu + abi.AUX_DIM
+        jac = np.zeros((rows, cols))
+        aux = np.ascontiguousarray(aux, np.float64)
+        act = np.ascontiguousarray(action, np.float64)
+        assert self.L.orc_env_step_jacobian(C.byref(self.desc), C.byref(envcfg), C.byref(s), _dp(aux), _dp(act),
+                                            _dp(jac)) == 0
+        return jac
 
 
 def state_arrays(m, s: OrcState) -> dict:

@@ -177,3 +177,60 @@ int orc_rollout(const mjlModelDesc* m, orcState* s, const double* ctrl, int nste
 }
 
 }  // extern "C"
+
+// ---- exact Jacobians by forward-mode dual numbers (the derivative reference of the HIP adjoint)
+
+
+namespace {
+constexpr int kND = 96;  // seeded inputs: qpos (nq) + qvel (nv) + ctrl/action (nu) + aux (9) <= 96
+using Dn = oracle::Dual<kND>;
+}  // namespace
+
+extern "C" {
+
+// jac [(nq+nv) x (nq+nv+nu)], row-major: d(qpos', qvel') / d(qpos, qvel, ctrl) of one mjx.step.
+// qacc_warmstart is held constant (it only seeds the solver).
+int orc_step_jacobian(const mjlModelDesc* m, const orcState* s, double* jac) {
+  const int nq = m->nq, nv = m->nv, nu = m->nu, ni = nq + nv + nu;
+  if (ni > kND) return -1;
+  oracle::Data<Dn> d;
+  load(*m, *s, d);
+  for (int i = 0; i < nq; i++) d.qpos[i].d[i] = 1.0;
+  for (int i = 0; i < nv; i++) d.qvel[i].d[nq + i] = 1.0;
+  for (int i = 0; i < nu; i++) d.ctrl[i].d[nq + nv + i] = 1.0;
+  oracle::step(*m, d);
+  for (int i = 0; i < nq; i++)
+    for (int k = 0; k < ni; k++) jac[i * ni + k] = d.qpos[i].d[k];
+  for (int i = 0; i < nv; i++)
+    for (int k = 0; k < ni; k++) jac[(nq + i) * ni + k] = d.qvel[i].d[k];
+  return 0;
+}
+
+// Env step (src/envs.py:333-492) Jacobian: rows (qpos', qvel', reward, aux'[9]), columns
+// (qpos, qvel, action[nu], aux[9]); jac [(nq+nv+1+9) x (nq+nv+nu+9)], row-major.
+int orc_env_step_jacobian(const mjlModelDesc* m, const mjlEnvConfig* c, const orcState* s, const double* aux_in,
+                          const double* act, double* jac) {
+  const int nq = m->nq, nv = m->nv, nu = m->nu, ni = nq + nv + nu + MJL_AUX_DIM;
+  if (ni > kND) return -1;
+  oracle::Data<Dn> d;
+  load(*m, *s, d);
+  Dn aux[MJL_AUX_DIM], a[MJL_MAXU];
+  for (int i = 0; i < nq; i++) d.qpos[i].d[i] = 1.0;
+  for (int i = 0; i < nv; i++) d.qvel[i].d[nq + i] = 1.0;
+  for (int i = 0; i < nu; i++) { a[i] = Dn(act[i]); a[i].d[nq + nv + i] = 1.0; }
+  for (int i = 0; i < MJL_AUX_DIM; i++) { aux[i] = Dn(aux_in[i]); aux[i].d[nq + nv + nu + i] = 1.0; }
+  oracle::EnvOut<Dn> out;
+  oracle::env_step(*m, *c, d, aux, a, out);
+  int r = 0;
+  for (int i = 0; i < nq; i++, r++)
+    for (int k = 0; k < ni; k++) jac[r * ni + k] = d.qpos[i].d[k];
+  for (int i = 0; i < nv; i++, r++)
+    for (int k = 0; k < ni; k++) jac[r * ni + k] = d.qvel[i].d[k];
+  for (int k = 0; k < ni; k++) jac[r * ni + k] = out.reward.d[k];
+  r++;
+  for (int i = 0; i < MJL_AUX_DIM; i++, r++)
+    for (int k = 0; k < ni; k++) jac[r * ni + k] = aux[i].d[k];
+  return 0;
+}
+
+}  // extern "C"

@@ -28,6 +28,7 @@
 #include <vector>
 
 #include "../include/mjx355.h"
+#include "dual.hpp"  // declared before the templates so qualified std:: math calls see the overloads
 
 namespace oracle {
 
