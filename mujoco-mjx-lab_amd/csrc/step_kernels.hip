@@ -57,10 +57,15 @@ __device__ unsigned long long* g_stamps;
     if ((lane) == 0 && g_stamps) g_stamps[(size_t)blockIdx.x * 16 + (slot)] += t_ - (var);      \
     (var) = t_;                                                                                  \
   } while (0)
+#define TCOUNT(slot, n, lane)                                                                    \
+  do {                                                                                           \
+    if ((lane) == 0 && g_stamps) g_stamps[(size_t)blockIdx.x * 16 + (slot)] += (n);             \
+  } while (0)
 #else
 #define STAMP(slot, lane) do { } while (0)
 #define TSTART(var) do { } while (0)
 #define TACC(slot, var, lane) do { } while (0)
+#define TCOUNT(slot, n, lane) do { } while (0)
 #endif
 
 typedef const CSTA ModelF* MP;
@@ -1116,13 +1121,17 @@ template <class D, bool G> INL void solver_hessian(MP m_, LDSA WS<D>* W, Rows<G>
   SYNC();
 }
 
-// exact line search along `search`: safeguarded Newton on the piecewise-linear f'(alpha)
+// MJX's zoom line search along `search` (mujoco-mjx 3.3.6 solver.py _linesearch, restated in
+// oracle/physics.hpp Solver::linesearch): bracket ends lo / hi around the root of f'(alpha); each
+// iteration evaluates the Newton steps from both ends and the midpoint (one pass over the rows for
+// all three points) and moves the ends by MJX's swap rules, until no end moves, an end's |f'| <
+// gtol, or ls_iterations. Returns the lower-cost end if it improves on alpha = 0, else 0.
+// Costs are relative to the Gauss term at alpha = 0 (common to every point, so comparisons hold).
 template <class D, bool G> INL float solver_linesearch(MP m_, LDSA WS<D>* W, Rows<G> R, int lane) {
   MP m = uniform_ptr(m_);
   const int nv = m->nv, nefc = W->nefc;
   float sn = (lane < nv) ? W->search[lane] * W->search[lane] : 0.f;
   float snorm = sqrtf(wsum(sn));
-  if (!(snorm >= kMinVal)) return 0.f;
   float gtol = m->tolerance * m->ls_tolerance * snorm / m->scale;
   float mvl = 0.f;
   if (lane < nv) { mvl = mrow<D>(W, W->search, lane); W->Mv[lane] = mvl; }
@@ -1135,37 +1144,91 @@ template <class D, bool G> INL float solver_linesearch(MP m_, LDSA WS<D>* W, Row
   float jv0 = 0.f, ja0 = 0.f, dd0 = 0.f, jv1 = 0.f, ja1 = 0.f, dd1 = 0.f;
   if (lane < nefc) { jv0 = R.Jv[lane]; ja0 = R.jar[lane]; dd0 = R.D[lane]; }
   if (lane + 64 < nefc) { jv1 = R.Jv[lane + 64]; ja1 = R.jar[lane + 64]; dd1 = R.D[lane + 64]; }
-  auto eval = [&](float al, float& der, float& hes) {
-    float dp = 0.f, hp = 0.f;
-    float j = ja0 + al * jv0;
-    if (j < 0.f) { float dj = dd0 * jv0; dp += dj * j; hp += dj * jv0; }
-    j = ja1 + al * jv1;
-    if (j < 0.f) { float dj = dd1 * jv1; dp += dj * j; hp += dj * jv1; }
-    for (int r = lane + 128; r < nefc; r += 64) {
-      float jv = R.Jv[r];
-      float jj = R.jar[r] + al * jv;
-      if (jj < 0.f) { float dj = R.D[r] * jv; dp += dj * jj; hp += dj * jv; }
+  // f'(al[k]), f''(al[k]) for K points (COST: the relative cost instead) in one pass over the rows
+  auto eval = [&](auto Kc, auto COSTc, const float* al, float* o0, float* o1) {
+    constexpr int K = decltype(Kc)::value;
+    constexpr bool COST = decltype(COSTc)::value;
+    float dp[K], hp[K];
+#pragma unroll
+    for (int k = 0; k < K; k++) { dp[k] = 0.f; hp[k] = 0.f; }
+    auto row = [&](float ja, float jv, float dd) {
+#pragma unroll
+      for (int k = 0; k < K; k++) {
+        float j = ja + al[k] * jv;
+        if (j < 0.f) {
+          if (COST) { dp[k] += dd * j * j; } else { float dj = dd * jv; dp[k] += dj * j; hp[k] += dj * jv; }
+        }
+      }
+    };
+    row(ja0, jv0, dd0);
+    row(ja1, jv1, dd1);
+    for (int r = lane + 128; r < nefc; r += 64) row(R.jar[r], R.Jv[r], R.D[r]);
+#pragma unroll
+    for (int k = 0; k < K; k++) {
+      if (COST) {
+        o0[k] = al[k] * c1 + 0.5f * al[k] * al[k] * c2 + 0.5f * wsum(dp[k]);
+      } else {
+        o0[k] = c1 + al[k] * c2 + wsum(dp[k]);
+        float h = c2 + wsum(hp[k]);
+        o1[k] = h + (h == 0.f ? kMinVal : 0.f);
+      }
     }
-    der = c1 + al * c2 + wsum(dp);
-    hes = c2 + wsum(hp);
   };
-  float der, hes;
-  eval(0.f, der, hes);
-  if (!(der < 0.f)) return 0.f;
-  float lo = 0.f, hi = -1.f;
-  float alpha = -der / hes;
+  using I1 = std::integral_constant<int, 1>;
+  using I3 = std::integral_constant<int, 3>;
+  using TF = std::false_type;
+  using TT = std::true_type;
+  // p0 and the Newton point q from it
+  float a0[1] = {0.f}, p0d0[1], p0d1[1];
+  eval(I1{}, TF{}, a0, p0d0, p0d1);
+  float a1[1] = {-p0d0[0] * __builtin_amdgcn_rcpf(p0d1[0])}, qd0[1], qd1[1];
+  eval(I1{}, TF{}, a1, qd0, qd1);
+  // exact segment: if no row changes activity between 0 and q, f' is linear there and q is its
+  // root, the minimiser MJX's iterations then only jitter around in rounding noise
+  {
+    bool same = true;
+    for (int r = lane; r < nefc; r += 64) same &= (R.jar[r] < 0.f) == (R.jar[r] + a1[0] * R.Jv[r] < 0.f);
+    if (__ballot(!same) == 0ull) { TCOUNT(15, 1, lane); return a1[0]; }
+  }
+  // lo = whichever of p0, q has the smaller f'
+  float loa, lod0, lod1, hia, hid0, hid1;
+  if (qd0[0] < p0d0[0]) { loa = a1[0]; lod0 = qd0[0]; lod1 = qd1[0]; hia = 0.f; hid0 = p0d0[0]; hid1 = p0d1[0]; }
+  else { loa = 0.f; lod0 = p0d0[0]; lod1 = p0d1[0]; hia = a1[0]; hid0 = qd0[0]; hid1 = qd1[0]; }
+  // MJX's gtol (tolerance * ls_tolerance * |search|) sits below the fp32 resolution of f', where
+  // MJX's fp32 iterations only shuffle lo / hi within rounding noise until ls_iterations: an end
+  // also counts as converged once |f'| is within kNoise of the magnitude of the terms summed into
+  // it (|c1| + |a| f'' + |row part|), and the search stops once the bracket is a few ulps wide
+  constexpr float kNoise = 2e-6f;
+  auto tol = [&](float a, float d0, float d1) {
+    return fmaxf(gtol, kNoise * (fabsf(c1) + fabsf(a) * d1 + fabsf(d0 - c1 - a * d1)));
+  };
+  float lot = tol(loa, lod0, lod1), hit = tol(hia, hid0, hid1);
   const int lsit = m->ls_iterations;
   for (int it = 0; it < lsit; it++) {
-    eval(alpha, der, hes);
-    if (fabsf(der) < gtol) break;
-    if (der < 0.f) lo = alpha; else hi = alpha;
-    float nxt = alpha - der / hes;
-    bool inside = nxt > lo && (hi < 0.f || nxt < hi);
-    if (!inside) nxt = hi < 0.f ? 2.f * alpha : 0.5f * (lo + hi);
-    if (nxt == alpha) break;
-    alpha = nxt;
+    if ((lod0 < 0.f && lod0 > -lot) || (hid0 > 0.f && hid0 < hit)) break;
+    if (fabsf(hia - loa) <= 1e-6f * fmaxf(fabsf(loa), fabsf(hia))) break;
+    float al[3] = {loa - lod0 * __builtin_amdgcn_rcpf(lod1), hia - hid0 * __builtin_amdgcn_rcpf(hid1), 0.5f * (loa + hia)};
+    float d0[3], d1[3];
+    eval(I3{}, TF{}, al, d0, d1);
+    bool s1 = lod0 > 0.f || lod0 < d0[0];
+    if (s1) { loa = al[0]; lod0 = d0[0]; lod1 = d1[0]; }
+    bool s2 = d0[2] < 0.f && lod0 < d0[2];
+    if (s2) { loa = al[2]; lod0 = d0[2]; lod1 = d1[2]; }
+    bool s3 = hid0 < 0.f || hid0 > d0[1];
+    if (s3) { hia = al[1]; hid0 = d0[1]; hid1 = d1[1]; }
+    bool s4 = d0[2] > 0.f && hid0 > d0[2];
+    if (s4) { hia = al[2]; hid0 = d0[2]; hid1 = d1[2]; }
+    TCOUNT(14, 1, lane);
+    if (!(s1 || s2 || s3 || s4)) break;
+    lot = tol(loa, lod0, lod1);
+    hit = tol(hia, hid0, hid1);
   }
-  return alpha;
+  TCOUNT(15, 1, lane);
+  float ac[3] = {0.f, loa, hia}, cost[3];
+  eval(I3{}, TT{}, ac, cost, nullptr);
+  const bool improved = cost[1] < cost[0] || cost[2] < cost[0];
+  const float alpha = cost[1] < cost[2] ? loa : hia;
+  return improved ? alpha : 0.f;
 }
 
 template <class D, bool G> PHASE void solver(MP m_, LDSA WS<D>* W, Rows<G> R, int lane) {
@@ -1222,7 +1285,7 @@ template <class D, bool G> PHASE void solver(MP m_, LDSA WS<D>* W, Rows<G> R, in
   for (bool first = true;; first = false) {
     if (!first) {
       float alpha = solver_linesearch<D, G>(m, W, R, lane);
-      if (!(alpha != 0.f)) break;  // also stops on NaN
+      if (!(alpha != 0.f)) { iter++; break; }  // no improvement: MJX's next cond stops (also on NaN)
       if (lane < nv) {
         W->qacc[lane] += alpha * W->search[lane];
         W->Ma[lane] += alpha * W->Mv[lane];
@@ -1234,6 +1297,10 @@ template <class D, bool G> PHASE void solver(MP m_, LDSA WS<D>* W, Rows<G> R, in
     }
     float oldcost = cost;
     cost = solver_update<D, G>(m, W, R, lane);
+    if (first && maxit != 1) {  // MJX cond before the first body (iterations == 1 runs one body)
+      float gp = (lane < nv) ? W->grad[lane] * W->grad[lane] : 0.f;
+      if (maxit <= 0 || scale * sqrtf(wsum(gp)) < m->tolerance) break;
+    }
     if (!first) {
       iter++;
       float gp = (lane < nv) ? W->grad[lane] * W->grad[lane] : 0.f;
@@ -1266,7 +1333,7 @@ template <class D, bool G> PHASE void solver(MP m_, LDSA WS<D>* W, Rows<G> R, in
       }
       num = wsum(num);
       den = wsum(den);
-      float beta = (!first && den > kMinVal) ? fmaxf(0.f, num / den) : 0.f;
+      float beta = first ? 0.f : fmaxf(0.f, num / fmaxf(kMinVal, den));  // PR, MJX's floored denominator
       if (lane < LD) W->search[lane] = (lane < nv) ? -x + beta * W->search[lane] : 0.f;
     }
     SYNC();

@@ -1,0 +1,184 @@
+"""APG (analytic policy gradients) over the native env step and its VJP (reference train_apg.py).
+
+Intended semantics of train_apg.py:161-209 (the shipped script is broken):
+  * every update resets all envs (v_reset), then rolls out `horizon` steps with no reset merge;
+  * obs = [qpos, qvel] (nq + nv), normalised after `obs_warmup_steps` updates as
+    clip((obs - mean) / (sqrt(var) + 1e-8), -10, 10) (train_apg.py:171-176);
+  * loss = -mean_envs sum_t disc_t r_t, disc_0 = 1, disc_{t+1} = disc_t gamma (1 - done_t);
+  * gradients flow through the policy and through every env step (jax.grad through mjx.step with
+    per-step remat, train_apg.py:187-189); clip_by_global_norm(0.3) then Adam(lr);
+  * observation statistics are updated every `rms_update_every` updates from the rollout's obs.
+
+Here the forward rollout records the pre-step state of every step (the remat tape); the backward
+sweeps the tape in reverse, restoring each state into the batch and calling `mjl_env_step_vjp`,
+whose action cotangent is pulled back through the policy by torch autograd. Data-parallel: each
+rank rolls out its own envs; gradients (one all-reduce) and observation statistics are averaged.
+"""
+from __future__ import annotations
+
+import json
+import os
+import time
+from typing import Optional
+
+import torch
+
+from .ppo import APGPolicy, RunningMeanStd, _flat_grads, _jsonable, _set_grads
+
+
+def apg_normalize(rms: RunningMeanStd, x: torch.Tensor) -> torch.Tensor:
+    """train_apg.py:171-176 (note sqrt(var) + 1e-8, unlike PPO's sqrt(var + 1e-8))."""
+    return torch.clamp((x - rms.mean) / (torch.sqrt(rms.var) + 1e-8), -10.0, 10.0)
+
+
+class APGTrainer:
+    """`env` exposes reset(), step(act, auto_reset=False) -> (obs, rew, term, trunc), step_vjp(...),
+    get_state() / set_state(tape entry), qpos_qvel() and num_envs, act_dim, nq, nv (HumanoidEnv
+    through `HumanoidAPGEnv`, or the differentiable stand-in of the CPU tests)."""
+
+    def __init__(self, cfg, env, device="cuda", dist=None, out_dir: Optional[str] = None):
+        self.cfg, self.env, self.dist = cfg, env, dist
+        self.rank = dist.get_rank() if dist is not None else 0
+        self.world = dist.get_world_size() if dist is not None else 1
+        self.device = torch.device(device)
+        self.obs_dim = env.nq + env.nv
+        g = torch.Generator().manual_seed(int(cfg.seed))
+        self.policy = APGPolicy(self.obs_dim, env.act_dim, cfg.hidden_size, cfg.hidden_depth, None, g).to(self.device)
+        if dist is not None:
+            for p in self.policy.parameters():
+                dist.broadcast(p.data, 0)
+        self.opt = torch.optim.Adam(self.policy.parameters(), lr=cfg.lr, betas=(0.9, 0.999), eps=1e-8)
+        self.rms = RunningMeanStd(self.obs_dim, self.device)
+        self.total_env_steps = 0.0
+        self.start = time.time()
+        self.out_dir = out_dir if self.rank == 0 else None
+        if self.out_dir:
+            for sub in ("checkpoints", "logs"):
+                os.makedirs(os.path.join(self.out_dir, sub), exist_ok=True)
+            with open(os.path.join(self.out_dir, "config.json"), "w") as f:
+                json.dump(_jsonable(cfg), f, indent=2)
+
+    def _obs(self, use_norm: bool):
+        o = self.env.qpos_qvel().detach().clone().requires_grad_(True)
+        return o, (apg_normalize(self.rms, o) if use_norm else o)
+
+    def loss_and_grad(self, use_norm: bool):
+        """One rollout + backward. Returns (loss, mean reward, obs trajectory); grads in .grad."""
+        cfg, env = self.cfg, self.env
+        H, B, gamma = cfg.horizon, env.num_envs, cfg.gamma
+        env.reset()
+        tape, obs_leaves, acts, discs = [], [], [], []
+        disc = ret = rsum = None  # created from the first reward (dtype follows the env)
+        obs_traj = []
+        for _ in range(H):
+            tape.append(env.get_state())
+            o, on = self._obs(use_norm)
+            a = self.policy(on)
+            obs_leaves.append(o)
+            acts.append(a)
+            obs_traj.append(o.detach())
+            _, r, te, tr = env.step(a.detach(), auto_reset=False)
+            if disc is None:
+                disc, ret, rsum = torch.ones_like(r), torch.zeros_like(r), torch.zeros_like(r[0])
+            discs.append(disc)
+            ret = ret + disc * r
+            rsum = rsum + r.mean()
+            disc = disc * gamma * (1.0 - torch.maximum(te, tr))
+        loss = -ret.mean()
+        # reverse sweep: state cotangents of step t+1 -> step t; action cotangents -> policy
+        self.opt.zero_grad(set_to_none=True)
+        gq = torch.zeros((B, env.nq), device=self.device)
+        gv = torch.zeros((B, env.nv), device=self.device)
+        gaux = None
+        for t in range(H - 1, -1, -1):
+            env.set_state(tape[t])
+            grew = -discs[t] / B
+            gq, gv, ga, gaux = env.step_vjp(acts[t].detach(), gq, gv, grew, gaux)
+            torch.autograd.backward(acts[t], grad_tensors=ga)
+            og = obs_leaves[t].grad
+            gq = gq + og[:, :env.nq]
+            gv = gv + og[:, env.nq:]
+        return loss.detach(), (rsum / H).detach(), torch.stack(obs_traj)
+
+    def update(self, step: int) -> dict:
+        cfg = self.cfg
+        if self.device.type == "cuda":
+            torch.cuda.synchronize(self.device)
+        t0 = time.time()
+        use_norm = step >= cfg.obs_warmup_steps and cfg.normalize_observations
+        loss, mean_r, obs_traj = self.loss_and_grad(use_norm)
+        params = list(self.policy.parameters())
+        g = _flat_grads(params)
+        stats = torch.stack([loss, mean_r])
+        if self.dist is not None:
+            self.dist.all_reduce(g)
+            g /= self.world
+            self.dist.all_reduce(stats)
+            stats /= self.world
+        gnorm = torch.linalg.vector_norm(g)
+        g = g * torch.clamp(cfg.grad_clip / (gnorm + 1e-16), max=1.0)  # optax.clip_by_global_norm
+        _set_grads(params, g)
+        self.opt.step()
+        if cfg.normalize_observations and step % cfg.rms_update_every == 0:
+            self.rms.update(obs_traj, self.dist)
+        if self.device.type == "cuda":
+            torch.cuda.synchronize(self.device)
+        dt = max(time.time() - t0, 1e-9)
+        steps = float(cfg.horizon * self.env.num_envs * self.world)
+        self.total_env_steps += steps
+        return {"loss": float(stats[0]), "return": float(-stats[0]), "mean_reward": float(stats[1]),
+                "grad_norm": float(gnorm), "env_steps_per_sec": steps / dt}
+
+    def train(self, steps: Optional[int] = None, verbose: bool = True):
+        n = self.cfg.total_steps if steps is None else steps
+        hist = []
+        for step in range(n):
+            m = self.update(step)
+            if not (m["loss"] == m["loss"]):  # NaN guard (train_apg.py:278-287)
+                if verbose and self.rank == 0:
+                    print(f"NaN loss at step {step}", flush=True)
+                break
+            m["total_env_steps"] = self.total_env_steps
+            m["elapsed_time"] = time.time() - self.start
+            if self.out_dir:
+                with open(os.path.join(self.out_dir, "logs", "metrics.jsonl"), "a") as f:
+                    f.write(json.dumps({"step": step, **m}) + "\n")
+                if (step + 1) % self.cfg.checkpoint_every == 0 or step == n - 1:
+                    torch.save({"step": step, "params": self.policy.state_dict(), "rms": self.rms.state_dict(),
+                                "opt": self.opt.state_dict()},
+                               os.path.join(self.out_dir, "checkpoints", f"checkpoint_{step:06d}.pt"))
+            if verbose and self.rank == 0 and (step < 10 or step % 10 == 0):
+                print(f"Step {step:5d} | Return: {m['return']:8.3f} | Reward: {m['mean_reward']:7.4f} | "
+                      f"GradNorm: {m['grad_norm']:8.3f} | Steps/s: {m['env_steps_per_sec']:9.0f}", flush=True)
+            hist.append(m)
+        return hist
+
+
+class HumanoidAPGEnv:
+    """HumanoidEnv adapter for APGTrainer: tape entries are the batch fields a step reads."""
+
+    FIELDS = ("qpos", "qvel", "qacc_warmstart", "aux", "time")
+
+    def __init__(self, env):
+        self.env = env
+        self.num_envs, self.act_dim = env.num_envs, env.act_dim
+        self.nq, self.nv = env.sys.nq, env.sys.nv
+
+    def reset(self):
+        return self.env.reset()
+
+    def step(self, act, auto_reset=False):
+        return self.env.step(act, auto_reset=auto_reset)
+
+    def qpos_qvel(self):
+        return torch.cat([self.env.data.get("qpos"), self.env.data.get("qvel")], 1)
+
+    def get_state(self):
+        return {k: self.env.data.get(k) for k in self.FIELDS}
+
+    def set_state(self, st):
+        for k in self.FIELDS:
+            self.env.data.set(k, st[k])
+
+    def step_vjp(self, act, gq, gv, grew, gaux):
+        return self.env.step_vjp(act, gq, gv, grew, gaux)

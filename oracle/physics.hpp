@@ -787,21 +787,33 @@ template <class R> struct Solver {
     for (int i = 0; i < nv; i++) Mgrad[i] = grad[i];
     chol_solve(d.L.data(), nv, Mgrad.data());
   }
-  // f'(alpha) and f''(alpha) of the cost along the search direction
-  void ls_eval(R alpha, R c1, R c2, R& der, R& hes) {
-    der = c1 + alpha * c2;
-    hes = c2;
+  // cost, f'(alpha) and f''(alpha) along the search direction (MJX solver.py _LSPoint.create:
+  // quad_gauss + the rows active at alpha; f'' gets mjMINVAL when the quadratic term is exactly 0)
+  struct LSPoint { R alpha, cost, d0, d1; };
+  LSPoint ls_point(R alpha, R gauss0, R c1, R c2) {
+    R q0 = gauss0, q1 = c1, q2 = R(0.5) * c2;
     for (int r = 0; r < nefc; r++) {
       R j = jar[r] + alpha * Jv[r];
-      if (j < 0) { der += d.efc_D[r] * j * Jv[r]; hes += d.efc_D[r] * Jv[r] * Jv[r]; }
+      if (j < 0) {
+        R D = d.efc_D[r];
+        q0 += R(0.5) * D * jar[r] * jar[r]; q1 += D * Jv[r] * jar[r]; q2 += R(0.5) * D * Jv[r] * Jv[r];
+      }
     }
+    LSPoint p;
+    p.alpha = alpha;
+    p.cost = alpha * alpha * q2 + alpha * q1 + q0;
+    p.d0 = 2 * alpha * q2 + q1;
+    p.d1 = 2 * q2 + (q2 == 0 ? R(kMinVal) : R(0));
+    return p;
   }
-  // exact 1-D minimisation of the convex piecewise-quadratic cost: safeguarded Newton on f'
+  // MJX's zoom line search (mujoco-mjx 3.3.6 solver.py _linesearch): a bracket [lo, hi] around the
+  // root of f', each iteration trying the Newton steps from lo and from hi and the midpoint, until
+  // no bracket end moves, an end's |f'| < gtol, or ls_iterations; then the lower-cost end, taken
+  // only if it improves on alpha = 0. Returns that alpha (0 = no improvement).
   R linesearch(R scale) {
     R snorm = 0;
     for (int i = 0; i < nv; i++) snorm += search[i] * search[i];
     snorm = std::sqrt(snorm);
-    if (snorm < R(kMinVal)) return 0;
     R gtol = R(m.tolerance * m.ls_tolerance) * snorm / scale;
     mulM(search.data(), Mv.data());
     for (int r = 0; r < nefc; r++) {
@@ -811,22 +823,30 @@ template <class R> struct Solver {
     }
     R c1 = 0, c2 = 0;
     for (int i = 0; i < nv; i++) { c1 += search[i] * (Ma[i] - d.qfrc_smooth[i]); c2 += search[i] * Mv[i]; }
-    R der, hes;
-    ls_eval(R(0), c1, c2, der, hes);
-    if (!(der < 0)) return 0;
-    R lo = 0, hi = -1;  // hi < 0: unbounded
-    R alpha = -der / hes;
+    LSPoint p0 = ls_point(R(0), gauss, c1, c2);
+    LSPoint lo = ls_point(p0.alpha - p0.d0 / p0.d1, gauss, c1, c2), hi;
+    if (lo.d0 < p0.d0) hi = p0; else { hi = lo; lo = p0; }
+    bool swap = true;
     for (int it = 0; it < m.ls_iterations; it++) {
-      ls_eval(alpha, c1, c2, der, hes);
-      if (std::abs(der) < gtol) break;
-      if (der < 0) lo = alpha; else hi = alpha;
-      R next = alpha - der / hes;
-      bool inside = next > lo && (hi < 0 || next < hi);
-      if (!inside) next = hi < 0 ? 2 * alpha : R(0.5) * (lo + hi);
-      if (next == alpha) break;
-      alpha = next;
+      if (!swap) break;
+      if (lo.d0 < 0 && lo.d0 > -gtol) break;
+      if (hi.d0 > 0 && hi.d0 < gtol) break;
+      LSPoint lo_next = ls_point(lo.alpha - lo.d0 / lo.d1, gauss, c1, c2);
+      LSPoint hi_next = ls_point(hi.alpha - hi.d0 / hi.d1, gauss, c1, c2);
+      LSPoint mid = ls_point(R(0.5) * (lo.alpha + hi.alpha), gauss, c1, c2);
+      bool s1 = lo.d0 > 0 || lo.d0 < lo_next.d0;
+      if (s1) lo = lo_next;
+      bool s2 = mid.d0 < 0 && lo.d0 < mid.d0;
+      if (s2) lo = mid;
+      bool s3 = hi.d0 < 0 || hi.d0 > hi_next.d0;
+      if (s3) hi = hi_next;
+      bool s4 = mid.d0 > 0 && hi.d0 > mid.d0;
+      if (s4) hi = mid;
+      swap = s1 || s2 || s3 || s4;
     }
-    return alpha;
+    bool improved = lo.cost < p0.cost || hi.cost < p0.cost;
+    R alpha = lo.cost < hi.cost ? lo.alpha : hi.alpha;
+    return improved ? alpha : R(0);
   }
 
   void run() {
@@ -854,30 +874,34 @@ template <class R> struct Solver {
     bool newton = m.solver == MJL_SOLVER_NEWTON;
     if (newton) newton_direction(); else cg_precondition();
     for (int i = 0; i < nv; i++) search[i] = -Mgrad[i];
+    // MJX solve(): while_loop(cond, body) with cond = niter < iterations && improvement >= tol &&
+    // |grad| >= tol (improvement = inf before the first body); iterations == 1 runs body once.
     int iter = 0;
-    while (iter < m.iterations) {
+    R gnorm0 = 0;
+    for (int i = 0; i < nv; i++) gnorm0 += grad[i] * grad[i];
+    bool go = m.iterations == 1 || (m.iterations > 0 && scale * std::sqrt(gnorm0) >= R(m.tolerance));
+    while (go) {
       R alpha = linesearch(scale);
-      if (alpha == 0) break;
       for (int i = 0; i < nv; i++) { d.qacc[i] += alpha * search[i]; Ma[i] += alpha * Mv[i]; }
       for (int r = 0; r < nefc; r++) jar[r] += alpha * Jv[r];
       R oldcost = cost;
-      if (!newton) { gradold = grad; Mgradold = Mgrad; }
+      gradold = grad; Mgradold = Mgrad;
       update();
       if (newton) newton_direction(); else cg_precondition();
       iter++;
+      if (newton) {
+        for (int i = 0; i < nv; i++) search[i] = -Mgrad[i];
+      } else {  // Polak-Ribiere, denominator floored at mjMINVAL
+        R num = 0, den = 0;
+        for (int i = 0; i < nv; i++) { num += grad[i] * (Mgrad[i] - Mgradold[i]); den += gradold[i] * Mgradold[i]; }
+        R beta = std::max(R(0), num / std::max(R(kMinVal), den));
+        for (int i = 0; i < nv; i++) search[i] = -Mgrad[i] + beta * search[i];
+      }
       R improvement = scale * (oldcost - cost);
       R gnorm = 0;
       for (int i = 0; i < nv; i++) gnorm += grad[i] * grad[i];
       gnorm = scale * std::sqrt(gnorm);
-      if (improvement < R(m.tolerance) || gnorm < R(m.tolerance)) break;
-      if (newton) {
-        for (int i = 0; i < nv; i++) search[i] = -Mgrad[i];
-      } else {  // Polak-Ribiere
-        R num = 0, den = 0;
-        for (int i = 0; i < nv; i++) { num += grad[i] * (Mgrad[i] - Mgradold[i]); den += gradold[i] * Mgradold[i]; }
-        R beta = den > R(kMinVal) ? std::max(R(0), num / den) : R(0);
-        for (int i = 0; i < nv; i++) search[i] = -Mgrad[i] + beta * search[i];
-      }
+      go = m.iterations != 1 && iter < m.iterations && improvement >= R(m.tolerance) && gnorm >= R(m.tolerance);
     }
     d.solver_niter = iter;
     for (int r = 0; r < nefc; r++) d.efc_jar[r] = jar[r];

@@ -111,6 +111,34 @@ def test_trajectory_parity():
         np.testing.assert_allclose(q[i], state_arrays(m, s)["qpos"], atol=1e-3)
 
 
+def test_cg_solver_parity():
+    """train_apg.py:101-105's solver override (CG, 4 iterations, 4 line-search iterations): one step
+    from every state of a random-control GPU trajectory vs the fp32 oracle from the same state.
+    With the line search cut at 4 iterations the answer depends on MJX's zoom rules (solver.py
+    _linesearch), not only on the minimiser, so this pins those rules. Tolerance 5e-3 * s on qvel
+    (s = 1 + max|qvel|; the worst measured step is ~1e-3 * s, at a chaotic contact switch)."""
+    from mjx_amd import mjcf
+    m = mjx_amd.load_model("humanoid_mjx")
+    m.solver, m.iterations, m.ls_iterations = mjcf.SOLVER_CG, 4, 4
+    sys_ = mjx.put_model(m)
+    rng = np.random.default_rng(11)
+    B, T = 48, 12
+    d = _load(sys_, _states(mjx_amd.load_model("humanoid_mjx"), n_random=B - m.nkey, seed=4))  # Newton-made
+    orc = Oracle(m, use_float=True)
+    errs = []
+    for t in range(T):
+        pre = [d.get(f).cpu().numpy().astype(np.float64) for f in ("qpos", "qvel", "qacc_warmstart")]
+        ctrl = rng.uniform(-1, 1, (B, m.nu)).astype(np.float32)
+        mjx.step(sys_, d, torch.tensor(ctrl, device="cuda"))
+        v1 = d.get("qvel").cpu().numpy()
+        for i in range(B):
+            a = state_arrays(m, orc.step(orc.new_state(pre[0][i], pre[1][i], pre[2][i], ctrl[i].astype(np.float64))))
+            errs.append(np.abs(v1[i] - a["qvel"]).max() / (1 + np.abs(a["qvel"]).max()))
+    errs = np.array(errs)
+    assert errs.max() <= 5e-3, f"worst step {errs.max():.2e}"
+    assert np.median(errs) <= 1e-4, f"median step {np.median(errs):.2e}"
+
+
 def test_speedtest_parity():
     m = mjx_amd.load_model("humanoid_mjx")
     sys_ = mjx.put_model(m)

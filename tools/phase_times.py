@@ -46,7 +46,8 @@ for mode in ("speedtest", "trajectory"):
     ok = s[:, 8] > 0
     d8 = np.diff(s[ok][:, [0, 1, 2, 3, 4, 5, 6, 7, 8]], axis=1)
     tot = d8.sum(1).mean()
-    print(f"{mode}: envs with LDS rows {ok.mean():.2f}; mean cycles/env-step {tot:.0f}")
+    print(f"{mode}: envs with LDS rows {ok.mean():.2f}; mean cycles/env-step {tot:.0f}; "
+          f"p50 / p99 / max {np.percentile(d8.sum(1), 50):.0f} / {np.percentile(d8.sum(1), 99):.0f} / {d8.sum(1).max():.0f}")
     for i, n in enumerate(names):
         print(f"   {n:28s} {d8[:, i].mean():9.0f}  {100 * d8[:, i].mean() / tot:5.1f}%")
     it = st[:, 2].mean()
@@ -55,4 +56,9 @@ for mode in ("speedtest", "trajectory"):
                                    "cholesky factor+solve"]):
         v = s[ok][:, i].mean()
         print(f"      {n:26s} {v:9.0f}  per iteration {v / max(it, 1e-9):8.0f}")
+    ls_calls = s[ok][:, 15].mean()
+    if ls_calls > 0:
+        print(f"      line searches per env-step {ls_calls:.2f}; "
+              f"3-point iterations per line search {s[ok][:, 14].mean() / ls_calls:.2f}; "
+              f"per env-step p99 / max {np.percentile(s[ok][:, 14], 99):.0f} / {s[ok][:, 14].max():.0f}")
     buf.zero_()
