@@ -1171,6 +1171,23 @@ template <class D, bool ENV> __global__ __launch_bounds__(64, 1) void vjp_kernel
   if (env >= P.nenv) return;
   const int nq = m->nq, nv = m->nv, nu = m->nu;
   const StateBuf& S = P.s;
+  {  // the VJP is linear in the cotangents: all-zero in -> all-zero out, without the recompute
+     // (envs past termination in an APG rollout; also keeps 0 * non-finite out of their outputs)
+    bool nz = false;
+    if (lane < nq) nz |= V.g_qpos[(size_t)env * nq + lane] != 0.f;
+    if (lane < nv) nz |= V.g_qvel[(size_t)env * nv + lane] != 0.f;
+    if (ENV) {
+      if (lane == 0) nz |= V.g_rew[env] != 0.f;
+      if (lane < MJL_AUX_DIM) nz |= V.g_aux[(size_t)env * MJL_AUX_DIM + lane] != 0.f;
+    }
+    if (__ballot(nz) == 0ull) {
+      if (lane < nq) V.o_qpos[(size_t)env * nq + lane] = 0.f;
+      if (lane < nv) V.o_qvel[(size_t)env * nv + lane] = 0.f;
+      if (lane < nu) V.o_ctrl[(size_t)env * nu + lane] = 0.f;
+      if (ENV && lane < MJL_AUX_DIM) V.o_aux[(size_t)env * MJL_AUX_DIM + lane] = 0.f;
+      return;
+    }
+  }
   float* scr_env = V.scratch + (size_t)env * (size_t)V.scratch_stride;
   GLBA float* scr_adj = (GLBA float*)(scr_env + V.row_floats);
   {  // zero the adjoint workspace and the LD-wide vectors of the forward one

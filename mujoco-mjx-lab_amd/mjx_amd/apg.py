@@ -58,21 +58,33 @@ class APGTrainer:
             with open(os.path.join(self.out_dir, "config.json"), "w") as f:
                 json.dump(_jsonable(cfg), f, indent=2)
 
-    def _obs(self, use_norm: bool):
+    def _obs(self, use_norm: bool, alive: torch.Tensor):
         o = self.env.qpos_qvel().detach().clone().requires_grad_(True)
-        return o, (apg_normalize(self.rms, o) if use_norm else o)
+        # envs out of the loss (past termination, or non-finite) see a zero input: their actions
+        # cannot matter, and where() keeps their non-finite values out of the policy gradient
+        x = torch.where(alive[:, None], o, torch.zeros_like(o))
+        return o, (apg_normalize(self.rms, x) if use_norm else x)
 
     def loss_and_grad(self, use_norm: bool):
-        """One rollout + backward. Returns (loss, mean reward, obs trajectory); grads in .grad."""
+        """One rollout + backward. Returns (loss, mean reward, obs trajectory, envs dropped as
+        non-finite); grads in .grad.
+
+        An env whose state or reward turns non-finite is treated as terminated from that step on
+        (its reward at that step is dropped); an env whose cotangents overflow in the reverse sweep is
+        cut from the gradient at that step. The reference has no such guard: one such env makes its
+        loss NaN and train_apg.py:278-287 stops the run; here the run continues and the count of
+        dropped envs is reported."""
         cfg, env = self.cfg, self.env
         H, B, gamma = cfg.horizon, env.num_envs, cfg.gamma
         env.reset()
         tape, obs_leaves, acts, discs = [], [], [], []
         disc = ret = rsum = None  # created from the first reward (dtype follows the env)
+        alive = torch.ones(B, dtype=torch.bool, device=self.device)
+        dropped = torch.zeros((), device=self.device)
         obs_traj = []
         for _ in range(H):
             tape.append(env.get_state())
-            o, on = self._obs(use_norm)
+            o, on = self._obs(use_norm, alive)
             a = self.policy(on)
             obs_leaves.append(o)
             acts.append(a)
@@ -80,10 +92,15 @@ class APGTrainer:
             _, r, te, tr = env.step(a.detach(), auto_reset=False)
             if disc is None:
                 disc, ret, rsum = torch.ones_like(r), torch.zeros_like(r), torch.zeros_like(r[0])
+            bad = alive & ~(torch.isfinite(r) & torch.isfinite(env.qpos_qvel()).all(1))
+            dropped = dropped + bad.sum()
+            alive = alive & ~bad
+            disc = torch.where(alive, disc, torch.zeros_like(disc))
             discs.append(disc)
-            ret = ret + disc * r
-            rsum = rsum + r.mean()
+            ret = ret + torch.where(alive, disc * r, torch.zeros_like(r))
+            rsum = rsum + torch.where(torch.isfinite(r), r, torch.zeros_like(r)).mean()  # mean(rewards)
             disc = disc * gamma * (1.0 - torch.maximum(te, tr))
+            alive = alive & (disc != 0)
         loss = -ret.mean()
         # reverse sweep: state cotangents of step t+1 -> step t; action cotangents -> policy
         self.opt.zero_grad(set_to_none=True)
@@ -94,11 +111,21 @@ class APGTrainer:
             env.set_state(tape[t])
             grew = -discs[t] / B
             gq, gv, ga, gaux = env.step_vjp(acts[t].detach(), gq, gv, grew, gaux)
+            # an env whose cotangents overflowed (a state blowing up while still in the loss) is cut
+            # from the gradient at this step, like the forward guard above
+            ok = torch.isfinite(gq).all(1) & torch.isfinite(gv).all(1) & torch.isfinite(ga).all(1)
+            if gaux is not None:
+                ok = ok & torch.isfinite(gaux).all(1)
+                gaux = torch.where(ok[:, None], gaux, torch.zeros_like(gaux))
+            dropped = dropped + (~ok).sum()
+            gq = torch.where(ok[:, None], gq, torch.zeros_like(gq))
+            gv = torch.where(ok[:, None], gv, torch.zeros_like(gv))
+            ga = torch.where(ok[:, None], ga, torch.zeros_like(ga))
             torch.autograd.backward(acts[t], grad_tensors=ga)
             og = obs_leaves[t].grad
             gq = gq + og[:, :env.nq]
             gv = gv + og[:, env.nq:]
-        return loss.detach(), (rsum / H).detach(), torch.stack(obs_traj)
+        return loss.detach(), (rsum / H).detach(), torch.stack(obs_traj), dropped
 
     def update(self, step: int) -> dict:
         cfg = self.cfg
@@ -106,28 +133,29 @@ class APGTrainer:
             torch.cuda.synchronize(self.device)
         t0 = time.time()
         use_norm = step >= cfg.obs_warmup_steps and cfg.normalize_observations
-        loss, mean_r, obs_traj = self.loss_and_grad(use_norm)
+        loss, mean_r, obs_traj, dropped = self.loss_and_grad(use_norm)
         params = list(self.policy.parameters())
         g = _flat_grads(params)
-        stats = torch.stack([loss, mean_r])
+        stats = torch.stack([loss, mean_r, dropped.to(loss.dtype)])
         if self.dist is not None:
             self.dist.all_reduce(g)
             g /= self.world
             self.dist.all_reduce(stats)
-            stats /= self.world
-        gnorm = torch.linalg.vector_norm(g)
-        g = g * torch.clamp(cfg.grad_clip / (gnorm + 1e-16), max=1.0)  # optax.clip_by_global_norm
+            stats[:2] /= self.world
+        gnorm = torch.linalg.vector_norm(g.double())  # fp64: an fp32 sum of squares overflows on blow-ups
+        g = g * torch.clamp(cfg.grad_clip / (gnorm + 1e-16), max=1.0).to(g.dtype)  # optax.clip_by_global_norm
         _set_grads(params, g)
         self.opt.step()
         if cfg.normalize_observations and step % cfg.rms_update_every == 0:
-            self.rms.update(obs_traj, self.dist)
+            flat = obs_traj.reshape(-1, obs_traj.shape[-1])
+            self.rms.update(flat[torch.isfinite(flat).all(1)], self.dist)
         if self.device.type == "cuda":
             torch.cuda.synchronize(self.device)
         dt = max(time.time() - t0, 1e-9)
         steps = float(cfg.horizon * self.env.num_envs * self.world)
         self.total_env_steps += steps
         return {"loss": float(stats[0]), "return": float(-stats[0]), "mean_reward": float(stats[1]),
-                "grad_norm": float(gnorm), "env_steps_per_sec": steps / dt}
+                "grad_norm": float(gnorm), "env_steps_per_sec": steps / dt, "nonfinite_envs": int(stats[2])}
 
     def train(self, steps: Optional[int] = None, verbose: bool = True):
         n = self.cfg.total_steps if steps is None else steps

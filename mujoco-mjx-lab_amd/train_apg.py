@@ -24,9 +24,15 @@ from mjx_amd.config import APGConfig  # noqa: E402
 from mjx_amd.envs import HumanoidEnv, resolve_ids  # noqa: E402
 
 
-def apg_model(cfg: APGConfig, name: str = None):
-    """Model with the APG solver options (training_utils.py:95-103, train_apg.py:101-105)."""
+def apg_model(cfg: APGConfig, name: str = None, solver: str = "cg"):
+    """Model with the APG solver options (training_utils.py:95-103, train_apg.py:101-105).
+    solver="model" keeps the MJCF's own solver (Newton 10/20 for humanoid_mjx): the reference forces
+    CG 4/4 because JAX differentiates through the Newton iterations (train_apg.py:101); the VJP here
+    differentiates the converged optimality conditions, so Newton is usable, and it avoids the
+    truncated-solve blow-ups."""
     m = mjx_amd.load_model(name or os.path.splitext(os.path.basename(cfg.xml_path))[0])
+    if solver == "model":
+        return m
     if cfg.lighten_solver:
         m.iterations, m.ls_iterations = 1, 1
     m.solver, m.iterations, m.ls_iterations = mjcf.SOLVER_CG, 4, 4
@@ -41,6 +47,8 @@ def main():
     ap.add_argument("--lr", type=float, default=None)
     ap.add_argument("--seed", type=int, default=None)
     ap.add_argument("--model", default=None, help="humanoid_mjx | humanoid | path to .xml")
+    ap.add_argument("--solver", default="cg", choices=["cg", "model"],
+                    help="cg = train_apg.py's CG 4/4 override; model = the MJCF's solver")
     ap.add_argument("--results-dir", default=None)
     a = ap.parse_args()
 
@@ -60,7 +68,7 @@ def main():
     if world > 1:
         import torch.distributed as dist
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    model = apg_model(cfg, a.model)
+    model = apg_model(cfg, a.model, a.solver)
     from mjx_amd.config import EnvConfig
     env = HumanoidEnv(mjx.put_model(model), resolve_ids(model, EnvConfig()), cfg.batch_size // world,
                       device=local, seed=cfg.seed * 7919 + rank)

@@ -75,7 +75,7 @@ def test_reverse_sweep_equals_autograd_through_rollout():
     tr.policy.double()
     tr.rms.mean = torch.randn(6, dtype=torch.float64) * 0.1
     tr.rms.var = torch.rand(6, dtype=torch.float64) + 0.5
-    loss, _, _ = tr.loss_and_grad(use_norm=True)
+    loss, _, _, _ = tr.loss_and_grad(use_norm=True)
     g_sweep = [p.grad.clone() for p in tr.policy.parameters()]
     # the same loss built as one autograd graph
     env2 = DiffPointEnv(cfg.batch_size, 0)
@@ -157,7 +157,7 @@ def test_humanoid_apg_gradient_matches_oracle_finite_differences():
             return self.env.reset(noise=torch.tensor(noise))
 
     tr = apg.APGTrainer(cfg, FixedReset(henv), device="cuda")
-    loss_gpu, _, _ = tr.loss_and_grad(use_norm=False)
+    loss_gpu, _, _, _ = tr.loss_and_grad(use_norm=False)
     params = list(tr.policy.parameters())
     grad = torch.cat([p.grad.reshape(-1) for p in params]).double().cpu()
     d = torch.randn(grad.numel(), generator=torch.Generator().manual_seed(1), dtype=torch.float64)

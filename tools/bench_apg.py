@@ -31,10 +31,7 @@ def main():
     a = ap.parse_args()
     cfg = APGConfig()
     cfg.batch_size, cfg.horizon = a.envs, a.horizon
-    m = apg_model(cfg)
-    if a.solver == "model":
-        import mjx_amd
-        m = mjx_amd.load_model("humanoid_mjx")
+    m = apg_model(cfg, solver=a.solver)
     env = HumanoidEnv(mjx.put_model(m), resolve_ids(m, EnvConfig()), cfg.batch_size, seed=cfg.seed)
     tr = APGTrainer(cfg, HumanoidAPGEnv(env), device="cuda")
     tr.update(0)  # warm-up
@@ -56,7 +53,8 @@ def main():
         "metric": "APG env-steps/s (rollout + backward through sim + Adam, synced)", "value": sps,
         "envs": cfg.batch_size, "horizon": cfg.horizon, "solver": a.solver, "update_s": upd,
         "forward_rollout_s": fwd, "backward_s_est": upd - fwd,
-        "returns": [r["return"] for r in res], "grad_norms": [r["grad_norm"] for r in res]}))
+        "returns": [r["return"] for r in res], "grad_norms": [r["grad_norm"] for r in res],
+        "nonfinite_envs": [r["nonfinite_envs"] for r in res]}))
 
 
 if __name__ == "__main__":
