@@ -223,6 +223,13 @@ int mjl_env_step_vjp(mjlBatch* batch, const float* act, const float* g_qpos, con
                      const float* g_rew, const float* g_aux, float* out_qpos, float* out_qvel,
                      float* out_act, float* out_aux, void* stream);
 
+/* Replaces compute_gae (train_ppo.py:171-202, a reverse lax.scan over the rollout): rew, term,
+ * trunc [T, B], val [T+1, B] (val[T] = value of the obs after the last step) -> adv, ret [T, B],
+ * delta = r + gamma V' (1 - term) - V, A = delta + gamma lam (1 - max(term, trunc)) A', ret = A + V.
+ * Device pointers, float32, row-major; bit-identical to the elementwise formula (no contraction). */
+int mjl_gae(const float* rew, const float* val, const float* term, const float* trunc, int T, int B,
+            double gamma, double lam, float* adv, float* ret, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

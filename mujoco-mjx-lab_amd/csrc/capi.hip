@@ -11,6 +11,7 @@
 
 #include "step_kernels.hip"
 #include "adjoint.hip"
+#include "ppo_kernels.hip"
 
 using namespace mjl;
 
@@ -551,3 +552,14 @@ int mjl_env_step_vjp(mjlBatch* B, const float* act, const float* g_qpos, const f
 }
 
 }  // extern "C"
+
+// ---------------------------------------------------------------- PPO host-loop kernels
+extern "C" int mjl_gae(const float* rew, const float* val, const float* term, const float* trunc, int T, int B,
+                       double gamma, double lam, float* adv, float* ret, void* stream) {
+  if (!rew || !val || !term || !trunc || !adv || !ret || T < 0 || B < 0) return fail(MJL_ERR_ARG, "bad argument");
+  if (T == 0 || B == 0) return MJL_OK;
+  hipLaunchKernelGGL(gae_kernel, dim3((B + 255) / 256), dim3(256), 0, (hipStream_t)stream, rew, val, term, trunc, T,
+                     B, (float)gamma, (float)(gamma * lam), adv, ret);
+  HIPCHK(hipGetLastError());
+  return MJL_OK;
+}
