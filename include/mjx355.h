@@ -200,6 +200,13 @@ int mjl_env_config(mjlBatch* batch, const mjlEnvConfig* cfg);
 int mjl_env_step(mjlBatch* batch, const float* act, float* obs, float* rew, float* term,
                  float* trunc, int auto_reset, uint64_t seed, uint64_t counter, void* stream);
 
+/* RNG counter base for hipGraph capture of env steps / resets: if dev_counter_base (a device
+ * uint64, may be NULL to detach) is set, the kernels draw with counter = the call's `counter` +
+ * *dev_counter_base read at execution time, so a captured sequence of calls with counters 1..T
+ * replays with fresh draws after the caller advances the base (src/envs.py:117 splits a fresh key
+ * per reset; train_ppo.py:150 draws per rollout step). Eager callers leave it unset. */
+int mjl_batch_set_counter_base(mjlBatch* batch, const uint64_t* dev_counter_base);
+
 /* Replaces v_reset (src/envs.py:115-202,494) restricted to envs with mask > 0.5 (mask may be
  * NULL = all). obs [nenv, obs_dim] is written for reset envs only. `noise` (device, may be NULL)
  * overrides the on-device RNG with explicit draws [nenv, nq-7 + nv + 2] in [0,1):

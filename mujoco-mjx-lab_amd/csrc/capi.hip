@@ -58,6 +58,7 @@ struct mjlBatch {
   int scratch_stride, gmax_efc, gmax_con;
   float* d_adj_scratch;  // step VJP: per env row slab + adjoint scratch (allocated on first use)
   int adj_stride, adj_row_floats;
+  const unsigned long long* ctr_base;  // device RNG counter base (mjl_batch_set_counter_base), or null
 };
 
 extern "C" {
@@ -414,6 +415,7 @@ static KParams make_params(mjlBatch* B) {
   P.scratch_stride = B->scratch_stride;
   P.gmax_efc = B->gmax_efc;
   P.gmax_con = B->gmax_con;
+  P.ctr_base = B->ctr_base;
   return P;
 }
 
@@ -486,6 +488,12 @@ int mjl_env_step(mjlBatch* B, const float* act, float* obs, float* rew, float* t
   P.seed_lo = (uint32_t)seed; P.seed_hi = (uint32_t)(seed >> 32);
   P.ctr_lo = (uint32_t)counter; P.ctr_hi = (uint32_t)(counter >> 32);
   return launch<MODE_ENV_STEP>(B, P, stream);
+}
+
+int mjl_batch_set_counter_base(mjlBatch* B, const uint64_t* dev_counter_base) {
+  if (!B) return fail(MJL_ERR_ARG, "null batch");
+  B->ctr_base = (const unsigned long long*)dev_counter_base;
+  return MJL_OK;
 }
 
 int mjl_env_reset(mjlBatch* B, const float* mask, uint64_t seed, uint64_t counter, const float* noise, float* obs,

@@ -116,6 +116,7 @@ struct KParams {
   int scratch_stride;    // floats per env
   int gmax_efc, gmax_con; // row / contact capacity of one scratch slab
   uint32_t seed_lo, seed_hi, ctr_lo, ctr_hi;
+  const unsigned long long* ctr_base;  // device counter base added to (ctr_hi, ctr_lo), or null
 };
 
 }  // namespace mjl

@@ -1697,7 +1697,11 @@ template <class D, int MODE> __global__ __launch_bounds__(64, MJL_MINWAVES) void
   EnvArgs A;
   A.cfg = P.env; A.noise = P.noise; A.scratch_env = P.scratch + (size_t)env * (size_t)P.scratch_stride;
   A.gmax_efc = P.gmax_efc; A.gmax_con = P.gmax_con; A.force_global = P.force_global_rows;
-  A.s0 = P.seed_lo; A.s1 = P.seed_hi; A.c0 = P.ctr_lo; A.c1 = P.ctr_hi;
+  A.s0 = P.seed_lo; A.s1 = P.seed_hi;
+  {  // RNG counter = launch counter + the batch's device counter base (hipGraph replays)
+    unsigned long long c = ((unsigned long long)P.ctr_hi << 32 | P.ctr_lo) + (P.ctr_base ? *P.ctr_base : 0ull);
+    A.c0 = (uint32_t)c; A.c1 = (uint32_t)(c >> 32);
+  }
 
   // vectors beyond nv must read as zero in the LD-wide row kernels
   for (int i = lane; i < LD; i += 64) {

@@ -21,7 +21,7 @@ EXPORTS = [
     "mjl_last_error", "mjl_version", "mjl_model_create", "mjl_model_destroy", "mjl_model_nefc_max",
     "mjl_batch_create", "mjl_batch_destroy", "mjl_batch_nenv", "mjl_batch_set_option", "mjl_get", "mjl_set",
     "mjl_forward", "mjl_step", "mjl_speedtest_step", "mjl_env_config", "mjl_env_step", "mjl_env_reset",
-    "mjl_step_vjp", "mjl_env_step_vjp", "mjl_gae",
+    "mjl_step_vjp", "mjl_env_step_vjp", "mjl_gae", "mjl_batch_set_counter_base",
 ]
 
 _lib = None
@@ -79,6 +79,7 @@ def lib() -> C.CDLL:
     L.mjl_env_config.argtypes = [vp, P(abi.EnvConfigC)]
     L.mjl_env_step.argtypes = [vp, f32p, f32p, f32p, f32p, f32p, i32, u64, u64, vp]
     L.mjl_env_reset.argtypes = [vp, f32p, u64, u64, f32p, f32p, vp]
+    L.mjl_batch_set_counter_base.argtypes = [vp, vp]
     L.mjl_gae.argtypes = [f32p, f32p, f32p, f32p, i32, i32, C.c_double, C.c_double, f32p, f32p, vp]
     L.mjl_step_vjp.argtypes = [vp, f32p, f32p, f32p, f32p, f32p, vp]
     L.mjl_env_step_vjp.argtypes = [vp, f32p, f32p, f32p, f32p, f32p, f32p, f32p, f32p, f32p, vp]

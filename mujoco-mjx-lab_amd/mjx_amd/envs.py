@@ -57,6 +57,10 @@ class HumanoidEnv:
         self.trunc = torch.zeros(self.num_envs, dtype=torch.float32, device=dev)
         self.seed = int(seed) & 0xFFFFFFFFFFFFFFFF
         self.counter = 0
+        # device RNG counter base (0 in eager use): a hipGraph-captured rollout passes counters
+        # 1..T and the trainer moves the base before each replay (mjl_batch_set_counter_base)
+        self.ctr_base = torch.zeros(1, dtype=torch.int64, device=dev)
+        check(lib().mjl_batch_set_counter_base(self.data.handle, C.c_void_p(self.ctr_base.data_ptr())))
 
     def _next_counter(self) -> int:
         self.counter += 1
@@ -72,15 +76,17 @@ class HumanoidEnv:
         return self.obs
 
     def step(self, act: torch.Tensor, auto_reset: bool = True,
-             out: Optional[Tuple[torch.Tensor, ...]] = None) -> Tuple[torch.Tensor, ...]:
+             out: Optional[Tuple[torch.Tensor, ...]] = None, counter: Optional[int] = None) -> Tuple[torch.Tensor, ...]:
         """v_step (src/envs.py:333-495) fused with merge_if_done (train_ppo.py:147-161).
-        Returns (obs, reward, terminated, truncated); obs is post-reset for finished envs."""
+        Returns (obs, reward, terminated, truncated); obs is post-reset for finished envs.
+        `counter` (graph capture) is the RNG counter relative to `ctr_base`; default: the next one."""
         act = act.to(self.obs.device, torch.float32).contiguous()
         if act.shape != (self.num_envs, self.act_dim):
             raise MjlError(f"action must have shape {(self.num_envs, self.act_dim)}")
         obs, rew, term, trunc = out if out is not None else (self.obs, self.rew, self.term, self.trunc)
         check(lib().mjl_env_step(self.data.handle, _ptr(act), _ptr(obs), _ptr(rew), _ptr(term), _ptr(trunc),
-                                 int(auto_reset), self.seed, self._next_counter(), _stream()))
+                                 int(auto_reset), self.seed, self._next_counter() if counter is None else int(counter),
+                                 _stream()))
         return obs, rew, term, trunc
 
     def step_vjp(self, act: torch.Tensor, g_qpos: torch.Tensor, g_qvel: torch.Tensor, g_rew: torch.Tensor,

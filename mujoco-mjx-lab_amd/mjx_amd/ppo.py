@@ -112,7 +112,10 @@ class RunningMeanStd:
         tot = self.count + n
         new_mean = self.mean + delta * n / tot
         m2 = self.var * self.count + bvar * n + delta * delta * self.count * n / tot
-        self.mean, self.var, self.count = new_mean, torch.clamp(m2 / tot, min=1e-4), tot
+        # in place: a captured rollout graph reads these tensors at replay time
+        self.mean.copy_(new_mean)
+        self.var.copy_(torch.clamp(m2 / tot, min=1e-4))
+        self.count.copy_(tot)
 
     def normalize(self, x, clip: float = 10.0):
         """normalize_obs + the clip to [-10, 10] the trainers apply (train_ppo.py:134-135)."""
@@ -122,7 +125,9 @@ class RunningMeanStd:
         return {"mean": self.mean, "var": self.var, "count": self.count}
 
     def load_state_dict(self, d):
-        self.mean, self.var, self.count = d["mean"], d["var"], d["count"]
+        self.mean.copy_(d["mean"])
+        self.var.copy_(d["var"])
+        self.count.copy_(d["count"])
 
 
 # ---------------------------------------------------------------------------------- PPO formulas
@@ -250,7 +255,8 @@ class PPOTrainer:
     """train_ppo.py:64-441 over any env exposing reset() -> obs, step(act) -> (obs, rew, term, trunc)
     with auto-reset (HumanoidEnv, or a stand-in in CPU tests), obs_dim, act_dim, num_envs."""
 
-    def __init__(self, cfg, env, eval_env=None, device="cuda", dist=None, out_dir: Optional[str] = None):
+    def __init__(self, cfg, env, eval_env=None, device="cuda", dist=None, out_dir: Optional[str] = None,
+                 use_graph: bool = True):
         self.cfg, self.env, self.eval_env, self.dist = cfg, env, eval_env, dist
         self.rank = dist.get_rank() if dist is not None else 0
         self.world = dist.get_world_size() if dist is not None else 1
@@ -269,6 +275,8 @@ class PPOTrainer:
         self.gen = torch.Generator(device=self.device).manual_seed(int(cfg.seed) * 1000 + self.rank)
         self.idx_gen = torch.Generator().manual_seed(int(cfg.seed) + 7919 * (self.rank + 1))
         self.obs = env.reset().clone()
+        self.use_graph = bool(use_graph)
+        self._buf, self._graph, self._rollouts = None, None, 0
         self.total_env_steps = 0.0
         self.start = time.time()
         self.out_dir = out_dir if self.rank == 0 else None
@@ -279,27 +287,59 @@ class PPOTrainer:
                 json.dump(_jsonable(cfg), f, indent=2)
 
     # train_ppo.py:128-169
+    def _rollout_buffers(self):
+        if self._buf is None:
+            T, B, env, dev = self.cfg.rollout_length, self.env.num_envs, self.env, self.device
+            self._buf = {
+                "obs": torch.empty((T, B, env.obs_dim), device=dev), "act": torch.empty((T, B, env.act_dim), device=dev),
+                "logp": torch.empty((T, B), device=dev), "rew": torch.empty((T, B), device=dev),
+                "term": torch.empty((T, B), device=dev), "trunc": torch.empty((T, B), device=dev),
+                "eps": torch.empty((T, B, env.act_dim), device=dev), "obs_in": torch.empty((B, env.obs_dim), device=dev)}
+        return self._buf
+
+    def _rollout_body(self, graph: bool):
+        """One rollout into the static buffers; with graph=True the RNG counters are relative to the
+        env's device counter base (the body is being captured)."""
+        bf, env = self._buf, self.env
+        obs = bf["obs_in"]
+        for t in range(self.cfg.rollout_length):
+            bf["obs"][t].copy_(obs)
+            mean, log_std = self.policy(self.rms.normalize(obs))
+            act = mean + torch.exp(log_std) * bf["eps"][t]
+            bf["act"][t].copy_(act)
+            bf["logp"][t].copy_(gaussian_logprob(mean, log_std, act))
+            # physics + reward + obs + merge_if_done, one launch
+            o2, r, te, tr = env.step(act, counter=t + 1) if graph else env.step(act)
+            bf["rew"][t].copy_(r)
+            bf["term"][t].copy_(te)
+            bf["trunc"][t].copy_(tr)
+            obs = o2
+        bf["obs_in"].copy_(obs)
+
     @torch.no_grad()
     def collect_rollout(self):
-        T, B, env = self.cfg.rollout_length, self.env.num_envs, self.env
-        dev = self.device
-        obs_t = torch.empty((T, B, env.obs_dim), device=dev)
-        act_t = torch.empty((T, B, env.act_dim), device=dev)
-        logp_t = torch.empty((T, B), device=dev)
-        r_t, te_t, tr_t = (torch.empty((T, B), device=dev) for _ in range(3))
-        obs = self.obs
-        for t in range(T):
-            obs_t[t] = obs
-            mean, log_std = self.policy(self.rms.normalize(obs))
-            eps = torch.randn(mean.shape, generator=self.gen, device=dev)
-            act = mean + torch.exp(log_std) * eps
-            act_t[t] = act
-            logp_t[t] = gaussian_logprob(mean, log_std, act)
-            o2, r, te, tr = env.step(act)  # physics + reward + obs + merge_if_done, one launch
-            r_t[t], te_t[t], tr_t[t] = r, te, tr
-            obs = o2
-        self.obs = obs.clone()
-        return obs_t, act_t, logp_t, r_t, te_t, tr_t
+        """Rollout of T steps. On the GPU the second and later rollouts replay one hipGraph of the
+        whole T-step loop (policy GEMMs, sampling, log-prob, env step; ~20 launches per step
+        otherwise): the sampling noise for all T steps is drawn before it, and the env RNG counters
+        come from the env's device counter base, so a replay is bit-identical to the eager loop."""
+        bf, env, T = self._rollout_buffers(), self.env, self.cfg.rollout_length
+        bf["eps"].normal_(generator=self.gen)
+        bf["obs_in"].copy_(self.obs)
+        use_graph = self.use_graph and self.device.type == "cuda" and hasattr(env, "ctr_base")
+        if use_graph and self._graph is None and self._rollouts > 0:
+            self._graph = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(self._graph):
+                self._rollout_body(graph=True)
+        if use_graph and self._graph is not None:
+            env.ctr_base.fill_(env.counter)
+            self._graph.replay()
+            env.counter += T
+            env.ctr_base.zero_()
+        else:
+            self._rollout_body(graph=False)
+        self._rollouts += 1
+        self.obs = bf["obs_in"]
+        return bf["obs"], bf["act"], bf["logp"], bf["rew"], bf["term"], bf["trunc"]
 
     def iteration(self, it: int) -> dict:
         cfg, dev = self.cfg, self.device

@@ -245,3 +245,29 @@ def test_native_gae_bit_identical_to_formula():
         a, ret = ppo.compute_gae(r, v, te, tr, 0.99, 0.95)
         a_ref, ret_ref = ppo.compute_gae_torch(r, v, te, tr, 0.99, 0.95)
         assert torch.equal(a, a_ref) and torch.equal(ret, ret_ref)
+
+
+@pytest.mark.gpu
+def test_graph_rollout_bit_identical_to_eager():
+    """The hipGraph replay of the T-step rollout (policy, sampling, log-prob, fused env step with
+    auto-reset) reproduces the eager loop bit for bit, including the env's reset RNG draws (device
+    counter base) and observation statistics updated in place between rollouts."""
+    import mjx_amd
+    from mjx_amd import mjx
+    from mjx_amd.envs import HumanoidEnv, resolve_ids
+    m = mjx_amd.load_model("humanoid_mjx")
+    cfg = small_cfg(num_envs=256, rollout_length=24)
+    cfg.env_config.max_episode_steps = 10  # truncations -> auto-resets inside the captured steps
+    ecfg = resolve_ids(m, cfg.env_config)
+    trs = [ppo.PPOTrainer(cfg, HumanoidEnv(mjx.put_model(m), ecfg, cfg.num_envs, seed=11), None, device="cuda",
+                          use_graph=g) for g in (False, True)]
+    for it in range(3):
+        outs = []
+        for tr in trs:
+            bufs = [x.clone() for x in tr.collect_rollout()]
+            tr.rms.update(bufs[0])
+            outs.append(bufs)
+        assert trs[1]._graph is not None or it == 0
+        for a, b in zip(*outs):
+            assert torch.equal(a, b), f"rollout {it}"
+        assert outs[0][5].sum() > 0  # truncations happened

@@ -35,6 +35,7 @@ def main():
     env = HumanoidEnv(sys_, ecfg, cfg.num_envs, seed=cfg.seed)
     tr = ppo.PPOTrainer(cfg, env, None, device="cuda")
     tr.iteration(0)  # warm-up (GEMM heuristics, allocator)
+    tr.iteration(0)  # second rollout captures the rollout hipGraph
     res, t_roll = [], []
     for it in range(1, a.iters + 1):
         torch.cuda.synchronize()
