@@ -27,6 +27,34 @@ ACTIVATIONS = {
 
 
 # ----------------------------------------------------------------------------------------- networks
+class _SplitKLinear(torch.autograd.Function):
+    """y = x Wᵀ + b whose weight gradient Wᵀ-shaped dY ᵀ X (K = the batch, 65,536 rows in a PPO
+    minibatch, output only 256 x 256) runs as `splits` batched GEMMs of K / splits rows plus one
+    sum: as a single GEMM the library tiles the small output into 32 workgroups and leaves most
+    of the 256 CUs idle (measured 37 TFLOP/s on MI355X)."""
+
+    @staticmethod
+    def forward(ctx, x, w, b, splits):
+        ctx.save_for_backward(x, w)
+        ctx.splits = splits
+        return torch.addmm(b, x, w.t())
+
+    @staticmethod
+    def backward(ctx, gy):
+        x, w = ctx.saved_tensors
+        s, n = ctx.splits, x.shape[0]
+        gx = gy @ w if ctx.needs_input_grad[0] else None
+        gw = torch.bmm(gy.reshape(s, n // s, -1).transpose(1, 2), x.reshape(s, n // s, -1)).sum(0)
+        return gx, gw, gy.sum(0), None
+
+
+def _linear(lin: nn.Linear, x: torch.Tensor) -> torch.Tensor:
+    n = x.shape[0] if x.dim() == 2 else 0
+    if x.is_cuda and torch.is_grad_enabled() and n >= 16384 and n % 2048 == 0:
+        return _SplitKLinear.apply(x, lin.weight, lin.bias, min(32, n // 2048))
+    return lin(x)
+
+
 class MLP(nn.Module):
     """src/networks.py:22-61: layers of (features, activation); Glorot-normal weights
     N(0, 2/(in+out)), zero biases (networks.py:32-53). Unknown activations fall back to tanh."""
@@ -46,7 +74,7 @@ class MLP(nn.Module):
 
     def forward(self, x):
         for lin, a in zip(self.layers, self.acts):
-            x = ACTIVATIONS.get(a, torch.tanh)(lin(x))
+            x = ACTIVATIONS.get(a, torch.tanh)(_linear(lin, x))
         return x
 
 

@@ -271,3 +271,23 @@ def test_graph_rollout_bit_identical_to_eager():
         for a, b in zip(*outs):
             assert torch.equal(a, b), f"rollout {it}"
         assert outs[0][5].sum() > 0  # truncations happened
+
+
+@pytest.mark.gpu
+def test_split_k_linear_gradients():
+    """The minibatch-size Linear (split-K weight gradient) matches nn.Linear's gradients within fp32
+    summation noise, for every layer shape of the reference nets."""
+    g = torch.Generator(device="cuda").manual_seed(0)
+    for fin, fout in ((54, 256), (256, 256), (256, 21), (256, 1)):
+        lin = torch.nn.Linear(fin, fout).cuda()
+        x = torch.randn((65536, fin), generator=g, device="cuda", requires_grad=True)
+        gy = torch.randn((65536, fout), generator=g, device="cuda")
+        y = ppo._linear(lin, x)
+        y.backward(gy)
+        got = [x.grad.clone(), lin.weight.grad.clone(), lin.bias.grad.clone()]
+        x.grad = None
+        lin.zero_grad()
+        torch.testing.assert_close(y, torch.nn.functional.linear(x, lin.weight, lin.bias), rtol=1e-5, atol=1e-5)
+        torch.nn.functional.linear(x, lin.weight, lin.bias).backward(gy)
+        for a, b in zip(got, [x.grad, lin.weight.grad, lin.bias.grad]):  # sums of 65,536 terms: scale-relative
+            assert (a - b).abs().max() <= 2e-5 * b.abs().max(), (fin, fout)
