@@ -162,10 +162,11 @@ class RunningMeanStd:
 LOG2PI = math.log(2.0 * math.pi)
 
 
-def gaussian_logprob(mean, log_std, action):
+def gaussian_logprob(mean, log_std, action, out=None):
     """train_ppo.py:121-126: diagonal Gaussian log-density summed over action dims."""
     var = torch.exp(2.0 * log_std)
-    return -0.5 * torch.sum((action - mean) ** 2 / var + 2.0 * log_std + LOG2PI, dim=-1)
+    s = torch.sum((action - mean) ** 2 / var + 2.0 * log_std + LOG2PI, dim=-1)
+    return s.mul_(-0.5) if out is None else torch.mul(s, -0.5, out=out)
 
 
 def gaussian_entropy(log_std, act_dim):
@@ -319,30 +320,30 @@ class PPOTrainer:
         if self._buf is None:
             T, B, env, dev = self.cfg.rollout_length, self.env.num_envs, self.env, self.device
             self._buf = {
-                "obs": torch.empty((T, B, env.obs_dim), device=dev), "act": torch.empty((T, B, env.act_dim), device=dev),
+                "obs": torch.empty((T + 1, B, env.obs_dim), device=dev), "act": torch.empty((T, B, env.act_dim), device=dev),
                 "logp": torch.empty((T, B), device=dev), "rew": torch.empty((T, B), device=dev),
                 "term": torch.empty((T, B), device=dev), "trunc": torch.empty((T, B), device=dev),
-                "eps": torch.empty((T, B, env.act_dim), device=dev), "obs_in": torch.empty((B, env.obs_dim), device=dev)}
+                "eps": torch.empty((T, B, env.act_dim), device=dev)}
         return self._buf
 
     def _rollout_body(self, graph: bool):
-        """One rollout into the static buffers; with graph=True the RNG counters are relative to the
-        env's device counter base (the body is being captured)."""
+        """One rollout into the static buffers: obs[t] is the obs before step t, the env writes
+        obs[t + 1], rew / term / trunc [t] in place (no copies). With graph=True the RNG counters are
+        relative to the env's device counter base (the body is being captured)."""
         bf, env = self._buf, self.env
-        obs = bf["obs_in"]
         for t in range(self.cfg.rollout_length):
-            bf["obs"][t].copy_(obs)
-            mean, log_std = self.policy(self.rms.normalize(obs))
-            act = mean + torch.exp(log_std) * bf["eps"][t]
-            bf["act"][t].copy_(act)
-            bf["logp"][t].copy_(gaussian_logprob(mean, log_std, act))
+            mean, log_std = self.policy(self.rms.normalize(bf["obs"][t]))
+            act = torch.addcmul(mean, torch.exp(log_std), bf["eps"][t], out=bf["act"][t])
+            gaussian_logprob(mean, log_std, act, out=bf["logp"][t])
             # physics + reward + obs + merge_if_done, one launch
-            o2, r, te, tr = env.step(act, counter=t + 1) if graph else env.step(act)
-            bf["rew"][t].copy_(r)
-            bf["term"][t].copy_(te)
-            bf["trunc"][t].copy_(tr)
-            obs = o2
-        bf["obs_in"].copy_(obs)
+            out = (bf["obs"][t + 1], bf["rew"][t], bf["term"][t], bf["trunc"][t])
+            if graph:
+                env.step(act, out=out, counter=t + 1)
+            elif hasattr(env, "ctr_base"):
+                env.step(act, out=out)
+            else:  # envs without output buffers (CPU stand-ins)
+                for dst, src in zip(out, env.step(act)):
+                    dst.copy_(src)
 
     @torch.no_grad()
     def collect_rollout(self):
@@ -352,7 +353,7 @@ class PPOTrainer:
         come from the env's device counter base, so a replay is bit-identical to the eager loop."""
         bf, env, T = self._rollout_buffers(), self.env, self.cfg.rollout_length
         bf["eps"].normal_(generator=self.gen)
-        bf["obs_in"].copy_(self.obs)
+        bf["obs"][0].copy_(self.obs)
         use_graph = self.use_graph and self.device.type == "cuda" and hasattr(env, "ctr_base")
         if use_graph and self._graph is None and self._rollouts > 0:
             self._graph = torch.cuda.CUDAGraph()
@@ -366,8 +367,8 @@ class PPOTrainer:
         else:
             self._rollout_body(graph=False)
         self._rollouts += 1
-        self.obs = bf["obs_in"]
-        return bf["obs"], bf["act"], bf["logp"], bf["rew"], bf["term"], bf["trunc"]
+        self.obs = bf["obs"][T]
+        return bf["obs"][:T], bf["act"], bf["logp"], bf["rew"], bf["term"], bf["trunc"]
 
     def iteration(self, it: int) -> dict:
         cfg, dev = self.cfg, self.device
