@@ -1221,6 +1221,7 @@ template <class D, bool ENV> __global__ __launch_bounds__(64, 1) void vjp_kernel
   }
   SYNC();
   // ---- forward (forward() + integrate(), rows in the env's global slab)
+  STAMP(0, lane);
   kinematics<D>(m, W, lane);
   com_pos_crb<D>(m, W, lane);
   velocity_stage<D>(m, W, lane);
@@ -1237,23 +1238,36 @@ template <class D, bool ENV> __global__ __launch_bounds__(64, 1) void vjp_kernel
   chol_factor_solve<D>(W->H, A->Lc, A->invdc, nv, W->frc_smooth, lane);
   SYNC();
   integrate<D>(m, W, lane, A->ap);
+  STAMP(1, lane);
   // ---- reverse
   const float* gq = V.g_qpos + (size_t)env * nq;
   if (lane < nv) A->vtmp[lane] = V.g_qvel[(size_t)env * nv + lane];
   SYNC();
   if (ENV) adj_env<D>(m, W, A, (CP)P.env, (const float*)aux, V.g_rew[env], V.g_aux + (size_t)env * MJL_AUX_DIM, lane);
   adj_integrate<D>(m, W, A, gq, lane);
+  STAMP(2, lane);
   adj_solver_rows<D>(m, W, A, R, scr_adj, P.gmax_efc, lane);
+  STAMP(3, lane);
   adj_contact_jac<D>(m, W, A, R, scr_adj, P.gmax_efc, lane);
+  STAMP(4, lane);
   adj_collision<D>(m, W, A, R, scr_adj, P.gmax_efc, lane);
+  STAMP(5, lane);
   adj_geom_frames<D>(m, A, lane);
+  STAMP(6, lane);
   adj_forces<D>(m, W, A, lane);
+  STAMP(7, lane);
   adj_rne<D>(m, W, A, lane);
+  STAMP(8, lane);
   adj_mass<D>(m, W, A, lane);
+  STAMP(9, lane);
   adj_crb<D>(m, A, lane);
+  STAMP(10, lane);
   adj_cinert<D>(m, W, A, lane);
+  STAMP(11, lane);
   adj_cdof<D>(m, W, A, lane);
+  STAMP(12, lane);
   adj_kinematics<D>(m, W, A, lane);
+  STAMP(13, lane);
   // ---- outputs
   if (lane < nq) V.o_qpos[(size_t)env * nq + lane] = A->qposb[lane];
   if (lane < nv) V.o_qvel[(size_t)env * nv + lane] = A->qvelb[lane];

@@ -102,6 +102,7 @@ class APGTrainer:
             disc = disc * gamma * (1.0 - torch.maximum(te, tr))
             alive = alive & (disc != 0)
         loss = -ret.mean()
+        final = env.get_state()
         # reverse sweep: state cotangents of step t+1 -> step t; action cotangents -> policy
         self.opt.zero_grad(set_to_none=True)
         gq = torch.zeros((B, env.nq), device=self.device)
@@ -109,6 +110,8 @@ class APGTrainer:
         gaux = None
         for t in range(H - 1, -1, -1):
             env.set_state(tape[t])
+            if hasattr(env, "set_warmstart"):  # the step's own solution seeds the VJP's recompute
+                env.set_warmstart((tape[t + 1] if t + 1 < H else final)["qacc_warmstart"])
             grew = -discs[t] / B
             gq, gv, ga, gaux = env.step_vjp(acts[t].detach(), gq, gv, grew, gaux)
             # an env whose cotangents overflowed (a state blowing up while still in the loss) is cut
@@ -207,6 +210,12 @@ class HumanoidAPGEnv:
     def set_state(self, st):
         for k in self.FIELDS:
             self.env.data.set(k, st[k])
+
+    def set_warmstart(self, qacc):
+        """The VJP recomputes the step to find its converged active set; seeding the solver with the
+        solution the forward step reached (the next tape entry's qacc_warmstart) cuts the recompute
+        to ~one Newton iteration."""
+        self.env.data.set("qacc_warmstart", qacc)
 
     def step_vjp(self, act, gq, gv, grew, gaux):
         return self.env.step_vjp(act, gq, gv, grew, gaux)
