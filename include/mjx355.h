@@ -207,6 +207,22 @@ int mjl_env_step(mjlBatch* batch, const float* act, float* obs, float* rew, floa
  * per reset; train_ppo.py:150 draws per rollout step). Eager callers leave it unset. */
 int mjl_batch_set_counter_base(mjlBatch* batch, const uint64_t* dev_counter_base);
 
+/* jax.random key modes: element i of a draw / split is threefry2x32(key, (0, i)) (jax >= 0.5
+ * default, jax_threefry_partitionable; the reference pins jax==0.7.2, requirements.txt:17), or
+ * the pre-0.5 layout (threefry over iota halves). */
+enum { MJL_RNG_JAX_PARTITIONABLE = 1, MJL_RNG_JAX_ORIGINAL = 2 };
+
+/* Replaces v_reset(keys) / merge_if_done's v_reset(random.split(key_reset, num_envs)) key input
+ * (src/envs.py:116-147, train_ppo.py:150-152): if dev_keys (device uint32 [nenv, 2], read at
+ * execution time; NULL detaches) is set, env resets — mjl_env_reset and the auto-reset of
+ * mjl_env_step — draw from env e's jax.random key exactly as single_reset does (split(key, 4);
+ * uniform(k1, (nq-7,)), uniform(k2, (nv,)), bernoulli(k3, .5), uniform(k4, (), 0, v_max)) instead of
+ * (seed, counter): identical reset states to MJX for identical keys. */
+int mjl_env_set_reset_keys(mjlBatch* batch, const uint32_t* dev_keys, int mode);
+
+/* jax.random.split(key, num) for n keys at once: keys uint32 [n, 2] -> out [n, num, 2] (device). */
+int mjl_prng_split(const uint32_t* keys, int n, int num, int mode, uint32_t* out, void* stream);
+
 /* Replaces v_reset (src/envs.py:115-202,494) restricted to envs with mask > 0.5 (mask may be
  * NULL = all). obs [nenv, obs_dim] is written for reset envs only. `noise` (device, may be NULL)
  * overrides the on-device RNG with explicit draws [nenv, nq-7 + nv + 2] in [0,1):

@@ -59,6 +59,8 @@ struct mjlBatch {
   float* d_adj_scratch;  // step VJP: per env row slab + adjoint scratch (allocated on first use)
   int adj_stride, adj_row_floats;
   const unsigned long long* ctr_base;  // device RNG counter base (mjl_batch_set_counter_base), or null
+  const uint32_t* reset_keys;           // per-env jax.random reset keys (mjl_env_set_reset_keys), or null
+  int key_mode;
 };
 
 extern "C" {
@@ -416,6 +418,8 @@ static KParams make_params(mjlBatch* B) {
   P.gmax_efc = B->gmax_efc;
   P.gmax_con = B->gmax_con;
   P.ctr_base = B->ctr_base;
+  P.keys = B->reset_keys;
+  P.key_mode = B->key_mode;
   return P;
 }
 
@@ -496,6 +500,15 @@ int mjl_batch_set_counter_base(mjlBatch* B, const uint64_t* dev_counter_base) {
   return MJL_OK;
 }
 
+int mjl_env_set_reset_keys(mjlBatch* B, const uint32_t* dev_keys, int mode) {
+  if (!B) return fail(MJL_ERR_ARG, "null batch");
+  if (dev_keys && mode != MJL_RNG_JAX_PARTITIONABLE && mode != MJL_RNG_JAX_ORIGINAL)
+    return fail(MJL_ERR_ARG, "unknown key mode %d", mode);
+  B->reset_keys = dev_keys;
+  B->key_mode = mode;
+  return MJL_OK;
+}
+
 int mjl_env_reset(mjlBatch* B, const float* mask, uint64_t seed, uint64_t counter, const float* noise, float* obs,
                   void* stream) {
   if (!B) return fail(MJL_ERR_ARG, "null batch");
@@ -568,6 +581,38 @@ extern "C" int mjl_gae(const float* rew, const float* val, const float* term, co
   if (T == 0 || B == 0) return MJL_OK;
   hipLaunchKernelGGL(gae_kernel, dim3((B + 255) / 256), dim3(256), 0, (hipStream_t)stream, rew, val, term, trunc, T,
                      B, (float)gamma, (float)(gamma * lam), adv, ret);
+  HIPCHK(hipGetLastError());
+  return MJL_OK;
+}
+
+// jax.random.split over a batch of keys (train_ppo.py:132,150: random.split(rng); random.split(key, num_envs))
+__global__ void prng_split_kernel(const uint32_t* __restrict__ keys, int n, int num, int mode, uint32_t* __restrict__ out) {
+  const int t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= n * num) return;
+  const int k = t / num, j = t % num;
+  const uint32_t k0 = keys[2 * (size_t)k], k1 = keys[2 * (size_t)k + 1];
+  uint32_t o0, o1;
+  if (mode == MJL_RNG_JAX_PARTITIONABLE) {
+    o0 = 0u; o1 = (uint32_t)j;
+    threefry2x32(k0, k1, o0, o1);
+  } else {  // words 2j, 2j + 1 of threefry_2x32(key, iota(2 num)): pairs (c, c + num)
+    const uint32_t w0 = (uint32_t)(2 * j), w1 = w0 + 1u, h = (uint32_t)num;
+    uint32_t a0 = w0 < h ? w0 : w0 - h, a1 = a0 + h, b0 = w1 < h ? w1 : w1 - h, b1 = b0 + h;
+    threefry2x32(k0, k1, a0, a1);
+    threefry2x32(k0, k1, b0, b1);
+    o0 = w0 < h ? a0 : a1;
+    o1 = w1 < h ? b0 : b1;
+  }
+  out[2 * (size_t)t] = o0;
+  out[2 * (size_t)t + 1] = o1;
+}
+
+extern "C" int mjl_prng_split(const uint32_t* keys, int n, int num, int mode, uint32_t* out, void* stream) {
+  if (!keys || !out || n < 0 || num < 1) return fail(MJL_ERR_ARG, "bad argument");
+  if (mode != MJL_RNG_JAX_PARTITIONABLE && mode != MJL_RNG_JAX_ORIGINAL) return fail(MJL_ERR_ARG, "unknown key mode %d", mode);
+  if (n == 0) return MJL_OK;
+  hipLaunchKernelGGL(prng_split_kernel, dim3((n * num + 255) / 256), dim3(256), 0, (hipStream_t)stream, keys, n, num,
+                     mode, out);
   HIPCHK(hipGetLastError());
   return MJL_OK;
 }

@@ -117,6 +117,8 @@ struct KParams {
   int gmax_efc, gmax_con; // row / contact capacity of one scratch slab
   uint32_t seed_lo, seed_hi, ctr_lo, ctr_hi;
   const unsigned long long* ctr_base;  // device counter base added to (ctr_hi, ctr_lo), or null
+  const uint32_t* keys;                // per-env jax.random reset keys [nenv, 2], or null
+  int key_mode;                        // MJL_RNG_* of `keys`
 };
 
 }  // namespace mjl

@@ -1552,12 +1552,48 @@ INL float uniform01(uint32_t s0, uint32_t s1, uint32_t c0, uint32_t c1, int env,
   return __uint_as_float((x0 >> 9) | 0x3f800000u) - 1.f;  // jax.random.uniform bit mapping
 }
 
+// jax.random on threefry2x32 (jax==0.7.2 `_threefry_split` / `_random_bits` / `_uniform`), for
+// resets drawn from per-env JAX keys exactly as single_reset (envs.py:116-147) draws them.
+// Partitionable mode (the jax_threefry_partitionable default since jax 0.5): element i of a draw
+// or of a split is threefry(key, (0, i)); random bits = x0 ^ x1, a split key = (x0, x1).
+// Original mode: a draw of n elements (n padded to even with a 0 count) is threefry(key, (c[j],
+// c[j + n'/2])) over c = iota(n), concatenated; split(key, 4) is that draw of 8 words reshaped (4, 2).
+INL float jax_bits_to_unit(uint32_t bits) { return __uint_as_float((bits >> 9) | 0x3F800000u) - 1.f; }
+INL void jax_split4(int mode, uint32_t k0, uint32_t k1, int j, uint32_t& o0, uint32_t& o1) {
+  if (mode == MJL_RNG_JAX_PARTITIONABLE) {
+    o0 = 0u; o1 = (uint32_t)j;
+    threefry2x32(k0, k1, o0, o1);
+  } else {  // words 2j, 2j+1 of threefry over (iota(4), iota(4) + 4)
+    uint32_t a0 = (uint32_t)((2 * j) & 3), a1 = a0 + 4u, b0 = a0 + 1u, b1 = b0 + 4u;
+    threefry2x32(k0, k1, a0, a1);
+    threefry2x32(k0, k1, b0, b1);
+    o0 = (2 * j < 4) ? a0 : a1;
+    o1 = (2 * j < 4) ? b0 : b1;
+  }
+}
+// element i of jax.random.uniform(key, (n,)) (n = 0 for shape ())
+INL float jax_uniform(int mode, uint32_t k0, uint32_t k1, int i, int n) {
+  if (mode == MJL_RNG_JAX_PARTITIONABLE) {
+    uint32_t x0 = 0u, x1 = (uint32_t)i;
+    threefry2x32(k0, k1, x0, x1);
+    return jax_bits_to_unit(x0 ^ x1);
+  }
+  const int np = (n < 1 ? 1 : n) + ((n < 1 ? 1 : n) & 1), h = np / 2;
+  auto cnt = [&](int j) { return (uint32_t)(j < (n < 1 ? 1 : n) ? j : 0); };  // iota padded with 0
+  const int j = i < h ? i : i - h;
+  uint32_t x0 = cnt(j), x1 = cnt(j + h);
+  threefry2x32(k0, k1, x0, x1);
+  return jax_bits_to_unit(i < h ? x0 : x1);
+}
+
 struct EnvArgs {  // per-launch env arguments
   const mjlEnvConfig* cfg;
   const float* noise;
   float* scratch_env;
   int gmax_efc, gmax_con, force_global;
   uint32_t s0, s1, c0, c1;
+  const uint32_t* keys;  // per-env jax.random keys [nenv, 2] (key mode) or null
+  int key_mode;
 };
 
 // single_reset (envs.py:115-202): random pose / velocity, forward, target, aux, obs
@@ -1568,7 +1604,20 @@ template <class D> NOINL void env_reset(MP m_, LDSA WS<D>* W, const EnvArgs* Ap,
   CP c = (CP)A.cfg;
   const int nj = m->nq - 7, nv = m->nv, nd = nj + nv + 2;
   float u = 0.f;
-  if (lane < nd) u = A.noise ? A.noise[(size_t)env * nd + lane] : uniform01(A.s0, A.s1, A.c0, A.c1, env, lane);
+  if (lane < nd) {
+    if (A.noise) {
+      u = A.noise[(size_t)env * nd + lane];
+    } else if (A.keys) {  // k1..k4 = split(key, 4); uniform(k1, (nq-7,)), uniform(k2, (nv,)), bernoulli(k3), uniform(k4)
+      const int which = lane < nj ? 0 : lane < nj + nv ? 1 : lane == nj + nv ? 2 : 3;
+      const int idx = which == 0 ? lane : which == 1 ? lane - nj : 0;
+      const int n = which == 0 ? nj : which == 1 ? nv : 0;
+      uint32_t s0, s1;
+      jax_split4(A.key_mode, A.keys[2 * (size_t)env], A.keys[2 * (size_t)env + 1], which, s0, s1);
+      u = jax_uniform(A.key_mode, s0, s1, idx, n);
+    } else {
+      u = uniform01(A.s0, A.s1, A.c0, A.c1, env, lane);
+    }
+  }
   if (lane < m->nq) W->qpos[lane] = m->qpos0[lane];
   if (lane < 32) W->ctrl[lane] = 0.f;
   if (lane < D::LD) { W->qacc_ws[lane] = 0.f; W->qvel[lane] = 0.f; }
@@ -1698,6 +1747,7 @@ template <class D, int MODE> __global__ __launch_bounds__(64, MJL_MINWAVES) void
   A.cfg = P.env; A.noise = P.noise; A.scratch_env = P.scratch + (size_t)env * (size_t)P.scratch_stride;
   A.gmax_efc = P.gmax_efc; A.gmax_con = P.gmax_con; A.force_global = P.force_global_rows;
   A.s0 = P.seed_lo; A.s1 = P.seed_hi;
+  A.keys = P.keys; A.key_mode = P.key_mode;
   {  // RNG counter = launch counter + the batch's device counter base (hipGraph replays)
     unsigned long long c = ((unsigned long long)P.ctr_hi << 32 | P.ctr_lo) + (P.ctr_base ? *P.ctr_base : 0ull);
     A.c0 = (uint32_t)c; A.c1 = (uint32_t)(c >> 32);

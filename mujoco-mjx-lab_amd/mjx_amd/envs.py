@@ -62,6 +62,18 @@ class HumanoidEnv:
         self.ctr_base = torch.zeros(1, dtype=torch.int64, device=dev)
         check(lib().mjl_batch_set_counter_base(self.data.handle, C.c_void_p(self.ctr_base.data_ptr())))
 
+    def set_reset_keys(self, keys: Optional[torch.Tensor], mode: int = 1):
+        """Draw resets (reset() and the auto-reset of step()) from per-env jax.random keys
+        [num_envs, 2] (int32/uint32 bits, device; read at execution time, so update in place), as
+        single_reset(key) does (src/envs.py:116-147); None returns to the (seed, counter) stream."""
+        if keys is not None:
+            if keys.shape != (self.num_envs, 2) or keys.dtype not in (torch.int32, torch.uint32) or not keys.is_cuda \
+                    or not keys.is_contiguous():
+                raise MjlError("reset keys must be a contiguous [num_envs, 2] int32 CUDA tensor")
+        self._keys = keys  # keep the buffer alive while the library points at it
+        check(lib().mjl_env_set_reset_keys(self.data.handle, None if keys is None else C.c_void_p(keys.data_ptr()),
+                                           int(mode)))
+
     def _next_counter(self) -> int:
         self.counter += 1
         return self.counter

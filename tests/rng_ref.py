@@ -37,3 +37,54 @@ def reset_noise(seed: int, counter: int, nenv: int, ndraw: int) -> np.ndarray:
     env = np.repeat(np.arange(nenv, dtype=np.uint64), ndraw)
     idx = np.tile(np.arange(ndraw, dtype=np.uint64), nenv)
     return uniform01(seed, counter, env, idx).reshape(nenv, ndraw)
+
+
+# ------------------------------------------------------------------ jax.random on threefry2x32
+# Partitionable layout (jax >= 0.5 default): element i of a draw / split = threefry(key, (0, i)).
+# Original layout: a draw of n words is threefry over (iota halves) of iota(n) padded with a 0.
+PARTITIONABLE, ORIGINAL = 1, 2
+
+
+def _words(key, n, mode):
+    k0, k1 = int(key[0]), int(key[1])
+    if mode == PARTITIONABLE:
+        x0, x1 = threefry2x32(k0, k1, np.zeros(n, np.uint64), np.arange(n, dtype=np.uint64))
+        return x0, x1
+    c = np.arange(n, dtype=np.uint64)
+    if n % 2:
+        c = np.concatenate([c, np.zeros(1, np.uint64)])
+    h = c.size // 2
+    y0, y1 = threefry2x32(k0, k1, c[:h], c[h:])
+    return np.concatenate([y0, y1])[:n], None
+
+
+def jax_split(key, num, mode=PARTITIONABLE):
+    """jax.random.split(key, num) -> uint32 [num, 2]."""
+    if mode == PARTITIONABLE:
+        x0, x1 = _words(key, num, mode)
+        return np.stack([x0, x1], 1).astype(np.uint32)
+    w, _ = _words(key, 2 * num, mode)
+    return w.reshape(num, 2).astype(np.uint32)
+
+
+def jax_uniform(key, n=None, mode=PARTITIONABLE):
+    """jax.random.uniform(key, (n,)) (n=None: shape ()) as float32."""
+    m = 1 if n is None else n
+    if mode == PARTITIONABLE:
+        x0, x1 = _words(key, m, mode)
+        bits = x0 ^ x1
+    else:
+        bits, _ = _words(key, m, mode)
+    f = (((bits >> np.uint64(9)) | np.uint64(0x3F800000)).astype(np.uint32)).view(np.float32) - np.float32(1.0)
+    return f[0] if n is None else f
+
+
+def jax_reset_noise(keys, nj, nv, mode=PARTITIONABLE):
+    """single_reset's draws (src/envs.py:117-141) from per-env keys [B, 2], in the device layout
+    [joint uniforms (nj) | velocity uniforms (nv) | flip uniform | initial-speed uniform]."""
+    out = []
+    for key in np.asarray(keys, np.uint32):
+        k1, k2, k3, k4 = jax_split(key, 4, mode)
+        out.append(np.concatenate([jax_uniform(k1, nj, mode), jax_uniform(k2, nv, mode),
+                                   [jax_uniform(k3, None, mode), jax_uniform(k4, None, mode)]]))
+    return np.array(out, np.float32)

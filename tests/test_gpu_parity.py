@@ -319,3 +319,36 @@ def test_sphere_speedtest_kat_on_gpu():
     mjx.step(sys_, d)
     q = d.get("qpos").cpu().numpy()
     np.testing.assert_allclose(q[:, 2], -9.81 * 0.002 ** 2, rtol=1e-5)
+
+
+def test_jax_key_resets_match_reference_draws():
+    """Resets from per-env jax.random keys (mjl_env_set_reset_keys) equal resets from the draws the
+    numpy restatement of jax.random makes for those keys (tests/rng_ref.py, pinned by JAX's printed
+    split(PRNGKey(0)) in both key layouts): bit-identical state and obs; mjl_prng_split is
+    bit-identical to jax.random.split; the auto-reset of env step consumes the same keys."""
+    from mjx_amd import jaxrng
+    from rng_ref import jax_reset_noise, jax_split
+    B = 16
+    m, env, _ = _env(B)
+    nj, nv = m.nq - 7, m.nv
+    for mode in (jaxrng.PARTITIONABLE, jaxrng.ORIGINAL):
+        root = jaxrng.prng_key(42 + mode)
+        keys = jaxrng.split(root, B, mode)
+        np.testing.assert_array_equal(keys.cpu().numpy().view(np.uint32),
+                                      jax_split(root.cpu().numpy().view(np.uint32), B, mode))
+        env.set_reset_keys(keys, mode)
+        o1 = env.reset().clone()
+        s1 = [env.data.get(f).clone() for f in ("qpos", "qvel", "aux")]
+        env.set_reset_keys(None)
+        noise = jax_reset_noise(keys.cpu().numpy().view(np.uint32), nj, nv, mode)
+        o2 = env.reset(noise=torch.tensor(noise)).clone()
+        s2 = [env.data.get(f).clone() for f in ("qpos", "qvel", "aux")]
+        assert torch.equal(o1, o2) and all(torch.equal(a, b) for a, b in zip(s1, s2))
+        # auto-reset inside env step: truncate every env, the merged state is the keyed reset
+        env.set_reset_keys(keys, mode)
+        aux = env.aux.clone()
+        aux[:, 8] = 999.0
+        env.data.set("aux", aux)
+        o3 = env.step(torch.zeros((B, m.nu), device="cuda"), auto_reset=True)[0].clone()
+        env.set_reset_keys(None)
+        assert torch.equal(o3, o2) and torch.equal(env.data.get("qpos"), s2[0])

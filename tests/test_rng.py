@@ -18,3 +18,24 @@ def test_uniform_range_and_moments():
     # different counters / envs give different streams
     assert not np.array_equal(reset_noise(42, 8, 4, 50), reset_noise(42, 7, 4, 50))
     assert not np.array_equal(u[0], u[1])
+
+
+def test_jax_split_known_answers():
+    """jax.random.split(jax.random.PRNGKey(0)) as JAX prints it: [[1797259609 2579123966]
+    [928981903 3453687069]] with jax_threefry_partitionable (default since jax 0.5; the reference
+    pins 0.7.2), [[4146024105 967050713] [2718843009 1272950319]] in the original layout."""
+    from rng_ref import ORIGINAL, PARTITIONABLE, jax_split
+    np.testing.assert_array_equal(jax_split((0, 0), 2, PARTITIONABLE), [[1797259609, 2579123966], [928981903, 3453687069]])
+    np.testing.assert_array_equal(jax_split((0, 0), 2, ORIGINAL), [[4146024105, 967050713], [2718843009, 1272950319]])
+
+
+def test_jax_uniform_layouts():
+    from rng_ref import ORIGINAL, PARTITIONABLE, jax_uniform
+    for mode in (PARTITIONABLE, ORIGINAL):
+        u = jax_uniform((7, 42), 4099, mode)
+        assert u.dtype == np.float32 and 0.0 <= u.min() and u.max() < 1.0 and abs(u.mean() - 0.5) < 0.02
+        # a shape-() draw is element 0 of any draw in the partitionable layout; in the original one it
+        # is the first word of threefry over the padded pair (0, 0)
+        s = jax_uniform((7, 42), None, mode)
+        if mode == PARTITIONABLE:
+            assert s == u[0]
