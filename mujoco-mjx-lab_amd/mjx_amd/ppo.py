@@ -285,7 +285,10 @@ class PPOTrainer:
     with auto-reset (HumanoidEnv, or a stand-in in CPU tests), obs_dim, act_dim, num_envs."""
 
     def __init__(self, cfg, env, eval_env=None, device="cuda", dist=None, out_dir: Optional[str] = None,
-                 use_graph: bool = True):
+                 use_graph: bool = True, jax_keys: bool = False):
+        """jax_keys: draw every env reset (initial, auto-reset, eval) from the jax.random key chain
+        train_ppo.py derives from cfg.seed (:88-118, :132/:150-151 per rollout step, :325, :359,
+        :419, eval :268-293), so the reset stream equals the reference's for the same seed."""
         self.cfg, self.env, self.eval_env, self.dist = cfg, env, eval_env, dist
         self.rank = dist.get_rank() if dist is not None else 0
         self.world = dist.get_world_size() if dist is not None else 1
@@ -303,6 +306,9 @@ class PPOTrainer:
         self.rms = RunningMeanStd(env.obs_dim, self.device)
         self.gen = torch.Generator(device=self.device).manual_seed(int(cfg.seed) * 1000 + self.rank)
         self.idx_gen = torch.Generator().manual_seed(int(cfg.seed) + 7919 * (self.rank + 1))
+        self.jax_keys = bool(jax_keys) and self.device.type == "cuda" and hasattr(env, "set_reset_keys")
+        if self.jax_keys:
+            self._jax_init()
         self.obs = env.reset().clone()
         self.use_graph = bool(use_graph)
         self._buf, self._graph, self._rollouts = None, None, 0
@@ -314,6 +320,39 @@ class PPOTrainer:
                 os.makedirs(os.path.join(self.out_dir, sub), exist_ok=True)
             with open(os.path.join(self.out_dir, "config.json"), "w") as f:
                 json.dump(_jsonable(cfg), f, indent=2)
+
+    # ------------------------------------------------------------------ jax.random key chain
+    def _jax_init(self):
+        from . import jaxrng
+        self._jr = jaxrng
+        B = self.env.num_envs
+        self._key_rows = (self.rank * B, (self.rank + 1) * B)  # this rank's rows of the global key array
+        rng = jaxrng.prng_key(self.cfg.seed, self.device)                 # train_ppo.py:88
+        rng = jaxrng.split(rng)[0]                                        # :96 init_rng_p
+        rng = jaxrng.split(rng)[0]                                        # :103 init_rng_v
+        sp = jaxrng.split(rng)                                            # :117
+        self._jax_rng = sp[0].clone()
+        self._roll_rng = torch.empty_like(self._jax_rng)
+        self._env_keys = torch.empty((B, 2), dtype=torch.int32, device=self.device)
+        self._env_keys.copy_(self._global_keys(sp[1]))                    # :118
+        self.env.set_reset_keys(self._env_keys, jaxrng.PARTITIONABLE)
+
+    def _global_keys(self, key):
+        r0, r1 = self._key_rows
+        return self._jr.split(key, self.env.num_envs * self.world)[r0:r1]
+
+    def _jax_split_main(self) -> torch.Tensor:
+        """rng, sub = random.split(rng) on the main chain; returns sub."""
+        sp = self._jr.split(self._jax_rng)
+        self._jax_rng.copy_(sp[0])
+        return sp[1]
+
+    def _jax_step_keys(self):
+        """One rollout step's splits (train_ppo.py:132 for the sampling key, :150-151 for the reset keys)."""
+        sp = self._jr.split(self._roll_rng)
+        sp2 = self._jr.split(sp[0])
+        self._roll_rng.copy_(sp2[0])
+        self._env_keys.copy_(self._global_keys(sp2[1]))
 
     # train_ppo.py:128-169
     def _rollout_buffers(self):
@@ -332,6 +371,8 @@ class PPOTrainer:
         relative to the env's device counter base (the body is being captured)."""
         bf, env = self._buf, self.env
         for t in range(self.cfg.rollout_length):
+            if self.jax_keys:
+                self._jax_step_keys()
             mean, log_std = self.policy(self.rms.normalize(bf["obs"][t]))
             act = torch.addcmul(mean, torch.exp(log_std), bf["eps"][t], out=bf["act"][t])
             gaussian_logprob(mean, log_std, act, out=bf["logp"][t])
@@ -354,6 +395,8 @@ class PPOTrainer:
         bf, env, T = self._rollout_buffers(), self.env, self.cfg.rollout_length
         bf["eps"].normal_(generator=self.gen)
         bf["obs"][0].copy_(self.obs)
+        if self.jax_keys:
+            self._roll_rng.copy_(self._jax_split_main())  # train_ppo.py:325 key_roll
         use_graph = self.use_graph and self.device.type == "cuda" and hasattr(env, "ctr_base")
         if use_graph and self._graph is None and self._rollouts > 0:
             self._graph = torch.cuda.CUDAGraph()
@@ -377,6 +420,8 @@ class PPOTrainer:
         t0 = time.time()
         obs_t, act_t, logp_t, r_t, te_t, tr_t = self.collect_rollout()
         T, B = r_t.shape
+        if self.jax_keys:
+            self._jax_split_main()  # train_ppo.py:359 rng_idx (the minibatch permutation is torch's)
         self.rms.update(obs_t, self.dist)
         with torch.no_grad():
             obs_n = self.rms.normalize(obs_t)
@@ -411,12 +456,24 @@ class PPOTrainer:
         env = self.eval_env
         if hasattr(env, "seed"):
             env.seed, env.counter = int(self.cfg.seed) + 10000 + it, 0
+        keyed = self.jax_keys and hasattr(env, "set_reset_keys")
+        if keyed:  # train_ppo.py:268-272, 292-293
+            jr = self._jr
+            sp = jr.split(jr.prng_key(int(self.cfg.seed) + 10000 + it, self.device))
+            rng, keys = sp[0].clone(), jr.split(sp[1], env.num_envs).contiguous()
+            env.set_reset_keys(keys, jr.PARTITIONABLE)
         obs = env.reset().clone()
         acc = torch.zeros(env.num_envs, device=self.device)
         for _ in range(steps):
+            if keyed:
+                sp = jr.split(rng)
+                rng.copy_(sp[0])
+                keys.copy_(jr.split(sp[1], env.num_envs))
             mean, _ = self.policy(self.rms.normalize(obs))
             obs, r, _, _ = env.step(mean)
             acc += r
+        if keyed:
+            env.set_reset_keys(None)
         return float(acc.mean())
 
     def save_checkpoint(self, it: int, metrics: dict):
@@ -454,6 +511,8 @@ class PPOTrainer:
             m = self.iteration(it)
             should_eval = (it % cfg.eval_interval == 0) and self.eval_env is not None
             should_ckpt = it % cfg.checkpoint_every == 0
+            if self.jax_keys and it % cfg.eval_interval == 0:
+                self._jax_split_main()  # train_ppo.py:419 key_eval (evaluate reseeds from cfg.seed)
             if should_eval and self.rank == 0:
                 m["eval_return"] = self.evaluate(it)
             if (it % cfg.log_interval == 0) or should_eval or should_ckpt or it == n - 1:

@@ -30,6 +30,8 @@ def main():
     ap.add_argument("--num-envs", type=int, default=None, help="total envs over all ranks")
     ap.add_argument("--model", default=None, help="humanoid_mjx | humanoid | path to .xml")
     ap.add_argument("--results-dir", default=None)
+    ap.add_argument("--jax-keys", action="store_true",
+                    help="draw env resets from train_ppo.py's jax.random key chain (same reset stream as the reference)")
     a = ap.parse_args()
 
     cfg = PPOConfig.from_json(a.config) if a.config else reference_ppo_config()
@@ -58,7 +60,7 @@ def main():
     out = None
     if rank == 0:
         out = os.path.join(cfg.results_dir, time.strftime("%Y%m%d_%H%M%S") + "_ppo")
-    tr = PPOTrainer(cfg, env, eval_env, device=f"cuda:{local}", dist=dist, out_dir=out)
+    tr = PPOTrainer(cfg, env, eval_env, device=f"cuda:{local}", dist=dist, out_dir=out, jax_keys=a.jax_keys)
     tr.train()
     if dist is not None:
         dist.destroy_process_group()

@@ -260,16 +260,20 @@ def test_graph_rollout_bit_identical_to_eager():
     cfg.env_config.max_episode_steps = 10  # truncations -> auto-resets inside the captured steps
     ecfg = resolve_ids(m, cfg.env_config)
     trs = [ppo.PPOTrainer(cfg, HumanoidEnv(mjx.put_model(m), ecfg, cfg.num_envs, seed=11), None, device="cuda",
-                          use_graph=g) for g in (False, True)]
+                          use_graph=g, jax_keys=jk) for g, jk in ((False, False), (True, False))]
+    trs += [ppo.PPOTrainer(cfg, HumanoidEnv(mjx.put_model(m), ecfg, cfg.num_envs, seed=11), None, device="cuda",
+                           use_graph=g, jax_keys=True) for g in (False, True)]
     for it in range(3):
         outs = []
         for tr in trs:
             bufs = [x.clone() for x in tr.collect_rollout()]
             tr.rms.update(bufs[0])
             outs.append(bufs)
-        assert trs[1]._graph is not None or it == 0
-        for a, b in zip(*outs):
+        assert (trs[1]._graph is not None and trs[3]._graph is not None) or it == 0
+        for a, b in zip(outs[0], outs[1]):
             assert torch.equal(a, b), f"rollout {it}"
+        for a, b in zip(outs[2], outs[3]):  # jax-key resets: keys split inside the captured steps
+            assert torch.equal(a, b), f"rollout {it} (jax keys)"
         assert outs[0][5].sum() > 0  # truncations happened
 
 
@@ -291,3 +295,32 @@ def test_split_k_linear_gradients():
         torch.nn.functional.linear(x, lin.weight, lin.bias).backward(gy)
         for a, b in zip(got, [x.grad, lin.weight.grad, lin.bias.grad]):  # sums of 65,536 terms: scale-relative
             assert (a - b).abs().max() <= 2e-5 * b.abs().max(), (fin, fout)
+
+
+@pytest.mark.gpu
+def test_jax_key_chain_follows_train_ppo():
+    """With jax_keys the trainer's reset keys are train_ppo.py's: PRNGKey(seed) -> two init splits ->
+    split -> split(key_reset, B) for the initial reset (:88-118); per iteration split -> key_roll
+    (:325), per rollout step split (sampling key, :132) then split -> split(key_reset, B) (:150-151).
+    Derived independently with the numpy restatement of jax.random (tests/rng_ref.py)."""
+    import mjx_amd
+    from mjx_amd import mjx
+    from mjx_amd.envs import HumanoidEnv, resolve_ids
+    from rng_ref import jax_split
+    m = mjx_amd.load_model("humanoid_mjx")
+    cfg = small_cfg(num_envs=64, rollout_length=5, seed=1234)
+    env = HumanoidEnv(mjx.put_model(m), resolve_ids(m, cfg.env_config), cfg.num_envs, seed=0)
+    tr = ppo.PPOTrainer(cfg, env, None, device="cuda", use_graph=False, jax_keys=True)
+    rng = np.array([0, 1234], np.uint32)
+    rng = jax_split(rng, 2)[0]
+    rng = jax_split(rng, 2)[0]
+    rng, key_reset = jax_split(rng, 2)
+    np.testing.assert_array_equal(tr._env_keys.cpu().numpy().view(np.uint32), jax_split(key_reset, 64))
+    tr.collect_rollout()
+    rng, roll = jax_split(rng, 2)
+    for _ in range(5):
+        roll = jax_split(jax_split(roll, 2)[0], 2)
+        keys = jax_split(roll[1], 64)
+        roll = roll[0]
+    np.testing.assert_array_equal(tr._env_keys.cpu().numpy().view(np.uint32), keys)
+    np.testing.assert_array_equal(tr._jax_rng.cpu().numpy().view(np.uint32), rng)
