@@ -352,3 +352,25 @@ def test_jax_key_resets_match_reference_draws():
         o3 = env.step(torch.zeros((B, m.nu), device="cuda"), auto_reset=True)[0].clone()
         env.set_reset_keys(None)
         assert torch.equal(o3, o2) and torch.equal(env.data.get("qpos"), s2[0])
+
+
+@pytest.mark.parametrize("solref,solimp", [((0.02, 1.0), (0.9, 0.95, 0.001, 0.5, 2.0)),
+                                           ((0.015, 1.0), (0.9, 0.99, 0.003, 0.5, 2.0))])
+def test_contact_equilibrium_kat_on_gpu(solref, solimp):
+    """The HIP step's resting penetration of a frictionless sphere equals the closed-form root of
+    MuJoCo's soft-contact model (tests/test_oracle_kat.py), within fp32 resolution."""
+    from mjx_amd import mjcf
+    from test_oracle_kat import _mj_impedance, _root
+    sr, si = " ".join(map(str, solref)), " ".join(map(str, solimp))
+    m = mjcf.compile_xml_string(f"""<mujoco><option timestep="0.002"/><worldbody>
+      <geom type="plane" size="0 0 1" condim="1" solref="{sr}" solimp="{si}"/>
+      <body pos="0 0 0.101"><freejoint/><geom type="sphere" size="0.1" condim="1" solref="{sr}" solimp="{si}"/>
+      </body></worldbody></mujoco>""")
+    sys_ = mjx.put_model(m)
+    d = mjx.make_data(sys_, 4)
+    for _ in range(4000):
+        mjx.step(sys_, d)
+    pen = d.get("qpos").cpu().numpy()[:, 2].astype(np.float64) - 0.1
+    k = 1.0 / (solimp[1] ** 2 * solref[0] ** 2 * solref[1] ** 2)
+    want = _root(lambda p: p * k * _mj_impedance(solimp, p) ** 2 + 9.81 * (1.0 - _mj_impedance(solimp, p)), -0.05, 0.0)
+    np.testing.assert_allclose(pen, want, rtol=2e-3)

@@ -140,3 +140,101 @@ def test_float_oracle_agrees(hm):
         assert a["ncon"] == b["ncon"] and a["nefc"] == b["nefc"]
         scale = 1 + np.abs(a["qacc"]).max()
         assert np.abs(a["qacc"] - b["qacc"]).max() < 1e-3 * scale
+
+
+def _mj_impedance(solimp, x):
+    """MuJoCo's impedance d(x) (documentation, Computation > Soft constraints; engine_core_constraint.c
+    getimpedance): x = |pos - margin| / width, y(x) a two-piece power sigmoid with midpoint `mid`."""
+    d0, dmax, width, mid, power = solimp
+    d0, dmax = min(max(d0, 1e-4), 0.9999), min(max(dmax, 1e-4), 0.9999)  # mjMINIMP / mjMAXIMP
+    r = abs(x) / width
+    if r >= 1.0:
+        return dmax
+    y = r ** power / mid ** (power - 1) if r <= mid else 1.0 - (1.0 - r) ** power / (1.0 - mid) ** (power - 1)
+    return d0 + y * (dmax - d0)
+
+
+@pytest.mark.parametrize("solref,solimp", [((0.02, 1.0), (0.9, 0.95, 0.001, 0.5, 2.0)),       # MuJoCo defaults
+                                           ((0.015, 1.0), (0.9, 0.99, 0.003, 0.5, 2.0)),      # humanoid_mjx bodies
+                                           ((0.03, 0.7), (0.8, 0.99, 0.01, 0.3, 3.0))])
+def test_contact_equilibrium_penetration_kat(solref, solimp):
+    """A frictionless sphere at rest on a plane sinks to where the soft-contact force carries its
+    weight. From MuJoCo's documented model (independent of the oracle's code): at rest a = 0, so
+    m g = D aref with D = 1/R, R = (1 - d)/d * diagApprox (diagApprox = 1/m for a free sphere) and
+    aref = -k d pos, k = 1/(dmax^2 tc^2 dr^2) => pos k d^2 = -g (1 - d), d = d(pos). The oracle's
+    steady state must sit on that root."""
+    sr, si = " ".join(map(str, solref)), " ".join(map(str, solimp))
+    # both geoms carry the parameters (MuJoCo mixes the pair's solref / solimp by solmix)
+    xml = f"""<mujoco><option timestep="0.002"/><worldbody>
+      <geom type="plane" size="0 0 1" condim="1" solref="{sr}" solimp="{si}"/>
+      <body pos="0 0 0.101"><freejoint/><geom type="sphere" size="0.1" condim="1" solref="{sr}" solimp="{si}"/>
+      </body></worldbody></mujoco>"""
+    m = mjcf.compile_xml_string(xml)
+    o = Oracle(m)
+    s = o.new_state()
+    o.step(s, 4000)
+    a = state_arrays(m, s)
+    assert np.abs(a["qvel"]).max() < 1e-7
+    pen = a["qpos"][2] - 0.1
+    tc, dr = max(solref[0], 2 * 0.002), solref[1]   # refsafe: timeconst >= 2 dt
+    k = 1.0 / (solimp[1] ** 2 * tc ** 2 * dr ** 2)
+    f = lambda p: p * k * _mj_impedance(solimp, p) ** 2 + 9.81 * (1.0 - _mj_impedance(solimp, p))  # noqa: E731
+    lo, hi = -0.05, 0.0                              # f(lo) < 0 < f(0): bisection
+    for _ in range(200):
+        mid = 0.5 * (lo + hi)
+        lo, hi = (mid, hi) if f(mid) < 0 else (lo, mid)
+    assert pen == pytest.approx(0.5 * (lo + hi), rel=1e-6, abs=1e-12)
+
+
+def _root(f, lo, hi):
+    for _ in range(200):
+        mid = 0.5 * (lo + hi)
+        lo, hi = (mid, hi) if f(mid) < 0 else (lo, mid)
+    return 0.5 * (lo + hi)
+
+
+def test_contact_parameter_mixing_kat():
+    """Different solref / solimp on the two geoms: MuJoCo mixes them by solmix weights (default 1
+    each, so the plain mean); the resting penetration is the closed-form root for the mean."""
+    a_ref, a_imp = (0.02, 1.0), (0.9, 0.95, 0.001, 0.5, 2.0)
+    b_ref, b_imp = (0.015, 1.0), (0.9, 0.99, 0.003, 0.5, 2.0)
+    xml = f"""<mujoco><option timestep="0.002"/><worldbody>
+      <geom type="plane" size="0 0 1" condim="1" solref="{' '.join(map(str, a_ref))}" solimp="{' '.join(map(str, a_imp))}"/>
+      <body pos="0 0 0.101"><freejoint/><geom type="sphere" size="0.1" condim="1" solref="{' '.join(map(str, b_ref))}"
+      solimp="{' '.join(map(str, b_imp))}"/></body></worldbody></mujoco>"""
+    m = mjcf.compile_xml_string(xml)
+    o = Oracle(m)
+    s = o.new_state()
+    o.step(s, 4000)
+    pen = state_arrays(m, s)["qpos"][2] - 0.1
+    sr = [(x + y) / 2 for x, y in zip(a_ref, b_ref)]
+    si = [(x + y) / 2 for x, y in zip(a_imp, b_imp)]
+    k = 1.0 / (si[1] ** 2 * sr[0] ** 2 * sr[1] ** 2)
+    want = _root(lambda p: p * k * _mj_impedance(si, p) ** 2 + 9.81 * (1.0 - _mj_impedance(si, p)), -0.05, 0.0)
+    assert pen == pytest.approx(want, rel=1e-6)
+
+
+@pytest.mark.parametrize("solimp", [(0.9, 0.95, 0.001, 0.5, 2.0), (0.0, 0.99, 0.01, 0.5, 2.0)])  # default; humanoid
+def test_joint_limit_equilibrium_kat(solimp):
+    """A rod on a hinge, pulled by gravity against its upper limit: at rest the limit force f = tau
+    (gravity torque m g c cos(q)) and f = -k d(pos)^2 pos I / (1 - d), pos = q_max - q (MuJoCo's soft
+    constraint model with diagApprox = dof_invweight0 = 1/I for one hinge)."""
+    si = " ".join(map(str, solimp))
+    xml = f"""<mujoco><option timestep="0.002"/><worldbody><body>
+      <joint type="hinge" axis="0 1 0" limited="true" range="-30 30" solimplimit="{si}"/>
+      <geom type="capsule" fromto="0 0 0 0.5 0 0" size="0.02"/></body></worldbody></mujoco>"""
+    m = mjcf.compile_xml_string(xml)
+    o = Oracle(m)
+    s = o.new_state()
+    o.step(s, 6000)
+    a = state_arrays(m, s)
+    assert abs(a["qvel"][0]) < 1e-8
+    pos = np.deg2rad(30.0) - a["qpos"][0]
+    kin = mjcf._fk_and_mass(m, np.zeros(1))
+    inertia, mass = kin["M"][0, 0], m.body_mass[1]
+    c = float(np.linalg.norm(kin["xipos"][1]))
+    k = 1.0 / (solimp[1] ** 2 * 0.02 ** 2)
+    tau = lambda p: mass * 9.81 * c * np.cos(np.deg2rad(30.0) - p)  # noqa: E731
+    want = _root(lambda p: p * k * _mj_impedance(solimp, p) ** 2 * inertia + tau(p) * (1.0 - _mj_impedance(solimp, p)),
+                 -0.5, 0.0)
+    assert pos == pytest.approx(want, rel=1e-6)
