@@ -246,6 +246,21 @@ int mjl_env_step_vjp(mjlBatch* batch, const float* act, const float* g_qpos, con
                      const float* g_rew, const float* g_aux, float* out_qpos, float* out_qvel,
                      float* out_act, float* out_aux, void* stream);
 
+/* Guarded env-step VJP for the APG reverse sweep: as mjl_env_step_vjp, but an env whose input
+ * cotangents come out non-finite (a state blowing up inside the horizon) gets all-zero outputs and
+ * increments *nonfinite_count (device float, may be NULL = unguarded). */
+int mjl_env_step_vjp_guarded(mjlBatch* batch, const float* act, const float* g_qpos, const float* g_qvel,
+                             const float* g_rew, const float* g_aux, float* out_qpos, float* out_qvel,
+                             float* out_act, float* out_aux, float* nonfinite_count, void* stream);
+
+/* The persistent per-env state (what a step reads and writes: Data.qpos, qvel, qacc_warmstart,
+ * time, plus the env aux) as packed rows [nenv, mjl_state_size] = [qpos | qvel | qacc_warmstart |
+ * aux | time]: the APG remat tape entry (train_apg.py:187-189 checkpoints each step's carry).
+ * mjl_set_state takes qacc_warmstart from ws_src (same row layout, may be NULL = from src). */
+int mjl_state_size(const mjlBatch* batch);
+int mjl_get_state(mjlBatch* batch, float* dst, void* stream);
+int mjl_set_state(mjlBatch* batch, const float* src, const float* ws_src, void* stream);
+
 /* Replaces compute_gae (train_ppo.py:171-202, a reverse lax.scan over the rollout): rew, term,
  * trunc [T, B], val [T+1, B] (val[T] = value of the obs after the last step) -> adv, ret [T, B],
  * delta = r + gamma V' (1 - term) - V, A = delta + gamma lam (1 - max(term, trunc)) A', ret = A + V.

@@ -1154,6 +1154,7 @@ struct VjpArgs {
   float *o_qpos, *o_qvel, *o_ctrl, *o_aux;
   float* scratch;                                     // per env: row slab, then the adjoint scratch
   int scratch_stride, row_floats;
+  float* nonfinite;  // optional: envs whose cotangents came out non-finite get zero outputs, counted here
 };
 
 // One wave per env: recompute the step from the batch state (not modified), then run the reverse
@@ -1269,6 +1270,18 @@ template <class D, bool ENV> __global__ __launch_bounds__(64, 1) void vjp_kernel
   adj_kinematics<D>(m, W, A, lane);
   STAMP(13, lane);
   // ---- outputs
+  if (V.nonfinite) {  // cut an env whose cotangents overflowed from the gradient (APG guard)
+    bool bad = (lane < nq && !isfinite(A->qposb[lane])) || (lane < nv && !isfinite(A->qvelb[lane])) ||
+               (lane < nu && !isfinite(A->ctrlb[lane])) || (ENV && lane < MJL_AUX_DIM && !isfinite(A->auxb[lane]));
+    if (__ballot(bad) != 0ull) {
+      if (lane < nq) V.o_qpos[(size_t)env * nq + lane] = 0.f;
+      if (lane < nv) V.o_qvel[(size_t)env * nv + lane] = 0.f;
+      if (lane < nu) V.o_ctrl[(size_t)env * nu + lane] = 0.f;
+      if (ENV && lane < MJL_AUX_DIM) V.o_aux[(size_t)env * MJL_AUX_DIM + lane] = 0.f;
+      if (lane == 0) atomicAdd(V.nonfinite, 1.f);
+      return;
+    }
+  }
   if (lane < nq) V.o_qpos[(size_t)env * nq + lane] = A->qposb[lane];
   if (lane < nv) V.o_qvel[(size_t)env * nv + lane] = A->qvelb[lane];
   if (lane < nu) {

@@ -404,6 +404,61 @@ extern "C" int mjl_set(mjlBatch* B, int field, const float* src, const float* ma
   return MJL_OK;
 }
 
+// packed persistent state rows [qpos | qvel | qacc_warmstart | aux | time] (APG tape)
+__global__ void pack_state_kernel(StateBuf S, int nenv, int nq, int nv, float* __restrict__ dst) {
+  const int w = nq + 2 * nv + MJL_AUX_DIM + 1;
+  const long t = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= (long)nenv * w) return;
+  const int e = (int)(t / w), k = (int)(t % w);
+  float v;
+  if (k < nq) v = S.qpos[(size_t)e * nq + k];
+  else if (k < nq + nv) v = S.qvel[(size_t)e * nv + k - nq];
+  else if (k < nq + 2 * nv) v = S.qacc_warmstart[(size_t)e * nv + k - nq - nv];
+  else if (k < nq + 2 * nv + MJL_AUX_DIM) v = S.aux[(size_t)e * MJL_AUX_DIM + k - nq - 2 * nv];
+  else v = S.time[e];
+  dst[t] = v;
+}
+__global__ void unpack_state_kernel(StateBuf S, int nenv, int nq, int nv, const float* __restrict__ src,
+                                    const float* __restrict__ ws_src) {
+  const int w = nq + 2 * nv + MJL_AUX_DIM + 1;
+  const long t = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= (long)nenv * w) return;
+  const int e = (int)(t / w), k = (int)(t % w);
+  const float v = src[t];
+  if (k < nq) S.qpos[(size_t)e * nq + k] = v;
+  else if (k < nq + nv) S.qvel[(size_t)e * nv + k - nq] = v;
+  else if (k < nq + 2 * nv) S.qacc_warmstart[(size_t)e * nv + k - nq - nv] = ws_src ? ws_src[t] : v;
+  else if (k < nq + 2 * nv + MJL_AUX_DIM) S.aux[(size_t)e * MJL_AUX_DIM + k - nq - 2 * nv] = v;
+  else S.time[e] = v;
+}
+
+extern "C" int mjl_state_size(const mjlBatch* B) {
+  if (!B) return -1;
+  return B->model->desc.nq + 2 * B->model->desc.nv + MJL_AUX_DIM + 1;
+}
+
+extern "C" int mjl_get_state(mjlBatch* B, float* dst, void* stream) {
+  if (!B || !dst) return fail(MJL_ERR_ARG, "bad argument");
+  HIPCHK(hipSetDevice(B->device));
+  const int nq = B->model->desc.nq, nv = B->model->desc.nv;
+  const long n = (long)B->nenv * (nq + 2 * nv + MJL_AUX_DIM + 1);
+  hipLaunchKernelGGL(pack_state_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, (hipStream_t)stream, B->s,
+                     B->nenv, nq, nv, dst);
+  HIPCHK(hipGetLastError());
+  return MJL_OK;
+}
+
+extern "C" int mjl_set_state(mjlBatch* B, const float* src, const float* ws_src, void* stream) {
+  if (!B || !src) return fail(MJL_ERR_ARG, "bad argument");
+  HIPCHK(hipSetDevice(B->device));
+  const int nq = B->model->desc.nq, nv = B->model->desc.nv;
+  const long n = (long)B->nenv * (nq + 2 * nv + MJL_AUX_DIM + 1);
+  hipLaunchKernelGGL(unpack_state_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, (hipStream_t)stream, B->s,
+                     B->nenv, nq, nv, src, ws_src);
+  HIPCHK(hipGetLastError());
+  return MJL_OK;
+}
+
 static KParams make_params(mjlBatch* B) {
   KParams P;
   std::memset(&P, 0, sizeof(P));
@@ -562,6 +617,13 @@ int mjl_step_vjp(mjlBatch* B, const float* g_qpos, const float* g_qvel, float* o
 int mjl_env_step_vjp(mjlBatch* B, const float* act, const float* g_qpos, const float* g_qvel, const float* g_rew,
                      const float* g_aux, float* out_qpos, float* out_qvel, float* out_act, float* out_aux,
                      void* stream) {
+  return mjl_env_step_vjp_guarded(B, act, g_qpos, g_qvel, g_rew, g_aux, out_qpos, out_qvel, out_act, out_aux, nullptr,
+                                  stream);
+}
+
+int mjl_env_step_vjp_guarded(mjlBatch* B, const float* act, const float* g_qpos, const float* g_qvel,
+                             const float* g_rew, const float* g_aux, float* out_qpos, float* out_qvel,
+                             float* out_act, float* out_aux, float* nonfinite_count, void* stream) {
   if (!B || !act || !g_qpos || !g_qvel || !g_rew || !g_aux || !out_qpos || !out_qvel || !out_act || !out_aux)
     return fail(MJL_ERR_ARG, "bad argument");
   if (!B->has_env) return fail(MJL_ERR_ARG, "mjl_env_config not called");
@@ -569,6 +631,7 @@ int mjl_env_step_vjp(mjlBatch* B, const float* act, const float* g_qpos, const f
   std::memset(&V, 0, sizeof(V));
   V.act = act; V.g_qpos = g_qpos; V.g_qvel = g_qvel; V.g_rew = g_rew; V.g_aux = g_aux;
   V.o_qpos = out_qpos; V.o_qvel = out_qvel; V.o_ctrl = out_act; V.o_aux = out_aux;
+  V.nonfinite = nonfinite_count;
   return launch_vjp<true>(B, V, stream);
 }
 

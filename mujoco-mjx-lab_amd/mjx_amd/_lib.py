@@ -22,7 +22,8 @@ EXPORTS = [
     "mjl_batch_create", "mjl_batch_destroy", "mjl_batch_nenv", "mjl_batch_set_option", "mjl_get", "mjl_set",
     "mjl_forward", "mjl_step", "mjl_speedtest_step", "mjl_env_config", "mjl_env_step", "mjl_env_reset",
     "mjl_step_vjp", "mjl_env_step_vjp", "mjl_gae", "mjl_batch_set_counter_base",
-    "mjl_env_set_reset_keys", "mjl_prng_split",
+    "mjl_env_set_reset_keys", "mjl_prng_split", "mjl_env_step_vjp_guarded", "mjl_state_size", "mjl_get_state",
+    "mjl_set_state",
 ]
 
 _lib = None
@@ -82,6 +83,10 @@ def lib() -> C.CDLL:
     L.mjl_env_reset.argtypes = [vp, f32p, u64, u64, f32p, f32p, vp]
     L.mjl_batch_set_counter_base.argtypes = [vp, vp]
     L.mjl_env_set_reset_keys.argtypes = [vp, vp, i32]
+    L.mjl_env_step_vjp_guarded.argtypes = [vp] + [vp] * 10 + [vp]
+    L.mjl_state_size.argtypes = [vp]
+    L.mjl_get_state.argtypes = [vp, vp, vp]
+    L.mjl_set_state.argtypes = [vp, vp, vp, vp]
     L.mjl_prng_split.argtypes = [vp, i32, i32, i32, vp, vp]
     L.mjl_gae.argtypes = [f32p, f32p, f32p, f32p, i32, i32, C.c_double, C.c_double, f32p, f32p, vp]
     L.mjl_step_vjp.argtypes = [vp, f32p, f32p, f32p, f32p, f32p, vp]

@@ -92,6 +92,8 @@ class APGTrainer:
             _, r, te, tr = env.step(a.detach(), auto_reset=False)
             if disc is None:
                 disc, ret, rsum = torch.ones_like(r), torch.zeros_like(r), torch.zeros_like(r[0])
+            # a non-finite post-step state must leave the loss at this step: next step its obs would
+            # reach the policy, and backward through tanh turns even a zero cotangent into NaN
             bad = alive & ~(torch.isfinite(r) & torch.isfinite(env.qpos_qvel()).all(1))
             dropped = dropped + bad.sum()
             alive = alive & ~bad
@@ -108,26 +110,28 @@ class APGTrainer:
         gq = torch.zeros((B, env.nq), device=self.device)
         gv = torch.zeros((B, env.nv), device=self.device)
         gaux = None
+        guarded = getattr(env, "guarded_vjp", False)
+        nonfinite = torch.zeros(1, device=self.device) if guarded else None
         for t in range(H - 1, -1, -1):
-            env.set_state(tape[t])
-            if hasattr(env, "set_warmstart"):  # the step's own solution seeds the VJP's recompute
-                env.set_warmstart((tape[t + 1] if t + 1 < H else final)["qacc_warmstart"])
+            # the VJP recomputes the step to find its converged active set; the solution the forward
+            # step reached (the next tape entry's qacc_warmstart) seeds that solve: ~1 Newton iteration
+            env.set_state(tape[t], tape[t + 1] if t + 1 < H else final)
             grew = -discs[t] / B
-            gq, gv, ga, gaux = env.step_vjp(acts[t].detach(), gq, gv, grew, gaux)
-            # an env whose cotangents overflowed (a state blowing up while still in the loss) is cut
-            # from the gradient at this step, like the forward guard above
-            ok = torch.isfinite(gq).all(1) & torch.isfinite(gv).all(1) & torch.isfinite(ga).all(1)
-            if gaux is not None:
-                ok = ok & torch.isfinite(gaux).all(1)
-                gaux = torch.where(ok[:, None], gaux, torch.zeros_like(gaux))
-            dropped = dropped + (~ok).sum()
-            gq = torch.where(ok[:, None], gq, torch.zeros_like(gq))
-            gv = torch.where(ok[:, None], gv, torch.zeros_like(gv))
-            ga = torch.where(ok[:, None], ga, torch.zeros_like(ga))
+            # an env whose cotangents overflow (a state blowing up while still in the loss) is cut from
+            # the gradient at this step, like the forward guard above (in the kernel when it can)
+            gq, gv, ga, gaux = env.step_vjp(acts[t].detach(), gq, gv, grew, gaux, nonfinite)
+            if not guarded:
+                ok = torch.isfinite(gq).all(1) & torch.isfinite(gv).all(1) & torch.isfinite(ga).all(1)
+                dropped = dropped + (~ok).sum()
+                gq = torch.where(ok[:, None], gq, torch.zeros_like(gq))
+                gv = torch.where(ok[:, None], gv, torch.zeros_like(gv))
+                ga = torch.where(ok[:, None], ga, torch.zeros_like(ga))
             torch.autograd.backward(acts[t], grad_tensors=ga)
             og = obs_leaves[t].grad
             gq = gq + og[:, :env.nq]
             gv = gv + og[:, env.nq:]
+        if guarded:
+            dropped = dropped + nonfinite[0]
         return loss.detach(), (rsum / H).detach(), torch.stack(obs_traj), dropped
 
     def update(self, step: int) -> dict:
@@ -186,9 +190,9 @@ class APGTrainer:
 
 
 class HumanoidAPGEnv:
-    """HumanoidEnv adapter for APGTrainer: tape entries are the batch fields a step reads."""
+    """HumanoidEnv adapter for APGTrainer: tape entries are packed state rows (mjl_get_state)."""
 
-    FIELDS = ("qpos", "qvel", "qacc_warmstart", "aux", "time")
+    guarded_vjp = True
 
     def __init__(self, env):
         self.env = env
@@ -205,17 +209,11 @@ class HumanoidAPGEnv:
         return torch.cat([self.env.data.get("qpos"), self.env.data.get("qvel")], 1)
 
     def get_state(self):
-        return {k: self.env.data.get(k) for k in self.FIELDS}
+        return self.env.get_state()
 
-    def set_state(self, st):
-        for k in self.FIELDS:
-            self.env.data.set(k, st[k])
+    def set_state(self, st, warm_from=None):
+        """Restore a tape entry; qacc_warmstart from `warm_from` (another entry) when given."""
+        self.env.set_state(st, warm_from)
 
-    def set_warmstart(self, qacc):
-        """The VJP recomputes the step to find its converged active set; seeding the solver with the
-        solution the forward step reached (the next tape entry's qacc_warmstart) cuts the recompute
-        to ~one Newton iteration."""
-        self.env.data.set("qacc_warmstart", qacc)
-
-    def step_vjp(self, act, gq, gv, grew, gaux):
-        return self.env.step_vjp(act, gq, gv, grew, gaux)
+    def step_vjp(self, act, gq, gv, grew, gaux, nonfinite=None):
+        return self.env.step_vjp(act, gq, gv, grew, gaux, nonfinite)

@@ -102,9 +102,11 @@ class HumanoidEnv:
         return obs, rew, term, trunc
 
     def step_vjp(self, act: torch.Tensor, g_qpos: torch.Tensor, g_qvel: torch.Tensor, g_rew: torch.Tensor,
-                 g_aux: Optional[torch.Tensor] = None) -> Tuple[torch.Tensor, ...]:
+                 g_aux: Optional[torch.Tensor] = None, nonfinite: Optional[torch.Tensor] = None) -> Tuple[torch.Tensor, ...]:
         """VJP of one env step (src/envs.py:333-492, no reset merge) at the current state and aux:
-        cotangents of (qpos', qvel', reward, aux') -> (qpos, qvel, action, aux). State unchanged."""
+        cotangents of (qpos', qvel', reward, aux') -> (qpos, qvel, action, aux). State unchanged.
+        With `nonfinite` (a device float counter) an env whose cotangents come out non-finite gets
+        zero outputs and is counted there."""
         dev, B = self.obs.device, self.num_envs
         f = lambda x, *shape: x.to(dev, torch.float32).reshape(B, *shape).contiguous()  # noqa: E731
         act = f(act, self.act_dim)
@@ -112,9 +114,25 @@ class HumanoidEnv:
         ga = torch.zeros((B, abi.AUX_DIM), device=dev) if g_aux is None else f(g_aux, abi.AUX_DIM)
         oq, ov = torch.empty_like(gq), torch.empty_like(gv)
         oa, oaux = torch.empty_like(act), torch.empty_like(ga)
-        check(lib().mjl_env_step_vjp(self.data.handle, _ptr(act), _ptr(gq), _ptr(gv), _ptr(gr), _ptr(ga), _ptr(oq),
-                                     _ptr(ov), _ptr(oa), _ptr(oaux), _stream()))
+        check(lib().mjl_env_step_vjp_guarded(self.data.handle, _ptr(act), _ptr(gq), _ptr(gv), _ptr(gr), _ptr(ga),
+                                             _ptr(oq), _ptr(ov), _ptr(oa), _ptr(oaux), _ptr(nonfinite), _stream()))
         return oq, ov, oa, oaux
+
+    @property
+    def state_size(self) -> int:
+        return int(lib().mjl_state_size(self.data.handle))
+
+    def get_state(self, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+        """The persistent per-env state as packed rows [num_envs, state_size] = [qpos | qvel |
+        qacc_warmstart | aux | time] (one launch)."""
+        if out is None:
+            out = torch.empty((self.num_envs, self.state_size), dtype=torch.float32, device=self.obs.device)
+        check(lib().mjl_get_state(self.data.handle, _ptr(out), _stream()))
+        return out
+
+    def set_state(self, src: torch.Tensor, ws_src: Optional[torch.Tensor] = None):
+        """Restore packed rows (get_state layout); qacc_warmstart from ws_src's rows if given."""
+        check(lib().mjl_set_state(self.data.handle, _ptr(src.contiguous()), _ptr(ws_src), _stream()))
 
     @property
     def aux(self) -> torch.Tensor:

@@ -47,10 +47,10 @@ class DiffPointEnv:
     def get_state(self):
         return (self.q.clone(), self.v.clone())
 
-    def set_state(self, st):
+    def set_state(self, st, warm_from=None):
         self.q, self.v = st[0].clone(), st[1].clone()
 
-    def step_vjp(self, act, gq, gv, grew, gaux):
+    def step_vjp(self, act, gq, gv, grew, gaux, nonfinite=None):
         q = self.q.clone().requires_grad_(True)
         v = self.v.clone().requires_grad_(True)
         a = act.double().clone().requires_grad_(True)
@@ -192,3 +192,43 @@ def test_humanoid_apg_gradient_matches_oracle_finite_differences():
     an = float(grad @ d)
     assert abs(float(loss_gpu) - loss64(theta)) <= 1e-3 * (1 + abs(loss64(theta)))
     assert an == pytest.approx(fd, rel=2e-2, abs=1e-3)
+
+
+@pytest.mark.gpu
+def test_packed_state_roundtrip_and_guarded_vjp():
+    """mjl_get_state / mjl_set_state restore every persistent field (with the warm-start override);
+    the guarded VJP zeroes and counts exactly the env whose cotangents are non-finite and leaves the
+    others equal to the unguarded VJP."""
+    import mjx_amd
+    from mjx_amd import mjx
+    from mjx_amd.config import reference_ppo_config
+    from mjx_amd.envs import HumanoidEnv, resolve_ids
+    m = mjx_amd.load_model("humanoid_mjx")
+    B = 8
+    env = HumanoidEnv(mjx.put_model(m), resolve_ids(m, reference_ppo_config().env_config), B, seed=2)
+    env.reset()
+    g = torch.Generator(device="cuda").manual_seed(0)
+    for _ in range(5):
+        env.step(torch.rand((B, m.nu), generator=g, device="cuda") * 2 - 1, auto_reset=False)
+    st = env.get_state().clone()
+    fields = {f: env.data.get(f).clone() for f in ("qpos", "qvel", "qacc_warmstart", "aux", "time")}
+    assert st.shape == (B, m.nq + 2 * m.nv + 9 + 1)
+    env.step(torch.zeros((B, m.nu), device="cuda"), auto_reset=False)
+    other = env.get_state().clone()
+    env.set_state(st)
+    for f, v in fields.items():
+        assert torch.equal(env.data.get(f), v), f
+    env.set_state(st, other)
+    assert torch.equal(env.data.get("qacc_warmstart"), other[:, m.nq + m.nv:m.nq + 2 * m.nv])
+    env.set_state(st)
+    act = torch.rand((B, m.nu), generator=g, device="cuda") * 2 - 1
+    gq, gv, gr = torch.randn((B, m.nq), device="cuda"), torch.randn((B, m.nv), device="cuda"), torch.randn(B, device="cuda")
+    ref = env.step_vjp(act, gq, gv, gr)
+    gq2 = gq.clone()
+    gq2[3, 0] = float("nan")
+    cnt = torch.zeros(1, device="cuda")
+    out = env.step_vjp(act, gq2, gv, gr, None, cnt)
+    assert float(cnt) == 1.0
+    keep = torch.arange(B, device="cuda") != 3
+    for a, b in zip(out, ref):
+        assert torch.all(a[3] == 0) and torch.equal(a[keep], b[keep])
