@@ -1237,7 +1237,7 @@ template <class D, bool G> PHASE void solver(MP m_, LDSA WS<D>* W, Rows<G> R, in
   const int nv = m->nv, nefc = W->nefc;
   const bool newton = m->solver == MJL_SOLVER_NEWTON;
   if (nefc == 0) {
-    if (lane < LD) { W->qacc[lane] = W->qacc_smooth[lane]; W->frc_con[lane] = 0.f; }
+    if (lane < LD) { W->qacc[lane] = W->qacc_ws[lane] = W->qacc_smooth[lane]; W->frc_con[lane] = 0.f; }
     if (lane == 0) W->niter = 0;
     SYNC();
     return;
@@ -1339,6 +1339,9 @@ template <class D, bool G> PHASE void solver(MP m_, LDSA WS<D>* W, Rows<G> R, in
     SYNC();
   }
   if (lane == 0) W->niter = iter;
+  // the solution seeds the next solve (MuJoCo mj_fwdConstraint, MJX solver.solve: qacc_warmstart =
+  // qacc), so it belongs to forward: a reset's forward leaves the warm start MJX leaves
+  if (lane < nv) W->qacc_ws[lane] = W->qacc[lane];
   SYNC();
 }
 
@@ -1456,10 +1459,7 @@ template <class D> PHASE void integrate(MP m_, LDSA WS<D>* W, int lane, LDSA flo
     qa = chol_factor_solve<D>(W->H, W->H, W->invd, nv, W->Mv, lane);
   }
   if (ap_out && lane < D::LD) ap_out[lane] = (lane < nv) ? qa : 0.f;  // a' for the step adjoint
-  if (lane < nv) {
-    W->qacc_ws[lane] = W->qacc[lane];
-    W->qvel[lane] += dt * qa;
-  }
+  if (lane < nv) W->qvel[lane] += dt * qa;
   SYNC();
   if (lane < m->njnt) {
     int j = lane, q = m->jnt_qposadr[j], d = m->jnt_dofadr[j];
@@ -1811,6 +1811,7 @@ template <class D, int MODE> __global__ __launch_bounds__(64, MJL_MINWAVES) void
     if (lane == 0) P.out_speed[env] = W->qpos[0];
     return;
   }
+  if (MODE == MODE_FORWARD && lane < nv) S.qacc_warmstart[(size_t)env * nv + lane] = W->qacc_ws[lane];
   if (MODE != MODE_FORWARD) {
     if (lane < nq) S.qpos[(size_t)env * nq + lane] = W->qpos[lane];
     if (lane < nv) {

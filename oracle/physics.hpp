@@ -967,6 +967,9 @@ template <class R> void forward(const mjlModelDesc& m, Data<R>& d) {
   chol_solve(d.L.data(), m.nv, d.qacc_smooth.data());
   Solver<R> s(m, d);
   s.run();
+  // the solution seeds the next solve (MuJoCo mj_fwdConstraint; MJX solver.solve returns
+  // qacc_warmstart = qacc), so it is part of forward, not of the integrator
+  d.qacc_warmstart = d.qacc;
   sensors(m, d);
 }
 
@@ -983,7 +986,6 @@ template <class R> void integrate(const mjlModelDesc& m, Data<R>& d) {
     for (int k = 0; k < nv; k++) qacc[k] = d.qfrc_smooth[k] + d.qfrc_constraint[k];
     chol_solve(L.data(), nv, qacc.data());
   }
-  d.qacc_warmstart = d.qacc;
   R dt = R(m.timestep);
   for (int k = 0; k < nv; k++) d.qvel[k] += dt * qacc[k];
   for (int j = 0; j < m.njnt; j++) {
