@@ -5,9 +5,9 @@
 set -o pipefail
 mkdir -p gpurun_out/curves
 export TMPDIR=/tmp
-run() {  # name, extra args
+run() {  # name, extra args (checkpoints are dropped: gpurun_out travels back only under 64 MiB)
   timeout -k 10 400 python mujoco-mjx-lab_amd/train_ppo.py --iterations 500 --results-dir gpurun_out/curves/$1 "${@:2}" \
-      > gpurun_out/curves/$1.log 2>&1
+      > gpurun_out/curves/$1.log 2>&1 && rm -rf gpurun_out/curves/$1/*/checkpoints
 }
 run s42_b2048 --num-envs 2048 &&
 run s43_b2048 --num-envs 2048 --config tools/configs/seed43.json &&
