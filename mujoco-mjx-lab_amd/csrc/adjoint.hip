@@ -119,7 +119,7 @@ template <class DM> struct WSA {
   float qpos0[MJL_MAXQ], qvel0[LD];    // pre-step state
   float cvel[NB][6], cacc[NB][6];      // recomputed in the RNE reverse
   alignas(16) float Lc[NV * LD];       // factor of Hc at the converged active set
-  float invdc[LD];
+  alignas(16) float invdc[LD];
   float ap[LD];                        // integrator acceleration a'
   float lp[NB][3], lq[NB][4];          // body transform in the parent frame
   float ftmp[NV][6];                   // scratch: f_i = I(crb) cdof_i, then its cotangent

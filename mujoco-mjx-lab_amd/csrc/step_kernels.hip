@@ -128,6 +128,7 @@ INL unsigned long long lanes_below(int lane) { return (1ull << lane) - 1ull; }
 // a packed model record as whole b128 loads from the constant model block
 typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
 typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
 template <class T> INL T ldrec(const CSTA T* p) {
   static_assert(sizeof(T) % 16 == 0, "records are 16-byte rows");
   union { u32x4 v[sizeof(T) / 16]; T t; } u;
@@ -155,7 +156,7 @@ template <class DM> struct WS {
   float tenJ[MJL_MAXTENDON][LD], tenlen[MJL_MAXTENDON];
   alignas(16) float M[NV * LD];
   alignas(16) float H[NV * LD];  // factor of M, Newton Hessian + factor, or implicit-integration factor
-  float invd[LD];                // 1 / diag of the factor in H
+  alignas(16) float invd[LD];    // 1 / diag of the factor in H
   alignas(16) float frc_bias[LD];
   alignas(16) float frc_passive[LD];
   alignas(16) float frc_act[LD];
@@ -325,15 +326,104 @@ template <class D> INL void chol_factor(LDSA float* A, LDSA float* invd_out, int
 }
 
 // Factor + solve in one pass, for the hot callers (M in forward / integrate, the Newton Hessian):
-// L L^T = S (S: n x n SPD in LDS at src, stride LD), L written to dst (upper zeroed) with
-// invd_out[i] = 1 / L[i][i]; returns (L L^T)^-1 rhs with row i's value in lanes i and i + 32.
+// L L^T = S (S: n x n SPD in LDS at src, stride LD), L written to dst (lower triangle; the upper
+// triangle is unspecified, chol_solve reads only the lower) with invd_out[i] = 1 / L[i][i];
+// returns (L L^T)^-1 rhs with row i's value in lanes i and i + 32.
+//
+// nv < 32 (chol_aug_factor_solve): rows of S in VGPRs, lane l and l + 32 both holding row l & 31,
+// and the right-hand side riding along as one more row, R = NV. The factor's own column
+// broadcasts then run the forward substitution: lane R ends with L[R][k] = y_k (L y = rhs). The
+// back substitution runs on the unit upper factor diag(L)^-1 L^T: lane i pre-scales its column
+// L[k][i] (k > i) by its own 1 / L[i][i], so each of the NV serial steps is one readlane and one
+// fma, with no lane masks in the chain. Trailing update of the first 16 columns on MFMA (below).
+template <class D> INL float chol_aug_factor_solve(const LDSA float* src, LDSA float* dst, LDSA float* invd_out,
+                                                   int n, const LDSA float* rhs, int lane) {
+  constexpr int NV = D::NV, LD = D::LD, R = NV;
+  static_assert(NV < 32 && LD % 4 == 0 && LD > NV, "augmented factor needs a spare row and 16-B rows");
+  constexpr int B1 = NV > 16 ? 16 : NV;
+  const int i = lane & 31, kh = lane >> 5;
+  float a[LD];
+  {  // row i of S (lanes i < n), the right-hand side (every other lane; kept by lane R)
+    const LDSA f32x4* rp = (const LDSA f32x4*)((i < n) ? src + i * LD : rhs);
+#pragma unroll
+    for (int q = 0; q < LD / 4; q++) {
+      const f32x4 v = rp[q];
+      a[4 * q] = v[0]; a[4 * q + 1] = v[1]; a[4 * q + 2] = v[2]; a[4 * q + 3] = v[3];
+    }
+  }
+  if (n != NV) {  // uniform: padded rows / columns act as the identity, rhs entries >= n are zero
+#pragma unroll
+    for (int j = 0; j < NV; j++) a[j] = (j < n && (i < n || i == R)) ? a[j] : (i == j ? 1.f : 0.f);
+  }
+#pragma unroll
+  for (int k = 0; k < B1; k++) {
+    const float inv = __builtin_amdgcn_rsqf(fmaxf(rdlane(a[k], k), 1e-30f));
+    a[k] *= inv;  // lane k: sqrt of its pivot
+#pragma unroll
+    for (int j = k + 1; j < B1; j++) a[j] = fmaf(-a[k], rdlane(a[k], j), a[j]);
+  }
+  if constexpr (NV > B1) {
+    f32x16 acc;
+#pragma unroll
+    for (int v = 0; v < 16; v++) acc[v] = 0.f;
+#pragma unroll
+    for (int t = 0; t < B1 / 2; t++) {
+      const float op = kh ? a[2 * t + 1] : a[2 * t];
+      acc = __builtin_amdgcn_mfma_f32_32x32x2f32(op, op, acc, 0, 0, 0);
+    }
+    float lo[16], hi[16];
+#pragma unroll
+    for (int v = B1 / 2; v < 16; v++) {
+      auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(acc[v]), __float_as_uint(acc[v]), false, false);
+      lo[v] = __uint_as_float(r[0]);
+      hi[v] = __uint_as_float(r[1]);
+    }
+#pragma unroll
+    for (int j = B1; j < NV; j++) {
+      const int v = (j & 3) + 4 * (j >> 3);
+      a[j] -= ((j >> 2) & 1) ? hi[v] : lo[v];
+    }
+#pragma unroll
+    for (int k = B1; k < NV; k++) {
+      const float inv = __builtin_amdgcn_rsqf(fmaxf(rdlane(a[k], k), 1e-30f));
+      a[k] *= inv;
+#pragma unroll
+      for (int j = k + 1; j < NV; j++) a[j] = fmaf(-a[k], rdlane(a[k], j), a[j]);
+    }
+  }
+  // rows of L to dst, y = L[R][0..NV) to invd_out (scratch until the reads below)
+  if (lane <= R) {
+    LDSA f32x4* wp = (LDSA f32x4*)((i == R) ? invd_out : dst + i * LD);
+#pragma unroll
+    for (int q = 0; q < LD / 4; q++) {
+      f32x4 v;
+      v[0] = a[4 * q]; v[1] = a[4 * q + 1]; v[2] = a[4 * q + 2]; v[3] = a[4 * q + 3];
+      wp[q] = v;
+    }
+  }
+  SYNC();
+  const float y = (i < NV) ? invd_out[i] : 0.f;
+  const float invd = (i < NV) ? __builtin_amdgcn_rcpf(dst[i * LD + i]) : 1.f;
+  float w[NV];
+#pragma unroll
+  for (int k = 0; k < NV; k++) w[k] = dst[k * LD + i];
+  if (lane < NV) invd_out[lane] = invd;  // after the y read (same wave: LDS requests complete in order)
+#pragma unroll
+  for (int k = 0; k < NV; k++) w[k] = (i < k) ? w[k] * invd : 0.f;  // L[k][i] / L[i][i]
+  float x = y * invd;
+#pragma unroll
+  for (int k = NV - 1; k >= 0; k--) x = fmaf(-w[k], rdlane(x, k), x);
+  return x;
+}
+
+// nv = 32 (chol_rows_factor_solve, the generic instantiation): explicit forward substitution.
 // Lanes l and l + 32 both hold row l & 31, so the trailing update of the two-block right-looking
 // factorisation, S22 -= L21 L21^T over the first 16 columns, is 8 fp32 MFMAs whose A and B
 // operands are the lane's own registers. The MFMA result C has row r of C in column r of the
 // C layout, i.e. C[i][j] sits in lane i (half (j >> 2) & 1) register (j & 3) + 4 (j >> 3);
 // v_permlane32_swap of a register with itself hands each lane both halves' values.
-template <class D> INL float chol_factor_solve(const LDSA float* src, LDSA float* dst, LDSA float* invd_out,
-                                               int n, const LDSA float* rhs, int lane) {
+template <class D> INL float chol_rows_factor_solve(const LDSA float* src, LDSA float* dst, LDSA float* invd_out,
+                                                    int n, const LDSA float* rhs, int lane) {
   constexpr int NV = D::NV, LD = D::LD;
   constexpr int B1 = NV > 16 ? 16 : NV;
   const int i = lane & 31, kh = lane >> 5;
@@ -404,6 +494,14 @@ template <class D> INL float chol_factor_solve(const LDSA float* src, LDSA float
     x = (i == k) ? zk : ((i < k) ? fmaf(-lc[k], zk, x) : x);
   }
   return x;
+}
+
+template <class D> INL float chol_factor_solve(const LDSA float* src, LDSA float* dst, LDSA float* invd_out,
+                                               int n, const LDSA float* rhs, int lane) {
+#ifndef MJL_CHOL_ROWS
+  if constexpr (D::NV < 32) return chol_aug_factor_solve<D>(src, dst, invd_out, n, rhs, lane);
+#endif
+  return chol_rows_factor_solve<D>(src, dst, invd_out, n, rhs, lane);
 }
 
 // x distributed (lane i holds b_i, zero for i >= n) -> (L L^T)^-1 b, L from chol_factor
