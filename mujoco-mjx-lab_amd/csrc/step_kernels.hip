@@ -336,19 +336,33 @@ template <class D> INL void chol_factor(LDSA float* A, LDSA float* invd_out, int
 // back substitution runs on the unit upper factor diag(L)^-1 L^T: lane i pre-scales its column
 // L[k][i] (k > i) by its own 1 / L[i][i], so each of the NV serial steps is one readlane and one
 // fma, with no lane masks in the chain. Trailing update of the first 16 columns on MFMA (below).
-template <class D> INL float chol_aug_factor_solve(const LDSA float* src, LDSA float* dst, LDSA float* invd_out,
-                                                   int n, const LDSA float* rhs, int lane) {
+// ADD: S = src + C, C a symmetric matrix in a v_mfma_f32_32x32x2_f32 accumulator (C layout: register
+// v of lane l holds C[(v&3) + 8(v>>2) + 4(l>>5)][l&31], zero outside nv x nv): by symmetry lane c's
+// registers hold row c at the columns of its half, and v_permlane32_swap hands it the other half's.
+template <class D, bool ADD> INL float chol_aug_factor_solve(const LDSA float* src, LDSA float* dst,
+                                                             LDSA float* invd_out, int n, const LDSA float* rhs,
+                                                             int lane, f32x16 C = {}) {
   constexpr int NV = D::NV, LD = D::LD, R = NV;
   static_assert(NV < 32 && LD % 4 == 0 && LD > NV, "augmented factor needs a spare row and 16-B rows");
   constexpr int B1 = NV > 16 ? 16 : NV;
   const int i = lane & 31, kh = lane >> 5;
   float a[LD];
+  if constexpr (ADD) {
+#pragma unroll
+    for (int v = 0; v < 16; v++) {
+      auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(C[v]), __float_as_uint(C[v]), false, false);
+      const int j0 = (v & 3) + 8 * (v >> 2);
+      if (j0 < LD) a[j0] = __uint_as_float(r[0]);
+      if (j0 + 4 < LD) a[j0 + 4] = __uint_as_float(r[1]);
+    }
+  }
   {  // row i of S (lanes i < n), the right-hand side (every other lane; kept by lane R)
     const LDSA f32x4* rp = (const LDSA f32x4*)((i < n) ? src + i * LD : rhs);
 #pragma unroll
     for (int q = 0; q < LD / 4; q++) {
       const f32x4 v = rp[q];
-      a[4 * q] = v[0]; a[4 * q + 1] = v[1]; a[4 * q + 2] = v[2]; a[4 * q + 3] = v[3];
+#pragma unroll
+      for (int e = 0; e < 4; e++) a[4 * q + e] = ADD ? a[4 * q + e] + v[e] : v[e];
     }
   }
   if (n != NV) {  // uniform: padded rows / columns act as the identity, rhs entries >= n are zero
@@ -499,7 +513,7 @@ template <class D> INL float chol_rows_factor_solve(const LDSA float* src, LDSA 
 template <class D> INL float chol_factor_solve(const LDSA float* src, LDSA float* dst, LDSA float* invd_out,
                                                int n, const LDSA float* rhs, int lane) {
 #ifndef MJL_CHOL_ROWS
-  if constexpr (D::NV < 32) return chol_aug_factor_solve<D>(src, dst, invd_out, n, rhs, lane);
+  if constexpr (D::NV < 32) return chol_aug_factor_solve<D, false>(src, dst, invd_out, n, rhs, lane);
 #endif
   return chol_rows_factor_solve<D>(src, dst, invd_out, n, rhs, lane);
 }
@@ -507,21 +521,22 @@ template <class D> INL float chol_factor_solve(const LDSA float* src, LDSA float
 // x distributed (lane i holds b_i, zero for i >= n) -> (L L^T)^-1 b, L from chol_factor
 template <class D> INL float chol_solve(const LDSA float* L, const LDSA float* invd_in, float x, int lane) {
   constexpr int NV = D::NV, LD = D::LD;
-  float row[NV];
-#pragma unroll
-  for (int j = 0; j < NV; j++) row[j] = (lane < NV) ? L[lane * LD + j] : 0.f;
-  float invd = (lane < NV) ? invd_in[lane] : 1.f;
+  // unit-triangular forms, each lane scaling its own row / column by its own 1 / L[i][i]:
+  // L y = b  <=>  (diag(L)^-1 L) y = diag(L)^-1 b;  L^T z = y  <=>  (L diag(L)^-1)^T z = diag(L)^-1 y,
+  // so every serial step is one readlane and one fma
+  const float invd = (lane < NV) ? invd_in[lane] : 1.f;
+  float wr[NV], wc[NV];
 #pragma unroll
   for (int k = 0; k < NV; k++) {
-    float yk = rdlane(x, k) * rdlane(invd, k);
-    x = (lane == k) ? yk : ((lane > k) ? fmaf(-row[k], yk, x) : x);
+    wr[k] = (lane < NV && lane > k) ? L[lane * LD + k] * invd : 0.f;  // L[i][k] / L[i][i]
+    wc[k] = (lane < k) ? L[k * LD + lane] * invd : 0.f;                // L[k][i] / L[i][i]
   }
+  x *= invd;
 #pragma unroll
-  for (int k = NV - 1; k >= 0; k--) {
-    float zk = rdlane(x, k) * rdlane(invd, k);
-    float lki = (lane < k) ? L[k * LD + lane] : 0.f;
-    x = (lane == k) ? zk : ((lane < k) ? fmaf(-lki, zk, x) : x);
-  }
+  for (int k = 0; k < NV; k++) x = fmaf(-wr[k], rdlane(x, k), x);
+  x *= invd;
+#pragma unroll
+  for (int k = NV - 1; k >= 0; k--) x = fmaf(-wc[k], rdlane(x, k), x);
   return x;
 }
 
@@ -1188,7 +1203,7 @@ template <class D, bool G> INL float solver_update(MP m_, LDSA WS<D>* W, Rows<G>
 // v_mfma_f32_32x32x2_f32 takes two constraint rows per instruction, lane l supplying
 // A[i][k] = D_r J[r][i] (active rows only) and B[k][j] = J[r][j] with i = j = l & 31, r = r0 + (l >> 5);
 // the 32x32 accumulator (nv <= 32) is H - M in the C layout row = (v&3) + 8(v>>2) + 4(l>>5), col = l&31.
-template <class D, bool G> INL void solver_hessian(MP m_, LDSA WS<D>* W, Rows<G> R, int lane) {
+template <class D, bool G> INL f32x16 solver_hessian_acc(MP m_, LDSA WS<D>* W, Rows<G> R, int lane) {
   MP m = uniform_ptr(m_);
   constexpr int LD = D::LD;
   const int nv = m->nv, nefc = W->nefc;
@@ -1202,7 +1217,7 @@ template <class D, bool G> INL void solver_hessian(MP m_, LDSA WS<D>* W, Rows<G>
     for (int u = 0; u < 4; u++) {  // loads of 4 row pairs first, then 4 MFMAs
       const int r = r0 + 2 * u + kh;
       a[u] = 0.f; b[u] = 0.f;
-      if (r < nefc && col < LD) {
+      if (r < nefc && col < nv) {
         const float j = R.J[r * LD + col];
         b[u] = j;
         a[u] = R.jar[r] < 0.f ? R.D[r] * j : 0.f;
@@ -1211,6 +1226,13 @@ template <class D, bool G> INL void solver_hessian(MP m_, LDSA WS<D>* W, Rows<G>
 #pragma unroll
     for (int u = 0; u < 4; u++) acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a[u], b[u], acc, 0, 0, 0);
   }
+  return acc;
+}
+template <class D, bool G> INL void solver_hessian(MP m_, LDSA WS<D>* W, Rows<G> R, int lane) {
+  constexpr int LD = D::LD;
+  const int nv = uniform_ptr(m_)->nv;
+  const int col = lane & 31, kh = lane >> 5;
+  const f32x16 acc = solver_hessian_acc<D, G>(m_, W, R, lane);
 #pragma unroll
   for (int v = 0; v < 16; v++) {
     const int row = (v & 3) + 8 * (v >> 2) + 4 * kh;
@@ -1414,9 +1436,16 @@ template <class D, bool G> PHASE void solver(MP m_, LDSA WS<D>* W, Rows<G> R, in
     TACC(11, ts, lane);
     if (newton) {
       if (exact_exit) active_masks(hm);
-      solver_hessian<D, G>(m, W, R, lane);
-      TACC(12, ts, lane);
-      float x = chol_factor_solve<D>(W->H, W->H, W->invd, nv, W->grad, lane);
+      float x;
+      if constexpr (D::NV < 32) {  // J'DJ goes from the MFMA accumulator straight into the factor's rows
+        const f32x16 acc = solver_hessian_acc<D, G>(m, W, R, lane);
+        TACC(12, ts, lane);
+        x = chol_aug_factor_solve<D, true>(W->M, W->H, W->invd, nv, W->grad, lane, acc);
+      } else {
+        solver_hessian<D, G>(m, W, R, lane);
+        TACC(12, ts, lane);
+        x = chol_factor_solve<D>(W->H, W->H, W->invd, nv, W->grad, lane);
+      }
       if (lane < nv) W->Mgrad[lane] = x;
       SYNC();
       TACC(13, ts, lane);
