@@ -1149,19 +1149,18 @@ template <class D, bool G> PHASE bool build_rows(MP m_, LDSA WS<D>* W, Rows<G> R
 // ---------------------------------------------------------------------------------------------
 // primal solver (Newton with exact line search; CG with Polak-Ribiere)   [solver.solve]
 // ---------------------------------------------------------------------------------------------
-template <class D> INL float mrow(LDSA WS<D>* W, LDSA float* v, int lane) {  // (M v)[lane]
-  constexpr int LD = D::LD;
-  float s = 0.f;
+// row . v over LD entries as four interleaved partial sums (four 7-long FMA chains, not one 28-long)
+template <int LD, class RowF, class VF> INL float rowdot(RowF* a, VF* v) {
+  float s[4] = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-  for (int k = 0; k < LD; k++) s += W->M[lane * LD + k] * v[k];
-  return s;
+  for (int k = 0; k < LD; k++) s[k & 3] = fmaf(a[k], v[k], s[k & 3]);
+  return (s[0] + s[1]) + (s[2] + s[3]);
+}
+template <class D> INL float mrow(LDSA WS<D>* W, LDSA float* v, int lane) {  // (M v)[lane]
+  return rowdot<D::LD>(W->M + lane * D::LD, v);
 }
 template <class D, class RowF> INL float jrow(RowF* J, LDSA float* v, int r) {  // (J v)[r]
-  constexpr int LD = D::LD;
-  float s = 0.f;
-#pragma unroll
-  for (int k = 0; k < LD; k++) s += J[r * LD + k] * v[k];
-  return s;
+  return rowdot<D::LD>(J + r * D::LD, v);
 }
 
 // forces, cost, qfrc_constraint and gradient at the current qacc / Ma / jar; returns the cost
@@ -1211,6 +1210,36 @@ template <class D, bool G> INL f32x16 solver_hessian_acc(MP m_, LDSA WS<D>* W, R
   f32x16 acc;
 #pragma unroll
   for (int v = 0; v < 16; v++) acc[v] = 0.f;
+#ifndef MJL_HESS_DENSE
+  // only active rows (jar < 0) contribute: take them in order from each 64-row ballot, 8 rows per
+  // trip (uniform row indices from s_ff1), loads of the trip first, then one MFMA per row pair
+  for (int base = 0; base < nefc; base += 64) {
+    unsigned long long am = __ballot(base + lane < nefc && R.jar[base + lane] < 0.f);
+    while (am) {
+      int rr[8];
+#pragma unroll
+      for (int u = 0; u < 8; u++) {
+        rr[u] = am ? base + (int)__builtin_ctzll(am) : -1;
+        am &= am - 1;
+      }
+      float a[4], b[4];
+#pragma unroll
+      for (int u = 0; u < 4; u++) {
+        const int r = kh ? rr[2 * u + 1] : rr[2 * u];
+        const bool ok = r >= 0 && col < nv;
+        const int rs = r >= 0 ? r : 0;
+        const float j = R.J[rs * LD + col];
+        const float dr = R.D[rs];
+        b[u] = ok ? j : 0.f;
+        a[u] = ok ? dr * j : 0.f;
+      }
+#pragma unroll
+      for (int u = 0; u < 4; u++)
+        if (rr[2 * u] >= 0) acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a[u], b[u], acc, 0, 0, 0);
+    }
+  }
+  return acc;
+#endif
   for (int r0 = 0; r0 < nefc; r0 += 8) {
     float a[4], b[4];
 #pragma unroll
@@ -1250,25 +1279,27 @@ template <class D, bool G> INL void solver_hessian(MP m_, LDSA WS<D>* W, Rows<G>
 template <class D, bool G> INL float solver_linesearch(MP m_, LDSA WS<D>* W, Rows<G> R, int lane) {
   MP m = uniform_ptr(m_);
   const int nv = m->nv, nefc = W->nefc;
-  float sn = (lane < nv) ? W->search[lane] * W->search[lane] : 0.f;
-  float snorm = sqrtf(wsum(sn));
-  float gtol = m->tolerance * m->ls_tolerance * snorm / m->scale;
-  float mvl = 0.f;
-  if (lane < nv) { mvl = mrow<D>(W, W->search, lane); W->Mv[lane] = mvl; }
-  for (int r = lane; r < nefc; r += 64) R.Jv[r] = jrow<D>(R.J, W->search, r);
-  float c1p = 0.f, c2p = 0.f;
-  if (lane < nv) { c1p = W->search[lane] * (W->Ma[lane] - W->frc_smooth[lane]); c2p = W->search[lane] * mvl; }
-  float c1 = wsum(c1p), c2 = wsum(c2p);
-  SYNC();
-  // the first 128 rows stay in registers across the line-search iterations
+  // M s, J s (the first 128 rows' J s, jar and D stay in registers across the iterations)
+  const float sv = (lane < nv) ? W->search[lane] : 0.f;
+  float mvl = 0.f, c1p = 0.f, c2p = 0.f;
+  if (lane < nv) {
+    mvl = mrow<D>(W, W->search, lane);
+    W->Mv[lane] = mvl;
+    c1p = sv * (W->Ma[lane] - W->frc_smooth[lane]);
+    c2p = sv * mvl;
+  }
   float jv0 = 0.f, ja0 = 0.f, dd0 = 0.f, jv1 = 0.f, ja1 = 0.f, dd1 = 0.f;
-  if (lane < nefc) { jv0 = R.Jv[lane]; ja0 = R.jar[lane]; dd0 = R.D[lane]; }
-  if (lane + 64 < nefc) { jv1 = R.Jv[lane + 64]; ja1 = R.jar[lane + 64]; dd1 = R.D[lane + 64]; }
-  // f'(al[k]), f''(al[k]) for K points (COST: the relative cost instead) in one pass over the rows
-  auto eval = [&](auto Kc, auto COSTc, const float* al, float* o0, float* o1) {
+  if (lane < nefc) { jv0 = jrow<D>(R.J, W->search, lane); ja0 = R.jar[lane]; dd0 = R.D[lane]; R.Jv[lane] = jv0; }
+  if (lane + 64 < nefc) {
+    jv1 = jrow<D>(R.J, W->search, lane + 64); ja1 = R.jar[lane + 64]; dd1 = R.D[lane + 64]; R.Jv[lane + 64] = jv1;
+  }
+  for (int r = lane + 128; r < nefc; r += 64) R.Jv[r] = jrow<D>(R.J, W->search, r);
+  SYNC();
+  // lane partial sums of f'(al[k]), f''(al[k]) for K points (COST: of the relative cost), one
+  // pass over the rows; `fin` turns them into the values (wave sums)
+  auto partial = [&](auto Kc, auto COSTc, const float* al, float* dp, float* hp) {
     constexpr int K = decltype(Kc)::value;
     constexpr bool COST = decltype(COSTc)::value;
-    float dp[K], hp[K];
 #pragma unroll
     for (int k = 0; k < K; k++) { dp[k] = 0.f; hp[k] = 0.f; }
     auto row = [&](float ja, float jv, float dd) {
@@ -1283,6 +1314,11 @@ template <class D, bool G> INL float solver_linesearch(MP m_, LDSA WS<D>* W, Row
     row(ja0, jv0, dd0);
     row(ja1, jv1, dd1);
     for (int r = lane + 128; r < nefc; r += 64) row(R.jar[r], R.Jv[r], R.D[r]);
+  };
+  float c1 = 0.f, c2 = 0.f;
+  auto fin = [&](auto Kc, auto COSTc, const float* al, const float* dp, const float* hp, float* o0, float* o1) {
+    constexpr int K = decltype(Kc)::value;
+    constexpr bool COST = decltype(COSTc)::value;
 #pragma unroll
     for (int k = 0; k < K; k++) {
       if (COST) {
@@ -1294,22 +1330,37 @@ template <class D, bool G> INL float solver_linesearch(MP m_, LDSA WS<D>* W, Row
       }
     }
   };
+  auto eval = [&](auto Kc, auto COSTc, const float* al, float* o0, float* o1) {
+    constexpr int K = decltype(Kc)::value;
+    float dp[K], hp[K];
+    partial(Kc, COSTc, al, dp, hp);
+    fin(Kc, COSTc, al, dp, hp, o0, o1);
+  };
   using I1 = std::integral_constant<int, 1>;
   using I3 = std::integral_constant<int, 3>;
   using TF = std::false_type;
   using TT = std::true_type;
-  // p0 and the Newton point q from it
-  float a0[1] = {0.f}, p0d0[1], p0d1[1];
-  eval(I1{}, TF{}, a0, p0d0, p0d1);
+  // |s|, the Gauss terms c1 = s'(Ma - f), c2 = s'Ms and p0 = f'(0), f''(0): one batch of wave sums
+  float a0[1] = {0.f}, p0d0[1], p0d1[1], snorm;
+  {
+    float dp[1], hp[1];
+    partial(I1{}, TF{}, a0, dp, hp);
+    snorm = sqrtf(wsum(sv * sv));
+    c1 = wsum(c1p);
+    c2 = wsum(c2p);
+    fin(I1{}, TF{}, a0, dp, hp, p0d0, p0d1);
+  }
+  const float gtol = m->tolerance * m->ls_tolerance * snorm / m->scale;
+  // the Newton point q from p0
   float a1[1] = {-p0d0[0] * __builtin_amdgcn_rcpf(p0d1[0])}, qd0[1], qd1[1];
-  eval(I1{}, TF{}, a1, qd0, qd1);
   // exact segment: if no row changes activity between 0 and q, f' is linear there and q is its
   // root, the minimiser MJX's iterations then only jitter around in rounding noise
   {
-    bool same = true;
-    for (int r = lane; r < nefc; r += 64) same &= (R.jar[r] < 0.f) == (R.jar[r] + a1[0] * R.Jv[r] < 0.f);
+    bool same = ((ja0 < 0.f) == (ja0 + a1[0] * jv0 < 0.f)) && ((ja1 < 0.f) == (ja1 + a1[0] * jv1 < 0.f));
+    for (int r = lane + 128; r < nefc; r += 64) same &= (R.jar[r] < 0.f) == (R.jar[r] + a1[0] * R.Jv[r] < 0.f);
     if (__ballot(!same) == 0ull) { TCOUNT(15, 1, lane); return a1[0]; }
   }
+  eval(I1{}, TF{}, a1, qd0, qd1);
   // lo = whichever of p0, q has the smaller f'
   float loa, lod0, lod1, hia, hid0, hid1;
   if (qd0[0] < p0d0[0]) { loa = a1[0]; lod0 = qd0[0]; lod1 = qd1[0]; hia = 0.f; hid0 = p0d0[0]; hid1 = p0d1[0]; }
