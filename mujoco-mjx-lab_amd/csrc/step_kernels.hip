@@ -47,19 +47,19 @@ __device__ unsigned long long* g_stamps;
 #define STAMP(slot, lane)                                                                        \
   do {                                                                                           \
     unsigned long long t_ = __builtin_amdgcn_s_memtime();                                        \
-    if ((lane) == 0 && g_stamps) g_stamps[(size_t)blockIdx.x * 16 + (slot)] = t_;               \
+    if ((lane) == 0 && g_stamps) g_stamps[(size_t)blockIdx.x * 32 + (slot)] = t_;               \
   } while (0)
 // accumulate the cycles since `var` into slot (solver sub-phases), restart `var`
 #define TSTART(var) unsigned long long var = __builtin_amdgcn_s_memtime()
 #define TACC(slot, var, lane)                                                                    \
   do {                                                                                           \
     unsigned long long t_ = __builtin_amdgcn_s_memtime();                                        \
-    if ((lane) == 0 && g_stamps) g_stamps[(size_t)blockIdx.x * 16 + (slot)] += t_ - (var);      \
+    if ((lane) == 0 && g_stamps) g_stamps[(size_t)blockIdx.x * 32 + (slot)] += t_ - (var);      \
     (var) = t_;                                                                                  \
   } while (0)
 #define TCOUNT(slot, n, lane)                                                                    \
   do {                                                                                           \
-    if ((lane) == 0 && g_stamps) g_stamps[(size_t)blockIdx.x * 16 + (slot)] += (n);             \
+    if ((lane) == 0 && g_stamps) g_stamps[(size_t)blockIdx.x * 32 + (slot)] += (n);             \
   } while (0)
 #else
 #define STAMP(slot, lane) do { } while (0)
@@ -336,6 +336,8 @@ template <class D> INL void chol_factor(LDSA float* A, LDSA float* invd_out, int
 // back substitution runs on the unit upper factor diag(L)^-1 L^T: lane i pre-scales its column
 // L[k][i] (k > i) by its own 1 / L[i][i], so each of the NV serial steps is one readlane and one
 // fma, with no lane masks in the chain. Trailing update of the first 16 columns on MFMA (below).
+// Padding contract (n < NV): S is the identity outside its n x n block (M is built that way, and
+// the Newton / implicit matrices inherit it) and rhs is zero beyond n.
 // ADD: S = src + C, C a symmetric matrix in a v_mfma_f32_32x32x2_f32 accumulator (C layout: register
 // v of lane l holds C[(v&3) + 8(v>>2) + 4(l>>5)][l&31], zero outside nv x nv): by symmetry lane c's
 // registers hold row c at the columns of its half, and v_permlane32_swap hands it the other half's.
@@ -346,6 +348,7 @@ template <class D, bool ADD> INL float chol_aug_factor_solve(const LDSA float* s
   static_assert(NV < 32 && LD % 4 == 0 && LD > NV, "augmented factor needs a spare row and 16-B rows");
   constexpr int B1 = NV > 16 ? 16 : NV;
   const int i = lane & 31, kh = lane >> 5;
+  (void)n;
   float a[LD];
   if constexpr (ADD) {
 #pragma unroll
@@ -356,8 +359,8 @@ template <class D, bool ADD> INL float chol_aug_factor_solve(const LDSA float* s
       if (j0 + 4 < LD) a[j0 + 4] = __uint_as_float(r[1]);
     }
   }
-  {  // row i of S (lanes i < n), the right-hand side (every other lane; kept by lane R)
-    const LDSA f32x4* rp = (const LDSA f32x4*)((i < n) ? src + i * LD : rhs);
+  {  // row i of S (lanes i < NV), the right-hand side (lanes >= NV; kept by lane R)
+    const LDSA f32x4* rp = (const LDSA f32x4*)((i < NV) ? src + i * LD : rhs);
 #pragma unroll
     for (int q = 0; q < LD / 4; q++) {
       const f32x4 v = rp[q];
@@ -365,10 +368,7 @@ template <class D, bool ADD> INL float chol_aug_factor_solve(const LDSA float* s
       for (int e = 0; e < 4; e++) a[4 * q + e] = ADD ? a[4 * q + e] + v[e] : v[e];
     }
   }
-  if (n != NV) {  // uniform: padded rows / columns act as the identity, rhs entries >= n are zero
-#pragma unroll
-    for (int j = 0; j < NV; j++) a[j] = (j < n && (i < n || i == R)) ? a[j] : (i == j ? 1.f : 0.f);
-  }
+
 #pragma unroll
   for (int k = 0; k < B1; k++) {
     const float inv = __builtin_amdgcn_rsqf(fmaxf(rdlane(a[k], k), 1e-30f));
@@ -546,6 +546,7 @@ template <class D> INL float chol_solve(const LDSA float* L, const LDSA float* i
 template <class D> PHASE void kinematics(MP m_, LDSA WS<D>* W, int lane) {
   MP m = uniform_ptr(m_);
   const int maxlevel = m->maxlevel, nbody = m->nbody, ngeom = m->ngeom, nsite = m->nsite, njnt = m->njnt;
+  TSTART(tk);
   // model records of this lane, loaded once: body `lane`, geom `lane`, site `lane - 32`, joint `lane`
   const bool isb = lane > 0 && lane < nbody;
   BodyRec br = ldrec(&m->brec[isb ? lane : 0]);
@@ -559,6 +560,7 @@ template <class D> PHASE void kinematics(MP m_, LDSA WS<D>* W, int lane) {
   }
   const JntRec jown = ldrec(&m->jrec[isj ? lane : 0]);
   const int jpar = jown.parent, jfree = isj ? jown.isfree : 1;
+  TACC(16, tk, lane);
   if (lane == 0) {
     W->xpos[0][0] = W->xpos[0][1] = W->xpos[0][2] = 0.f;
     W->xquat[0][0] = 1.f; W->xquat[0][1] = W->xquat[0][2] = W->xquat[0][3] = 0.f;
@@ -575,6 +577,24 @@ template <class D> PHASE void kinematics(MP m_, LDSA WS<D>* W, int lane) {
     }
     W->tenlen[t] = len;
   }
+  // hinge rotations, one joint per lane (all sincos at once): ql_j = [cos(t/2), axis sin(t/2)]
+  float jq[4] = {1.f, 0.f, 0.f, 0.f};
+  if (isj && !jfree) {
+    float s, c;
+    sincosf(0.5f * (W->qpos[jown.qadr] - jown.qpos0), &s, &c);
+    jq[0] = c; jq[1] = jown.axis[0] * s; jq[2] = jown.axis[1] * s; jq[3] = jown.axis[2] * s;
+  }
+  // a body's first three joints: records loaded together up front, rotations from the joint lanes
+  constexpr int KJ = 3;
+  JntRec jr3[KJ];
+  float ql3[KJ][4];
+#pragma unroll
+  for (int k = 0; k < KJ; k++) {
+    const int j = (isb && k < br.jntnum) ? br.jntadr + k : 0;
+    jr3[k] = ldrec(&m->jrec[j]);
+#pragma unroll
+    for (int e = 0; e < 4; e++) ql3[k][e] = __shfl(jq[e], j);
+  }
   // body transform relative to its parent (lane = body, all bodies at once); hinge anchors and
   // axes are left in the parent frame in xanchor / xaxis and moved to world after the tree pass
   float lp[3], lq[4];
@@ -587,7 +607,25 @@ template <class D> PHASE void kinematics(MP m_, LDSA WS<D>* W, int lane) {
     } else {
       lp[0] = br.pos[0]; lp[1] = br.pos[1]; lp[2] = br.pos[2];
       lq[0] = br.quat[0]; lq[1] = br.quat[1]; lq[2] = br.quat[2]; lq[3] = br.quat[3];
-      for (int j = br.jntadr; j < br.jntadr + br.jntnum; j++) {
+#pragma unroll
+      for (int k = 0; k < KJ; k++) {
+        if (k >= br.jntnum) break;
+        const int j = br.jntadr + k;
+        const JntRec& jr = jr3[k];
+        float mat[9], anc[3], ax[3];
+        q2m(mat, lq);
+        mv3(anc, mat, jr.pos);
+        anc[0] += lp[0]; anc[1] += lp[1]; anc[2] += lp[2];
+        mv3(ax, mat, jr.axis);
+        W->xanchor[j][0] = anc[0]; W->xanchor[j][1] = anc[1]; W->xanchor[j][2] = anc[2];
+        W->xaxis[j][0] = ax[0]; W->xaxis[j][1] = ax[1]; W->xaxis[j][2] = ax[2];
+        qmul(lq, lq, ql3[k]);
+        float off[3];
+        q2m(mat, lq);
+        mv3(off, mat, jr.pos);
+        lp[0] = anc[0] - off[0]; lp[1] = anc[1] - off[1]; lp[2] = anc[2] - off[2];
+      }
+      for (int j = br.jntadr + KJ; j < br.jntadr + br.jntnum; j++) {  // bodies with more hinges
         const JntRec jr = ldrec(&m->jrec[j]);
         float mat[9], anc[3], ax[3];
         q2m(mat, lq);
@@ -608,34 +646,50 @@ template <class D> PHASE void kinematics(MP m_, LDSA WS<D>* W, int lane) {
     }
   }
   SYNC();
-  // tree pass: compose with the parent's world frame, one level at a time  [smooth.kinematics]
+  TACC(17, tk, lane);
+  // tree pass: compose with the parent's world frame, one level at a time  [smooth.kinematics].
+  // A body's frame stays in its lane's registers; children read it with ds_bpermute (no LDS
+  // round trip and no barrier per level), the parent's rotation matrix recomputed from its quat.
   float bm[4] = {0.f, 0.f, 0.f, 0.f};  // this body's mass moment and mass
-  for (int L = 1; L <= maxlevel; L++) {
-    if (isb && br.level == L) {
-      float pos[3], quat[4], mat[9];
-      if (br.isfree) {
-        pos[0] = lp[0]; pos[1] = lp[1]; pos[2] = lp[2];
-        quat[0] = lq[0]; quat[1] = lq[1]; quat[2] = lq[2]; quat[3] = lq[3];
-      } else {
-        const int p = br.parent;
-        mv3(pos, W->xmat[p], lp);
-        pos[0] += W->xpos[p][0]; pos[1] += W->xpos[p][1]; pos[2] += W->xpos[p][2];
-        qmul(quat, W->xquat[p], lq);
-        qnorm(quat);
+  float wp[3] = {0.f, 0.f, 0.f}, wq[4] = {1.f, 0.f, 0.f, 0.f};  // lane 0: the world frame
+  {
+    const int par = isb ? br.parent : 0;
+    for (int L = 1; L <= maxlevel; L++) {
+      float pp[3], pq[4];
+#pragma unroll
+      for (int i = 0; i < 3; i++) pp[i] = __shfl(wp[i], par);
+#pragma unroll
+      for (int i = 0; i < 4; i++) pq[i] = __shfl(wq[i], par);
+      if (isb && br.level == L) {
+        if (br.isfree) {
+          wp[0] = lp[0]; wp[1] = lp[1]; wp[2] = lp[2];
+          wq[0] = lq[0]; wq[1] = lq[1]; wq[2] = lq[2]; wq[3] = lq[3];
+        } else {
+          float pm[9];
+          q2m(pm, pq);
+          mv3(wp, pm, lp);
+          wp[0] += pp[0]; wp[1] += pp[1]; wp[2] += pp[2];
+          qmul(wq, pq, lq);
+          qnorm(wq);
+        }
       }
-      q2m(mat, quat);
-      const int b = lane;
-      for (int i = 0; i < 3; i++) W->xpos[b][i] = pos[i];
-      for (int i = 0; i < 4; i++) W->xquat[b][i] = quat[i];
-      for (int i = 0; i < 9; i++) W->xmat[b][i] = mat[i];
-      float ip[3];
-      mv3(ip, mat, br.ipos);
-      W->xipos[b][0] = pos[0] + ip[0]; W->xipos[b][1] = pos[1] + ip[1]; W->xipos[b][2] = pos[2] + ip[2];
-      bm[0] = br.mass * W->xipos[b][0]; bm[1] = br.mass * W->xipos[b][1]; bm[2] = br.mass * W->xipos[b][2];
-      bm[3] = br.mass;
     }
-    SYNC();
   }
+  if (isb) {
+    float mat[9], ip[3];
+    q2m(mat, wq);
+    const int b = lane;
+    for (int i = 0; i < 3; i++) W->xpos[b][i] = wp[i];
+    for (int i = 0; i < 4; i++) W->xquat[b][i] = wq[i];
+    for (int i = 0; i < 9; i++) W->xmat[b][i] = mat[i];
+    mv3(ip, mat, br.ipos);
+    ip[0] += wp[0]; ip[1] += wp[1]; ip[2] += wp[2];
+    W->xipos[b][0] = ip[0]; W->xipos[b][1] = ip[1]; W->xipos[b][2] = ip[2];
+    bm[0] = br.mass * ip[0]; bm[1] = br.mass * ip[1]; bm[2] = br.mass * ip[2];
+    bm[3] = br.mass;
+  }
+  SYNC();
+  TACC(18, tk, lane);
   if (isj) {  // joint anchors / axes to world (lane = joint)
     float anc[3], ax[3];
     if (jfree) {  // free joint: anchor = body position, axis = body z
@@ -667,6 +721,7 @@ template <class D> PHASE void kinematics(MP m_, LDSA WS<D>* W, int lane) {
       for (int j = 0; j < 3; j++)
         W->smat[s][3 * i + j] = W->xmat[sb][3 * i] * sm[j] + W->xmat[sb][3 * i + 1] * sm[3 + j] + W->xmat[sb][3 * i + 2] * sm[6 + j];
   }
+  TACC(19, tk, lane);
   // subtree com of the kinematic roots, the only subtree com the dynamics reads (cinert, cdof and
   // contact Jacobians are taken about scom[rootid]); a root's subtree is lanes [r, subtree_end)
   for (int q = 0; q < m->nroot; q++) {
@@ -690,6 +745,7 @@ template <class D> PHASE void com_pos_crb(MP m_, LDSA WS<D>* W, int lane) {
   const bool isb = lane < nbody, iscd = lane >= 32 && lane - 32 < nv, iscol = lane < nv;
   const BodyRec br = ldrec(&m->brec[isb ? lane : 0]);
   const DofRec dcd = ldrec(&m->drec[iscd ? lane - 32 : 0]), dcol = ldrec(&m->drec[iscol ? lane : 0]);
+  TSTART(tc);
   float t[6];
   for (int i = 0; i < 6; i++) t[i] = isb ? m->body_inertia[lane][i] : 0.f;
   if (isb) {
@@ -740,6 +796,7 @@ template <class D> PHASE void com_pos_crb(MP m_, LDSA WS<D>* W, int lane) {
     }
   }
   SYNC();
+  TACC(23, tc, lane);
   if (isb) {
     const int b = lane;
     float s[10];
@@ -749,7 +806,9 @@ template <class D> PHASE void com_pos_crb(MP m_, LDSA WS<D>* W, int lane) {
     for (int i = 0; i < 10; i++) W->crb[b][i] = s[i];
   }
   for (int i = lane; i < D::NV * LD; i += 64) W->M[i] = 0.f;
+  if (lane >= nv && lane < D::NV) W->M[lane * LD + lane] = 1.f;  // padded rows / cols: the identity
   SYNC();
+  TACC(24, tc, lane);
   if (iscol) {  // column `lane` of M along the ancestor chain  [smooth.crb / make_m]
     const int i = lane;
     float f[6], c6[6], cr[10];
@@ -781,6 +840,7 @@ template <class D> PHASE void velocity_stage(MP m_, LDSA WS<D>* W, int lane) {
   const BodyRec br = ldrec(&m->brec[isb ? lane : 0]);
   const DofRec dr = ldrec(&m->drec[isd ? lane : 0]);
   int udof = 0, ulim = 0;
+  TSTART(tv);
   float ugear = 0.f, ulo = 0.f, uhi = 0.f;
   if (isu) {
     udof = m->actuator_dof[lane]; ulim = m->actuator_ctrllimited[lane]; ugear = m->actuator_gear[lane];
@@ -815,29 +875,36 @@ template <class D> PHASE void velocity_stage(MP m_, LDSA WS<D>* W, int lane) {
     }
   }
   SYNC();
-  for (int L = 1; L <= maxlevel; L++) {
-    if (isb && br.level == L) {
-      const int p = br.parent;
-      float cv[6], ca[6], x[6];
-      for (int i = 0; i < 6; i++) { cv[i] = W->cvel[p][i]; ca[i] = W->cacc[p][i]; }
-      cross_motion(x, cv, U);
-      for (int i = 0; i < 6; i++) { W->cvel[lane][i] = cv[i] + S[i]; W->cacc[lane][i] = ca[i] + x[i] + T[i]; }
+  TACC(25, tv, lane);
+  // cvel / cacc by levels in registers, the parent's read with ds_bpermute (lane 0: the world,
+  // cvel 0 and cacc = -gravity)
+  float wv[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  float wa[6] = {0.f, 0.f, 0.f, -m->gravity[0], -m->gravity[1], -m->gravity[2]};
+  {
+    const int par = isb ? br.parent : 0;
+    for (int L = 1; L <= maxlevel; L++) {
+      float cv[6], ca[6];
+#pragma unroll
+      for (int i = 0; i < 6; i++) { cv[i] = __shfl(wv[i], par); ca[i] = __shfl(wa[i], par); }
+      if (isb && br.level == L) {
+        float x[6];
+        cross_motion(x, cv, U);
+        for (int i = 0; i < 6; i++) { wv[i] = cv[i] + S[i]; wa[i] = ca[i] + x[i] + T[i]; }
+      }
     }
-    SYNC();
   }
+  TACC(26, tv, lane);
   // body forces cfrc = I*a + v x* (I*v), written over cacc
   float f[6];
   if (isb) {
-    float f1[6], iv[6], f2[6], cv[6], ca[6], ci[10];
-    for (int i = 0; i < 6; i++) { cv[i] = W->cvel[lane][i]; ca[i] = W->cacc[lane][i]; }
+    float f1[6], iv[6], f2[6], ci[10];
     for (int i = 0; i < 10; i++) ci[i] = W->cinert[lane][i];
-    inert_vec(f1, ci, ca);
-    inert_vec(iv, ci, cv);
-    cross_force(f2, cv, iv);
+    inert_vec(f1, ci, wa);
+    inert_vec(iv, ci, wv);
+    cross_force(f2, wv, iv);
     for (int i = 0; i < 6; i++) f[i] = f1[i] + f2[i];
+    for (int i = 0; i < 6; i++) W->cacc[lane][i] = f[i];
   }
-  SYNC();
-  if (isb) for (int i = 0; i < 6; i++) W->cacc[lane][i] = f[i];
   SYNC();
   if (isb) {  // subtree sums of cfrc into cvel (cvel is no longer needed)
     float s[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
@@ -847,6 +914,7 @@ template <class D> PHASE void velocity_stage(MP m_, LDSA WS<D>* W, int lane) {
   }
   if (lane < D::LD) W->frc_act[lane] = 0.f;
   SYNC();
+  TACC(27, tv, lane);
   if (isu) {  // motors with joint transmission
     float c = W->ctrl[lane];
     if (ulim) c = fminf(fmaxf(c, ulo), uhi);
@@ -1009,6 +1077,7 @@ template <class D, bool G> PHASE bool build_rows(MP m_, LDSA WS<D>* W, Rows<G> R
   typedef typename Rows<G>::F RF;
   const int nv = m->nv, cap = R.cap, capc = R.capc;
   int nl = 0;
+  TSTART(tr);
   {  // joint limits (lane = joint), then tendon limits (lane = tendon), ballot-compacted
     bool act = false;
     float dist = 0.f, sgn = 0.f;
@@ -1052,6 +1121,7 @@ template <class D, bool G> PHASE bool build_rows(MP m_, LDSA WS<D>* W, Rows<G> R
   // contacts: one pass over candidate pairs (lane = pair), active ones compacted in pair order
   int nc = 0, nr = nl;
   const int npair = m->npair;
+  TACC(20, tr, lane);
   for (int base = 0; base < npair; base += 64) {
     const int p = base + lane;
     const bool isp = p < npair;
@@ -1088,6 +1158,7 @@ template <class D, bool G> PHASE bool build_rows(MP m_, LDSA WS<D>* W, Rows<G> R
   }
   if (lane == 0) { W->ncon = nc; W->nefc = nr; W->nlim = nl; }
   SYNC();
+  TACC(21, tr, lane);
   if (nr > cap || nc > capc) return false;
   // contact Jacobian rows: lanes 0..31 -> contact c, lanes 32..63 -> contact c+1; lane%32 = dof
   const int d = lane & 31;
@@ -1126,6 +1197,7 @@ template <class D, bool G> PHASE bool build_rows(MP m_, LDSA WS<D>* W, Rows<G> R
     }
   }
   SYNC();
+  TACC(22, tr, lane);
   // per-row impedance, D and reference acceleration (lane = row)
   for (int r = lane; r < nr; r += 64) {
     int meta = R.emeta[r], type = meta >> 16, id = meta & 0xffff;

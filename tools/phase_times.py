@@ -21,7 +21,7 @@ L.mjl_debug_set_stamps.argtypes = [C.c_void_p]
 m = mjx_amd.load_model("humanoid_mjx")
 sys_ = mjx.put_model(m)
 B = 2048
-buf = torch.zeros((B, 16), dtype=torch.int64, device="cuda")
+buf = torch.zeros((B, 32), dtype=torch.int64, device="cuda")
 L.mjl_debug_set_stamps(C.c_void_p(buf.data_ptr()))
 for mode in ("speedtest", "trajectory"):
     d = mjx.make_data(sys_, B)
@@ -56,6 +56,12 @@ for mode in ("speedtest", "trajectory"):
                                    "cholesky factor+solve"]):
         v = s[ok][:, i].mean()
         print(f"      {n:26s} {v:9.0f}  per iteration {v / max(it, 1e-9):8.0f}")
+    subs = {16: "kin: record loads", 17: "kin: local transforms", 18: "kin: level compose", 19: "kin: joints/geoms/sites",
+            20: "rows: limits", 21: "rows: collision pass", 22: "rows: contact Jacobians",
+            23: "crb: cinert+cdof", 24: "crb: subtree crb", 25: "vel: joint terms", 26: "vel: level pass",
+            27: "vel: forces + subtree sums"}
+    for i, n in subs.items():
+        print(f"      {n:26s} {s[ok][:, i].mean():9.0f}")
     ls_calls = s[ok][:, 15].mean()
     if ls_calls > 0:
         print(f"      line searches per env-step {ls_calls:.2f}; "
