@@ -737,6 +737,30 @@ template <class D> PHASE void kinematics(MP m_, LDSA WS<D>* W, int lane) {
   SYNC();
 }
 
+// Subtree sums over the DFS-contiguous body ranges, out[b][j] = sum_{c in [b, end_b)} in[c][j] for
+// bodies 1..16 (nbody <= 17), as four v_mfma_f32_16x16x4_f32: A = the 0/1 subtree indicator
+// (output body x contracted body), B = the per-body rows. Products with 0/1 and an f32
+// accumulate chain in ascending body order: the same sums, bit for bit, as the serial loop.
+// `end_lane`: this lane's body's subtree_end (lanes 1..16).
+template <int NC, class Src, class Dst> INL void subtree_sums16(Src in, Dst out, int nbody, int end_lane, int lane) {
+  const int bi = (lane & 15) + 1, k = lane >> 4, j = lane & 15;
+  const int endb = __shfl(end_lane, bi);
+  typedef float f32x4v __attribute__((ext_vector_type(4)));
+  f32x4v acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int t = 0; t < 4; t++) {
+    const int c = 1 + k + 4 * t;
+    const float a = (c >= bi && c < endb) ? 1.f : 0.f;
+    const float bv = (c < nbody && j < NC) ? in[c][j] : 0.f;
+    acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a, bv, acc, 0, 0, 0);
+  }
+#pragma unroll
+  for (int r = 0; r < 4; r++) {
+    const int b = 1 + 4 * k + r;
+    if (b < nbody && j < NC) out[b][j] = acc[r];
+  }
+}
+
 // cinert (lane = body) and cdof (lane 32 + dof); crb (lane = body); M columns (lane = dof)
 template <class D> PHASE void com_pos_crb(MP m_, LDSA WS<D>* W, int lane) {
   MP m = uniform_ptr(m_);
@@ -797,7 +821,9 @@ template <class D> PHASE void com_pos_crb(MP m_, LDSA WS<D>* W, int lane) {
   }
   SYNC();
   TACC(23, tc, lane);
-  if (isb) {
+  if (nbody <= 17) {  // bodies 1..16 on the matrix core (crb[0] is never read)
+    subtree_sums16<10>(W->cinert, W->crb, nbody, br.subtree_end, lane);
+  } else if (isb) {
     const int b = lane;
     float s[10];
     for (int i = 0; i < 10; i++) s[i] = 0.f;
@@ -906,7 +932,9 @@ template <class D> PHASE void velocity_stage(MP m_, LDSA WS<D>* W, int lane) {
     for (int i = 0; i < 6; i++) W->cacc[lane][i] = f[i];
   }
   SYNC();
-  if (isb) {  // subtree sums of cfrc into cvel (cvel is no longer needed)
+  if (nbody <= 17) {  // subtree sums of cfrc into cvel (cvel is no longer needed)
+    subtree_sums16<6>(W->cacc, W->cvel, nbody, br.subtree_end, lane);
+  } else if (isb) {
     float s[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
     for (int c = lane; c < br.subtree_end; c++)
       for (int i = 0; i < 6; i++) s[i] += W->cacc[c][i];
