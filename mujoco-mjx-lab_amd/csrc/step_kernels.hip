@@ -766,9 +766,9 @@ template <class D> PHASE void com_pos_crb(MP m_, LDSA WS<D>* W, int lane) {
   MP m = uniform_ptr(m_);
   constexpr int LD = D::LD;
   const int nbody = m->nbody, nv = m->nv;
-  const bool isb = lane < nbody, iscd = lane >= 32 && lane - 32 < nv, iscol = lane < nv;
+  const bool isb = lane < nbody, iscd = lane >= 32 && lane - 32 < nv;
   const BodyRec br = ldrec(&m->brec[isb ? lane : 0]);
-  const DofRec dcd = ldrec(&m->drec[iscd ? lane - 32 : 0]), dcol = ldrec(&m->drec[iscol ? lane : 0]);
+  const DofRec dcd = ldrec(&m->drec[iscd ? lane - 32 : 0]), dcol = ldrec(&m->drec[(lane & 31) < nv ? (lane & 31) : 0]);
   TSTART(tc);
   float t[6];
   for (int i = 0; i < 6; i++) t[i] = isb ? m->body_inertia[lane][i] : 0.f;
@@ -835,21 +835,30 @@ template <class D> PHASE void com_pos_crb(MP m_, LDSA WS<D>* W, int lane) {
   if (lane >= nv && lane < D::NV) W->M[lane * LD + lane] = 1.f;  // padded rows / cols: the identity
   SYNC();
   TACC(24, tc, lane);
-  if (iscol) {  // column `lane` of M along the ancestor chain  [smooth.crb / make_m]
-    const int i = lane;
+  {  // M[i][j] = cdof_j . (crb_body(i) cdof_i) for j in the ancestor chain of i  [smooth.crb / make_m]:
+     // every product cdof_r . f_c at once as three v_mfma_f32_32x32x2_f32 (K = 6), lane (c, half)
+     // supplying cdof_c[k] and f_c[k]; the lane holding column c keeps the rows in c's chain
+    const int i = lane & 31, h = lane >> 5;
+    const bool isdof = i < nv;
     float f[6], c6[6], cr[10];
-    for (int k = 0; k < 6; k++) c6[k] = W->cdof[i][k];
-    for (int k = 0; k < 10; k++) cr[k] = W->crb[dcol.bodyid][k];
+    for (int k = 0; k < 6; k++) c6[k] = isdof ? W->cdof[i][k] : 0.f;
+    for (int k = 0; k < 10; k++) cr[k] = isdof ? W->crb[dcol.bodyid][k] : 0.f;
     inert_vec(f, cr, c6);
-    uint32_t anc = dcol.ancmask;
-    while (anc) {
-      const int j = 31 - __builtin_clz(anc);
-      anc &= ~(1u << j);
-      LDSA float* c = W->cdof[j];
-      float v = c[0] * f[0] + c[1] * f[1] + c[2] * f[2] + c[3] * f[3] + c[4] * f[4] + c[5] * f[5];
-      if (j == i) v += dcol.armature;
-      W->M[i * LD + j] = v;
-      W->M[j * LD + i] = v;
+    f32x16 acc;
+#pragma unroll
+    for (int v = 0; v < 16; v++) acc[v] = 0.f;
+#pragma unroll
+    for (int t = 0; t < 3; t++)
+      acc = __builtin_amdgcn_mfma_f32_32x32x2f32(h ? c6[2 * t + 1] : c6[2 * t], h ? f[2 * t + 1] : f[2 * t], acc, 0, 0, 0);
+    const uint32_t anc = isdof ? dcol.ancmask : 0u;
+#pragma unroll
+    for (int v = 0; v < 16; v++) {
+      const int row = (v & 3) + 8 * (v >> 2) + 4 * h;
+      if ((anc >> row) & 1u) {
+        const float val = acc[v] + (row == i ? dcol.armature : 0.f);
+        W->M[i * LD + row] = val;
+        W->M[row * LD + i] = val;
+      }
     }
   }
   SYNC();
