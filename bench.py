@@ -160,7 +160,7 @@ def main():
     ds.set("qvel", qv)
     mjx.forward(sys_, ds)
     wst = ds.get("stats").double().mean(0).cpu().numpy()
-    fl = flops_mod.step_flops(model, float(wst[0]), float(wst[1]), float(wst[2]))
+    fl = flops_mod.step_flops(model, float(wst[0]), float(wst[1]), float(wst[2]), nact=float(wst[3]))
     achieved_tflops = fl["total"] * B / (kern_ms * 1e-3) / 1e12
     bytes_per_env = 8  # speed test: 4 B vel in + 4 B qpos[0] out; the state never leaves LDS
     achieved_gbs = bytes_per_env * B / (kern_ms * 1e-3) / 1e9
@@ -223,6 +223,7 @@ def main():
                          "kernel": SPEEDTEST_KERNEL, "kernel_ms": kern_ms,
                          "flops_per_env_step": fl["total"],
                          "workload_mean_ncon_nefc_iter": [float(x) for x in wst[:3]],
+                         "workload_mean_active_rows_per_hessian": float(wst[3]),
                          "hbm_algorithmic_bytes_per_launch": bytes_per_env * B,
                          "hbm_achieved_gbs": achieved_gbs, "hbm_frac": achieved_gbs / HBM_PEAK_GBS,
                          "note": "FP32 roof (dense MFMA = vector peak); achieved = algorithmic FP32 FLOPs "

@@ -135,7 +135,8 @@ enum {
   MJL_FIELD_QFRC_ACTUATOR = 8, /* [nv]   Data.qfrc_actuator */
   MJL_FIELD_SENSORDATA = 9,    /* [nsensordata] Data.sensordata */
   MJL_FIELD_AUX = 10,          /* [9]    env aux state (src/envs.py:15) */
-  MJL_FIELD_STATS = 11,        /* [4]    ncon_active, nefc_active, solver_iter, nan_flag */
+  MJL_FIELD_STATS = 11,        /* [4]    ncon_active, nefc_active, solver_iter, and nan_flag (env
+                                          step) or the mean active rows per Newton Hessian (others) */
   MJL_FIELD_QFRC_BIAS = 12,    /* [nv]   Data.qfrc_bias */
   MJL_FIELD_QFRC_PASSIVE = 13, /* [nv]   Data.qfrc_passive */
   MJL_FIELD_QFRC_CONSTRAINT = 14, /* [nv] Data.qfrc_constraint */

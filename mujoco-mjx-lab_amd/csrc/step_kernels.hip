@@ -192,7 +192,7 @@ static_assert(sizeof(WS<DHum>) <= kLdsBudget, "humanoid workspace exceeds the 8-
 
 // scalar slots in WS::sc
 enum { SC_FLIP = 0, SC_HEIGHT, SC_ROLL, SC_PITCH, SC_YAW, SC_TF0, SC_TF1, SC_REW, SC_TERM, SC_TRUNC, SC_DONE,
-       SC_NAN, SC_TIME };
+       SC_NAN, SC_TIME, SC_NACT };
 
 // constraint-row storage: the LDS arrays of WS, or the env's slab of global scratch
 template <bool G> struct RowAS;
@@ -1518,7 +1518,7 @@ template <class D, bool G> PHASE void solver(MP m_, LDSA WS<D>* W, Rows<G> R, in
   const bool newton = m->solver == MJL_SOLVER_NEWTON;
   if (nefc == 0) {
     if (lane < LD) { W->qacc[lane] = W->qacc_ws[lane] = W->qacc_smooth[lane]; W->frc_con[lane] = 0.f; }
-    if (lane == 0) W->niter = 0;
+    if (lane == 0) { W->niter = 0; W->sc[SC_NACT] = 0.f; }
     SYNC();
     return;
   }
@@ -1555,6 +1555,7 @@ template <class D, bool G> PHASE void solver(MP m_, LDSA WS<D>* W, Rows<G> R, in
   const int maxit = m->iterations;
   const bool exact_exit = newton && nefc <= 256;
   unsigned long long hm[4] = {0ull, 0ull, 0ull, 0ull};
+  int nhess = 0, nact = 0;  // Hessians built, active rows summed over them (bench FLOP model)
   auto active_masks = [&](unsigned long long* out) {
 #pragma unroll
     for (int c = 0; c < 4; c++) {
@@ -1595,7 +1596,11 @@ template <class D, bool G> PHASE void solver(MP m_, LDSA WS<D>* W, Rows<G> R, in
     }
     TACC(11, ts, lane);
     if (newton) {
-      if (exact_exit) active_masks(hm);
+      if (exact_exit) {
+        active_masks(hm);
+        nact += __popcll(hm[0]) + __popcll(hm[1]) + __popcll(hm[2]) + __popcll(hm[3]);
+        nhess++;
+      }
       float x;
       if constexpr (D::NV < 32) {  // J'DJ goes from the MFMA accumulator straight into the factor's rows
         const f32x16 acc = solver_hessian_acc<D, G>(m, W, R, lane);
@@ -1625,7 +1630,7 @@ template <class D, bool G> PHASE void solver(MP m_, LDSA WS<D>* W, Rows<G> R, in
     }
     SYNC();
   }
-  if (lane == 0) W->niter = iter;
+  if (lane == 0) { W->niter = iter; W->sc[SC_NACT] = nhess ? (float)nact / (float)nhess : 0.f; }
   // the solution seeds the next solve (MuJoCo mj_fwdConstraint, MJX solver.solve: qacc_warmstart =
   // qacc), so it belongs to forward: a reset's forward leaves the warm start MJX leaves
   if (lane < nv) W->qacc_ws[lane] = W->qacc[lane];
@@ -2125,7 +2130,7 @@ template <class D, int MODE> __global__ __launch_bounds__(64, MJL_MINWAVES) void
       S.stats[(size_t)env * 4 + 0] = (float)W->ncon;
       S.stats[(size_t)env * 4 + 1] = (float)W->nefc;
       S.stats[(size_t)env * 4 + 2] = (float)W->niter;
-      S.stats[(size_t)env * 4 + 3] = (MODE == MODE_ENV_STEP) ? W->sc[SC_NAN] : 0.f;
+      S.stats[(size_t)env * 4 + 3] = (MODE == MODE_ENV_STEP) ? W->sc[SC_NAN] : W->sc[SC_NACT];
     }
   }
 }

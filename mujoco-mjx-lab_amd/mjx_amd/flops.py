@@ -15,9 +15,12 @@ def cholesky(n: int) -> float:
     return 2.0 * (n ** 3 / 3.0 + 2.0 * n * n)
 
 
-def step_flops(m, ncon: float, nefc: float, iters: float, ls_evals: float = 3.0) -> dict:
-    """FP32 FLOPs of one env-step, by stage. `m` is a CompiledModel (sizes only)."""
+def step_flops(m, ncon: float, nefc: float, iters: float, ls_evals: float = 3.0, nact=None) -> dict:
+    """FP32 FLOPs of one env-step, by stage. `m` is a CompiledModel (sizes only). `nact`: mean
+    active rows per Newton Hessian (stats[3]); the Hessian counts only those rows, as the kernel
+    computes only those (MJX's dense J'DJ multiplies the inactive rows by D = 0)."""
     nv, nb, nj, npair = m.nv, m.nbody, m.njnt, m.npair
+    nh = nefc if nact is None else nact
     f = {}
     # kinematics: per joint local quaternion (sincos, qmul, 2 quat->mat, 2 mat-vec),
     # per body compose with the parent (qmul, quat->mat, 2 mat-vec), geom and site frames
@@ -35,9 +38,9 @@ def step_flops(m, ncon: float, nefc: float, iters: float, ls_evals: float = 3.0)
     f["factor_M"] = cholesky(nv)
     f["integrate"] = cholesky(nv) + 2.0 * nv * 4
     # Newton solver: warm-start costs (M q, J q for two candidates), then per iteration:
-    # Hessian J'DJ (full nv x nv over the rows), factor + solve, line search (M s, J s,
+    # Hessian J'DJ (full nv x nv over the active rows), factor + solve, line search (M s, J s,
     # ls_evals evaluations of the rows), update (J'f, gradient)
-    per_it = (2.0 * nv * nv * nefc + cholesky(nv) + 2.0 * (nv * nv + nv * nefc + ls_evals * 4 * nefc)
+    per_it = (2.0 * nv * nv * nh + cholesky(nv) + 2.0 * (nv * nv + nv * nefc + ls_evals * 4 * nefc)
               + 2.0 * (nv * nefc + 4 * nv))
     f["solver"] = 2.0 * 2 * (nv * nv + nv * nefc) + iters * per_it
     f["total"] = sum(f.values())
