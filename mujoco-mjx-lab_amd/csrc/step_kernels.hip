@@ -1387,23 +1387,27 @@ template <class D, bool G> INL void solver_hessian(MP m_, LDSA WS<D>* W, Rows<G>
 // Costs are relative to the Gauss term at alpha = 0 (common to every point, so comparisons hold).
 template <class D, bool G> INL float solver_linesearch(MP m_, LDSA WS<D>* W, Rows<G> R, int lane) {
   MP m = uniform_ptr(m_);
+  TSTART(tl);
   const int nv = m->nv, nefc = W->nefc;
   // M s, J s (the first 128 rows' J s, jar and D stay in registers across the iterations)
-  const float sv = (lane < nv) ? W->search[lane] : 0.f;
-  float mvl = 0.f, c1p = 0.f, c2p = 0.f;
-  if (lane < nv) {
-    mvl = mrow<D>(W, W->search, lane);
-    W->Mv[lane] = mvl;
-    c1p = sv * (W->Ma[lane] - W->frc_smooth[lane]);
-    c2p = sv * mvl;
-  }
+  // (clamped row indices: the M s and J s loads issue together, no branch between them)
+  const int mi = lane < nv ? lane : 0, ri = lane < nefc ? lane : 0;
+  const float mva = mrow<D>(W, W->search, mi), jva = jrow<D>(R.J, W->search, ri);
+  const float sv = (lane < nv) ? W->search[mi] : 0.f;
+  const float mvl = (lane < nv) ? mva : 0.f;
+  const float c1p = sv * (W->Ma[mi] - W->frc_smooth[mi]), c2p = sv * mvl;
+  if (lane < nv) W->Mv[lane] = mvl;
   float jv0 = 0.f, ja0 = 0.f, dd0 = 0.f, jv1 = 0.f, ja1 = 0.f, dd1 = 0.f;
-  if (lane < nefc) { jv0 = jrow<D>(R.J, W->search, lane); ja0 = R.jar[lane]; dd0 = R.D[lane]; R.Jv[lane] = jv0; }
+  {
+    const float ja = R.jar[ri], dd = R.D[ri];
+    if (lane < nefc) { jv0 = jva; ja0 = ja; dd0 = dd; R.Jv[lane] = jv0; }
+  }
   if (lane + 64 < nefc) {
     jv1 = jrow<D>(R.J, W->search, lane + 64); ja1 = R.jar[lane + 64]; dd1 = R.D[lane + 64]; R.Jv[lane + 64] = jv1;
   }
   for (int r = lane + 128; r < nefc; r += 64) R.Jv[r] = jrow<D>(R.J, W->search, r);
   SYNC();
+  TACC(28, tl, lane);
   // lane partial sums of f'(al[k]), f''(al[k]) for K points (COST: of the relative cost), one
   // pass over the rows; `fin` turns them into the values (wave sums)
   auto partial = [&](auto Kc, auto COSTc, const float* al, float* dp, float* hp) {
@@ -1460,6 +1464,7 @@ template <class D, bool G> INL float solver_linesearch(MP m_, LDSA WS<D>* W, Row
     fin(I1{}, TF{}, a0, dp, hp, p0d0, p0d1);
   }
   const float gtol = m->tolerance * m->ls_tolerance * snorm / m->scale;
+  TACC(29, tl, lane);
   // the Newton point q from p0
   float a1[1] = {-p0d0[0] * __builtin_amdgcn_rcpf(p0d1[0])}, qd0[1], qd1[1];
   // exact segment: if no row changes activity between 0 and q, f' is linear there and q is its
@@ -1470,6 +1475,7 @@ template <class D, bool G> INL float solver_linesearch(MP m_, LDSA WS<D>* W, Row
     if (__ballot(!same) == 0ull) { TCOUNT(15, 1, lane); return a1[0]; }
   }
   eval(I1{}, TF{}, a1, qd0, qd1);
+  TACC(30, tl, lane);
   // lo = whichever of p0, q has the smaller f'
   float loa, lod0, lod1, hia, hid0, hid1;
   if (qd0[0] < p0d0[0]) { loa = a1[0]; lod0 = qd0[0]; lod1 = qd1[0]; hia = 0.f; hid0 = p0d0[0]; hid1 = p0d1[0]; }
@@ -1505,6 +1511,7 @@ template <class D, bool G> INL float solver_linesearch(MP m_, LDSA WS<D>* W, Row
   }
   TCOUNT(15, 1, lane);
   float ac[3] = {0.f, loa, hia}, cost[3];
+  TACC(31, tl, lane);
   eval(I3{}, TT{}, ac, cost, nullptr);
   const bool improved = cost[1] < cost[0] || cost[2] < cost[0];
   const float alpha = cost[1] < cost[2] ? loa : hia;
@@ -1524,24 +1531,33 @@ template <class D, bool G> PHASE void solver(MP m_, LDSA WS<D>* W, Rows<G> R, in
   }
   const float scale = m->scale;
   TSTART(ts);
-  // warm start: the cheaper of qacc_warmstart and qacc_smooth
+  // warm start: the cheaper of qacc_warmstart and qacc_smooth. M q and J q (rows < 64) of both
+  // candidates with clamped row indices, so every load issues before the first wait; the chosen
+  // candidate's M q and J q - aref are kept as Ma and jar (the same values a recompute would give)
+  const int mi = lane < nv ? lane : 0, ri = lane < nefc ? lane : 0;
+  LDSA float* qc[2] = {W->qacc_ws, W->qacc_smooth};
+  float mq[2], jq[2];
+#pragma unroll
+  for (int w = 0; w < 2; w++) { mq[w] = mrow<D>(W, qc[w], mi); jq[w] = jrow<D>(R.J, qc[w], ri); }
+  const float fs = W->frc_smooth[mi], qs = W->qacc_smooth[mi], ar = R.aref[ri], dr = R.D[ri];
   float cost2[2];
+#pragma unroll
   for (int w = 0; w < 2; w++) {
-    LDSA float* q = w == 0 ? W->qacc_ws : W->qacc_smooth;
-    float g = 0.f;
-    if (lane < nv) g = 0.5f * (mrow<D>(W, q, lane) - W->frc_smooth[lane]) * (q[lane] - W->qacc_smooth[lane]);
-    float c = 0.f;
-    for (int r = lane; r < nefc; r += 64) {
-      float j = jrow<D>(R.J, q, r) - R.aref[r];
-      if (j < 0.f) c += 0.5f * R.D[r] * j * j;
+    const float g = lane < nv ? 0.5f * (mq[w] - fs) * (qc[w][mi] - qs) : 0.f;
+    const float j = jq[w] - ar;
+    float c = (lane < nefc && j < 0.f) ? 0.5f * dr * j * j : 0.f;
+    for (int r = lane + 64; r < nefc; r += 64) {
+      float jr = jrow<D>(R.J, qc[w], r) - R.aref[r];
+      if (jr < 0.f) c += 0.5f * R.D[r] * jr * jr;
     }
     cost2[w] = wsum(g + c);
   }
-  LDSA float* q0 = cost2[0] < cost2[1] ? W->qacc_ws : W->qacc_smooth;
+  const int wsel = cost2[0] < cost2[1] ? 0 : 1;
+  LDSA float* q0 = qc[wsel];
   if (lane < LD) W->qacc[lane] = q0[lane];
-  SYNC();
-  if (lane < nv) W->Ma[lane] = mrow<D>(W, W->qacc, lane);
-  for (int r = lane; r < nefc; r += 64) R.jar[r] = jrow<D>(R.J, W->qacc, r) - R.aref[r];
+  if (lane < nv) W->Ma[lane] = mq[wsel];
+  if (lane < nefc) R.jar[lane] = jq[wsel] - ar;
+  for (int r = lane + 64; r < nefc; r += 64) R.jar[r] = jrow<D>(R.J, q0, r) - R.aref[r];
   SYNC();
   TACC(9, ts, lane);
   // Newton / CG iterations, written so that each helper appears once in the loop body.

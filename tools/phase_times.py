@@ -59,7 +59,8 @@ for mode in ("speedtest", "trajectory"):
     subs = {16: "kin: record loads", 17: "kin: local transforms", 18: "kin: level compose", 19: "kin: joints/geoms/sites",
             20: "rows: limits", 21: "rows: collision pass", 22: "rows: contact Jacobians",
             23: "crb: cinert+cdof", 24: "crb: subtree crb", 25: "vel: joint terms", 26: "vel: level pass",
-            27: "vel: forces + subtree sums"}
+            27: "vel: forces + subtree sums", 28: "ls: M s, J s", 29: "ls: |s|, c1, c2, p0",
+            30: "ls: segment test + q", 31: "ls: 3-point loop"}
     for i, n in subs.items():
         print(f"      {n:26s} {s[ok][:, i].mean():9.0f}")
     ls_calls = s[ok][:, 15].mean()
