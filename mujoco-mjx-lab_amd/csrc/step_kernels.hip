@@ -47,19 +47,19 @@ __device__ unsigned long long* g_stamps;
 #define STAMP(slot, lane)                                                                        \
   do {                                                                                           \
     unsigned long long t_ = __builtin_amdgcn_s_memtime();                                        \
-    if ((lane) == 0 && g_stamps) g_stamps[(size_t)blockIdx.x * 32 + (slot)] = t_;               \
+    if ((lane) == 0 && g_stamps) g_stamps[(size_t)blockIdx.x * 48 + (slot)] = t_;               \
   } while (0)
 // accumulate the cycles since `var` into slot (solver sub-phases), restart `var`
 #define TSTART(var) unsigned long long var = __builtin_amdgcn_s_memtime()
 #define TACC(slot, var, lane)                                                                    \
   do {                                                                                           \
     unsigned long long t_ = __builtin_amdgcn_s_memtime();                                        \
-    if ((lane) == 0 && g_stamps) g_stamps[(size_t)blockIdx.x * 32 + (slot)] += t_ - (var);      \
+    if ((lane) == 0 && g_stamps) g_stamps[(size_t)blockIdx.x * 48 + (slot)] += t_ - (var);      \
     (var) = t_;                                                                                  \
   } while (0)
 #define TCOUNT(slot, n, lane)                                                                    \
   do {                                                                                           \
-    if ((lane) == 0 && g_stamps) g_stamps[(size_t)blockIdx.x * 32 + (slot)] += (n);             \
+    if ((lane) == 0 && g_stamps) g_stamps[(size_t)blockIdx.x * 48 + (slot)] += (n);             \
   } while (0)
 #else
 #define STAMP(slot, lane) do { } while (0)
@@ -124,6 +124,14 @@ INL float wsum(float v) {
   return rdlane(v, 63);
 }
 INL unsigned long long lanes_below(int lane) { return (1ull << lane) - 1ull; }
+// The lane index through an opaque move: lane masks compared against it are computed where they
+// are used. Against a plain lane index the compiler hoists a loop's 27 mask compares out of the
+// Newton loop and spills them to VGPR lanes (two readlanes to restore each mask per use).
+INL int opaque_int(int x) {
+  int z;
+  asm volatile("v_mov_b32 %0, 0" : "=v"(z));
+  return x + z;
+}
 
 // a packed model record as whole b128 loads from the constant model block
 typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
@@ -350,6 +358,7 @@ template <class D, bool ADD> INL float chol_aug_factor_solve(const LDSA float* s
   const int i = lane & 31, kh = lane >> 5;
   (void)n;
   float a[LD];
+  TSTART(tch);
   if constexpr (ADD) {
 #pragma unroll
     for (int v = 0; v < 16; v++) {
@@ -368,6 +377,7 @@ template <class D, bool ADD> INL float chol_aug_factor_solve(const LDSA float* s
       for (int e = 0; e < 4; e++) a[4 * q + e] = ADD ? a[4 * q + e] + v[e] : v[e];
     }
   }
+  TACC(32, tch, lane);
 
 #pragma unroll
   for (int k = 0; k < B1; k++) {
@@ -406,6 +416,7 @@ template <class D, bool ADD> INL float chol_aug_factor_solve(const LDSA float* s
     }
   }
   // rows of L to dst, y = L[R][0..NV) to invd_out (scratch until the reads below)
+  TACC(33, tch, lane);
   if (lane <= R) {
     LDSA f32x4* wp = (LDSA f32x4*)((i == R) ? invd_out : dst + i * LD);
 #pragma unroll
@@ -422,11 +433,14 @@ template <class D, bool ADD> INL float chol_aug_factor_solve(const LDSA float* s
 #pragma unroll
   for (int k = 0; k < NV; k++) w[k] = dst[k * LD + i];
   if (lane < NV) invd_out[lane] = invd;  // after the y read (same wave: LDS requests complete in order)
+  TACC(34, tch, lane);
+  const int io = opaque_int(i);
 #pragma unroll
-  for (int k = 0; k < NV; k++) w[k] = (i < k) ? w[k] * invd : 0.f;  // L[k][i] / L[i][i]
+  for (int k = 0; k < NV; k++) w[k] = (io < k) ? w[k] * invd : 0.f;  // L[k][i] / L[i][i]
   float x = y * invd;
 #pragma unroll
   for (int k = NV - 1; k >= 0; k--) x = fmaf(-w[k], rdlane(x, k), x);
+  TACC(35, tch, lane);
   return x;
 }
 
@@ -524,12 +538,15 @@ template <class D> INL float chol_solve(const LDSA float* L, const LDSA float* i
   // unit-triangular forms, each lane scaling its own row / column by its own 1 / L[i][i]:
   // L y = b  <=>  (diag(L)^-1 L) y = diag(L)^-1 b;  L^T z = y  <=>  (L diag(L)^-1)^T z = diag(L)^-1 y,
   // so every serial step is one readlane and one fma
-  const float invd = (lane < NV) ? invd_in[lane] : 1.f;
+  // (clamped addresses, loads unconditional; masks against an opaque lane index, see opaque_int)
+  const int li = lane < NV ? lane : 0, lo = opaque_int(lane);
+  const float invd = (lane < NV) ? invd_in[li] : 1.f;
   float wr[NV], wc[NV];
 #pragma unroll
   for (int k = 0; k < NV; k++) {
-    wr[k] = (lane < NV && lane > k) ? L[lane * LD + k] * invd : 0.f;  // L[i][k] / L[i][i]
-    wc[k] = (lane < k) ? L[k * LD + lane] * invd : 0.f;                // L[k][i] / L[i][i]
+    const float r = L[li * LD + k], c = L[k * LD + li];
+    wr[k] = (lo < NV && lo > k) ? r * invd : 0.f;  // L[i][k] / L[i][i]
+    wc[k] = (lo < k) ? c * invd : 0.f;             // L[k][i] / L[i][i]
   }
   x *= invd;
 #pragma unroll
@@ -1277,15 +1294,25 @@ template <class D, bool G> INL float solver_update(MP m_, LDSA WS<D>* W, Rows<G>
   MP m = uniform_ptr(m_);
   constexpr int LD = D::LD;
   const int nv = m->nv, nefc = W->nefc;
+  // clamped indices throughout: each group of loads issues before its first use
   float c = 0.f;
-  for (int r = lane; r < nefc; r += 64) {
+  {
+    const int ri = lane < nefc ? lane : 0;
+    const float j = R.jar[ri], dr = R.D[ri];
+    const bool act = lane < nefc && j < 0.f;
+    if (lane < nefc) R.force[lane] = act ? -dr * j : 0.f;
+    c = act ? 0.5f * dr * j * j : 0.f;
+  }
+  for (int r = lane + 64; r < nefc; r += 64) {
     float j = R.jar[r];
     float f = j < 0.f ? -R.D[r] * j : 0.f;
     R.force[r] = f;
     if (j < 0.f) c += 0.5f * R.D[r] * j * j;
   }
+  const int mi = lane < nv ? lane : 0;
+  const float ma = W->Ma[mi], fs = W->frc_smooth[mi], qa = W->qacc[mi], qsm = W->qacc_smooth[mi];
   SYNC();
-  int d = lane & 31, h = lane >> 5;  // J' f : lane%32 = dof, lane/32 = row parity
+  const int d = lane & 31, h = lane >> 5;  // J' f : lane%32 = dof, lane/32 = row parity
   float s = 0.f;
   if (d < nv) {
     int r = h;
@@ -1298,9 +1325,8 @@ template <class D, bool G> INL float solver_update(MP m_, LDSA WS<D>* W, Rows<G>
   float g = 0.f;
   if (lane < nv) {
     W->frc_con[lane] = s;
-    float ma = W->Ma[lane];
-    g = 0.5f * (ma - W->frc_smooth[lane]) * (W->qacc[lane] - W->qacc_smooth[lane]);
-    W->grad[lane] = ma - W->frc_smooth[lane] - s;
+    g = 0.5f * (ma - fs) * (qa - qsm);
+    W->grad[lane] = ma - fs - s;
   }
   float cost = wsum(g + c);
   SYNC();

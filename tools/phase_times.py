@@ -21,7 +21,7 @@ L.mjl_debug_set_stamps.argtypes = [C.c_void_p]
 m = mjx_amd.load_model("humanoid_mjx")
 sys_ = mjx.put_model(m)
 B = 2048
-buf = torch.zeros((B, 32), dtype=torch.int64, device="cuda")
+buf = torch.zeros((B, 48), dtype=torch.int64, device="cuda")
 L.mjl_debug_set_stamps(C.c_void_p(buf.data_ptr()))
 for mode in ("speedtest", "trajectory"):
     d = mjx.make_data(sys_, B)
@@ -60,7 +60,8 @@ for mode in ("speedtest", "trajectory"):
             20: "rows: limits", 21: "rows: collision pass", 22: "rows: contact Jacobians",
             23: "crb: cinert+cdof", 24: "crb: subtree crb", 25: "vel: joint terms", 26: "vel: level pass",
             27: "vel: forces + subtree sums", 28: "ls: M s, J s", 29: "ls: |s|, c1, c2, p0",
-            30: "ls: segment test + q", 31: "ls: 3-point loop"}
+            30: "ls: segment test + q", 31: "ls: 3-point loop", 32: "chol(all): load rows",
+            33: "chol(all): factor", 34: "chol(all): store + reload", 35: "chol(all): back subst"}
     for i, n in subs.items():
         print(f"      {n:26s} {s[ok][:, i].mean():9.0f}")
     ls_calls = s[ok][:, 15].mean()
