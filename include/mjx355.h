@@ -269,6 +269,19 @@ int mjl_set_state(mjlBatch* batch, const float* src, const float* ws_src, void* 
 int mjl_gae(const float* rew, const float* val, const float* term, const float* trunc, int T, int B,
             double gamma, double lam, float* adv, float* ret, void* stream);
 
+/* The rollout step's elementwise work around the policy GEMMs (train_ppo.py:128-169), two launches
+ * instead of the ~20 framework ops it takes as jnp / torch expressions:
+ * mjl_obs_normalize replaces normalize_obs + clip (src/training_utils.py:52-56, train_ppo.py:134-135):
+ *   y[n, dim] = clip((x - mean) / sqrt(var + 1e-8), -clip, clip).
+ * mjl_policy_head replaces GaussianPolicy's tanh head + sampling + gaussian_logprob
+ * (src/networks.py:82-112, train_ppo.py:121-126,136-139): z [B, A] = the MLP's last (linear) layer,
+ *   mean = tanh(z), s = clip(log_std, -20, 2), act = mean + exp(s) eps, logp[B] = -0.5 sum((act -
+ *   mean)^2 / exp(2 s) + 2 s + log 2 pi). Device pointers, float32, row-major. */
+int mjl_obs_normalize(const float* x, const float* mean, const float* var, int n, int dim, float clip, float* y,
+                      void* stream);
+int mjl_policy_head(const float* z, const float* log_std, const float* eps, int B, int A, float* act, float* logp,
+                    void* stream);
+
 #ifdef __cplusplus
 }
 #endif

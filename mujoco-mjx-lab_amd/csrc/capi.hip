@@ -648,6 +648,27 @@ extern "C" int mjl_gae(const float* rew, const float* val, const float* term, co
   return MJL_OK;
 }
 
+extern "C" int mjl_obs_normalize(const float* x, const float* mean, const float* var, int n, int dim, float clip,
+                                 float* y, void* stream) {
+  if (!x || !mean || !var || !y || n < 0 || dim <= 0) return fail(MJL_ERR_ARG, "bad argument");
+  if (n == 0) return MJL_OK;
+  const long long tot = (long long)n * dim;
+  hipLaunchKernelGGL(obs_normalize_kernel, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, (hipStream_t)stream, x,
+                     mean, var, n, dim, clip, y);
+  HIPCHK(hipGetLastError());
+  return MJL_OK;
+}
+
+extern "C" int mjl_policy_head(const float* z, const float* log_std, const float* eps, int B, int A, float* act,
+                               float* logp, void* stream) {
+  if (!z || !log_std || !eps || !act || !logp || B < 0 || A <= 0) return fail(MJL_ERR_ARG, "bad argument");
+  if (B == 0) return MJL_OK;
+  hipLaunchKernelGGL(policy_head_kernel, dim3((B + 255) / 256), dim3(256), 0, (hipStream_t)stream, z, log_std, eps, B,
+                     A, act, logp);
+  HIPCHK(hipGetLastError());
+  return MJL_OK;
+}
+
 // jax.random.split over a batch of keys (train_ppo.py:132,150: random.split(rng); random.split(key, num_envs))
 __global__ void prng_split_kernel(const uint32_t* __restrict__ keys, int n, int num, int mode, uint32_t* __restrict__ out) {
   const int t = blockIdx.x * blockDim.x + threadIdx.x;

@@ -1132,6 +1132,7 @@ template <class D, bool G> PHASE bool build_rows(MP m_, LDSA WS<D>* W, Rows<G> R
   const int nv = m->nv, cap = R.cap, capc = R.capc;
   int nl = 0;
   TSTART(tr);
+  PairRec pr_next = ldrec(&m->prec[lane < m->npair ? lane : 0]);  // in flight during the limit rows
   {  // joint limits (lane = joint), then tendon limits (lane = tendon), ballot-compacted
     bool act = false;
     float dist = 0.f, sgn = 0.f;
@@ -1179,7 +1180,11 @@ template <class D, bool G> PHASE bool build_rows(MP m_, LDSA WS<D>* W, Rows<G> R
   for (int base = 0; base < npair; base += 64) {
     const int p = base + lane;
     const bool isp = p < npair;
-    const PairRec pr = ldrec(&m->prec[isp ? p : 0]);
+    const PairRec pr = pr_next;
+    {  // the next trip's records load while this trip collides
+      const int pn = p + 64;
+      pr_next = ldrec(&m->prec[pn < npair ? pn : 0]);
+    }
     for (int k = 0; k < 2; k++) {
       bool act = false;
       float dist = 0.f, pos[3], fr[9];

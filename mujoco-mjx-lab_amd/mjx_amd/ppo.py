@@ -162,6 +162,25 @@ class RunningMeanStd:
 LOG2PI = math.log(2.0 * math.pi)
 
 
+def obs_normalize_native(x, mean, var, clip, out):
+    """RunningMeanStd.normalize on device as one launch (mjl_obs_normalize)."""
+    from ._lib import check, lib
+    n, dim = x.numel() // x.shape[-1], x.shape[-1]
+    check(lib().mjl_obs_normalize(x.data_ptr(), mean.data_ptr(), var.data_ptr(), n, dim, float(clip), out.data_ptr(),
+                                  torch.cuda.current_stream(x.device).cuda_stream))
+    return out
+
+
+def policy_head_native(z, log_std, eps, act_out, logp_out):
+    """tanh head + sampling + gaussian_logprob of one rollout step as one launch (mjl_policy_head)."""
+    from ._lib import check, lib
+    B, A = z.shape
+    if not (z.is_contiguous() and eps.is_contiguous() and act_out.is_contiguous() and logp_out.is_contiguous()):
+        raise ValueError("policy_head_native: contiguous [B, A] / [B] tensors expected")
+    check(lib().mjl_policy_head(z.data_ptr(), log_std.detach().contiguous().data_ptr(), eps.data_ptr(), B, A,
+                                act_out.data_ptr(), logp_out.data_ptr(), torch.cuda.current_stream(z.device).cuda_stream))
+
+
 def gaussian_logprob(mean, log_std, action, out=None):
     """train_ppo.py:121-126: diagonal Gaussian log-density summed over action dims."""
     var = torch.exp(2.0 * log_std)
@@ -362,7 +381,7 @@ class PPOTrainer:
                 "obs": torch.empty((T + 1, B, env.obs_dim), device=dev), "act": torch.empty((T, B, env.act_dim), device=dev),
                 "logp": torch.empty((T, B), device=dev), "rew": torch.empty((T, B), device=dev),
                 "term": torch.empty((T, B), device=dev), "trunc": torch.empty((T, B), device=dev),
-                "eps": torch.empty((T, B, env.act_dim), device=dev)}
+                "eps": torch.empty((T, B, env.act_dim), device=dev), "xn": torch.empty((B, env.obs_dim), device=dev)}
         return self._buf
 
     def _rollout_body(self, graph: bool):
@@ -370,12 +389,18 @@ class PPOTrainer:
         obs[t + 1], rew / term / trunc [t] in place (no copies). With graph=True the RNG counters are
         relative to the env's device counter base (the body is being captured)."""
         bf, env = self._buf, self.env
+        native = bf["obs"].is_cuda  # normalisation and the policy head as two native launches
         for t in range(self.cfg.rollout_length):
             if self.jax_keys:
                 self._jax_step_keys()
-            mean, log_std = self.policy(self.rms.normalize(bf["obs"][t]))
-            act = torch.addcmul(mean, torch.exp(log_std), bf["eps"][t], out=bf["act"][t])
-            gaussian_logprob(mean, log_std, act, out=bf["logp"][t])
+            if native:
+                obs_normalize_native(bf["obs"][t], self.rms.mean, self.rms.var, 10.0, bf["xn"])
+                act = bf["act"][t]
+                policy_head_native(self.policy.mlp(bf["xn"]), self.policy.log_std, bf["eps"][t], act, bf["logp"][t])
+            else:
+                mean, log_std = self.policy(self.rms.normalize(bf["obs"][t]))
+                act = torch.addcmul(mean, torch.exp(log_std), bf["eps"][t], out=bf["act"][t])
+                gaussian_logprob(mean, log_std, act, out=bf["logp"][t])
             # physics + reward + obs + merge_if_done, one launch
             out = (bf["obs"][t + 1], bf["rew"][t], bf["term"][t], bf["trunc"][t])
             if graph:

@@ -248,6 +248,34 @@ def test_native_gae_bit_identical_to_formula():
 
 
 @pytest.mark.gpu
+def test_native_rollout_head_matches_formulas():
+    """mjl_obs_normalize matches RunningMeanStd.normalize to fp32 rounding (ragged size too);
+    mjl_policy_head (tanh head, sampling, log-prob) matches the torch formulas to fp32 rounding, with
+    log_std outside the [-20, 2] clip on some entries."""
+    g = torch.Generator(device="cuda").manual_seed(3)
+    for n, dim in ((2048, 54), (37, 5)):
+        x = torch.randn((n, dim), generator=g, device="cuda") * 20
+        rms = ppo.RunningMeanStd(dim, "cuda")
+        rms.mean.copy_(torch.randn(dim, generator=g, device="cuda"))
+        rms.var.copy_(torch.rand(dim, generator=g, device="cuda") + 1e-3)
+        out = torch.empty_like(x)
+        ppo.obs_normalize_native(x, rms.mean, rms.var, 10.0, out)
+        torch.testing.assert_close(out, rms.normalize(x), rtol=2e-7, atol=1e-6)
+    for B, A in ((2048, 21), (5, 3)):
+        z = torch.randn((B, A), generator=g, device="cuda") * 2
+        ls = torch.randn(A, generator=g, device="cuda")
+        ls[0] = -25.0
+        ls[-1] = 3.0
+        eps = torch.randn((B, A), generator=g, device="cuda")
+        act, lp = torch.empty_like(z), torch.empty(B, device="cuda")
+        ppo.policy_head_native(z, ls, eps, act, lp)
+        mean, s = torch.tanh(z), torch.clamp(ls, -20.0, 2.0)
+        act_ref = mean + torch.exp(s) * eps
+        torch.testing.assert_close(act, act_ref, rtol=1e-6, atol=1e-6)
+        torch.testing.assert_close(lp, ppo.gaussian_logprob(mean, s, act), rtol=1e-5, atol=1e-3)
+
+
+@pytest.mark.gpu
 def test_graph_rollout_bit_identical_to_eager():
     """The hipGraph replay of the T-step rollout (policy, sampling, log-prob, fused env step with
     auto-reset) reproduces the eager loop bit for bit, including the env's reset RNG draws (device
