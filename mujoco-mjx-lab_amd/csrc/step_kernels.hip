@@ -1439,6 +1439,16 @@ template <class D, bool G> INL float solver_linesearch(MP m_, LDSA WS<D>* W, Row
   for (int r = lane + 128; r < nefc; r += 64) R.Jv[r] = jrow<D>(R.J, W->search, r);
   SYNC();
   TACC(28, tl, lane);
+  // the step qacc += a s, Ma += a M s, jar += a J s from the registers the search already holds
+  auto apply = [&](float alpha) -> float {
+    if (alpha != 0.f) {
+      if (lane < nv) { W->qacc[lane] += alpha * sv; W->Ma[lane] += alpha * mvl; }
+      if (lane < nefc) R.jar[lane] = ja0 + alpha * jv0;
+      if (lane + 64 < nefc) R.jar[lane + 64] = ja1 + alpha * jv1;
+      for (int r = lane + 128; r < nefc; r += 64) R.jar[r] += alpha * R.Jv[r];
+    }
+    return alpha;
+  };
   // lane partial sums of f'(al[k]), f''(al[k]) for K points (COST: of the relative cost), one
   // pass over the rows; `fin` turns them into the values (wave sums)
   auto partial = [&](auto Kc, auto COSTc, const float* al, float* dp, float* hp) {
@@ -1503,7 +1513,7 @@ template <class D, bool G> INL float solver_linesearch(MP m_, LDSA WS<D>* W, Row
   {
     bool same = ((ja0 < 0.f) == (ja0 + a1[0] * jv0 < 0.f)) && ((ja1 < 0.f) == (ja1 + a1[0] * jv1 < 0.f));
     for (int r = lane + 128; r < nefc; r += 64) same &= (R.jar[r] < 0.f) == (R.jar[r] + a1[0] * R.Jv[r] < 0.f);
-    if (__ballot(!same) == 0ull) { TCOUNT(15, 1, lane); return a1[0]; }
+    if (__ballot(!same) == 0ull) { TCOUNT(15, 1, lane); return apply(a1[0]); }
   }
   eval(I1{}, TF{}, a1, qd0, qd1);
   TACC(30, tl, lane);
@@ -1546,7 +1556,7 @@ template <class D, bool G> INL float solver_linesearch(MP m_, LDSA WS<D>* W, Row
   eval(I3{}, TT{}, ac, cost, nullptr);
   const bool improved = cost[1] < cost[0] || cost[2] < cost[0];
   const float alpha = cost[1] < cost[2] ? loa : hia;
-  return improved ? alpha : 0.f;
+  return apply(improved ? alpha : 0.f);
 }
 
 template <class D, bool G> PHASE void solver(MP m_, LDSA WS<D>* W, Rows<G> R, int lane) {
@@ -1614,12 +1624,8 @@ template <class D, bool G> PHASE void solver(MP m_, LDSA WS<D>* W, Rows<G> R, in
     if (!first) {
       float alpha = solver_linesearch<D, G>(m, W, R, lane);
       if (!(alpha != 0.f)) { iter++; break; }  // no improvement: MJX's next cond stops (also on NaN)
-      if (lane < nv) {
-        W->qacc[lane] += alpha * W->search[lane];
-        W->Ma[lane] += alpha * W->Mv[lane];
-        if (!newton) { W->gradold[lane] = W->grad[lane]; W->Mgradold[lane] = W->Mgrad[lane]; }
-      }
-      for (int r = lane; r < nefc; r += 64) R.jar[r] += alpha * R.Jv[r];
+      // (the line search applied the step to qacc, Ma and jar)
+      if (!newton && lane < nv) { W->gradold[lane] = W->grad[lane]; W->Mgradold[lane] = W->Mgrad[lane]; }
       SYNC();
       TACC(10, ts, lane);
     }
