@@ -48,10 +48,13 @@ class _SplitKLinear(torch.autograd.Function):
         return gx, gw, gy.sum(0), None
 
 
+SPLIT_ROWS = 2048  # rows per split of the split-K weight gradient (32 splits at a 65,536 minibatch)
+
+
 def _linear(lin: nn.Linear, x: torch.Tensor) -> torch.Tensor:
     n = x.shape[0] if x.dim() == 2 else 0
-    if x.is_cuda and torch.is_grad_enabled() and n >= 16384 and n % 2048 == 0:
-        return _SplitKLinear.apply(x, lin.weight, lin.bias, min(32, n // 2048))
+    if x.is_cuda and torch.is_grad_enabled() and n >= 16384 and n % SPLIT_ROWS == 0:
+        return _SplitKLinear.apply(x, lin.weight, lin.bias, min(64, n // SPLIT_ROWS))
     return lin(x)
 
 
@@ -257,7 +260,7 @@ def value_loss(value, obs, returns):
 def make_index_batches(total: int, minibatch: int, epochs: int, generator: torch.Generator, device):
     """train_ppo.py:222-231: a fresh permutation per epoch, the last partial minibatch dropped."""
     per = total // minibatch
-    out = [torch.randperm(total, generator=generator, device="cpu")[: per * minibatch].view(per, minibatch)
+    out = [torch.randperm(total, generator=generator, device=generator.device)[: per * minibatch].view(per, minibatch)
            for _ in range(epochs)]
     return torch.cat(out, 0).to(device)
 
@@ -320,11 +323,14 @@ class PPOTrainer:
             for p in list(self.policy.parameters()) + list(self.value.parameters()):
                 dist.broadcast(p.data, 0)
         # optax.adam defaults (b1 .9, b2 .999, eps 1e-8) = torch.optim.Adam defaults
-        self.opt_p = torch.optim.Adam(self.policy.parameters(), lr=cfg.lr_policy, betas=(0.9, 0.999), eps=1e-8)
-        self.opt_v = torch.optim.Adam(self.value.parameters(), lr=cfg.lr_value, betas=(0.9, 0.999), eps=1e-8)
+        # (fused: one multi-tensor kernel per step on the GPU, the same update formula)
+        fused = {"fused": True} if self.device.type == "cuda" else {}
+        self.opt_p = torch.optim.Adam(self.policy.parameters(), lr=cfg.lr_policy, betas=(0.9, 0.999), eps=1e-8, **fused)
+        self.opt_v = torch.optim.Adam(self.value.parameters(), lr=cfg.lr_value, betas=(0.9, 0.999), eps=1e-8, **fused)
         self.rms = RunningMeanStd(env.obs_dim, self.device)
         self.gen = torch.Generator(device=self.device).manual_seed(int(cfg.seed) * 1000 + self.rank)
-        self.idx_gen = torch.Generator().manual_seed(int(cfg.seed) + 7919 * (self.rank + 1))
+        # minibatch permutations drawn on the device they index (4 host randperms of T*B took ~30 ms)
+        self.idx_gen = torch.Generator(device=self.device).manual_seed(int(cfg.seed) + 7919 * (self.rank + 1))
         self.jax_keys = bool(jax_keys) and self.device.type == "cuda" and hasattr(env, "set_reset_keys")
         if self.jax_keys:
             self._jax_init()

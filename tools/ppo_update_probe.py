@@ -1,0 +1,46 @@
+"""Diagnostic: wall time of one PPO update (4 epochs x 8 minibatches of 65,536 at 2048 envs x 256
+steps) on synthetic rollout data, for optimizer / split-K variants. Not product code."""
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "mujoco-mjx-lab_amd"))
+import torch  # noqa: E402
+
+from mjx_amd import ppo  # noqa: E402
+from mjx_amd.config import reference_ppo_config  # noqa: E402
+
+
+def run(fused: bool, splits: int, reps: int = 3):
+    cfg = reference_ppo_config()
+    g = torch.Generator().manual_seed(0)
+    pol = ppo.GaussianPolicy(54, 21, cfg.policy_hidden_layer_specs, cfg.log_std_init, g).cuda()
+    val = ppo.ValueNet(54, cfg.value_hidden_layer_specs, g).cuda()
+    kw = {"fused": True} if fused else {}
+    op = torch.optim.Adam(pol.parameters(), lr=3e-4, **kw)
+    ov = torch.optim.Adam(val.parameters(), lr=3e-4, **kw)
+    N = 2048 * 256
+    gd = torch.Generator(device="cuda").manual_seed(1)
+    obs = torch.randn((N, 54), generator=gd, device="cuda")
+    act = torch.randn((N, 21), generator=gd, device="cuda").clamp(-1, 1)
+    logp = torch.randn(N, generator=gd, device="cuda") - 20
+    ret = torch.randn(N, generator=gd, device="cuda")
+    adv = torch.randn(N, generator=gd, device="cuda")
+    ppo.SPLIT_ROWS = 65536 // splits
+    ts = []
+    for r in range(reps + 1):
+        idx = ppo.make_index_batches(N, cfg.minibatch_size, cfg.epochs, torch.Generator().manual_seed(r), "cuda")
+        torch.cuda.synchronize()
+        t0 = time.time()
+        ppo.ppo_update(pol, val, op, ov, obs, act, logp, ret, adv, idx, cfg)
+        torch.cuda.synchronize()
+        if r:
+            ts.append(time.time() - t0)
+    return sum(ts) / len(ts)
+
+
+if __name__ == "__main__":
+    for fused in (False, True):
+        for splits in (32, 64):
+            print(f"fused={fused} splits={splits}: {run(fused, splits) * 1e3:.1f} ms per update", flush=True)
