@@ -40,7 +40,33 @@ def run(fused: bool, splits: int, reps: int = 3):
     return sum(ts) / len(ts)
 
 
+def enqueue_vs_wall():
+    """Host enqueue time of one update vs its synced wall time (CPU-bound if they are close)."""
+    cfg = reference_ppo_config()
+    g = torch.Generator().manual_seed(0)
+    pol = ppo.GaussianPolicy(54, 21, cfg.policy_hidden_layer_specs, cfg.log_std_init, g).cuda()
+    val = ppo.ValueNet(54, cfg.value_hidden_layer_specs, g).cuda()
+    op = torch.optim.Adam(pol.parameters(), lr=3e-4, fused=True)
+    ov = torch.optim.Adam(val.parameters(), lr=3e-4, fused=True)
+    N = 2048 * 256
+    gd = torch.Generator(device="cuda").manual_seed(1)
+    obs, act = torch.randn((N, 54), generator=gd, device="cuda"), torch.randn((N, 21), generator=gd, device="cuda")
+    logp, ret, adv = (torch.randn(N, generator=gd, device="cuda") for _ in range(3))
+    for r in range(3):
+        idx = ppo.make_index_batches(N, cfg.minibatch_size, cfg.epochs, torch.Generator(device="cuda").manual_seed(r), "cuda")
+        torch.cuda.synchronize()
+        t0 = time.time()
+        ppo.ppo_update(pol, val, op, ov, obs, act, logp, ret, adv, idx, cfg)
+        t1 = time.time()
+        torch.cuda.synchronize()
+        t2 = time.time()
+        print(f"enqueue {1e3 * (t1 - t0):.1f} ms, wall {1e3 * (t2 - t0):.1f} ms", flush=True)
+
+
 if __name__ == "__main__":
+    if len(sys.argv) > 1 and sys.argv[1] == "enqueue":
+        enqueue_vs_wall()
+        sys.exit(0)
     for fused in (False, True):
         for splits in (32, 64):
             print(f"fused={fused} splits={splits}: {run(fused, splits) * 1e3:.1f} ms per update", flush=True)
