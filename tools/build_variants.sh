@@ -13,7 +13,7 @@ if [ "$1" == "--keep-prev" ]; then
   cp "$ROOT/mujoco-mjx-lab_amd/mjx_amd/libmjx355.so" "$OUT/libmjx355_a_prev.so"
   shift
 fi
-F="-O2 -std=c++17 -fPIC -shared --offload-arch=gfx950 -Wno-unused-result -fapprox-func"
+F="-O2 -std=c++17 -fPIC -shared --offload-arch=gfx950 -Wno-unused-result -fapprox-func -fno-slp-vectorize"
 pids=()
 while [ $# -ge 2 ]; do
   name=$1; flags=$2; shift 2
