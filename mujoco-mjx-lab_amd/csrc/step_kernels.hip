@@ -333,6 +333,61 @@ template <class D> INL void chol_factor(LDSA float* A, LDSA float* invd_out, int
   SYNC();
 }
 
+// One panel of the right-looking factor on rows held in registers (lane l and l + 32: row l & 31):
+// columns [P0, P1) factored on the VALU (a readlane broadcast + fma per element), then their
+// rank-(P1 - P0) update of the columns >= P1 as (P1 - P0) / 2 v_mfma_f32_32x32x2_f32, whose A and
+// B operands are the lane's own registers. The MFMA result C has row r of C in column r of the C
+// layout, i.e. C[i][j] sits in lane i (half (j >> 2) & 1) register (j & 3) + 4 (j >> 3); one
+// v_permlane32_swap of a register with itself hands each lane both halves' values.
+#ifndef MJL_CHOL_PANEL
+#define MJL_CHOL_PANEL 8
+#endif
+template <int LD, int NV, int P0, int P1> INL void chol_panel(float (&a)[LD], int kh) {
+  static_assert(P0 % 2 == 0 && P1 <= NV && NV <= 32, "panels start on a K = 2 boundary");
+#pragma unroll
+  for (int k = P0; k < P1; k++) {
+    // the column's broadcasts read the unscaled a_jk (they do not wait for the pivot's rsq) and
+    // each lane's multiplier is L_ik / L_kk instead; fminf after v_rsq is the 1e-30 pivot floor
+    // (rsq(1e-30)) off the readlane -> rsq chain (an fmaxf before it needs a canonicalising v_max)
+    const float inv = fminf(__builtin_amdgcn_rsqf(rdlane(a[k], k)), 1e15f);
+    float s[P1];
+#pragma unroll
+    for (int j = k + 1; j < P1; j++) s[j] = rdlane(a[k], j);
+    a[k] *= inv;  // lane k: sqrt of its pivot
+    const float t = a[k] * inv;
+#pragma unroll
+    for (int j = k + 1; j < P1; j++) a[j] = fmaf(-t, s[j], a[j]);
+  }
+  if constexpr (P1 < NV) {
+    static_assert(P1 % 2 == 0, "interior panel ends on a K = 2 boundary");
+    f32x16 acc;
+#pragma unroll
+    for (int v = 0; v < 16; v++) acc[v] = 0.f;
+#pragma unroll
+    for (int t = P0 / 2; t < P1 / 2; t++) {
+      const float op = kh ? a[2 * t + 1] : a[2 * t];
+      acc = __builtin_amdgcn_mfma_f32_32x32x2f32(op, op, acc, 0, 0, 0);
+    }
+    float lo[16], hi[16];
+#pragma unroll
+    for (int v = 0; v < 16; v++) {
+      bool used = false;
+#pragma unroll
+      for (int j = P1; j < NV; j++) used |= ((j & 3) + 4 * (j >> 3)) == v;
+      if (used) {
+        auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(acc[v]), __float_as_uint(acc[v]), false, false);
+        lo[v] = __uint_as_float(r[0]);
+        hi[v] = __uint_as_float(r[1]);
+      }
+    }
+#pragma unroll
+    for (int j = P1; j < NV; j++) {
+      const int v = (j & 3) + 4 * (j >> 3);
+      a[j] -= ((j >> 2) & 1) ? hi[v] : lo[v];
+    }
+  }
+}
+
 // Factor + solve in one pass, for the hot callers (M in forward / integrate, the Newton Hessian):
 // L L^T = S (S: n x n SPD in LDS at src, stride LD), L written to dst (lower triangle; the upper
 // triangle is unspecified, chol_solve reads only the lower) with invd_out[i] = 1 / L[i][i];
@@ -343,7 +398,7 @@ template <class D> INL void chol_factor(LDSA float* A, LDSA float* invd_out, int
 // broadcasts then run the forward substitution: lane R ends with L[R][k] = y_k (L y = rhs). The
 // back substitution runs on the unit upper factor diag(L)^-1 L^T: lane i pre-scales its column
 // L[k][i] (k > i) by its own 1 / L[i][i], so each of the NV serial steps is one readlane and one
-// fma, with no lane masks in the chain. Trailing update of the first 16 columns on MFMA (below).
+// fma, with no lane masks in the chain. The factor runs in 8-column panels (chol_panel).
 // Padding contract (n < NV): S is the identity outside its n x n block (M is built that way, and
 // the Newton / implicit matrices inherit it) and rhs is zero beyond n.
 // ADD: S = src + C, C a symmetric matrix in a v_mfma_f32_32x32x2_f32 accumulator (C layout: register
@@ -379,42 +434,15 @@ template <class D, bool ADD> INL float chol_aug_factor_solve(const LDSA float* s
   }
   TACC(32, tch, lane);
 
-#pragma unroll
-  for (int k = 0; k < B1; k++) {
-    const float inv = __builtin_amdgcn_rsqf(fmaxf(rdlane(a[k], k), 1e-30f));
-    a[k] *= inv;  // lane k: sqrt of its pivot
-#pragma unroll
-    for (int j = k + 1; j < B1; j++) a[j] = fmaf(-a[k], rdlane(a[k], j), a[j]);
-  }
-  if constexpr (NV > B1) {
-    f32x16 acc;
-#pragma unroll
-    for (int v = 0; v < 16; v++) acc[v] = 0.f;
-#pragma unroll
-    for (int t = 0; t < B1 / 2; t++) {
-      const float op = kh ? a[2 * t + 1] : a[2 * t];
-      acc = __builtin_amdgcn_mfma_f32_32x32x2f32(op, op, acc, 0, 0, 0);
-    }
-    float lo[16], hi[16];
-#pragma unroll
-    for (int v = B1 / 2; v < 16; v++) {
-      auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(acc[v]), __float_as_uint(acc[v]), false, false);
-      lo[v] = __uint_as_float(r[0]);
-      hi[v] = __uint_as_float(r[1]);
-    }
-#pragma unroll
-    for (int j = B1; j < NV; j++) {
-      const int v = (j & 3) + 4 * (j >> 3);
-      a[j] -= ((j >> 2) & 1) ? hi[v] : lo[v];
-    }
-#pragma unroll
-    for (int k = B1; k < NV; k++) {
-      const float inv = __builtin_amdgcn_rsqf(fmaxf(rdlane(a[k], k), 1e-30f));
-      a[k] *= inv;
-#pragma unroll
-      for (int j = k + 1; j < NV; j++) a[j] = fmaf(-a[k], rdlane(a[k], j), a[j]);
-    }
-  }
+#if MJL_CHOL_PANEL == 8
+  chol_panel<LD, NV, 0, (NV < 8 ? NV : 8)>(a, kh);
+  if constexpr (NV > 8) chol_panel<LD, NV, 8, (NV < 16 ? NV : 16)>(a, kh);
+  if constexpr (NV > 16) chol_panel<LD, NV, 16, (NV < 24 ? NV : 24)>(a, kh);
+  if constexpr (NV > 24) chol_panel<LD, NV, 24, NV>(a, kh);
+#else
+  chol_panel<LD, NV, 0, B1>(a, kh);
+  if constexpr (NV > B1) chol_panel<LD, NV, B1, NV>(a, kh);
+#endif
   // rows of L to dst, y = L[R][0..NV) to invd_out (scratch until the reads below)
   TACC(33, tch, lane);
   if (lane <= R) {
