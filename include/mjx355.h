@@ -282,6 +282,14 @@ int mjl_obs_normalize(const float* x, const float* mean, const float* var, int n
 int mjl_policy_head(const float* z, const float* log_std, const float* eps, int B, int A, float* act, float* logp,
                     void* stream);
 
+/* PPO update (train_ppo.py:233-252, the bias-gradient column sums of every dense layer's backward
+ * in value_and_grad of ppo_loss_fn / value_loss_fn, and the split-K weight-gradient sum):
+ * out[d] = sum over rows of x[n, d] (row-major, float32, device), in a fixed order (two launches
+ * when n > 256: per-chunk sums into `scratch`, then their sum). mjl_colsum_scratch(n, d) = the
+ * scratch floats mjl_colsum needs (0: none, scratch may be NULL). */
+long long mjl_colsum_scratch(int n, int d);
+int mjl_colsum(const float* x, int n, int d, float* scratch, float* out, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

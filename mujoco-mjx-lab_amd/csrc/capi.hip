@@ -669,6 +669,33 @@ extern "C" int mjl_policy_head(const float* z, const float* log_std, const float
   return MJL_OK;
 }
 
+extern "C" long long mjl_colsum_scratch(int n, int d) {
+  if (n <= 0 || d <= 0) return 0;
+  const ColsumPlan p(n, d);
+  return p.R > 1 ? (long long)p.R * d : 0;
+}
+
+extern "C" int mjl_colsum(const float* x, int n, int d, float* scratch, float* out, void* stream) {
+  if ((!x && n > 0) || !out || n < 0 || d <= 0) return fail(MJL_ERR_ARG, "bad argument");
+  hipStream_t s = (hipStream_t)stream;
+  if (n == 0) {
+    HIPCHK(hipMemsetAsync(out, 0, sizeof(float) * (size_t)d, s));
+    return MJL_OK;
+  }
+  const ColsumPlan p(n, d);
+  if (p.R > 1 && !scratch) return fail(MJL_ERR_ARG, "colsum needs mjl_colsum_scratch(n, d) floats of scratch");
+  const unsigned tiles1 = (unsigned)((d + p.dc1 - 1) / p.dc1);
+  hipLaunchKernelGGL(colsum_kernel, dim3(tiles1, (unsigned)p.R), dim3(256), 0, s, x, n, d, p.dc1, p.chunk,
+                     p.R > 1 ? scratch : out);
+  HIPCHK(hipGetLastError());
+  if (p.R > 1) {
+    const unsigned tiles2 = (unsigned)((d + p.dc2 - 1) / p.dc2);
+    hipLaunchKernelGGL(colsum_kernel, dim3(tiles2, 1), dim3(256), 0, s, scratch, p.R, d, p.dc2, p.R, out);
+    HIPCHK(hipGetLastError());
+  }
+  return MJL_OK;
+}
+
 // jax.random.split over a batch of keys (train_ppo.py:132,150: random.split(rng); random.split(key, num_envs))
 __global__ void prng_split_kernel(const uint32_t* __restrict__ keys, int n, int num, int mode, uint32_t* __restrict__ out) {
   const int t = blockIdx.x * blockDim.x + threadIdx.x;

@@ -15,7 +15,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 def test_header_symbols_exported():
     hdr = open(os.path.join(ROOT, "include", "mjx355.h")).read()
-    declared = set(re.findall(r"^\s*(?:const char\*|int|void)\s+(mjl_\w+)\(", hdr, re.M))
+    declared = set(re.findall(r"^\s*(?:const char\*|long long|int|void)\s+(mjl_\w+)\(", hdr, re.M))
     assert declared == set(_lib.EXPORTS)
     L = _lib.lib()
     for name in declared:

@@ -276,6 +276,40 @@ def test_native_rollout_head_matches_formulas():
 
 
 @pytest.mark.gpu
+def test_native_colsum_matches_torch():
+    """mjl_colsum (bias gradients, split-K sums of the update) equals x.sum(0) in fp64 to fp32
+    accumulation error: the update's shapes, one-chunk and two-stage sizes, ragged and
+    single-column ones, and n = 0; a repeat run is bit-identical (fixed summation order)."""
+    g = torch.Generator(device="cuda").manual_seed(5)
+    for n, d in ((65536, 256), (65536, 21), (65536, 1), (32, 65536), (32, 13824), (1000, 3), (257, 300),
+                 (7, 5), (0, 4)):
+        x = torch.randn((n, d), generator=g, device="cuda")
+        out = ppo.colsum_native(x)
+        ref = x.double().sum(0)
+        tol = 1e-5 * math.sqrt(max(n, 1)) + 1e-6
+        assert out.shape == (d,)
+        scale = max(1.0, float(x.abs().max())) if n else 1.0
+        assert float((out.double() - ref).abs().max()) <= tol * scale, (n, d)
+        assert torch.equal(out, ppo.colsum_native(x)), (n, d)
+
+
+@pytest.mark.gpu
+def test_splitk_linear_backward_matches_autograd():
+    """The split-K linear's backward (weight gradient as batched GEMMs + column sums, bias gradient
+    as a column sum) matches nn.Linear's autograd gradients on the update's minibatch shape."""
+    g = torch.Generator(device="cuda").manual_seed(6)
+    lin = torch.nn.Linear(54, 256).cuda()
+    x = torch.randn((65536, 54), generator=g, device="cuda", requires_grad=True)
+    gy = torch.randn((65536, 256), generator=g, device="cuda")
+    y = ppo._linear(lin, x)
+    gx, gw, gb = torch.autograd.grad(y, (x, lin.weight, lin.bias), gy)
+    gx_r, gw_r, gb_r = torch.autograd.grad(torch.nn.functional.linear(x, lin.weight, lin.bias), (x, lin.weight, lin.bias), gy)
+    torch.testing.assert_close(gx, gx_r, rtol=1e-4, atol=1e-4)
+    torch.testing.assert_close(gw, gw_r, rtol=1e-4, atol=5e-2)
+    torch.testing.assert_close(gb, gb_r, rtol=1e-4, atol=5e-2)
+
+
+@pytest.mark.gpu
 def test_graph_rollout_bit_identical_to_eager():
     """The hipGraph replay of the T-step rollout (policy, sampling, log-prob, fused env step with
     auto-reset) reproduces the eager loop bit for bit, including the env's reset RNG draws (device
