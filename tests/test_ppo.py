@@ -294,6 +294,24 @@ def test_native_colsum_matches_torch():
 
 
 @pytest.mark.gpu
+def test_minibatch_logprob_backward_matches_autograd():
+    """The update-size log-prob (hand-written backward, native column sum for d/d log_std) equals
+    autograd of the reference's elementwise formula (train_ppo.py:121-126) to fp32 rounding."""
+    g = torch.Generator(device="cuda").manual_seed(8)
+    mean = torch.randn((65536, 21), generator=g, device="cuda").requires_grad_()
+    ls = (0.3 * torch.randn(21, generator=g, device="cuda")).requires_grad_()
+    act = torch.randn((65536, 21), generator=g, device="cuda")
+    gout = torch.randn(65536, generator=g, device="cuda")
+    lp = ppo.gaussian_logprob(mean, ls, act)
+    ref = torch.sum((act - mean) ** 2 / torch.exp(2.0 * ls) + 2.0 * ls + ppo.LOG2PI, dim=-1) * -0.5
+    torch.testing.assert_close(lp, ref, rtol=1e-5, atol=1e-4)
+    gm, gs = torch.autograd.grad(lp, (mean, ls), gout)
+    gm_r, gs_r = torch.autograd.grad(ref, (mean, ls), gout)
+    torch.testing.assert_close(gm, gm_r, rtol=1e-5, atol=1e-5)
+    torch.testing.assert_close(gs, gs_r, rtol=1e-4, atol=1e-2)
+
+
+@pytest.mark.gpu
 def test_splitk_linear_backward_matches_autograd():
     """The split-K linear's backward (weight gradient as batched GEMMs + column sums, bias gradient
     as a column sum) matches nn.Linear's autograd gradients on the update's minibatch shape."""

@@ -33,3 +33,10 @@ for n, d in ((65536, 256), (65536, 21), (65536, 1), (32, 65536), (32, 5376)):
           "native %.1f us" % bench(lambda: ppo.colsum_native(x)),
           "maxdiff sum0 %.2e native %.2e" % ((x.sum(0).double() - r0).abs().max(),
                                              (ppo.colsum_native(x).double() - r0).abs().max()), flush=True)
+
+# the split-K weight-gradient sum over the splits, as the 3-D tensor the batched GEMM returns
+for shp in ((32, 256, 256), (32, 256, 54), (32, 21, 256), (32, 1, 256)):
+    g3 = torch.randn(shp, device="cuda")
+    print(shp, "sum0(3d) %.1f us" % bench(lambda: g3.sum(0)),
+          "sum0(2d) %.1f us" % bench(lambda: g3.view(shp[0], -1).sum(0)),
+          "native %.1f us" % bench(lambda: ppo.colsum_native(g3.view(shp[0], -1))), flush=True)
