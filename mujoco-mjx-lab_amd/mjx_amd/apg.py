@@ -77,7 +77,7 @@ class APGTrainer:
         cfg, env = self.cfg, self.env
         H, B, gamma = cfg.horizon, env.num_envs, cfg.gamma
         env.reset()
-        tape, obs_leaves, acts, discs = [], [], [], []
+        tape, obs_leaves, acts, discs, pol_in = [], [], [], [], []
         disc = ret = rsum = None  # created from the first reward (dtype follows the env)
         alive = torch.ones(B, dtype=torch.bool, device=self.device)
         dropped = torch.zeros((), device=self.device)
@@ -86,6 +86,7 @@ class APGTrainer:
             tape.append(env.get_state())
             o, on = self._obs(use_norm, alive)
             a = self.policy(on)
+            pol_in.append(on.detach())
             obs_leaves.append(o)
             acts.append(a)
             obs_traj.append(o.detach())
@@ -112,6 +113,7 @@ class APGTrainer:
         gaux = None
         guarded = getattr(env, "guarded_vjp", False)
         nonfinite = torch.zeros(1, device=self.device) if guarded else None
+        gas = [None] * H
         for t in range(H - 1, -1, -1):
             # the VJP recomputes the step to find its converged active set; the solution the forward
             # step reached (the next tape entry's qacc_warmstart) seeds that solve: ~1 Newton iteration
@@ -126,10 +128,15 @@ class APGTrainer:
                 gq = torch.where(ok[:, None], gq, torch.zeros_like(gq))
                 gv = torch.where(ok[:, None], gv, torch.zeros_like(gv))
                 ga = torch.where(ok[:, None], ga, torch.zeros_like(ga))
-            torch.autograd.backward(acts[t], grad_tensors=ga)
-            og = obs_leaves[t].grad
+            # the chain needs only the observation cotangent here; the parameter gradient (a sum over
+            # steps) is taken once below from all steps' action cotangents
+            og, = torch.autograd.grad(acts[t], obs_leaves[t], grad_outputs=ga)
+            gas[t] = ga
             gq = gq + og[:, :env.nq]
             gv = gv + og[:, env.nq:]
+        # parameter gradient: sum_t (d a_t / d theta)^T ga_t as one forward + backward over the H * B
+        # policy inputs of the rollout (the same inputs; per step it was H small backward passes)
+        torch.autograd.backward(self.policy(torch.cat(pol_in)), grad_tensors=torch.cat(gas))
         if guarded:
             dropped = dropped + nonfinite[0]
         return loss.detach(), (rsum / H).detach(), torch.stack(obs_traj), dropped
