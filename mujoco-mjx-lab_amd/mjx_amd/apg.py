@@ -69,9 +69,9 @@ class APGTrainer:
         """One rollout + backward. Returns (loss, mean reward, obs trajectory, envs dropped as
         non-finite); grads in .grad.
 
-        An env whose state or reward turns non-finite is treated as terminated from that step on
-        (its reward at that step is dropped); an env whose cotangents overflow in the reverse sweep is
-        cut from the gradient at that step. The reference has no such guard: one such env makes its
+        An env whose state or reward turns non-finite, or whose max |qvel| passes cfg.diverge_qvel,
+        is treated as terminated from that step on (its reward at that step is dropped); an env whose
+        cotangents overflow in the reverse sweep is cut from the gradient at that step. The reference has no such guard: one such env makes its
         loss NaN and train_apg.py:278-287 stops the run; here the run continues and the count of
         dropped envs is reported."""
         cfg, env = self.cfg, self.env
@@ -94,8 +94,13 @@ class APGTrainer:
             if disc is None:
                 disc, ret, rsum = torch.ones_like(r), torch.zeros_like(r), torch.zeros_like(r[0])
             # a non-finite post-step state must leave the loss at this step: next step its obs would
-            # reach the policy, and backward through tanh turns even a zero cotangent into NaN
-            bad = alive & ~(torch.isfinite(r) & torch.isfinite(env.qpos_qvel()).all(1))
+            # reach the policy, and backward through tanh turns even a zero cotangent into NaN; so does
+            # a diverged one (max |qvel| > cfg.diverge_qvel: truncated solves)
+            qq = env.qpos_qvel()
+            ok = torch.isfinite(r) & torch.isfinite(qq).all(1)
+            if getattr(cfg, "diverge_qvel", None):
+                ok = ok & (qq[:, env.nq:].abs().amax(1) <= cfg.diverge_qvel)
+            bad = alive & ~ok
             dropped = dropped + bad.sum()
             alive = alive & ~bad
             disc = torch.where(alive, disc, torch.zeros_like(disc))

@@ -81,6 +81,10 @@ class APGConfig(BaseConfig):
     grad_clip: float = 0.3           # optax.clip_by_global_norm(0.3), train_apg.py:142-146
     obs_warmup_steps: int = 100      # train_apg.py:256,262
     rms_update_every: int = 10       # train_apg.py:290-292
+    # not in the reference: an env whose max |qvel| passes this bound is treated like a non-finite one
+    # (dropped from the loss from that step on). Truncated solves (CG 4/4) diverge for some envs under
+    # MJX's integrator rules (DESIGN.md "Truncated solves"); the reference's loss turns NaN/huge there.
+    diverge_qvel: float = 1e3
 
 
 @dataclass

@@ -73,11 +73,36 @@ def lib():
         L.orc_rollout.argtypes = [P(abi.ModelDesc), P(OrcState), P(f64), C.c_int, C.c_int]
         L.orc_step_jacobian.argtypes = [P(abi.ModelDesc), P(OrcState), P(f64)]
         L.orc_env_step_jacobian.argtypes = [P(abi.ModelDesc), P(abi.EnvConfigC), P(OrcState), P(f64), P(f64), P(f64)]
+        L.orc_set_diag.argtypes = [C.c_int]
+        L.orc_take_cost_log.argtypes = [P(f64), C.c_int]
+        L.orc_take_cost_log.restype = C.c_int
         assert L.orc_state_size() == C.sizeof(OrcState), "OrcState layout mismatch"
         assert L.orc_desc_size() == C.sizeof(abi.ModelDesc), "ModelDesc layout mismatch"
         assert L.orc_envcfg_size() == C.sizeof(abi.EnvConfigC), "EnvConfig layout mismatch"
         _lib = L
     return _lib
+
+
+DIAG_TRACE, DIAG_SOLVER_QACC, DIAG_COST_LOG = 1, 2, 4  # physics.hpp kDiag*
+
+
+def set_diag(flags: int) -> None:
+    """Truncated-solve diagnostics (physics.hpp kDiag*); 0 restores the restated algorithm."""
+    lib().orc_set_diag(int(flags))
+
+
+def take_cost_log() -> list:
+    """Per solve since the last call: [cost at the start, after iteration 1, ...] (needs DIAG_COST_LOG)."""
+    buf = np.zeros(1 << 20)
+    n = lib().orc_take_cost_log(_dp(buf), buf.size)
+    out, cur = [], None
+    for x in buf[:n]:
+        if np.isnan(x):
+            cur = []
+            out.append(cur)
+        else:
+            cur.append(float(x))
+    return out
 
 
 def _dp(a: np.ndarray):

@@ -118,6 +118,15 @@ template <class R> int env_step(const mjlModelDesc* m, const mjlEnvConfig* c, or
 
 extern "C" {
 
+// Diagnostics of the truncated-solve study (physics.hpp kDiag*): flags, and the cost log.
+void orc_set_diag(int flags) { oracle::g_diag = flags; }
+int orc_take_cost_log(double* buf, int cap) {
+  int n = (int)std::min<size_t>(oracle::g_cost_log.size(), (size_t)cap);
+  std::copy(oracle::g_cost_log.begin(), oracle::g_cost_log.begin() + n, buf);
+  oracle::g_cost_log.clear();
+  return n;
+}
+
 // mode 0: forward only (mjx.forward); mode 1: step (mjx.step). nstep repeats (state carried).
 int orc_run(const mjlModelDesc* m, orcState* s, int mode, int nstep, int use_float) {
   return use_float ? run<float>(m, s, mode, nstep) : run<double>(m, s, mode, nstep);

@@ -24,7 +24,9 @@
 #pragma once
 #include <algorithm>
 #include <cmath>
+#include <cstdio>
 #include <cstring>
+#include <limits>
 #include <vector>
 
 #include "../include/mjx355.h"
@@ -35,6 +37,18 @@ namespace oracle {
 constexpr double kMinVal = 1e-15;  // mjMINVAL
 constexpr double kMinImp = 0.0001; // mjMINIMP
 constexpr double kMaxImp = 0.9999; // mjMAXIMP
+
+// Diagnostics of the truncated-solve study (tests/test_solver_truncation.py, tools/solver_trace.py;
+// DESIGN.md "Truncated solves"). Off by default; none changes a result unless kDiagSolverQacc is set.
+enum : int {
+  kDiagTrace = 1,        // per-solve / per-iteration / line-search trace on stderr
+  kDiagSolverQacc = 2,   // counterfactual integrator: force = M qacc (the solver's own acceleration)
+                         // instead of qfrc_smooth + qfrc_constraint (MJX forward.py euler/implicit)
+  kDiagCostLog = 4,      // record the cost before and after every solver iteration in g_cost_log
+};
+inline int g_diag = 0;
+inline std::vector<double> g_cost_log;  // per solve: NaN marker, cost at the start, after each iteration
+template <class R> double dbl(const R& x) { return (double)x; }
 
 template <class R> struct Contact {
   R dist, pos[3], frame[9];  // frame rows: normal, tangent1, tangent2
@@ -766,6 +780,7 @@ template <class R> struct Solver {
     cost = gauss + c;
     for (int i = 0; i < nv; i++) grad[i] = Ma[i] - d.qfrc_smooth[i] - d.qfrc_constraint[i];
   }
+  int nactive() const { int n = 0; for (int r = 0; r < nefc; r++) n += jar[r] < 0; return n; }
   void newton_direction() {  // Mgrad = H^-1 grad, H = M + J' D_active J
     for (int i = 0; i < nv * nv; i++) H[i] = d.M[i];
     for (int r = 0; r < nefc; r++) {
@@ -846,6 +861,16 @@ template <class R> struct Solver {
     }
     bool improved = lo.cost < p0.cost || hi.cost < p0.cost;
     R alpha = lo.cost < hi.cost ? lo.alpha : hi.alpha;
+    if (g_diag & kDiagTrace) {  // the zoom's result beside a brute-force scan of alpha in (0, 4]
+      R best = 0, bc = p0.cost;
+      for (int k = 1; k <= 4000; k++) {
+        LSPoint p = ls_point(R(k) * R(0.001), gauss, c1, c2);
+        if (p.cost < bc) { bc = p.cost; best = p.alpha; }
+      }
+      fprintf(stderr, "   ls: f(0) %.6g f'(0) %.4g | lo a %.4g f %.6g f' %.4g | hi a %.4g f %.6g f' %.4g | scan a %.4g f %.6g\n",
+              dbl(p0.cost), dbl(p0.d0), dbl(lo.alpha), dbl(lo.cost), dbl(lo.d0), dbl(hi.alpha), dbl(hi.cost),
+              dbl(hi.d0), dbl(best), dbl(bc));
+    }
     return improved ? alpha : R(0);
   }
 
@@ -871,6 +896,13 @@ template <class R> struct Solver {
       jar[r] = s;
     }
     update();
+    if (g_diag & kDiagTrace)
+      fprintf(stderr, " solve nefc %d warm start from %s (cost %.6g vs %.6g) active %d\n", nefc,
+              cw < cs ? "qacc_warmstart" : "qacc_smooth", dbl(cw), dbl(cs), nactive());
+    if (g_diag & kDiagCostLog) {
+      g_cost_log.push_back(std::numeric_limits<double>::quiet_NaN());
+      g_cost_log.push_back(dbl(cost));
+    }
     bool newton = m.solver == MJL_SOLVER_NEWTON;
     if (newton) newton_direction(); else cg_precondition();
     for (int i = 0; i < nv; i++) search[i] = -Mgrad[i];
@@ -901,6 +933,10 @@ template <class R> struct Solver {
       R gnorm = 0;
       for (int i = 0; i < nv; i++) gnorm += grad[i] * grad[i];
       gnorm = scale * std::sqrt(gnorm);
+      if (g_diag & kDiagCostLog) g_cost_log.push_back(dbl(cost));
+      if (g_diag & kDiagTrace)
+        fprintf(stderr, "  iteration %d alpha %.4g cost %.6g -> %.6g scaled |grad| %.4g active %d\n", iter,
+                dbl(alpha), dbl(oldcost), dbl(cost), dbl(gnorm), nactive());
       go = m.iterations != 1 && iter < m.iterations && improvement >= R(m.tolerance) && gnorm >= R(m.tolerance);
     }
     d.solver_niter = iter;
@@ -984,7 +1020,22 @@ template <class R> void integrate(const mjlModelDesc& m, Data<R>& d) {
     for (int k = 0; k < nv; k++) MI[k * nv + k] += R(m.timestep) * R(m.dof_damping[k]);
     cholesky(MI.data(), L.data(), nv);
     for (int k = 0; k < nv; k++) qacc[k] = d.qfrc_smooth[k] + d.qfrc_constraint[k];
+    if (g_diag & kDiagSolverQacc)
+      for (int k = 0; k < nv; k++) {
+        R s = 0;
+        for (int i = 0; i < nv; i++) s += d.M[k * nv + i] * d.qacc[i];
+        qacc[k] = s;
+      }
     chol_solve(L.data(), nv, qacc.data());
+    if (g_diag & kDiagTrace) {
+      double a = 0, b = 0, c = 0;
+      for (int k = 0; k < nv; k++) {
+        a = std::max(a, std::abs(dbl(d.qacc[k])));
+        b = std::max(b, std::abs(dbl(qacc[k])));
+        c = std::max(c, std::abs(dbl(d.qfrc_constraint[k])));
+      }
+      fprintf(stderr, " integrate: max|qacc| solver %.4g integrator %.4g, max|qfrc_constraint| %.4g\n", a, b, c);
+    }
   }
   R dt = R(m.timestep);
   for (int k = 0; k < nv; k++) d.qvel[k] += dt * qacc[k];
