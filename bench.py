@@ -31,22 +31,48 @@ F32_PEAK_TFLOPS = 157.3           # MI355X_MICROARCH.md: peak FP32 matrix (dense
 SPEEDTEST_KERNEL = "step_kernel<mjl::Dims<27, 17, 22, 20, 48, 16>, 2>"  # rocprofv3 kernel name
 
 
-def parse():
+def parse(argv=None):
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
-    p.add_argument("--steps", type=int, default=50)
-    p.add_argument("--warmup", type=int, default=5)
-    p.add_argument("--envs", type=int, default=2048)
+    p.add_argument("--workload", default="speedtest", choices=["speedtest", "ppo"])
+    p.add_argument("--steps", type=int, default=None, help="timed steps (speedtest launches: 50; ppo iterations: 3)")
+    p.add_argument("--warmup", type=int, default=None, help="untimed steps (speedtest: 5; ppo: 2, graph capture)")
+    p.add_argument("--envs", type=int, default=None, help="envs per GPU (speedtest: 2048; ppo: 1024)")
     p.add_argument("--model", default="humanoid_mjx")
-    p.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU-baseline sample budget")
+    p.add_argument("--cpu-steps", type=int, default=10000, help="CPU baseline: steps per env (C1: 10,000)")
+    p.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline")
     p.add_argument("--no-extras", action="store_true", help="skip the secondary measurements")
-    return p.parse_args()
+    a = p.parse_args(argv)
+    ppo = a.workload == "ppo"
+    if a.steps is None:
+        a.steps = 3 if ppo else 50
+    if a.warmup is None:
+        a.warmup = 2 if ppo else 5
+    if a.envs is None:
+        a.envs = 1024 if ppo else 2048
+    return a
+
+
+def launch_cmd(argv, n: int, port: int):
+    """The child command that runs this script on n ranks of one node (rendezvous on 127.0.0.1)."""
+    return [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+            "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__)] + list(argv)
+
+
+def free_port() -> int:
+    import socket
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        return sk.getsockname()[1]
 
 
 def dist_setup(args):
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        raise SystemExit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}; launch with "
+                         f"torch.distributed.run --nproc-per-node {args.gpus}, or without WORLD_SIZE")
     if world > 1:
         import torch.distributed as dist
         torch.cuda.set_device(local)
@@ -107,35 +133,133 @@ def pmc_traffic(B: int):
     return t.get("bytes_per_launch")
 
 
-def cpu_baseline(model, budget_s: float):
-    """Oracle (CPU restatement, fp64) on the same speed-test workload, one env per host thread."""
+def cpu_model_name() -> str:
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    import platform
+    return platform.processor() or "unknown"
+
+
+def cpu_baseline(steps: int):
+    """BASELINE config C1 (mjx_humanoid_speed_test.py:140 HUMANOID row): humanoid.xml,
+    1 env x `steps` carried steps from qpos0, ctrl = 0 and ctrl ~ U[-1,1] (seed 0); single thread,
+    best of 3, then one env per core on every core this process may use, best of 3; warm-up run
+    excluded. MuJoCo is not importable on the box (plan B), so the timed CPU path is this
+    build's serial C++ restatement (oracle/, kind "port") in its fp32 instantiation, the GPU's
+    arithmetic type. `cores` = the threads used: the CPUs in this process's affinity mask, capped by
+    OMP_NUM_THREADS when set (the pool's CPU share per GPU, 16; os.cpu_count() shows the host)."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     from concurrent.futures import ThreadPoolExecutor
 
+    import mjx_amd
     from oracle import Oracle
-    orc = Oracle(model)
-    probe = np.linspace(0.0, 1.0, 8)
-    t = time.perf_counter()
-    orc.speedtest(probe)
-    per = (time.perf_counter() - t) / probe.size
+    m = mjx_amd.load_model("humanoid")
     avail = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
-    threads = max(1, min(16, avail))
-    n_per_thread = max(8, int(budget_s / max(per, 1e-6) / 2))
-    vel = np.linspace(0.0, 1.0, n_per_thread)
-    workers = [Oracle(model) for _ in range(threads)]
-    t = time.perf_counter()
-    with ThreadPoolExecutor(threads) as ex:
-        list(ex.map(lambda w: w.speedtest(vel), workers))
-    dt = time.perf_counter() - t
-    total = threads * n_per_thread
-    return {"value": total / dt, "unit": "env-steps/s", "cores": threads, "kind": "port",
-            "sample": f"{total} humanoid_mjx speed-test steps (fresh qpos0 state, qvel[0]=linspace(0,1)), "
-                      f"fp64 oracle, {threads} host threads, {dt:.1f} s; single-thread {1.0 / per:.0f} steps/s"}
+    share = int(os.environ.get("OMP_NUM_THREADS", "0") or 0)
+    threads = max(1, min(avail, share) if share > 0 else avail)
+    rng = np.random.default_rng(0)
+    ctrls = {"ctrl0": np.zeros((steps, m.nu)), "ctrlU": rng.uniform(-1.0, 1.0, (steps, m.nu))}
+
+    def run(ctrl):
+        o = Oracle(m, use_float=True)
+        s = o.new_state()
+        t = time.perf_counter()
+        o.rollout(s, ctrl)
+        return time.perf_counter() - t
+
+    res = {}
+    t_all = time.perf_counter()
+    for name, ctrl in ctrls.items():
+        run(ctrl[:200])  # warm-up (page-in, allocator), not timed
+        single = min(run(ctrl) for _ in range(3))
+        best = None
+        with ThreadPoolExecutor(threads) as ex:
+            for _ in range(3):
+                t = time.perf_counter()
+                list(ex.map(lambda _i: run(ctrl), range(threads)))
+                dt = time.perf_counter() - t
+                best = dt if best is None else min(best, dt)
+        res[name] = (steps / single, threads * steps / best)
+    total_s = time.perf_counter() - t_all
+    return {"value": res["ctrlU"][1], "unit": "env-steps/s", "cores": threads, "kind": "port",
+            "cpu_model": cpu_model_name(), "host_cpus": os.cpu_count(), "affinity_cpus": avail,
+            "single_thread": {k: v[0] for k, v in res.items()}, "all_cores": {k: v[1] for k, v in res.items()},
+            "sample": f"C1: humanoid.xml (Newton 100/50, Euler + eulerdamp), 1 env x {steps} carried steps "
+                      f"from qpos0 per thread, ctrl U[-1,1] seed 0 (value) and ctrl 0; oracle/ C++ "
+                      f"restatement, fp32; single thread best of 3, then {threads} threads x 1 env, best of 3; "
+                      f"{total_s:.1f} s in all"}
+
+
+def run_ppo(args, dist, rank, world, local):
+    """BASELINE config C5 (C3 at N = 1): PPO with src/config.json values, args.envs envs per rank,
+    T = 256, 4 epochs, global minibatch 65,536 (each rank takes its share of every minibatch), one
+    RCCL all-reduce of the flattened policy + value gradients per minibatch (train_ppo.py:233-252)."""
+    from mjx_amd import mjx, ppo
+    from mjx_amd.config import reference_ppo_config
+    from mjx_amd.envs import HumanoidEnv, resolve_ids
+    import mjx_amd
+    cfg = reference_ppo_config()
+    cfg.num_envs, cfg.rollout_length = args.envs * world, 256
+    m = mjx_amd.load_model(args.model)
+    env = HumanoidEnv(mjx.put_model(m), resolve_ids(m, cfg.env_config), args.envs, device=local,
+                      seed=cfg.seed * 7919 + rank)
+    tr = ppo.PPOTrainer(cfg, env, None, device=f"cuda:{local}", dist=dist)
+    for it in range(max(2, args.warmup)):  # >= 2: the second rollout captures the rollout graph
+        tr.iteration(it)
+    tr.allreduce_events = []
+    torch.cuda.synchronize()
+    barrier(dist)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    res = [tr.iteration(it) for it in range(args.steps)]
+    torch.cuda.synchronize()
+    barrier(dist)
+    torch.cuda.synchronize()
+    wall = max_over_ranks(time.perf_counter() - t0, dist, local)
+    ar = [a.elapsed_time(b) for a, b in tr.allreduce_events]
+    ar_ms = max_over_ranks(sum(ar) / len(ar) if ar else 0.0, dist, local)
+    nmb = len(ar) // max(1, args.steps)
+    total = float(args.envs * world * cfg.rollout_length * args.steps)
+    grad_numel = sum(p.numel() for p in list(tr.policy.parameters()) + list(tr.value.parameters()))
+    return {
+        "metric": "humanoid PPO env-steps/sec (whole node)", "value": total / wall, "unit": "env-steps/s",
+        "n_gpus": world, "steps": args.steps, "warmup": max(2, args.warmup), "ms_per_step": wall / args.steps * 1e3,
+        "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f32",
+        "data": "synthetic (env resets drawn on the device; random-init policy / value nets)",
+        "config": {"workload": f"PPO src/config.json: {args.envs} envs per GPU x {cfg.rollout_length} rollout x "
+                               f"{cfg.epochs} epochs, global minibatch {cfg.minibatch_size}",
+                   "envs_per_gpu": args.envs, "global_envs": args.envs * world,
+                   "parallelism": f"env-sharded x{world}, RCCL all-reduce per minibatch" if world > 1 else "1 GPU"},
+        "step": "one PPO iteration (rollout + GAE + updates), synced",
+        "rccl_ranks": world if dist is not None else 0,
+        "allreduce_ms_per_minibatch": ar_ms if dist is not None else None,
+        "minibatches_per_iteration": nmb if dist is not None else cfg.epochs * (args.envs * cfg.rollout_length // cfg.minibatch_size),
+        "allreduce_bytes": 4 * grad_numel,
+        "train_return_avg": [r["train_return_avg"] for r in res],
+        "roofline": None, "cpu_baseline": None,
+    }
 
 
 def main():
     args = parse()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        # launch the N ranks as a child process (nothing here has touched the GPU yet) and pass
+        # its status through; rank 0 of the child prints the JSON line
+        import subprocess
+        sys.exit(subprocess.run(launch_cmd(sys.argv[1:], args.gpus, free_port())).returncode)
     dist, rank, world, local = dist_setup(args)
+    if args.workload == "ppo":
+        line = run_ppo(args, dist, rank, world, local)
+        if rank == 0:
+            print(json.dumps(line), flush=True)
+        if dist is not None:
+            dist.destroy_process_group()
+        return
     import mjx_amd
     from mjx_amd import mjx
 
@@ -201,7 +325,7 @@ def main():
         extras["speedtest_b4096_vs_readme"] = extras["speedtest_b4096_steps_per_s"] / REF_DEVICE_STEPS_PER_S
 
     if rank == 0:
-        cpu = cpu_baseline(model, args.cpu_seconds) if world == 1 else None
+        cpu = cpu_baseline(args.cpu_steps) if world == 1 and not args.no_cpu else None
         line = {
             "metric": "humanoid env-steps/sec (whole node)",
             "value": value,

@@ -65,7 +65,7 @@ class APGTrainer:
         x = torch.where(alive[:, None], o, torch.zeros_like(o))
         return o, (apg_normalize(self.rms, x) if use_norm else x)
 
-    def loss_and_grad(self, use_norm: bool):
+    def loss_and_grad(self, use_norm: bool, per_step_param_grad: bool = False):
         """One rollout + backward. Returns (loss, mean reward, obs trajectory, envs dropped as
         non-finite); grads in .grad.
 
@@ -135,13 +135,19 @@ class APGTrainer:
                 ga = torch.where(ok[:, None], ga, torch.zeros_like(ga))
             # the chain needs only the observation cotangent here; the parameter gradient (a sum over
             # steps) is taken once below from all steps' action cotangents
-            og, = torch.autograd.grad(acts[t], obs_leaves[t], grad_outputs=ga)
+            if per_step_param_grad:  # the unbatched form (tests): parameter gradient accumulated per step
+                og, *pg = torch.autograd.grad(acts[t], [obs_leaves[t]] + list(self.policy.parameters()), grad_outputs=ga)
+                for p_, g_ in zip(self.policy.parameters(), pg):
+                    p_.grad = g_ if p_.grad is None else p_.grad + g_
+            else:
+                og, = torch.autograd.grad(acts[t], obs_leaves[t], grad_outputs=ga)
             gas[t] = ga
             gq = gq + og[:, :env.nq]
             gv = gv + og[:, env.nq:]
         # parameter gradient: sum_t (d a_t / d theta)^T ga_t as one forward + backward over the H * B
         # policy inputs of the rollout (the same inputs; per step it was H small backward passes)
-        torch.autograd.backward(self.policy(torch.cat(pol_in)), grad_tensors=torch.cat(gas))
+        if not per_step_param_grad:
+            torch.autograd.backward(self.policy(torch.cat(pol_in)), grad_tensors=torch.cat(gas))
         if guarded:
             dropped = dropped + nonfinite[0]
         return loss.detach(), (rsum / H).detach(), torch.stack(obs_traj), dropped

@@ -61,7 +61,7 @@ class BaseConfig:
     log_interval: int = 10
     eval_interval: int = 50
     results_dir: str = "results"
-    save_video: bool = False  # rendering is out of scope
+    save_video: bool = False  # a qpos-history .npz per eval for offline rendering (mjx_amd/rendering.py)
     render_fps: int = 60
     render_duration: float = 6.0
     camera_name: str = "side_view"

@@ -10,7 +10,7 @@ done flags are exactly those of the reference's merge.
 from __future__ import annotations
 
 import ctypes as C
-from typing import Optional, Tuple
+from typing import NamedTuple, Optional, Tuple
 
 import torch
 
@@ -139,8 +139,66 @@ class HumanoidEnv:
         return self.data.get("aux")
 
 
-def create_env_functions(sys: Model, cfg: EnvConfig, num_envs: int, device: int = 0, seed: int = 0):
-    """Reference `create_env_functions` (src/envs.py:26) returns (single_reset, single_step,
-    v_reset, v_step); the batched pair is what the trainers use. Here: (env, v_reset, v_step)."""
-    env = HumanoidEnv(sys, cfg, num_envs, device=device, seed=seed)
-    return env, env.reset, env.step
+class EnvState(NamedTuple):
+    """The `(mjx.Data, aux)` pair v_reset / v_step pass around (src/envs.py:200,490). `data` is the
+    device-resident batch, updated in place by v_step; `aux` [B, 9] is a view of its aux rows."""
+    data: Data
+    aux: torch.Tensor
+
+
+def create_env_functions(sys: Model, cfg: EnvConfig, q0=None, nq: Optional[int] = None, nv: Optional[int] = None,
+                         device: int = 0, key_mode: int = 1):
+    """Reference `create_env_functions(sys, cfg, q0, nq, nv)` (src/envs.py:26,494-497): returns
+    `(single_reset, single_step, v_reset, v_step)` with the reference's argument meaning.
+
+    * `v_reset(keys [B, 2] uint32/int32)` -> `(EnvState, obs [B, obs_dim])`: every env reset from its
+      jax.random key exactly as `single_reset(key)` draws it (src/envs.py:115-202; `mjl_env_set_reset_keys`);
+    * `v_step(state, action [B, nu])` -> `(EnvState, obs, reward, terminated, truncated)` (floats
+      {0, 1}), no reset merge (src/envs.py:333-492; train_ppo.py merges, here `HumanoidEnv.step`
+      does it in the same launch);
+    * `single_reset(key [2])` / `single_step(state, action [nu])`: the same on a one-env batch.
+
+    Not functional: the returned state aliases the batch, which v_step advances in place (the
+    library owns the device state; keeping old states would mean copying the pytree every step, the
+    cost the fused step avoids). One batch per B is built on first use. `q0` must be the model's
+    qpos0 (the reset base; the kernel takes it from the model), `nq` / `nv` the model's sizes.
+    The trainers use `HumanoidEnv` directly (step with the fused auto-reset)."""
+    import numpy as np
+    if nq is not None and nq != sys.nq or nv is not None and nv != sys.nv:
+        raise MjlError(f"nq/nv ({nq}, {nv}) do not match the model ({sys.nq}, {sys.nv})")
+    if q0 is not None and not np.allclose(np.asarray(q0, np.float64), np.asarray(sys.m.qpos0, np.float64), atol=1e-6):
+        raise MjlError("q0 must equal the model's qpos0 (the reset base of the native env)")
+    envs = {}
+
+    def _env(B: int) -> HumanoidEnv:
+        if B not in envs:
+            envs[B] = HumanoidEnv(sys, cfg, B, device=device)
+        return envs[B]
+
+    def v_reset(keys: torch.Tensor):
+        keys = torch.as_tensor(keys)
+        if keys.dim() != 2 or keys.shape[1] != 2:
+            raise MjlError("keys must have shape [B, 2]")
+        env = _env(keys.shape[0])
+        k = keys.to(torch.int64).to(torch.int32).to(env.obs.device).contiguous()
+        env.set_reset_keys(k, key_mode)
+        obs = env.reset().clone()
+        env.set_reset_keys(None)
+        return EnvState(env.data, env.aux), obs
+
+    def v_step(state: EnvState, action: torch.Tensor):
+        env = next((e for e in envs.values() if e.data is state.data), None)
+        if env is None:
+            raise MjlError("state does not come from this v_reset")
+        obs, rew, term, trunc = env.step(action, auto_reset=False)
+        return EnvState(env.data, env.aux), obs.clone(), rew.clone(), term.clone(), trunc.clone()
+
+    def single_reset(key: torch.Tensor):
+        st, obs = v_reset(torch.as_tensor(key).reshape(1, 2))
+        return st, obs[0]
+
+    def single_step(state: EnvState, action: torch.Tensor):
+        st, obs, rew, term, trunc = v_step(state, torch.as_tensor(action).reshape(1, -1))
+        return st, obs[0], rew[0], term[0], trunc[0]
+
+    return single_reset, single_step, v_reset, v_step

@@ -330,9 +330,11 @@ def _set_grads(params: List[torch.Tensor], flat: torch.Tensor):
         o += n
 
 
-def ppo_update(policy, value, opt_p, opt_v, obs, acts, logp, ret, adv, index_batches, cfg, dist=None, world=1):
+def ppo_update(policy, value, opt_p, opt_v, obs, acts, logp, ret, adv, index_batches, cfg, dist=None, world=1,
+               events: Optional[list] = None):
     """train_ppo.py:233-252: per minibatch, a policy Adam step then a value Adam step. Data-parallel:
-    each rank takes its share of every minibatch; gradients of both nets travel in one all-reduce."""
+    each rank takes its share of every minibatch; gradients of both nets travel in one all-reduce.
+    `events` (a list) collects a (start, end) CUDA event pair around each all-reduce (bench.py)."""
     pp, vp = list(policy.parameters()), list(value.parameters())
     for idx in index_batches:
         o, a, ol, r, ad = obs[idx], acts[idx], logp[idx], ret[idx], adv[idx]
@@ -342,7 +344,13 @@ def ppo_update(policy, value, opt_p, opt_v, obs, acts, logp, ret, adv, index_bat
         value_loss(value, o, r).backward()
         if dist is not None:
             g = _flat_grads(pp + vp)
+            if events is not None:
+                ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+                ev[0].record()
             dist.all_reduce(g)
+            if events is not None:
+                ev[1].record()
+                events.append(ev)
             g /= world
             _set_grads(pp + vp, g)
         opt_p.step()
@@ -390,6 +398,7 @@ class PPOTrainer:
         self.obs = env.reset().clone()
         self.use_graph = bool(use_graph)
         self._buf, self._graph, self._rollouts = None, None, 0
+        self.allreduce_events = None  # a list to time the per-minibatch all-reduce (bench.py --workload ppo)
         self.total_env_steps = 0.0
         self.start = time.time()
         self.out_dir = out_dir if self.rank == 0 else None
@@ -516,7 +525,7 @@ class PPOTrainer:
         idx = make_index_batches(T * B, mb, cfg.epochs, self.idx_gen, dev)
         ppo_update(self.policy, self.value, self.opt_p, self.opt_v, obs_n.reshape(T * B, -1),
                    act_t.reshape(T * B, -1), logp_t.reshape(-1), ret.reshape(-1), adv.reshape(-1), idx, cfg,
-                   self.dist, self.world)
+                   self.dist, self.world, self.allreduce_events if self.device.type == "cuda" else None)
         if dev.type == "cuda":
             torch.cuda.synchronize(dev)
         dt = max(time.time() - t0, 1e-9)
@@ -559,6 +568,25 @@ class PPOTrainer:
         if keyed:
             env.set_reset_keys(None)
         return float(acc.mean())
+
+    def dump_qpos_history(self, it: int) -> Optional[str]:
+        """train_ppo.py:433-456 render_video (save_video): one env, deterministic mean action of the
+        normalised obs for render_duration seconds, reset to its initial state when done; the qpos
+        history goes to <training_dir>/videos/iter_<it+1:06d>.npz (mjx_amd/rendering.py)."""
+        if not self.out_dir or self.eval_env is None or not hasattr(self.eval_env, "get_state"):
+            return None
+        from . import rendering
+        from .envs import HumanoidEnv
+        if getattr(self, "_render_env", None) is None:
+            ev = self.eval_env
+            self._render_env = HumanoidEnv(ev.sys, ev.cfg, 1, device=self.device.index or 0,
+                                           seed=int(self.cfg.seed) + 20000)
+        pol = lambda o: self.policy(self.rms.normalize(o))[0]  # noqa: E731
+        qpos, act = rendering.rollout_qpos_history(self._render_env, pol, float(self.cfg.render_duration))
+        path = os.path.join(self.out_dir, "videos", f"iter_{it + 1:06d}.npz")
+        return rendering.save_qpos_history(path, qpos[:, 0], act[:, 0], float(self._render_env.sys.m.timestep),
+                                           int(self.cfg.render_fps), os.path.basename(str(self.cfg.xml_path)),
+                                           str(self.cfg.camera_name))
 
     def save_checkpoint(self, it: int, metrics: dict):
         """checkpoint_utils.py:38-61 layout (results/<ts>_ppo/checkpoints/), torch state dicts."""
@@ -609,5 +637,7 @@ class PPOTrainer:
                     print(s, flush=True)
             if should_ckpt:
                 self.save_checkpoint(it, m)
+            if cfg.save_video and it % cfg.eval_interval == 0 and self.rank == 0:
+                self.dump_qpos_history(it)
             hist.append(m)
         return hist
