@@ -166,7 +166,8 @@ def test_evaluate_32x500_against_stepwise_loop_and_oracle():
         sp = jr.split(rng)
         rng.copy_(sp[0])
         keys.copy_(jr.split(sp[1], 32))
-        mean, _ = tr.policy(tr.rms.normalize(obs))
+        with torch.no_grad():
+            mean, _ = tr.policy(tr.rms.normalize(obs))
         o, r, te, trn = ev.step(mean)
         rec.append((keys.clone(), mean.clone(), r.clone(), torch.maximum(te, trn).clone()))
         obs = o
