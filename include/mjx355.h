@@ -168,8 +168,13 @@ int mjl_batch_nenv(const mjlBatch* batch);
 /* Batch options. MJL_OPT_STORE_DERIVED (default 1): step/env kernels also write the derived
  * per-env outputs (xpos, xquat, qacc, forces, sensordata, stats) readable with mjl_get; set 0 to
  * keep only the state + env outputs in the hot loop. MJL_OPT_FORCE_GLOBAL_ROWS (default 0, test
- * hook): keep constraint rows in the global-memory scratch even when they fit in LDS. */
-enum { MJL_OPT_STORE_DERIVED = 0, MJL_OPT_FORCE_GLOBAL_ROWS = 1 };
+ * hook): keep constraint rows in the global-memory scratch even when they fit in LDS.
+ * MJL_OPT_VJP_UNROLLED (default 0): the step VJPs differentiate the constraint solve's iterations
+ * as executed (what jax.grad through MJX's fixed-count solver computes; reference train_apg.py:
+ * 101-105,187-189 runs CG 4/4) instead of the implicit derivative at the converged active set; the
+ * integrator's input is then qfrc_smooth + qfrc_constraint of the stopped solve. The VJP must see
+ * the pre-step qacc_warmstart the forward step saw (the recompute replays that solve). */
+enum { MJL_OPT_STORE_DERIVED = 0, MJL_OPT_FORCE_GLOBAL_ROWS = 1, MJL_OPT_VJP_UNROLLED = 2 };
 int mjl_batch_set_option(mjlBatch* batch, int option, int value);
 
 /* Copy a per-env field to / from a device buffer [nenv, dim] (async on stream). `mask` (device,
@@ -253,6 +258,18 @@ int mjl_env_step_vjp(mjlBatch* batch, const float* act, const float* g_qpos, con
 int mjl_env_step_vjp_guarded(mjlBatch* batch, const float* act, const float* g_qpos, const float* g_qvel,
                              const float* g_rew, const float* g_aux, float* out_qpos, float* out_qvel,
                              float* out_act, float* out_aux, float* nonfinite_count, void* stream);
+
+/* Full-state VJPs: as mjl_step_vjp / mjl_env_step_vjp_guarded, plus the carried warm start.
+ * g_qacc_ws [nenv,nv] is the cotangent of the output qacc_warmstart (= the step's qacc, MJX
+ * solver.solve); out_qacc_ws [nenv,nv] receives the cotangent of the input qacc_warmstart, nonzero
+ * only in MJL_OPT_VJP_UNROLLED mode when the truncated solve started from it (jax.grad through the
+ * Data carry sees this path; a converged solve does not depend on its seed). Either may be NULL. */
+int mjl_step_vjp_full(mjlBatch* batch, const float* g_qpos, const float* g_qvel, const float* g_qacc_ws,
+                      float* out_qpos, float* out_qvel, float* out_qacc_ws, float* out_ctrl, void* stream);
+int mjl_env_step_vjp_full(mjlBatch* batch, const float* act, const float* g_qpos, const float* g_qvel,
+                          const float* g_qacc_ws, const float* g_rew, const float* g_aux, float* out_qpos,
+                          float* out_qvel, float* out_qacc_ws, float* out_act, float* out_aux,
+                          float* nonfinite_count, void* stream);
 
 /* The persistent per-env state (what a step reads and writes: Data.qpos, qvel, qacc_warmstart,
  * time, plus the env aux) as packed rows [nenv, mjl_state_size] = [qpos | qvel | qacc_warmstart |

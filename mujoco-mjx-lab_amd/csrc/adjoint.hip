@@ -4,9 +4,14 @@
 // One wave per env, like the forward kernel: the step is recomputed in LDS (per-step remat, as
 // train_apg.py:187-189 checkpoints every step), then the reverse passes run phase by phase.
 // Derivative conventions (DESIGN.md "APG"):
-//  * the constraint solve is differentiated at its converged active set A (implicit function):
-//    qacc = Hc^-1 (qfrc_smooth + J_A' D_A aref_A), Hc = M + J_A' D_A J_A; and the total force that
-//    enters the integrator, qfrc_smooth + J' f, equals M qacc there;
+//  * implicit mode (default): the constraint solve is differentiated at its converged active set A
+//    (implicit function): qacc = Hc^-1 (qfrc_smooth + J_A' D_A aref_A), Hc = M + J_A' D_A J_A; and
+//    the total force that enters the integrator, qfrc_smooth + J' f, equals M qacc there;
+//  * unrolled mode (MJL_OPT_VJP_UNROLLED): the solve's iterations as executed are differentiated,
+//    branch decisions fixed (what jax.grad through MJX's fixed-count solver computes; the reference
+//    APG runs CG 4/4, train_apg.py:101-105,187-189): the recompute records a tape (SolveTape) and
+//    adj_solver_unrolled sweeps it backwards (algorithm: tests/unrolled_solver_ref.py); the
+//    integrator's force is qfrc_smooth + qfrc_constraint of the stopped solve, as forward.py has it;
 //  * qacc_warmstart only seeds the solver and gets no cotangent;
 //  * piecewise-constant quantities (contact/limit activity, target jumps, flags) follow the branch
 //    the primal takes, as reverse-mode autodiff of the reference does.
@@ -131,12 +136,105 @@ template <class DM> struct WSA {
   float cdofb[NV][6], cinertb[NB][10], crbb[NB][10], cvelb[NB][6], caccb[NB][6], cfrcb[NB][6], cfsubb[NB][6];
   float Sb[NB][6], Ub[NB][6], Tb[NB][6];
   alignas(16) float Mb[NV * LD];
+  float qfcb[LD];                      // unrolled mode: cotangent of the final qfrc_constraint
+  float wsb[LD];                       // unrolled mode: cotangent of the input qacc_warmstart
+  alignas(16) float uv[3][LD];         // unrolled mode: vectors staged for M v / J v products
 };
 
 // per-env global scratch of the adjoint (after the env's row slab): per row (alpha, gamma, posbar),
 // per contact kConAdjW floats: pos 3, frame 9, dist 1, geom1 (pos, axis) 6, geom2 (pos, axis) 6
 constexpr int kConAdjW = 25;
 __host__ __device__ inline int adj_scratch_floats(int nefc_max, int ncon_max) { return 3 * nefc_max + kConAdjW * ncon_max; }
+
+// ------------------------------------------------------------------- unrolled mode: the solve tape
+// Per env, in the unrolled scratch (capi.hip launch_vjp): the tape, then per-row accumulators.
+//   header [4]: number of updates, of line searches, warm-start choice (0 qacc_warmstart, 1 smooth)
+//   update k (k < KU): q_k [LD], grad_k [LD], Mgrad_k [LD], beta_k, num_k, den_k, -, active mask [2 NW]
+//   line search k (k < KL): s_k [LD], alpha_k, nsets, -, -, weights [64], N [64], Q2 [64],
+//     parent active masks [64][2 NW]: the accepted alpha_k = sum_j w_j N_j, where N_j = -Q1_j / Q2_j
+//     is the Newton point of a point whose active set was A_j (tests/unrolled_solver_ref.py)
+//   rows: arefb, Db, ca, cb [nefc_max] each, Jbar [nefc_max][LD]
+struct TapeDims {
+  int LD, NW, KU, KL, US, LSS, tape, stride;
+  __host__ __device__ void init(int ld, int nefc_max, int iterations) {
+    LD = ld;
+    NW = (nefc_max + 63) / 64;
+    if (NW < 1) NW = 1;
+    const int it = iterations > 1 ? iterations : 1;
+    KU = it + 1;
+    KL = it;
+    US = 3 * LD + 4 + 2 * NW;
+    LSS = LD + 4 + 3 * 64 + 64 * 2 * NW;
+    tape = 4 + KU * US + KL * LSS;
+    stride = (tape + 4 * nefc_max + nefc_max * LD + 3) & ~3;
+  }
+};
+
+struct SolveTape {
+  static constexpr bool on = true;
+  GLBA float* t;
+  TapeDims d;
+  int nup, nls, nsets, overflow;
+  INL GLBA float* upd(int k) const { return t + 4 + k * d.US; }
+  INL GLBA float* ls(int k) const { return t + 4 + d.KU * d.US + k * d.LSS; }
+  INL void put_mask(GLBA float* dst, int w, unsigned long long b, int lane) const {
+    if (lane == 0) { dst[2 * w] = __uint_as_float((uint32_t)b); dst[2 * w + 1] = __uint_as_float((uint32_t)(b >> 32)); }
+  }
+  INL void warm(int wsel, int lane) {
+    if (lane == 0) t[2] = (float)wsel;
+  }
+  template <class DD, bool G> INL void update(LDSA WS<DD>* W, Rows<G> R, int lane) {
+    if (nup >= d.KU) { overflow = 1; return; }
+    GLBA float* u = upd(nup);
+    if (lane < d.LD) { u[lane] = W->qacc[lane]; u[d.LD + lane] = W->grad[lane]; u[2 * d.LD + lane] = 0.f; }
+    for (int w = 0; w < d.NW; w++) {
+      const int r = lane + 64 * w;
+      put_mask(u + 3 * d.LD + 4, w, __ballot(r < W->nefc && R.jar[r] < 0.f), lane);
+    }
+    if (lane == 0) { u[3 * d.LD] = 0.f; u[3 * d.LD + 1] = 0.f; u[3 * d.LD + 2] = 0.f; }
+    nup++;
+  }
+  INL void direction(float mg, float beta, float num, float den, int lane) {
+    if (nup < 1 || overflow) return;
+    GLBA float* u = upd(nup - 1);
+    if (lane < d.LD) u[2 * d.LD + lane] = mg;
+    if (lane == 0) { u[3 * d.LD] = beta; u[3 * d.LD + 1] = num; u[3 * d.LD + 2] = den; }
+  }
+  template <class DD> INL void ls_begin(LDSA WS<DD>* W, int lane) {
+    nsets = 0;
+    if (nls >= d.KL) { overflow = 1; return; }
+    if (lane < d.LD) ls(nls)[lane] = W->search[lane];
+  }
+  // record the Newton point a_new of a point at a_par with f'' = d1 (its active set from the rows'
+  // register / scratch copies exactly as the search's `partial` evaluates it); returns its index
+  template <bool G> INL int add_set(Rows<G> R, int nefc, float a_par, float d1, float a_new, float ja0, float jv0,
+                                    float ja1, float jv1, int lane) {
+    const int idx = nsets < 64 ? nsets : 63;
+    if (nsets >= 64) overflow = 1;
+    nsets = nsets < 64 ? nsets + 1 : 64;
+    if (nls >= d.KL) return idx;
+    GLBA float* l = ls(nls);
+    if (lane == 0) { l[d.LD + 4 + 64 + idx] = a_new; l[d.LD + 4 + 128 + idx] = d1; }
+    GLBA float* mk = l + d.LD + 4 + 192 + idx * 2 * d.NW;
+    put_mask(mk, 0, __ballot(ja0 + a_par * jv0 < 0.f), lane);
+    if (d.NW > 1) put_mask(mk, 1, __ballot(ja1 + a_par * jv1 < 0.f), lane);
+    for (int w = 2; w < d.NW; w++) {
+      const int r = lane + 64 * w;
+      put_mask(mk, w, __ballot(r < nefc && R.jar[r] + a_par * R.Jv[r] < 0.f), lane);
+    }
+    return idx;
+  }
+  INL void ls_end(float alpha, float rec, int lane) {
+    if (nls >= d.KL) return;
+    GLBA float* l = ls(nls);
+    if (lane == 0) { l[d.LD] = alpha; l[d.LD + 1] = (float)nsets; }
+    l[d.LD + 4 + lane] = rec;
+    nls++;
+  }
+  INL void finish(int lane) {
+    if (lane == 0) { t[0] = (float)nup; t[1] = (float)nls; t[3] = (float)overflow; }
+  }
+};
 
 // wave sum of a 3-vector contribution into LDS dst (lane 0 writes)
 INL void wsum3_into(LDSA float* dst, const float* v, int lane) {
@@ -246,8 +344,9 @@ template <class D> INL void adj_env(MP m, LDSA WS<D>* W, LDSA WSA<D>* A, CP c, c
 
 // ------------------------------------------------------------------- integration (forward.py)
 // in: A->vtmp = cotangent of qvel', gq = cotangent of qpos' (global). out: A->qposb, A->qvelb,
-// A->qaccb, A->Mb (implicit / eulerdamp matrix path).
-template <class D> INL void adj_integrate(MP m, LDSA WS<D>* W, LDSA WSA<D>* A, const float* gq, int lane) {
+// A->qaccb, A->Mb (implicit / eulerdamp matrix path); unrolled mode: the matrix path's force is
+// qfrc_smooth + qfrc_constraint (A->frcsb, A->qfcb), not M qacc.
+template <class D> INL void adj_integrate(MP m, LDSA WS<D>* W, LDSA WSA<D>* A, const float* gq, bool unr, int lane) {
   constexpr int LD = D::LD;
   const int nv = m->nv;
   const float dt = m->timestep;
@@ -296,8 +395,14 @@ template <class D> INL void adj_integrate(MP m, LDSA WS<D>* W, LDSA WSA<D>* A, c
     SYNC();
     if (lane < nv) {
       const float rl = A->rb[lane];
-      for (int k = 0; k < nv; k++) A->Mb[lane * LD + k] += rl * (W->qacc[k] - A->ap[k]);
-      A->qaccb[lane] += mrow<D>(W, A->rb, lane);
+      if (unr) {  // a' = Hd^-1 (qfrc_smooth + qfrc_constraint)
+        for (int k = 0; k < nv; k++) A->Mb[lane * LD + k] -= rl * A->ap[k];
+        A->frcsb[lane] += rl;
+        A->qfcb[lane] += rl;
+      } else {
+        for (int k = 0; k < nv; k++) A->Mb[lane * LD + k] += rl * (W->qacc[k] - A->ap[k]);
+        A->qaccb[lane] += mrow<D>(W, A->rb, lane);
+      }
     }
   } else if (lane < nv) {
     A->qaccb[lane] += apb;
@@ -306,47 +411,37 @@ template <class D> INL void adj_integrate(MP m, LDSA WS<D>* W, LDSA WSA<D>* A, c
 }
 
 // ------------------------------------------------------------------- constraint solve + rows
-// Implicit derivative at the converged active set; per row alpha (J-bar coefficient of qvel),
-// gamma (of qacc; the coefficient of mu is the row force), posbar -> global scratch.
-template <class D> INL void adj_solver_rows(MP m, LDSA WS<D>* W, LDSA WSA<D>* A, Rows<true> R, GLBA float* scr,
-                                            int nefc_max, int lane) {
-  constexpr int LD = D::LD;
-  const int nv = m->nv, nefc = W->nefc;
+// Per row, from the cotangents of its aref and D: alpha (J-bar coefficient of qvel: aref = -b J qvel
+// - k imp pos), gamma (J-bar coefficient of qacc, implicit mode), posbar -> global scratch; then
+// qvel-bar += sum_r alpha_r J_r and the limit rows' pos -> qpos-bar.
+template <class D> INL void adj_row_map(MP m, Rows<true> R, GLBA float* scr, int nefc_max, int r, float arefb,
+                                        float Db, float gam) {
   GLBA float* alpha = scr;
   GLBA float* gamma = scr + nefc_max;
   GLBA float* posb = scr + 2 * nefc_max;
-  const float mu = chol_solve<D>(A->Lc, A->invdc, lane < nv ? A->qaccb[lane] : 0.f, lane);
-  if (lane < LD) A->mu[lane] = (lane < nv) ? mu : 0.f;
-  SYNC();
-  if (lane < nv) {
-    A->frcsb[lane] += A->mu[lane];
-    const float ml = A->mu[lane];
-    for (int k = 0; k < nv; k++) A->Mb[lane * LD + k] -= ml * W->qacc[k];
-  }
-  for (int r = lane; r < nefc; r += 64) {
-    const int meta = R.emeta[r], type = meta >> 16, id = meta & 0xffff;
-    const float jar = R.jar[r], Dr = R.D[r];
-    const bool act = jar < 0.f;
-    float jm = 0.f;
-    for (int k = 0; k < LD; k++) jm += R.J[r * LD + k] * A->mu[k];
-    const float arefb = act ? Dr * jm : 0.f;
-    const float Db = act ? -jm * jar : 0.f;
-    const CSTA float *sr, *si;
-    if (type == 0) { sr = m->jnt_solref[id]; si = m->jnt_solimp[id]; }
-    else if (type == 1) { sr = m->tendon_solref[id]; si = m->tendon_solimp[id]; }
-    else { sr = m->pair_solref[id]; si = m->pair_solimp[id]; }
-    float k, b, imp;
-    const float pos = R.epos[r];
-    kbi(m->timestep, sr, si, pos, k, b, imp);
-    const float invw = R.einvw[r];
-    const float rr = invw * (1.f - imp) / imp;
-    const float dDdimp = (rr > kMinVal) ? 1.f / (invw * (1.f - imp) * (1.f - imp)) : 0.f;
-    const float impb = -k * pos * arefb + Db * dDdimp;
-    alpha[r] = -b * arefb;
-    gamma[r] = act ? -Dr * jm : 0.f;
-    posb[r] = -k * imp * arefb + impb * imp_dpos(si, pos);
-  }
-  SYNC();
+  const int meta = R.emeta[r], type = meta >> 16, id = meta & 0xffff;
+  const CSTA float *sr, *si;
+  if (type == 0) { sr = m->jnt_solref[id]; si = m->jnt_solimp[id]; }
+  else if (type == 1) { sr = m->tendon_solref[id]; si = m->tendon_solimp[id]; }
+  else { sr = m->pair_solref[id]; si = m->pair_solimp[id]; }
+  float k, b, imp;
+  const float pos = R.epos[r];
+  kbi(m->timestep, sr, si, pos, k, b, imp);
+  const float invw = R.einvw[r];
+  const float rr = invw * (1.f - imp) / imp;
+  const float dDdimp = (rr > kMinVal) ? 1.f / (invw * (1.f - imp) * (1.f - imp)) : 0.f;
+  const float impb = -k * pos * arefb + Db * dDdimp;
+  alpha[r] = -b * arefb;
+  gamma[r] = gam;
+  posb[r] = -k * imp * arefb + impb * imp_dpos(si, pos);
+}
+
+template <class D> INL void adj_rows_tail(MP m, LDSA WS<D>* W, LDSA WSA<D>* A, Rows<true> R, GLBA float* scr,
+                                          int nefc_max, int lane) {
+  constexpr int LD = D::LD;
+  const int nv = m->nv, nefc = W->nefc;
+  GLBA float* alpha = scr;
+  GLBA float* posb = scr + 2 * nefc_max;
   if (lane < nv) {  // qvel-bar += sum_r alpha_r J_r  (aref depends on J qvel)
     float s = 0.f;
     for (int r = 0; r < nefc; r++) s += alpha[r] * R.J[r * LD + lane];
@@ -371,12 +466,232 @@ template <class D> INL void adj_solver_rows(MP m, LDSA WS<D>* W, LDSA WSA<D>* A,
   SYNC();
 }
 
+// Implicit mode: derivative at the converged active set (mu = Hc^-1 qacc-bar).
+template <class D> INL void adj_solver_rows(MP m, LDSA WS<D>* W, LDSA WSA<D>* A, Rows<true> R, GLBA float* scr,
+                                            int nefc_max, int lane) {
+  constexpr int LD = D::LD;
+  const int nv = m->nv, nefc = W->nefc;
+  const float mu = chol_solve<D>(A->Lc, A->invdc, lane < nv ? A->qaccb[lane] : 0.f, lane);
+  if (lane < LD) A->mu[lane] = (lane < nv) ? mu : 0.f;
+  SYNC();
+  if (lane < nv) {
+    A->frcsb[lane] += A->mu[lane];
+    const float ml = A->mu[lane];
+    for (int k = 0; k < nv; k++) A->Mb[lane * LD + k] -= ml * W->qacc[k];
+  }
+  for (int r = lane; r < nefc; r += 64) {
+    const float jar = R.jar[r], Dr = R.D[r];
+    const bool act = jar < 0.f;
+    float jm = 0.f;
+    for (int k = 0; k < LD; k++) jm += R.J[r * LD + k] * A->mu[k];
+    adj_row_map<D>(m, R, scr, nefc_max, r, act ? Dr * jm : 0.f, act ? -jm * jar : 0.f, act ? -Dr * jm : 0.f);
+  }
+  SYNC();
+  adj_rows_tail<D>(m, W, A, R, scr, nefc_max, lane);
+}
+
+// Unrolled mode: reverse sweep of the taped solve (tests/unrolled_solver_ref.py solve_vjp, line by
+// line). In: A->qaccb, A->qfcb (cotangents of the final qacc and qfrc_constraint). Out: A->Mb,
+// A->frcsb, the per-row aref / D cotangents (mapped by adj_row_map) and J-bar rows (u.rows Jbar,
+// read by adj_contact_jac). Vectors are lane-resident (lane = dof); uv[] stages M v / J v operands.
+template <class D> INL void adj_solver_unrolled(MP m, LDSA WS<D>* W, LDSA WSA<D>* A, Rows<true> R, GLBA float* scr,
+                                                int nefc_max, const SolveTape& tp, int lane) {
+  constexpr int LD = D::LD;
+  const int nv = m->nv, nefc = W->nefc;
+  const bool cg = m->solver != MJL_SOLVER_NEWTON;
+  const TapeDims& d = tp.d;
+  GLBA float* arefb = tp.t + d.tape;
+  GLBA float* Dbar = arefb + nefc_max;
+  GLBA float* ca = arefb + 2 * nefc_max;
+  GLBA float* cb = arefb + 3 * nefc_max;
+  GLBA float* Jbar = arefb + 4 * nefc_max;
+  LDSA float* V1 = A->uv[0];
+  LDSA float* V2 = A->uv[1];
+  LDSA float* V3 = A->uv[2];
+  const bool isd = lane < nv;
+  auto ld = [&](auto p) -> float { return isd ? p[lane] : 0.f; };
+  auto stage = [&](LDSA float* dst, float v) { if (lane < LD) dst[lane] = isd ? v : 0.f; };
+  auto bit = [&](GLBA const float* mk, int r) -> bool {
+    const uint32_t w = __float_as_uint(mk[2 * (r >> 6) + ((r >> 5) & 1)]);
+    return (w >> (r & 31)) & 1u;
+  };
+  // J-bar rows += ca (x) va + cb (x) vb (ca, cb per row in scratch; va, vb in LDS)
+  auto jbar_add = [&](LDSA const float* va, LDSA const float* vb) {
+    SYNC();
+    if (isd) {
+      const float a = va[lane], b = vb[lane];
+      for (int r = 0; r < nefc; r++) Jbar[r * LD + lane] += ca[r] * a + cb[r] * b;
+    }
+  };
+  auto jt = [&](GLBA const float* c) -> float {  // (J' c)[lane]
+    float x = 0.f;
+    if (isd)
+      for (int r = 0; r < nefc; r++) x += R.J[r * LD + lane] * c[r];
+    return x;
+  };
+  auto mb_outer = [&](float a, LDSA const float* v) {  // Mb[lane][:] += a v'
+    if (isd)
+      for (int k = 0; k < nv; k++) A->Mb[lane * LD + k] += a * v[k];
+  };
+  for (int r = lane; r < nefc; r += 64) { arefb[r] = 0.f; Dbar[r] = 0.f; }
+  if (isd)
+    for (int r = 0; r < nefc; r++) Jbar[r * LD + lane] = 0.f;
+  const int nup = (int)tp.t[0], nls = (int)tp.t[1], K = nup - 1;
+  const int wsel = nup > 0 ? (int)tp.t[2] : 1;
+  // L(M) in A->Lc (CG preconditioner; the smooth warm start)
+  stage(V1, 0.f);
+  SYNC();
+  chol_factor_solve<D>(W->M, A->Lc, A->invdc, nv, V1, lane);
+  SYNC();
+  float qb = ld(A->qaccb), sb = 0.f, gb = 0.f, mgb = 0.f;
+  for (int k = K; k >= 0; k--) {
+    GLBA const float* u = tp.upd(k);
+    const float q_k = ld(u), grad_k = ld(u + LD), mg_k = ld(u + 2 * LD);
+    float sbp = 0.f, gbp = 0.f, mgbp = 0.f;
+    if (k < nls) {  // s_k = -Mg_k + beta_k s_{k-1} was used by line search k
+      mgb -= sb;
+      if (cg && k >= 1) {
+        GLBA const float* up = tp.upd(k - 1);
+        const float betab = wsum(sb * ld(tp.ls(k - 1)));
+        const float beta = u[3 * LD], num = u[3 * LD + 1], den_raw = u[3 * LD + 2];
+        sbp += beta * sb;
+        const float den = fmaxf(kMinVal, den_raw);
+        if (num / den > 0.f) {
+          const float nb = betab / den;
+          gb += nb * (mg_k - ld(up + 2 * LD));
+          mgb += nb * grad_k;
+          mgbp -= nb * grad_k;
+          if (den_raw > kMinVal) {
+            const float denb = -betab * num / (den * den);
+            gbp += denb * ld(up + 2 * LD);
+            mgbp += denb * ld(up + LD);
+          }
+        }
+      }
+    }
+    // Mg_k = P_k^-1 grad_k
+    if (__ballot(isd && mgb != 0.f) != 0ull) {
+      float lam;
+      stage(V1, mgb);
+      stage(V2, mg_k);
+      SYNC();
+      if (cg) {
+        lam = chol_solve<D>(A->Lc, A->invdc, mgb, lane);
+      } else {  // H_k = M + J' D_A J over update k's active rows (the tape's mask)
+        for (int r = lane; r < nefc; r += 64) R.jar[r] = bit(u + 3 * LD + 4, r) ? -1.f : 1.f;
+        SYNC();
+        if constexpr (D::NV < 32) {
+          const f32x16 acc = solver_hessian_acc<D, true>(m, W, R, lane);
+          lam = chol_aug_factor_solve<D, true>(W->M, A->Lc, A->invdc, nv, V1, lane, acc);
+        } else {
+          solver_hessian<D, true>(m, W, R, lane);
+          lam = chol_factor_solve<D>(W->H, W->H, W->invd, nv, V1, lane);
+        }
+        SYNC();
+        stage(V3, lam);
+        SYNC();
+        for (int r = lane; r < nefc; r += 64) {
+          const bool act = bit(u + 3 * LD + 4, r);
+          const float Jl = rowdot<LD>(R.J + r * LD, V3), Jm = rowdot<LD>(R.J + r * LD, V2), Dr = R.D[r];
+          if (act) Dbar[r] -= Jl * Jm;
+          ca[r] = act ? -Dr * Jm : 0.f;
+          cb[r] = act ? -Dr * Jl : 0.f;
+        }
+        jbar_add(V3, V2);
+      }
+      if (!isd) lam = 0.f;
+      mb_outer(-lam, V2);
+      gb += lam;
+      SYNC();
+    }
+    // grad_k = M q_k - f - J' force_k  (+ the final qfrc_constraint's cotangent at k = K)
+    const float qfcb = -gb + (k == K ? ld(A->qfcb) : 0.f);
+    if (isd) A->frcsb[lane] -= gb;
+    stage(V1, gb);
+    stage(V2, q_k);
+    stage(V3, qfcb);
+    SYNC();
+    qb += isd ? mrow<D>(W, V1, lane) : 0.f;
+    mb_outer(gb, V2);
+    for (int r = lane; r < nefc; r += 64) {
+      const bool act = bit(u + 3 * LD + 4, r);
+      const float jar = rowdot<LD>(R.J + r * LD, V2) - R.aref[r], Dr = R.D[r];
+      const float force = act ? -Dr * jar : 0.f;
+      const float forceb = rowdot<LD>(R.J + r * LD, V3);
+      ca[r] = force;
+      cb[r] = act ? -forceb * Dr : 0.f;  // jar-bar
+      if (act) { Dbar[r] -= forceb * jar; arefb[r] += forceb * Dr; }
+    }
+    jbar_add(V3, V2);
+    SYNC();
+    qb += jt(cb);
+    if (k == 0) break;
+    // line search k-1 and q_k = q_{k-1} + alpha s_{k-1}
+    GLBA const float* l = tp.ls(k - 1);
+    GLBA const float* up = tp.upd(k - 1);
+    const float s = ld(l), qp = ld(up), alpha = l[LD];
+    const int ns = (int)l[LD + 1];
+    const float alphab = wsum(qb * s);
+    sbp += alpha * qb;
+    float q1b = 0.f, q2b = 0.f;
+    if (lane < ns) {
+      const float w = l[LD + 4 + lane], N = l[LD + 4 + 64 + lane], Q2 = l[LD + 4 + 128 + lane];
+      if (w != 0.f) { q1b = alphab * w * (-1.f / Q2); q2b = alphab * w * (-N / Q2); }
+    }
+    const float c1b = wsum(q1b), c2b = wsum(q2b);
+    stage(V1, s);
+    stage(V2, qp);
+    SYNC();
+    for (int r = lane; r < nefc; r += 64) {
+      float ra = 0.f, rb = 0.f;
+      for (int j = 0; j < ns; j++) {
+        const float a = rdlane(q1b, j), b = rdlane(q2b, j);
+        if (bit(l + LD + 4 + 192 + j * 2 * d.NW, r)) { ra += a; rb += b; }
+      }
+      const float jar = rowdot<LD>(R.J + r * LD, V2) - R.aref[r], Jv = rowdot<LD>(R.J + r * LD, V1), Dr = R.D[r];
+      Dbar[r] += ra * Jv * jar + rb * Jv * Jv;
+      ca[r] = ra * Dr * jar + 2.f * rb * Dr * Jv;  // Jv-bar
+      cb[r] = ra * Dr * Jv;                        // jar-bar
+      arefb[r] -= ra * Dr * Jv;
+    }
+    jbar_add(V1, V2);
+    SYNC();
+    const float Ms = isd ? mrow<D>(W, V1, lane) : 0.f, Mq = isd ? mrow<D>(W, V2, lane) : 0.f;
+    const float f = ld(W->frc_smooth);
+    sbp += c1b * (Mq - f) + 2.f * c2b * Ms + jt(ca);
+    qb += c1b * Ms + jt(cb);
+    mb_outer(c1b * s, V2);
+    mb_outer(c2b * s, V1);
+    if (isd) A->frcsb[lane] -= c1b * s;
+    sb = sbp;
+    gb = gbp;
+    mgb = mgbp;
+    SYNC();
+  }
+  if (wsel == 1) {  // q_0 = qacc_smooth = M^-1 f (Newton's Hessians overwrote A->Lc: refactor M)
+    stage(V1, qb);
+    SYNC();
+    float lam;
+    if (cg) lam = chol_solve<D>(A->Lc, A->invdc, qb, lane);
+    else lam = chol_factor_solve<D>(W->M, A->Lc, A->invdc, nv, V1, lane);
+    if (!isd) lam = 0.f;
+    if (isd) A->frcsb[lane] += lam;
+    mb_outer(-lam, W->qacc_smooth);
+  } else if (isd) {  // q_0 = qacc_warmstart: jax.grad carries this cotangent to the previous step
+    A->wsb[lane] = qb;
+  }
+  SYNC();
+  for (int r = lane; r < nefc; r += 64) adj_row_map<D>(m, R, scr, nefc_max, r, arefb[r], Dbar[r], 0.f);
+  SYNC();
+  adj_rows_tail<D>(m, W, A, R, scr, nefc_max, lane);
+}
+
 // ------------------------------------------------------------------- contact Jacobians
 // J rows of contact c from Jp_d = s_d (cdof_lin_d + cdof_ang_d x (pos - scom_root)); lanes 0..31 =
 // dof. Accumulates cdof-bar (lane-owned), scom-bar (per root), and the contact's pos / frame /
 // dist cotangents into the scratch record.
 template <class D> INL void adj_contact_jac(MP m, LDSA WS<D>* W, LDSA WSA<D>* A, Rows<true> R, GLBA float* scr,
-                                            int nefc_max, int lane) {
+                                            int nefc_max, GLBA const float* Jbar, int lane) {
   constexpr int LD = D::LD;
   const int nv = m->nv, ncon = W->ncon;
   GLBA float* alpha = scr;
@@ -400,6 +715,7 @@ template <class D> INL void adj_contact_jac(MP m, LDSA WS<D>* W, LDSA WSA<D>* A,
       for (int q = 0; q < nrow; q++) {
         const int r = r0 + q;
         Jb[q] = alpha[r] * qv + R.force[r] * mu + gamma[r] * qa;
+        if (Jbar) Jb[q] += Jbar[r * D::LD + d];  // unrolled mode: the full J-bar rows
       }
       if (dim == 1) jn = Jb[0];
       else { jn = Jb[0] + Jb[1] + Jb[2] + Jb[3]; jt1 = muf * (Jb[0] - Jb[1]); jt2 = muf * (Jb[2] - Jb[3]); }
@@ -1155,6 +1471,10 @@ struct VjpArgs {
   float* scratch;                                     // per env: row slab, then the adjoint scratch
   int scratch_stride, row_floats;
   float* nonfinite;  // optional: envs whose cotangents came out non-finite get zero outputs, counted here
+  float* unr;        // unrolled mode (MJL_OPT_VJP_UNROLLED): per env tape + row accumulators, else null
+  TapeDims td;
+  const float* g_ws; // optional: cotangent of the output qacc_warmstart (= qacc)
+  float* o_ws;       // optional: cotangent of the input qacc_warmstart (unrolled mode, warm start taken)
 };
 
 // One wave per env: recompute the step from the batch state (not modified), then run the reverse
@@ -1177,6 +1497,7 @@ template <class D, bool ENV> __global__ __launch_bounds__(64, 1) void vjp_kernel
     bool nz = false;
     if (lane < nq) nz |= V.g_qpos[(size_t)env * nq + lane] != 0.f;
     if (lane < nv) nz |= V.g_qvel[(size_t)env * nv + lane] != 0.f;
+    if (V.g_ws && lane < nv) nz |= V.g_ws[(size_t)env * nv + lane] != 0.f;
     if (ENV) {
       if (lane == 0) nz |= V.g_rew[env] != 0.f;
       if (lane < MJL_AUX_DIM) nz |= V.g_aux[(size_t)env * MJL_AUX_DIM + lane] != 0.f;
@@ -1186,6 +1507,7 @@ template <class D, bool ENV> __global__ __launch_bounds__(64, 1) void vjp_kernel
       if (lane < nv) V.o_qvel[(size_t)env * nv + lane] = 0.f;
       if (lane < nu) V.o_ctrl[(size_t)env * nu + lane] = 0.f;
       if (ENV && lane < MJL_AUX_DIM) V.o_aux[(size_t)env * MJL_AUX_DIM + lane] = 0.f;
+      if (V.o_ws && lane < nv) V.o_ws[(size_t)env * nv + lane] = 0.f;
       return;
     }
   }
@@ -1233,11 +1555,24 @@ template <class D, bool ENV> __global__ __launch_bounds__(64, 1) void vjp_kernel
   }
   Rows<true> R = global_rows<D>(scr_env, P.gmax_efc, P.gmax_con);
   build_rows<D, true>(m, W, R, lane);
-  solver<D, true>(m, W, R, lane);
+  const bool unr = V.unr != nullptr;
+  SolveTape tp;
+  tp.t = unr ? (GLBA float*)(V.unr + (size_t)env * V.td.stride) : nullptr;
+  tp.d = V.td;
+  tp.nup = tp.nls = tp.nsets = tp.overflow = 0;
+  if (unr) {
+    solver_t<D, true>(m, W, R, lane, tp);  // the same solve, recording its tape
+    tp.finish(lane);
+    SYNC();
+  } else {
+    solver<D, true>(m, W, R, lane);
+  }
   sensors<D, true>(m, W, R, lane);
-  solver_hessian<D, true>(m, W, R, lane);  // Hc at the converged active set
-  chol_factor_solve<D>(W->H, A->Lc, A->invdc, nv, W->frc_smooth, lane);
-  SYNC();
+  if (!unr) {
+    solver_hessian<D, true>(m, W, R, lane);  // Hc at the converged active set
+    chol_factor_solve<D>(W->H, A->Lc, A->invdc, nv, W->frc_smooth, lane);
+    SYNC();
+  }
   integrate<D>(m, W, lane, A->ap);
   STAMP(1, lane);
   // ---- reverse
@@ -1245,11 +1580,15 @@ template <class D, bool ENV> __global__ __launch_bounds__(64, 1) void vjp_kernel
   if (lane < nv) A->vtmp[lane] = V.g_qvel[(size_t)env * nv + lane];
   SYNC();
   if (ENV) adj_env<D>(m, W, A, (CP)P.env, (const float*)aux, V.g_rew[env], V.g_aux + (size_t)env * MJL_AUX_DIM, lane);
-  adj_integrate<D>(m, W, A, gq, lane);
+  adj_integrate<D>(m, W, A, gq, unr, lane);
+  if (V.g_ws && lane < nv) A->qaccb[lane] += V.g_ws[(size_t)env * nv + lane];  // output warm start = qacc
+  SYNC();
   STAMP(2, lane);
-  adj_solver_rows<D>(m, W, A, R, scr_adj, P.gmax_efc, lane);
+  if (unr) adj_solver_unrolled<D>(m, W, A, R, scr_adj, P.gmax_efc, tp, lane);
+  else adj_solver_rows<D>(m, W, A, R, scr_adj, P.gmax_efc, lane);
   STAMP(3, lane);
-  adj_contact_jac<D>(m, W, A, R, scr_adj, P.gmax_efc, lane);
+  adj_contact_jac<D>(m, W, A, R, scr_adj, P.gmax_efc, unr ? (GLBA const float*)(tp.t + V.td.tape + 4 * P.gmax_efc) : nullptr,
+                     lane);
   STAMP(4, lane);
   adj_collision<D>(m, W, A, R, scr_adj, P.gmax_efc, lane);
   STAMP(5, lane);
@@ -1272,18 +1611,21 @@ template <class D, bool ENV> __global__ __launch_bounds__(64, 1) void vjp_kernel
   // ---- outputs
   if (V.nonfinite) {  // cut an env whose cotangents overflowed from the gradient (APG guard)
     bool bad = (lane < nq && !isfinite(A->qposb[lane])) || (lane < nv && !isfinite(A->qvelb[lane])) ||
-               (lane < nu && !isfinite(A->ctrlb[lane])) || (ENV && lane < MJL_AUX_DIM && !isfinite(A->auxb[lane]));
+               (lane < nu && !isfinite(A->ctrlb[lane])) || (ENV && lane < MJL_AUX_DIM && !isfinite(A->auxb[lane])) ||
+               (lane < nv && !isfinite(A->wsb[lane]));
     if (__ballot(bad) != 0ull) {
       if (lane < nq) V.o_qpos[(size_t)env * nq + lane] = 0.f;
       if (lane < nv) V.o_qvel[(size_t)env * nv + lane] = 0.f;
       if (lane < nu) V.o_ctrl[(size_t)env * nu + lane] = 0.f;
       if (ENV && lane < MJL_AUX_DIM) V.o_aux[(size_t)env * MJL_AUX_DIM + lane] = 0.f;
+      if (V.o_ws && lane < nv) V.o_ws[(size_t)env * nv + lane] = 0.f;
       if (lane == 0) atomicAdd(V.nonfinite, 1.f);
       return;
     }
   }
   if (lane < nq) V.o_qpos[(size_t)env * nq + lane] = A->qposb[lane];
   if (lane < nv) V.o_qvel[(size_t)env * nv + lane] = A->qvelb[lane];
+  if (V.o_ws && lane < nv) V.o_ws[(size_t)env * nv + lane] = A->wsb[lane];
   if (lane < nu) {
     if (ENV) {  // ctrl = clip(flip ? act[perm] * sign : act, -1, 1)
       const mjlEnvConfig* c = P.env;

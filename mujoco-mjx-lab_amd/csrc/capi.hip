@@ -57,6 +57,9 @@ struct mjlBatch {
   float* d_scratch;
   int scratch_stride, gmax_efc, gmax_con;
   float* d_adj_scratch;  // step VJP: per env row slab + adjoint scratch (allocated on first use)
+  int vjp_unrolled;      // MJL_OPT_VJP_UNROLLED
+  float* d_unr;          // unrolled VJP: per env solve tape + row accumulators (allocated on first use)
+  TapeDims unr_dims;
   int adj_stride, adj_row_floats;
   const unsigned long long* ctr_base;  // device RNG counter base (mjl_batch_set_counter_base), or null
   const uint32_t* reset_keys;           // per-env jax.random reset keys (mjl_env_set_reset_keys), or null
@@ -358,6 +361,7 @@ void mjl_batch_destroy(mjlBatch* B) {
   (void)hipSetDevice(B->device);
   (void)hipFree(B->d_state); (void)hipFree(B->d_model); (void)hipFree(B->d_env); (void)hipFree(B->d_scratch);
   (void)hipFree(B->d_adj_scratch);
+  (void)hipFree(B->d_unr);
   delete B;
 }
 
@@ -367,6 +371,12 @@ int mjl_batch_set_option(mjlBatch* B, int option, int value) {
   if (!B) return fail(MJL_ERR_ARG, "null batch");
   if (option == MJL_OPT_STORE_DERIVED) { B->store_derived = value != 0; return MJL_OK; }
   if (option == MJL_OPT_FORCE_GLOBAL_ROWS) { B->force_global_rows = value != 0; return MJL_OK; }
+  if (option == MJL_OPT_VJP_UNROLLED) {
+    if (value && B->model->desc.iterations > 256)
+      return fail(MJL_ERR_ARG, "unrolled VJP: %d solver iterations (at most 256 are taped)", B->model->desc.iterations);
+    B->vjp_unrolled = value != 0;
+    return MJL_OK;
+  }
   return fail(MJL_ERR_ARG, "unknown option %d", option);
 }
 
@@ -589,8 +599,15 @@ template <bool ENV> static int launch_vjp(mjlBatch* B, const VjpArgs& V0, void* 
     hipError_t e = hipMalloc(&B->d_adj_scratch, (size_t)B->adj_stride * B->nenv * sizeof(float));
     if (e != hipSuccess) { B->d_adj_scratch = nullptr; return fail(MJL_ERR_HIP, "adjoint scratch: %s", hipGetErrorString(e)); }
   }
+  if (B->vjp_unrolled && !B->d_unr) {
+    B->unr_dims.init(B->model->nvc == 0 ? DHum::LD : DGen::LD, B->gmax_efc, B->model->desc.iterations);
+    hipError_t e = hipMalloc(&B->d_unr, (size_t)B->unr_dims.stride * B->nenv * sizeof(float));
+    if (e != hipSuccess) { B->d_unr = nullptr; return fail(MJL_ERR_HIP, "unrolled VJP tape: %s", hipGetErrorString(e)); }
+  }
   KParams P = make_params(B);
   VjpArgs V = V0;
+  V.unr = B->vjp_unrolled ? B->d_unr : nullptr;
+  V.td = B->unr_dims;
   V.scratch = B->d_adj_scratch;
   V.scratch_stride = B->adj_stride;
   V.row_floats = B->adj_row_floats;
@@ -631,6 +648,32 @@ int mjl_env_step_vjp_guarded(mjlBatch* B, const float* act, const float* g_qpos,
   std::memset(&V, 0, sizeof(V));
   V.act = act; V.g_qpos = g_qpos; V.g_qvel = g_qvel; V.g_rew = g_rew; V.g_aux = g_aux;
   V.o_qpos = out_qpos; V.o_qvel = out_qvel; V.o_ctrl = out_act; V.o_aux = out_aux;
+  V.nonfinite = nonfinite_count;
+  return launch_vjp<true>(B, V, stream);
+}
+
+int mjl_step_vjp_full(mjlBatch* B, const float* g_qpos, const float* g_qvel, const float* g_qacc_ws,
+                      float* out_qpos, float* out_qvel, float* out_qacc_ws, float* out_ctrl, void* stream) {
+  if (!B || !g_qpos || !g_qvel || !out_qpos || !out_qvel || !out_ctrl) return fail(MJL_ERR_ARG, "bad argument");
+  VjpArgs V;
+  std::memset(&V, 0, sizeof(V));
+  V.g_qpos = g_qpos; V.g_qvel = g_qvel; V.o_qpos = out_qpos; V.o_qvel = out_qvel; V.o_ctrl = out_ctrl;
+  V.g_ws = g_qacc_ws; V.o_ws = out_qacc_ws;
+  return launch_vjp<false>(B, V, stream);
+}
+
+int mjl_env_step_vjp_full(mjlBatch* B, const float* act, const float* g_qpos, const float* g_qvel,
+                          const float* g_qacc_ws, const float* g_rew, const float* g_aux, float* out_qpos,
+                          float* out_qvel, float* out_qacc_ws, float* out_act, float* out_aux,
+                          float* nonfinite_count, void* stream) {
+  if (!B || !act || !g_qpos || !g_qvel || !g_rew || !g_aux || !out_qpos || !out_qvel || !out_act || !out_aux)
+    return fail(MJL_ERR_ARG, "bad argument");
+  if (!B->has_env) return fail(MJL_ERR_ARG, "mjl_env_config not called");
+  VjpArgs V;
+  std::memset(&V, 0, sizeof(V));
+  V.act = act; V.g_qpos = g_qpos; V.g_qvel = g_qvel; V.g_rew = g_rew; V.g_aux = g_aux;
+  V.o_qpos = out_qpos; V.o_qvel = out_qvel; V.o_ctrl = out_act; V.o_aux = out_aux;
+  V.g_ws = g_qacc_ws; V.o_ws = out_qacc_ws;
   V.nonfinite = nonfinite_count;
   return launch_vjp<true>(B, V, stream);
 }

@@ -1444,7 +1444,9 @@ template <class D, bool G> INL void solver_hessian(MP m_, LDSA WS<D>* W, Rows<G>
 // all three points) and moves the ends by MJX's swap rules, until no end moves, an end's |f'| <
 // gtol, or ls_iterations. Returns the lower-cost end if it improves on alpha = 0, else 0.
 // Costs are relative to the Gauss term at alpha = 0 (common to every point, so comparisons hold).
-template <class D, bool G> INL float solver_linesearch(MP m_, LDSA WS<D>* W, Rows<G> R, int lane) {
+// TP: tape hooks (NoTape in the primal kernels; the APG VJP's unrolled mode records every Newton
+// point's parent active set and the accepted alpha's weights over them, adjoint.hip SolveTape).
+template <class D, bool G, class TP> INL float solver_linesearch(MP m_, LDSA WS<D>* W, Rows<G> R, int lane, TP& tp) {
   MP m = uniform_ptr(m_);
   TSTART(tl);
   const int nv = m->nv, nefc = W->nefc;
@@ -1466,6 +1468,7 @@ template <class D, bool G> INL float solver_linesearch(MP m_, LDSA WS<D>* W, Row
   }
   for (int r = lane + 128; r < nefc; r += 64) R.Jv[r] = jrow<D>(R.J, W->search, r);
   SYNC();
+  if constexpr (TP::on) tp.ls_begin(W, lane);
   TACC(28, tl, lane);
   // the step qacc += a s, Ma += a M s, jar += a J s from the registers the search already holds
   auto apply = [&](float alpha) -> float {
@@ -1536,12 +1539,19 @@ template <class D, bool G> INL float solver_linesearch(MP m_, LDSA WS<D>* W, Row
   TACC(29, tl, lane);
   // the Newton point q from p0
   float a1[1] = {-p0d0[0] * __builtin_amdgcn_rcpf(p0d1[0])}, qd0[1], qd1[1];
+  // tape: a point's alpha as weights over the recorded parent sets (lane j = set j); p0's alpha is 0
+  float rec_q = 0.f, rec_lo = 0.f, rec_hi = 0.f;
+  if constexpr (TP::on) rec_q = (lane == tp.add_set(R, nefc, 0.f, p0d1[0], a1[0], ja0, jv0, ja1, jv1, lane)) ? 1.f : 0.f;
   // exact segment: if no row changes activity between 0 and q, f' is linear there and q is its
   // root, the minimiser MJX's iterations then only jitter around in rounding noise
   {
     bool same = ((ja0 < 0.f) == (ja0 + a1[0] * jv0 < 0.f)) && ((ja1 < 0.f) == (ja1 + a1[0] * jv1 < 0.f));
     for (int r = lane + 128; r < nefc; r += 64) same &= (R.jar[r] < 0.f) == (R.jar[r] + a1[0] * R.Jv[r] < 0.f);
-    if (__ballot(!same) == 0ull) { TCOUNT(15, 1, lane); return apply(a1[0]); }
+    if (__ballot(!same) == 0ull) {
+      TCOUNT(15, 1, lane);
+      if constexpr (TP::on) tp.ls_end(a1[0], rec_q, lane);
+      return apply(a1[0]);
+    }
   }
   eval(I1{}, TF{}, a1, qd0, qd1);
   TACC(30, tl, lane);
@@ -1549,6 +1559,7 @@ template <class D, bool G> INL float solver_linesearch(MP m_, LDSA WS<D>* W, Row
   float loa, lod0, lod1, hia, hid0, hid1;
   if (qd0[0] < p0d0[0]) { loa = a1[0]; lod0 = qd0[0]; lod1 = qd1[0]; hia = 0.f; hid0 = p0d0[0]; hid1 = p0d1[0]; }
   else { loa = 0.f; lod0 = p0d0[0]; lod1 = p0d1[0]; hia = a1[0]; hid0 = qd0[0]; hid1 = qd1[0]; }
+  if constexpr (TP::on) { if (qd0[0] < p0d0[0]) rec_lo = rec_q; else rec_hi = rec_q; }
   // MJX's gtol (tolerance * ls_tolerance * |search|) sits below the fp32 resolution of f', where
   // MJX's fp32 iterations only shuffle lo / hi within rounding noise until ls_iterations: an end
   // also counts as converged once |f'| is within kNoise of the magnitude of the terms summed into
@@ -1563,16 +1574,22 @@ template <class D, bool G> INL float solver_linesearch(MP m_, LDSA WS<D>* W, Row
     if ((lod0 < 0.f && lod0 > -lot) || (hid0 > 0.f && hid0 < hit)) break;
     if (fabsf(hia - loa) <= 1e-6f * fmaxf(fabsf(loa), fabsf(hia))) break;
     float al[3] = {loa - lod0 * __builtin_amdgcn_rcpf(lod1), hia - hid0 * __builtin_amdgcn_rcpf(hid1), 0.5f * (loa + hia)};
+    float rc[3] = {0.f, 0.f, 0.f};
+    if constexpr (TP::on) {
+      rc[0] = (lane == tp.add_set(R, nefc, loa, lod1, al[0], ja0, jv0, ja1, jv1, lane)) ? 1.f : 0.f;
+      rc[1] = (lane == tp.add_set(R, nefc, hia, hid1, al[1], ja0, jv0, ja1, jv1, lane)) ? 1.f : 0.f;
+      rc[2] = 0.5f * (rec_lo + rec_hi);
+    }
     float d0[3], d1[3];
     eval(I3{}, TF{}, al, d0, d1);
     bool s1 = lod0 > 0.f || lod0 < d0[0];
-    if (s1) { loa = al[0]; lod0 = d0[0]; lod1 = d1[0]; }
+    if (s1) { loa = al[0]; lod0 = d0[0]; lod1 = d1[0]; if constexpr (TP::on) rec_lo = rc[0]; }
     bool s2 = d0[2] < 0.f && lod0 < d0[2];
-    if (s2) { loa = al[2]; lod0 = d0[2]; lod1 = d1[2]; }
+    if (s2) { loa = al[2]; lod0 = d0[2]; lod1 = d1[2]; if constexpr (TP::on) rec_lo = rc[2]; }
     bool s3 = hid0 < 0.f || hid0 > d0[1];
-    if (s3) { hia = al[1]; hid0 = d0[1]; hid1 = d1[1]; }
+    if (s3) { hia = al[1]; hid0 = d0[1]; hid1 = d1[1]; if constexpr (TP::on) rec_hi = rc[1]; }
     bool s4 = d0[2] > 0.f && hid0 > d0[2];
-    if (s4) { hia = al[2]; hid0 = d0[2]; hid1 = d1[2]; }
+    if (s4) { hia = al[2]; hid0 = d0[2]; hid1 = d1[2]; if constexpr (TP::on) rec_hi = rc[2]; }
     TCOUNT(14, 1, lane);
     if (!(s1 || s2 || s3 || s4)) break;
     lot = tol(loa, lod0, lod1);
@@ -1584,10 +1601,16 @@ template <class D, bool G> INL float solver_linesearch(MP m_, LDSA WS<D>* W, Row
   eval(I3{}, TT{}, ac, cost, nullptr);
   const bool improved = cost[1] < cost[0] || cost[2] < cost[0];
   const float alpha = cost[1] < cost[2] ? loa : hia;
+  if constexpr (TP::on) tp.ls_end(improved ? alpha : 0.f, improved ? (cost[1] < cost[2] ? rec_lo : rec_hi) : 0.f, lane);
   return apply(improved ? alpha : 0.f);
 }
 
-template <class D, bool G> PHASE void solver(MP m_, LDSA WS<D>* W, Rows<G> R, int lane) {
+// tape hooks of the primal kernels: none (every `if constexpr (TP::on)` block compiles away)
+struct NoTape {
+  static constexpr bool on = false;
+};
+
+template <class D, bool G, class TP> PHASE void solver_t(MP m_, LDSA WS<D>* W, Rows<G> R, int lane, TP& tp) {
   MP m = uniform_ptr(m_);
   constexpr int LD = D::LD;
   const int nv = m->nv, nefc = W->nefc;
@@ -1628,6 +1651,7 @@ template <class D, bool G> PHASE void solver(MP m_, LDSA WS<D>* W, Rows<G> R, in
   if (lane < nefc) R.jar[lane] = jq[wsel] - ar;
   for (int r = lane + 64; r < nefc; r += 64) R.jar[r] = jrow<D>(R.J, q0, r) - R.aref[r];
   SYNC();
+  if constexpr (TP::on) tp.warm(wsel, lane);
   TACC(9, ts, lane);
   // Newton / CG iterations, written so that each helper appears once in the loop body.
   // Exact early exit (Newton): rows are affine in alpha, so if the active set at the new point
@@ -1650,7 +1674,7 @@ template <class D, bool G> PHASE void solver(MP m_, LDSA WS<D>* W, Rows<G> R, in
   };
   for (bool first = true;; first = false) {
     if (!first) {
-      float alpha = solver_linesearch<D, G>(m, W, R, lane);
+      float alpha = solver_linesearch<D, G>(m, W, R, lane, tp);
       if (!(alpha != 0.f)) { iter++; break; }  // no improvement: MJX's next cond stops (also on NaN)
       // (the line search applied the step to qacc, Ma and jar)
       if (!newton && lane < nv) { W->gradold[lane] = W->grad[lane]; W->Mgradold[lane] = W->Mgrad[lane]; }
@@ -1659,6 +1683,7 @@ template <class D, bool G> PHASE void solver(MP m_, LDSA WS<D>* W, Rows<G> R, in
     }
     float oldcost = cost;
     cost = solver_update<D, G>(m, W, R, lane);
+    if constexpr (TP::on) tp.update(W, R, lane);
     if (first && maxit != 1) {  // MJX cond before the first body (iterations == 1 runs one body)
       float gp = (lane < nv) ? W->grad[lane] * W->grad[lane] : 0.f;
       if (maxit <= 0 || scale * sqrtf(wsum(gp)) < m->tolerance) break;
@@ -1695,6 +1720,7 @@ template <class D, bool G> PHASE void solver(MP m_, LDSA WS<D>* W, Rows<G> R, in
       if (lane < nv) W->Mgrad[lane] = x;
       SYNC();
       TACC(13, ts, lane);
+      if constexpr (TP::on) tp.direction(x, 0.f, 0.f, 0.f, lane);
       if (lane < LD) W->search[lane] = (lane < nv) ? -x : 0.f;
     } else {
       float x = chol_solve<D>(W->H, W->invd, lane < nv ? W->grad[lane] : 0.f, lane);  // H holds L(M)
@@ -1707,6 +1733,7 @@ template <class D, bool G> PHASE void solver(MP m_, LDSA WS<D>* W, Rows<G> R, in
       num = wsum(num);
       den = wsum(den);
       float beta = first ? 0.f : fmaxf(0.f, num / fmaxf(kMinVal, den));  // PR, MJX's floored denominator
+      if constexpr (TP::on) tp.direction(x, beta, num, den, lane);
       if (lane < LD) W->search[lane] = (lane < nv) ? -x + beta * W->search[lane] : 0.f;
     }
     SYNC();
@@ -1716,6 +1743,10 @@ template <class D, bool G> PHASE void solver(MP m_, LDSA WS<D>* W, Rows<G> R, in
   // qacc), so it belongs to forward: a reset's forward leaves the warm start MJX leaves
   if (lane < nv) W->qacc_ws[lane] = W->qacc[lane];
   SYNC();
+}
+template <class D, bool G> PHASE void solver(MP m_, LDSA WS<D>* W, Rows<G> R, int lane) {
+  NoTape nt;
+  solver_t<D, G>(m_, W, R, lane, nt);
 }
 
 // touch sensors (lane = sensor)   [sensor.sensor_acc, MuJoCo mjSENS_TOUCH]

@@ -24,6 +24,7 @@ EXPORTS = [
     "mjl_step_vjp", "mjl_env_step_vjp", "mjl_gae", "mjl_batch_set_counter_base",
     "mjl_env_set_reset_keys", "mjl_prng_split", "mjl_env_step_vjp_guarded", "mjl_state_size", "mjl_get_state",
     "mjl_set_state", "mjl_obs_normalize", "mjl_policy_head", "mjl_colsum_scratch", "mjl_colsum",
+    "mjl_step_vjp_full", "mjl_env_step_vjp_full",
 ]
 
 _lib = None
@@ -96,6 +97,8 @@ def lib() -> C.CDLL:
     L.mjl_colsum.argtypes = [f32p, i32, i32, f32p, f32p, vp]
     L.mjl_step_vjp.argtypes = [vp, f32p, f32p, f32p, f32p, f32p, vp]
     L.mjl_env_step_vjp.argtypes = [vp, f32p, f32p, f32p, f32p, f32p, f32p, f32p, f32p, f32p, vp]
+    L.mjl_step_vjp_full.argtypes = [vp] + [f32p] * 7 + [vp]
+    L.mjl_env_step_vjp_full.argtypes = [vp] + [f32p] * 12 + [vp]
     _lib = L
     return L
 

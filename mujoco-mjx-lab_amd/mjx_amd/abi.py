@@ -15,6 +15,7 @@ AUX_DIM = 9
 
 OPT_STORE_DERIVED = 0
 OPT_FORCE_GLOBAL_ROWS = 1
+OPT_VJP_UNROLLED = 2  # step VJPs differentiate the solver iterations as executed (jax.grad semantics)
 
 FIELD = {
     "qpos": 0, "qvel": 1, "qacc_warmstart": 2, "time": 3, "ctrl": 4, "qacc": 5, "xpos": 6,

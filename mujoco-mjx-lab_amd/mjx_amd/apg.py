@@ -118,6 +118,8 @@ class APGTrainer:
         gaux = None
         guarded = getattr(env, "guarded_vjp", False)
         nonfinite = torch.zeros(1, device=self.device) if guarded else None
+        # unrolled VJP: the next solve depends on the carried qacc_warmstart, so its cotangent rides along
+        gws = torch.zeros((B, env.nv), device=self.device) if getattr(env, "vjp_carries_ws", False) else None
         gas = [None] * H
         for t in range(H - 1, -1, -1):
             # the VJP recomputes the step to find its converged active set; the solution the forward
@@ -126,7 +128,10 @@ class APGTrainer:
             grew = -discs[t] / B
             # an env whose cotangents overflow (a state blowing up while still in the loss) is cut from
             # the gradient at this step, like the forward guard above (in the kernel when it can)
-            gq, gv, ga, gaux = env.step_vjp(acts[t].detach(), gq, gv, grew, gaux, nonfinite)
+            if gws is not None:
+                gq, gv, gws, ga, gaux = env.step_vjp_full(acts[t].detach(), gq, gv, gws, grew, gaux, nonfinite)
+            else:
+                gq, gv, ga, gaux = env.step_vjp(acts[t].detach(), gq, gv, grew, gaux, nonfinite)
             if not guarded:
                 ok = torch.isfinite(gq).all(1) & torch.isfinite(gv).all(1) & torch.isfinite(ga).all(1)
                 dropped = dropped + (~ok).sum()
@@ -208,11 +213,23 @@ class APGTrainer:
 
 
 class HumanoidAPGEnv:
-    """HumanoidEnv adapter for APGTrainer: tape entries are packed state rows (mjl_get_state)."""
+    """HumanoidEnv adapter for APGTrainer: tape entries are packed state rows (mjl_get_state).
+
+    vjp="unrolled": the VJP differentiates the constraint solve's iterations as executed, what
+    jax.grad through MJX's fixed-count solver computes (train_apg.py:101-105,187-189, CG 4/4); the
+    recompute must replay the forward's solve, so it starts from the tape entry's own warm start.
+    vjp="implicit": the derivative at the converged active set (exact for a converged solve, e.g.
+    the MJCF's Newton 10/20); the recompute is seeded with the forward's solution (~1 iteration)."""
 
     guarded_vjp = True
 
-    def __init__(self, env):
+    def __init__(self, env, vjp: str = "implicit"):
+        from . import abi
+        if vjp not in ("implicit", "unrolled"):
+            raise ValueError(f"vjp must be 'implicit' or 'unrolled', not {vjp!r}")
+        self.vjp = vjp
+        self.vjp_carries_ws = vjp == "unrolled"  # jax.grad also differentiates the carried warm start
+        env.data.set_option(abi.OPT_VJP_UNROLLED, int(vjp == "unrolled"))
         self.env = env
         self.num_envs, self.act_dim = env.num_envs, env.act_dim
         self.nq, self.nv = env.sys.nq, env.sys.nv
@@ -230,8 +247,12 @@ class HumanoidAPGEnv:
         return self.env.get_state()
 
     def set_state(self, st, warm_from=None):
-        """Restore a tape entry; qacc_warmstart from `warm_from` (another entry) when given."""
-        self.env.set_state(st, warm_from)
+        """Restore a tape entry; qacc_warmstart from `warm_from` (another entry) when given and the
+        VJP is implicit (the unrolled VJP replays the forward's own solve)."""
+        self.env.set_state(st, warm_from if self.vjp == "implicit" else None)
 
     def step_vjp(self, act, gq, gv, grew, gaux, nonfinite=None):
         return self.env.step_vjp(act, gq, gv, grew, gaux, nonfinite)
+
+    def step_vjp_full(self, act, gq, gv, gws, grew, gaux, nonfinite=None):
+        return self.env.step_vjp_full(act, gq, gv, gws, grew, gaux, nonfinite)

@@ -118,6 +118,24 @@ class HumanoidEnv:
                                              _ptr(oq), _ptr(ov), _ptr(oa), _ptr(oaux), _ptr(nonfinite), _stream()))
         return oq, ov, oa, oaux
 
+    def step_vjp_full(self, act: torch.Tensor, g_qpos: torch.Tensor, g_qvel: torch.Tensor, g_ws: torch.Tensor,
+                      g_rew: torch.Tensor, g_aux: Optional[torch.Tensor] = None,
+                      nonfinite: Optional[torch.Tensor] = None) -> Tuple[torch.Tensor, ...]:
+        """step_vjp plus the carried warm start (mjl_env_step_vjp_full): g_ws is the cotangent of the
+        output qacc_warmstart; returns (qpos, qvel, qacc_warmstart, action, aux) cotangents. The
+        warm-start cotangent is nonzero only with the unrolled VJP (jax.grad through the Data carry)."""
+        dev, B = self.obs.device, self.num_envs
+        f = lambda x, *shape: x.to(dev, torch.float32).reshape(B, *shape).contiguous()  # noqa: E731
+        act = f(act, self.act_dim)
+        gq, gv, gw, gr = f(g_qpos, self.sys.nq), f(g_qvel, self.sys.nv), f(g_ws, self.sys.nv), f(g_rew)
+        ga = torch.zeros((B, abi.AUX_DIM), device=dev) if g_aux is None else f(g_aux, abi.AUX_DIM)
+        oq, ov, ow = torch.empty_like(gq), torch.empty_like(gv), torch.empty_like(gw)
+        oa, oaux = torch.empty_like(act), torch.empty_like(ga)
+        check(lib().mjl_env_step_vjp_full(self.data.handle, _ptr(act), _ptr(gq), _ptr(gv), _ptr(gw), _ptr(gr),
+                                          _ptr(ga), _ptr(oq), _ptr(ov), _ptr(ow), _ptr(oa), _ptr(oaux),
+                                          _ptr(nonfinite), _stream()))
+        return oq, ov, ow, oa, oaux
+
     @property
     def state_size(self) -> int:
         return int(lib().mjl_state_size(self.data.handle))

@@ -168,3 +168,17 @@ def step_vjp(sys: Model, d: Data, g_qpos: torch.Tensor, g_qvel: torch.Tensor):
     oc = torch.empty((d.nenv, sys.nu), dtype=torch.float32, device=dev)
     check(lib().mjl_step_vjp(d.handle, _ptr(gq), _ptr(gv), _ptr(oq), _ptr(ov), _ptr(oc), _stream()))
     return oq, ov, oc
+
+
+def step_vjp_full(sys: Model, d: Data, g_qpos: torch.Tensor, g_qvel: torch.Tensor, g_qacc_ws: torch.Tensor):
+    """step_vjp with the carried warm start (mjl_step_vjp_full): cotangents of (qpos', qvel',
+    qacc_warmstart') -> (qpos, qvel, qacc_warmstart, ctrl)."""
+    dev = d.device
+    gq = g_qpos.to(dev, torch.float32).reshape(d.nenv, sys.nq).contiguous()
+    gv = g_qvel.to(dev, torch.float32).reshape(d.nenv, sys.nv).contiguous()
+    gw = g_qacc_ws.to(dev, torch.float32).reshape(d.nenv, sys.nv).contiguous()
+    oq, ov, ow = torch.empty_like(gq), torch.empty_like(gv), torch.empty_like(gw)
+    oc = torch.empty((d.nenv, sys.nu), dtype=torch.float32, device=dev)
+    check(lib().mjl_step_vjp_full(d.handle, _ptr(gq), _ptr(gv), _ptr(gw), _ptr(oq), _ptr(ov), _ptr(ow), _ptr(oc),
+                                  _stream()))
+    return oq, ov, ow, oc

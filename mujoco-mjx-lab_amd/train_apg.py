@@ -27,9 +27,9 @@ from mjx_amd.envs import HumanoidEnv, resolve_ids  # noqa: E402
 def apg_model(cfg: APGConfig, name: str = None, solver: str = "cg"):
     """Model with the APG solver options (training_utils.py:95-103, train_apg.py:101-105).
     solver="model" keeps the MJCF's own solver (Newton 10/20 for humanoid_mjx): the reference forces
-    CG 4/4 because JAX differentiates through the Newton iterations (train_apg.py:101); the VJP here
-    differentiates the converged optimality conditions, so Newton is usable, and it avoids the
-    truncated-solve blow-ups."""
+    CG 4/4 because JAX differentiates through the Newton iterations (train_apg.py:101); with the
+    implicit VJP (the converged optimality conditions) Newton is usable, and it avoids the
+    truncated-solve blow-ups (DESIGN.md "Truncated solves")."""
     m = mjx_amd.load_model(name or os.path.splitext(os.path.basename(cfg.xml_path))[0])
     if solver == "model":
         return m
@@ -49,6 +49,9 @@ def main():
     ap.add_argument("--model", default=None, help="humanoid_mjx | humanoid | path to .xml")
     ap.add_argument("--solver", default="cg", choices=["cg", "model"],
                     help="cg = train_apg.py's CG 4/4 override; model = the MJCF's solver")
+    ap.add_argument("--vjp", default=None, choices=["unrolled", "implicit"],
+                    help="solver derivative: unrolled = jax.grad through the iterations (default with --solver cg), "
+                         "implicit = at the converged active set (default with --solver model)")
     ap.add_argument("--results-dir", default=None)
     a = ap.parse_args()
 
@@ -73,7 +76,8 @@ def main():
     env = HumanoidEnv(mjx.put_model(model), resolve_ids(model, EnvConfig()), cfg.batch_size // world,
                       device=local, seed=cfg.seed * 7919 + rank)
     out = os.path.join(cfg.results_dir, time.strftime("%Y%m%d_%H%M%S") + "_apg") if rank == 0 else None
-    tr = APGTrainer(cfg, HumanoidAPGEnv(env), device=f"cuda:{local}", dist=dist, out_dir=out)
+    vjp = a.vjp or ("unrolled" if a.solver == "cg" else "implicit")
+    tr = APGTrainer(cfg, HumanoidAPGEnv(env, vjp), device=f"cuda:{local}", dist=dist, out_dir=out)
     tr.train()
     if dist is not None:
         dist.destroy_process_group()

@@ -79,6 +79,11 @@ template <class R> void env_reset(const mjlModelDesc& m, const mjlEnvConfig& c, 
     R vx = dxy > R(1e-6) ? vmag * dx / dxy : R(0);
     R vy = dxy > R(1e-6) ? vmag * dy / dxy : R(0);
     d.qvel[0] = vx; d.qvel[1] = vy;
+    // single_pipeline_init(qpos, qvel) again: a fresh make_data (qacc_warmstart = 0, src/envs.py:109-113),
+    // not the first forward's solution (it matters once the solve is truncated, e.g. CG 4/4)
+    std::vector<R> q = d.qpos, v = d.qvel;
+    make_data(m, d);
+    d.qpos = q; d.qvel = v;
     forward(m, d);
     bp = &d.xpos[3 * c.pelvis_body_id];
   }

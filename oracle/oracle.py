@@ -73,6 +73,9 @@ def lib():
         L.orc_rollout.argtypes = [P(abi.ModelDesc), P(OrcState), P(f64), C.c_int, C.c_int]
         L.orc_step_jacobian.argtypes = [P(abi.ModelDesc), P(OrcState), P(f64)]
         L.orc_env_step_jacobian.argtypes = [P(abi.ModelDesc), P(abi.EnvConfigC), P(OrcState), P(f64), P(f64), P(f64)]
+        L.orc_step_jacobian_ws.argtypes = [P(abi.ModelDesc), P(OrcState), P(f64)]
+        L.orc_env_step_jacobian_ws.argtypes = [P(abi.ModelDesc), P(abi.EnvConfigC), P(OrcState), P(f64), P(f64),
+                                               P(f64)]
         L.orc_set_diag.argtypes = [C.c_int]
         L.orc_take_cost_log.argtypes = [P(f64), C.c_int]
         L.orc_take_cost_log.restype = C.c_int
@@ -186,6 +189,25 @@ class Oracle:
         act = np.ascontiguousarray(action, np.float64)
         assert self.L.orc_env_step_jacobian(C.byref(self.desc), C.byref(envcfg), C.byref(s), _dp(aux), _dp(act),
                                             _dp(jac)) == 0
+        return jac
+
+    def step_jacobian_ws(self, s: OrcState) -> np.ndarray:
+        """d(qpos', qvel', qacc_warmstart')/d(qpos, qvel, qacc_warmstart, ctrl): the carried warm start
+        as state (what jax.grad through the Data carry differentiates)."""
+        m = self.m
+        jac = np.zeros((m.nq + 2 * m.nv, m.nq + 2 * m.nv + m.nu))
+        assert self.L.orc_step_jacobian_ws(C.byref(self.desc), C.byref(s), _dp(jac)) == 0
+        return jac
+
+    def env_step_jacobian_ws(self, envcfg, s: OrcState, aux: np.ndarray, action: np.ndarray) -> np.ndarray:
+        """d(qpos', qvel', qacc_warmstart', reward, aux')/d(qpos, qvel, qacc_warmstart, action, aux)."""
+        m = self.m
+        rows, cols = m.nq + 2 * m.nv + 1 + abi.AUX_DIM, m.nq + 2 * m.nv + m.nu + abi.AUX_DIM
+        jac = np.zeros((rows, cols))
+        aux = np.ascontiguousarray(aux, np.float64)
+        act = np.ascontiguousarray(action, np.float64)
+        assert self.L.orc_env_step_jacobian_ws(C.byref(self.desc), C.byref(envcfg), C.byref(s), _dp(aux), _dp(act),
+                                               _dp(jac)) == 0
         return jac
 
 

@@ -243,3 +243,62 @@ int orc_env_step_jacobian(const mjlModelDesc* m, const mjlEnvConfig* c, const or
 }
 
 }  // extern "C"
+
+// The same with the carried warm start as one more state block: jax.grad through the Data carry
+// differentiates the next solve's dependence on qacc_warmstart (a truncated solve depends on it).
+namespace {
+constexpr int kNW = 128;
+using Dw = oracle::Dual<kNW>;
+}  // namespace
+
+extern "C" {
+
+// rows (qpos', qvel', qacc_warmstart'), columns (qpos, qvel, qacc_warmstart, ctrl)
+int orc_step_jacobian_ws(const mjlModelDesc* m, const orcState* s, double* jac) {
+  const int nq = m->nq, nv = m->nv, nu = m->nu, ni = nq + 2 * nv + nu;
+  if (ni > kNW) return -1;
+  oracle::Data<Dw> d;
+  load(*m, *s, d);
+  for (int i = 0; i < nq; i++) d.qpos[i].d[i] = 1.0;
+  for (int i = 0; i < nv; i++) { d.qvel[i].d[nq + i] = 1.0; d.qacc_warmstart[i].d[nq + nv + i] = 1.0; }
+  for (int i = 0; i < nu; i++) d.ctrl[i].d[nq + 2 * nv + i] = 1.0;
+  oracle::step(*m, d);
+  int r = 0;
+  for (int i = 0; i < nq; i++, r++)
+    for (int k = 0; k < ni; k++) jac[r * ni + k] = d.qpos[i].d[k];
+  for (int i = 0; i < nv; i++, r++)
+    for (int k = 0; k < ni; k++) jac[r * ni + k] = d.qvel[i].d[k];
+  for (int i = 0; i < nv; i++, r++)
+    for (int k = 0; k < ni; k++) jac[r * ni + k] = d.qacc_warmstart[i].d[k];
+  return 0;
+}
+
+// rows (qpos', qvel', qacc_warmstart', reward, aux'), columns (qpos, qvel, qacc_warmstart, action, aux)
+int orc_env_step_jacobian_ws(const mjlModelDesc* m, const mjlEnvConfig* c, const orcState* s,
+                             const double* aux_in, const double* act, double* jac) {
+  const int nq = m->nq, nv = m->nv, nu = m->nu, ni = nq + 2 * nv + nu + MJL_AUX_DIM;
+  if (ni > kNW) return -1;
+  oracle::Data<Dw> d;
+  load(*m, *s, d);
+  Dw aux[MJL_AUX_DIM], a[MJL_MAXU];
+  for (int i = 0; i < nq; i++) d.qpos[i].d[i] = 1.0;
+  for (int i = 0; i < nv; i++) { d.qvel[i].d[nq + i] = 1.0; d.qacc_warmstart[i].d[nq + nv + i] = 1.0; }
+  for (int i = 0; i < nu; i++) { a[i] = Dw(act[i]); a[i].d[nq + 2 * nv + i] = 1.0; }
+  for (int i = 0; i < MJL_AUX_DIM; i++) { aux[i] = Dw(aux_in[i]); aux[i].d[nq + 2 * nv + nu + i] = 1.0; }
+  oracle::EnvOut<Dw> out;
+  oracle::env_step(*m, *c, d, aux, a, out);
+  int r = 0;
+  for (int i = 0; i < nq; i++, r++)
+    for (int k = 0; k < ni; k++) jac[r * ni + k] = d.qpos[i].d[k];
+  for (int i = 0; i < nv; i++, r++)
+    for (int k = 0; k < ni; k++) jac[r * ni + k] = d.qvel[i].d[k];
+  for (int i = 0; i < nv; i++, r++)
+    for (int k = 0; k < ni; k++) jac[r * ni + k] = d.qacc_warmstart[i].d[k];
+  for (int k = 0; k < ni; k++) jac[r * ni + k] = out.reward.d[k];
+  r++;
+  for (int i = 0; i < MJL_AUX_DIM; i++, r++)
+    for (int k = 0; k < ni; k++) jac[r * ni + k] = aux[i].d[k];
+  return 0;
+}
+
+}  // extern "C"

@@ -4,9 +4,9 @@ the reference-shaped env functions, evaluation and the qpos-history dump.
 * C3: PPOTrainer iterations at src/config.json values with 1024 envs x 256 steps x 4 epochs x
   minibatch 65,536 (train_ppo.py:320-441): finite metrics, metrics.jsonl keys, and the captured
   rollout graph replays the eager rollout bit for bit at that size.
-* C4: one APG update at 2048 envs x 128 steps with train_apg.py's CG 4/4 override: finite loss and
-  gradient (diverging envs leave the loss, DESIGN.md "Truncated solves"); the batched parameter
-  gradient equals the per-step accumulation.
+* C4: one APG update at 2048 envs x 128 steps with train_apg.py's CG 4/4 override and the unrolled
+  VJP (jax.grad semantics): finite loss and gradient (diverging envs leave the loss, DESIGN.md
+  "Truncated solves"); the batched parameter gradient equals the per-step accumulation.
 * A17: evaluate() at 32 envs x 500 deterministic steps with the reference's key chain, against the
   same loop run here step by step, and its first steps against the oracle env.
 """
@@ -115,7 +115,7 @@ def _apg_trainer(B, H, seed=0):
     cfg = APGConfig()
     cfg.batch_size, cfg.horizon, cfg.seed = B, H, seed
     env = HumanoidEnv(mjx.put_model(m), resolve_ids(m, EnvConfig()), B, seed=seed * 7919)
-    return cfg, env, apg.APGTrainer(cfg, apg.HumanoidAPGEnv(env), device="cuda")
+    return cfg, env, apg.APGTrainer(cfg, apg.HumanoidAPGEnv(env, "unrolled"), device="cuda")
 
 
 def test_apg_c4_update_at_full_size_is_finite():

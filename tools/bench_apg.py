@@ -28,12 +28,15 @@ def main():
     ap.add_argument("--horizon", type=int, default=128)
     ap.add_argument("--updates", type=int, default=5)
     ap.add_argument("--solver", default="cg", choices=["cg", "model"], help="cg = train_apg.py override")
+    ap.add_argument("--vjp", default=None, choices=["unrolled", "implicit"],
+                    help="default: unrolled with --solver cg (jax.grad semantics), implicit with --solver model")
     a = ap.parse_args()
+    vjp = a.vjp or ("unrolled" if a.solver == "cg" else "implicit")
     cfg = APGConfig()
     cfg.batch_size, cfg.horizon = a.envs, a.horizon
     m = apg_model(cfg, solver=a.solver)
     env = HumanoidEnv(mjx.put_model(m), resolve_ids(m, EnvConfig()), cfg.batch_size, seed=cfg.seed)
-    tr = APGTrainer(cfg, HumanoidAPGEnv(env), device="cuda")
+    tr = APGTrainer(cfg, HumanoidAPGEnv(env, vjp), device="cuda")
     tr.update(0)  # warm-up
     res = [tr.update(i) for i in range(1, a.updates + 1)]
     sps = sum(r["env_steps_per_sec"] for r in res) / len(res)
@@ -51,7 +54,7 @@ def main():
     upd = cfg.batch_size * cfg.horizon / sps
     print(json.dumps({
         "metric": "APG env-steps/s (rollout + backward through sim + Adam, synced)", "value": sps,
-        "envs": cfg.batch_size, "horizon": cfg.horizon, "solver": a.solver, "update_s": upd,
+        "envs": cfg.batch_size, "horizon": cfg.horizon, "solver": a.solver, "vjp": vjp, "update_s": upd,
         "forward_rollout_s": fwd, "backward_s_est": upd - fwd,
         "returns": [r["return"] for r in res], "grad_norms": [r["grad_norm"] for r in res],
         "nonfinite_envs": [r["nonfinite_envs"] for r in res]}))
