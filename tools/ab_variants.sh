@@ -3,7 +3,7 @@
 set -o pipefail
 mkdir -p gpurun_out
 for f in mujoco-mjx-lab_amd/mjx_amd/variants/*.so; do
-  MJX355_LIB=$PWD/$f timeout -k 10 120 python bench.py --no-extras --cpu-seconds 0.2 --steps 40 > gpurun_out/ab_$(basename $f .so).log 2>&1
+  MJX355_LIB=$PWD/$f timeout -k 10 120 python bench.py --no-extras --no-cpu --steps 40 > gpurun_out/ab_$(basename $f .so).log 2>&1
   rc=$?
   case $rc in 124|137|134|139) echo "$f rc=$rc"; exit $rc;; esac
   python -c "import json,sys; d=json.loads(open('gpurun_out/ab_$(basename $f .so).log').read().strip().splitlines()[-1]); print('$f', round(d['value']), round(d['roofline']['kernel_ms'],4))"

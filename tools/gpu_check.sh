@@ -10,7 +10,7 @@ echo "pytest rc=$rc" >> gpurun_out/pytest_gpu.log
 timeout -k 10 120 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1 &&
 timeout -k 10 300 python bench.py > gpurun_out/bench.log 2>&1 &&
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o bench -- \
-    python bench.py --steps 20 --no-extras --cpu-seconds 1 > gpurun_out/prof.log 2>&1
+    python bench.py --steps 20 --no-extras --no-cpu > gpurun_out/prof.log 2>&1
 rc=$?
 echo "final rc=$rc"
 exit $rc

@@ -6,7 +6,7 @@
 set -o pipefail
 mkdir -p gpurun_out/prof
 export TMPDIR=/tmp
-B="python bench.py --no-extras --cpu-seconds 1 --steps 50"
+B="python bench.py --no-extras --no-cpu --steps 50"
 timeout -k 10 400 python bench.py > gpurun_out/prof/bench.json 2> gpurun_out/prof/bench.err &&
 timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof/trace -o trace -- \
     $B > gpurun_out/prof/trace.log 2>&1 &&
