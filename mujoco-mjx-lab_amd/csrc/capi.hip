@@ -536,10 +536,21 @@ int mjl_env_config(mjlBatch* B, const mjlEnvConfig* cfg) {
       cfg->touch_sensor_left_id < 0 || cfg->touch_sensor_left_id >= d.nsensordata)
     return fail(MJL_ERR_ARG, "touch sensor id out of range");
   if (d.nbody < 2 || d.jnt_type[0] != MJL_JNT_FREE) return fail(MJL_ERR_UNSUPPORTED, "env needs a free-floating root");
-  for (int i = 0; i < d.nu; i++)
+  // the flip tables must be permutations: the action VJP writes each source's cotangent once
+  // (adjoint.hip, o_ctrl[act_perm[lane]]), which covers every entry only for a bijection
+  unsigned long long seen = 0;
+  for (int i = 0; i < d.nu; i++) {
     if (cfg->act_perm[i] < 0 || cfg->act_perm[i] >= d.nu) return fail(MJL_ERR_ARG, "act_perm out of range");
-  for (int i = 0; i < cfg->obs_dim; i++)
+    seen |= 1ull << cfg->act_perm[i];
+  }
+  if (seen != (d.nu == 64 ? ~0ull : (1ull << d.nu) - 1)) return fail(MJL_ERR_ARG, "act_perm is not a permutation");
+  seen = 0;
+  for (int i = 0; i < cfg->obs_dim; i++) {
     if (cfg->obs_perm[i] < 0 || cfg->obs_perm[i] >= cfg->obs_dim) return fail(MJL_ERR_ARG, "obs_perm out of range");
+    seen |= 1ull << cfg->obs_perm[i];
+  }
+  if (seen != (cfg->obs_dim == 64 ? ~0ull : (1ull << cfg->obs_dim) - 1))
+    return fail(MJL_ERR_ARG, "obs_perm is not a permutation");
   HIPCHK(hipSetDevice(B->device));
   HIPCHK(hipMemcpy(B->d_env, cfg, sizeof(mjlEnvConfig), hipMemcpyHostToDevice));
   B->has_env = 1;

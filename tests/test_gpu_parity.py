@@ -374,3 +374,19 @@ def test_contact_equilibrium_kat_on_gpu(solref, solimp):
     k = 1.0 / (solimp[1] ** 2 * solref[0] ** 2 * solref[1] ** 2)
     want = _root(lambda p: p * k * _mj_impedance(solimp, p) ** 2 + 9.81 * (1.0 - _mj_impedance(solimp, p)), -0.05, 0.0)
     np.testing.assert_allclose(pen, want, rtol=2e-3)
+
+
+def test_env_config_rejects_non_permutation_flip_tables():
+    """mjl_env_config refuses flip tables that are not permutations (the action VJP writes each
+    source entry once, which covers the output only for a bijection)."""
+    import ctypes as C
+    from mjx_amd._lib import MjlError, check, lib
+    m, env, cfg_c = _env(4)
+    check(lib().mjl_env_config(env.data.handle, C.byref(cfg_c)))
+    cfg_c.act_perm[1] = cfg_c.act_perm[0]
+    with pytest.raises(MjlError, match="act_perm is not a permutation"):
+        check(lib().mjl_env_config(env.data.handle, C.byref(cfg_c)))
+    m, env, cfg_c = _env(4)
+    cfg_c.obs_perm[5] = cfg_c.obs_perm[6]
+    with pytest.raises(MjlError, match="obs_perm is not a permutation"):
+        check(lib().mjl_env_config(env.data.handle, C.byref(cfg_c)))

@@ -35,6 +35,56 @@ def test_pair_counts():
     assert sum(mjcf.COL_NCON[k] for k in m1.pair_kind) == 116
 
 
+@pytest.mark.skipif(not os.path.isdir(REF_MODELS), reason="reference models not mounted")
+def test_humanoid_xml_pair_filter_by_mujoco_rules():
+    """humanoid.xml's 159 candidate pairs, derived here from the XML's body tree (xml.etree, not the
+    compiler) by MuJoCo's documented filter (Modeling > Contact > Selection): of C(20,2) = 190 geom
+    pairs drop (1) pairs inside one weld body (a body without joints is welded to its parent: head
+    to torso, hands to lower arms) — 3 same-body + 4 same-weld; (2) parent-child weld bodies
+    ("filterparent": weld(b1) == weld(parent(weld(b2))) or vice versa) — 17 direct parent-child +
+    the 5 below that only the weld makes parent-child; (3) the two <exclude> pairs; contype/
+    conaffinity are the defaults (1/1) and keep everything else: 190 - 7 - 22 - 2 = 159. SURVEY.md
+    §8's 164 omitted the 5 weld-parent pairs."""
+    import xml.etree.ElementTree as ET
+    root = ET.parse(os.path.join(REF_MODELS, "humanoid.xml")).getroot()
+    parent, has_joint, geoms = {"world": None}, {"world": False}, []
+
+    def walk(el, body):
+        for ch in el:
+            if ch.tag == "body":
+                name = ch.get("name")
+                parent[name] = body
+                has_joint[name] = any(c.tag in ("joint", "freejoint") for c in ch)
+                walk(ch, name)
+            elif ch.tag == "geom":
+                geoms.append((ch.get("name"), body))
+    walk(root.find("worldbody"), "world")
+    weld = lambda b: b if b == "world" or has_joint[b] else weld(parent[b])  # noqa: E731
+    excl = {frozenset((e.get("body1"), e.get("body2"))) for e in root.find("contact") if e.tag == "exclude"}
+    assert len(geoms) == 20 and len(excl) == 2
+    kept, weld_parent = set(), set()
+    for i in range(20):
+        for j in range(i + 1, 20):
+            (g1, b1), (g2, b2) = geoms[i], geoms[j]
+            w1, w2 = weld(b1), weld(b2)
+            if w1 == w2:
+                continue
+            if w1 != "world" and w2 != "world" and (w1 == weld(parent[w2]) or w2 == weld(parent[w1])):
+                if parent[b1] != b2 and parent[b2] != b1:
+                    weld_parent.add(frozenset((b1, b2)))
+                continue
+            if frozenset((b1, b2)) in excl:
+                continue
+            kept.add(frozenset((g1, g2)))
+    assert weld_parent == {frozenset(p) for p in (("head", "waist_lower"), ("head", "upper_arm_right"),
+                                                  ("head", "upper_arm_left"), ("upper_arm_right", "hand_right"),
+                                                  ("upper_arm_left", "hand_left"))}
+    assert len(kept) == 159
+    m = mjx_amd.load_model("humanoid")
+    gn = m.names["geom"]
+    assert {frozenset((gn[a], gn[b])) for a, b in zip(m.pair_geom1, m.pair_geom2)} == kept
+
+
 def _capsule(r, h, rho=1000.0):
     mc = rho * math.pi * r * r * h
     ms = rho * 4.0 / 3.0 * math.pi * r ** 3
