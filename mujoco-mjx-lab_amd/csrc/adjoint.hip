@@ -1545,9 +1545,12 @@ template <class D, bool ENV> __global__ __launch_bounds__(64, 1) void vjp_kernel
   SYNC();
   // ---- forward (forward() + integrate(), rows in the env's global slab)
   STAMP(0, lane);
-  kinematics<D>(m, W, lane);
-  com_pos_crb<D>(m, W, lane);
-  velocity_stage<D>(m, W, lane);
+  {
+    const KinPre kp = kin_prefetch(m, lane);
+    kinematics<D>(m, W, lane, kp);
+    com_pos_crb<D>(m, W, lane, kp);
+    velocity_stage<D>(m, W, lane, kp);
+  }
   {
     const float x = chol_factor_solve<D>(W->M, W->H, W->invd, nv, W->frc_smooth, lane);
     if (lane < LD) W->qacc_smooth[lane] = (lane < nv) ? x : 0.f;

@@ -251,6 +251,22 @@ int mjl_model_create(const mjlModelDesc* d, mjlModel** out) {
     for (int i = 0; i < 3; i++) { r.pos[i] = f.body_pos[b][i]; r.ipos[i] = f.body_ipos[b][i]; }
     for (int i = 0; i < 4; i++) r.quat[i] = f.body_quat[b][i];
     r.mass = f.body_mass[b];
+    for (int i = 0; i < 6; i++) r.inertia[i] = f.body_inertia[b][i];
+    for (int k = 0; k < 3 && k < d->body_jntnum[b]; k++) {
+      const int j = d->body_jntadr[b] + k;
+      for (int i = 0; i < 3; i++) { f.bhinge[b][k].pos[i] = f.jnt_pos[j][i]; f.bhinge[b][k].axis[i] = f.jnt_axis[j][i]; }
+    }
+  }
+  for (int g = 0; g < d->ngeom; g++) {
+    FrameRec& r = f.frec[g];
+    r.body = f.geom_bodyid[g];
+    for (int i = 0; i < 3; i++) { r.pos[i] = f.geom_pos[g][i]; r.mat[i] = f.geom_zaxis[g][i]; }
+  }
+  for (int st = 0; st < d->nsite; st++) {
+    FrameRec& r = f.frec[32 + st];
+    r.body = f.site_bodyid[st];
+    for (int i = 0; i < 3; i++) r.pos[i] = f.site_pos[st][i];
+    for (int i = 0; i < 9; i++) r.mat[i] = f.site_mat[st][i];
   }
   for (int j = 0; j < d->njnt; j++) {
     JntRec& r = f.jrec[j];
@@ -282,6 +298,23 @@ int mjl_model_create(const mjlModelDesc* d, mjlModel** out) {
     r.includemargin = f.pair_includemargin[p]; r.mu = f.pair_mu[p]; r.invweight = f.pair_invweight[p];
     r.b1 = d->geom_bodyid[r.g1]; r.b2 = d->geom_bodyid[r.g2];
     r.mask1 = f.body_dofmask[r.b1]; r.mask2 = f.body_dofmask[r.b2];
+  }
+  for (int j = 0; j < d->njnt; j++) {
+    LimRec& r = f.jlim[j];
+    r.on = f.jnt_limited[j] && f.jnt_type[j] == MJL_JNT_HINGE;
+    r.qadr = f.jnt_qposadr[j]; r.dofadr = f.jnt_dofadr[j];
+    r.lo = f.jnt_range[j][0]; r.hi = f.jnt_range[j][1]; r.margin = f.jnt_margin[j];
+    r.invweight = f.dof_invweight0[r.dofadr];
+    for (int i = 0; i < 2; i++) r.solref[i] = f.jnt_solref[j][i];
+    for (int i = 0; i < 5; i++) r.solimp[i] = f.jnt_solimp[j][i];
+  }
+  for (int t = 0; t < d->ntendon; t++) {
+    LimRec& r = f.tlim[t];
+    r.on = f.tendon_limited[t];
+    r.lo = f.tendon_range[t][0]; r.hi = f.tendon_range[t][1]; r.margin = f.tendon_margin[t];
+    r.invweight = f.tendon_invweight0[t];
+    for (int i = 0; i < 2; i++) r.solref[i] = f.tendon_solref[t][i];
+    for (int i = 0; i < 5; i++) r.solimp[i] = f.tendon_solimp[t][i];
   }
   M->nefc_max = nefc_max;
   M->ncon_max = ncon_max;

@@ -17,6 +17,20 @@ struct alignas(16) BodyRec {
   float pos[3], mass;
   float quat[4];
   float ipos[3], pad2;
+  float inertia[6], pad3[2];  // body_inertia (local principal frame: xx yy zz xy xz yz)
+};
+// the first three hinges of a body (kinematics' local transform), by body: one load with the body's
+// own record instead of a second load through jntadr
+struct alignas(16) HingeRec {
+  float pos[3], pad0;
+  float axis[3], pad1;
+};
+// geom (index < 32) / site (index 32 + s) frame constants, by lane: body, local pos, local z axis
+// (geoms, mat[0..2]) or local rotation (sites)
+struct alignas(16) FrameRec {
+  int body, pad0, pad1, pad2;
+  float pos[3], pad3;
+  float mat[9], pad4[3];
 };
 struct alignas(16) JntRec {  // hinge joints (local frame of the body)
   float pos[3], qpos0;
@@ -37,6 +51,13 @@ struct alignas(16) PairRec {
   float includemargin, mu, invweight, pad;
   uint32_t mask1, mask2;  // body_dofmask of both bodies
   int b1, b2;
+};
+// a limit-row candidate: lane = joint (limited hinge) or lane = tendon (limited tendon); everything
+// the row needs, including its impedance parameters, in one record
+struct alignas(16) LimRec {
+  int on, qadr, dofadr, pad;  // on: the joint / tendon is a limit-row candidate
+  float lo, hi, margin, invweight;
+  float solref[2], solimp[5], pad1;
 };
 
 struct ModelF {
@@ -86,6 +107,9 @@ struct ModelF {
   JntRec jrec[MJL_MAXJNT];
   DofRec drec[MJL_MAXV];
   PairRec prec[MJL_MAXPAIR];
+  LimRec jlim[MJL_MAXJNT], tlim[MJL_MAXTENDON];
+  HingeRec bhinge[MJL_MAXBODY][3];
+  FrameRec frec[64];
 };
 
 enum Mode { MODE_FORWARD = 0, MODE_STEP = 1, MODE_SPEEDTEST = 2, MODE_ENV_STEP = 3, MODE_ENV_RESET = 4 };

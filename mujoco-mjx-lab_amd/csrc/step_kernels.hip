@@ -349,12 +349,23 @@ template <int LD, int NV, int P0, int P1> INL void chol_panel(float (&a)[LD], in
     // the column's broadcasts read the unscaled a_jk (they do not wait for the pivot's rsq) and
     // each lane's multiplier is L_ik / L_kk instead; fminf after v_rsq is the 1e-30 pivot floor
     // (rsq(1e-30)) off the readlane -> rsq chain (an fmaxf before it needs a canonicalising v_max)
-    const float inv = fminf(__builtin_amdgcn_rsqf(rdlane(a[k], k)), 1e15f);
+    const float piv = rdlane(a[k], k);
+    const float inv = fminf(__builtin_amdgcn_rsqf(piv), 1e15f);
+#ifdef MJL_CHOL_RCP
+    // the multiplier L_ik / L_kk = a_ik / pivot from v_rcp beside the v_rsq: one multiply on the
+    // column-to-column chain instead of two (a_ik * inv * inv)
+    const float rp = fminf(__builtin_amdgcn_rcpf(piv), 1e30f);
+#endif
     float s[P1];
 #pragma unroll
     for (int j = k + 1; j < P1; j++) s[j] = rdlane(a[k], j);
+#ifdef MJL_CHOL_RCP
+    const float t = a[k] * rp;
+    a[k] *= inv;  // lane k: sqrt of its pivot
+#else
     a[k] *= inv;  // lane k: sqrt of its pivot
     const float t = a[k] * inv;
+#endif
 #pragma unroll
     for (int j = k + 1; j < P1; j++) a[j] = fmaf(-t, s[j], a[j]);
   }
@@ -454,12 +465,17 @@ template <class D, bool ADD> INL float chol_aug_factor_solve(const LDSA float* s
       wp[q] = v;
     }
   }
-  SYNC();
-  const float y = (i < NV) ? invd_out[i] : 0.f;
-  const float invd = (i < NV) ? __builtin_amdgcn_rcpf(dst[i * LD + i]) : 1.f;
+  // No wait for the stores: one wave's LDS requests complete in order, so the column reads below
+  // see them (the compiler keeps the reads after the stores to the same arrays). All reads are
+  // unconditional (lanes >= NV read column 0 and mask it) and issue together, the back
+  // substitution's first columns (k = NV - 1 ...) first.
+  const int ic = (i < NV) ? i : 0;
+  const float dg = dst[ic * LD + ic], yv = invd_out[ic];
   float w[NV];
 #pragma unroll
-  for (int k = 0; k < NV; k++) w[k] = dst[k * LD + i];
+  for (int k = NV - 1; k >= 0; k--) w[k] = dst[k * LD + ic];
+  const float y = (i < NV) ? yv : 0.f;
+  const float invd = (i < NV) ? __builtin_amdgcn_rcpf(dg) : 1.f;
   if (lane < NV) invd_out[lane] = invd;  // after the y read (same wave: LDS requests complete in order)
   TACC(34, tch, lane);
   const int io = opaque_int(i);
@@ -588,22 +604,43 @@ template <class D> INL float chol_solve(const LDSA float* L, const LDSA float* i
 // ---------------------------------------------------------------------------------------------
 // position stage: kinematics, tendons, geom/site frames, subtree com   [smooth.kinematics]
 // ---------------------------------------------------------------------------------------------
-template <class D> PHASE void kinematics(MP m_, LDSA WS<D>* W, int lane) {
+// The smooth phases' per-lane model records, issued together before the first of them waits (the
+// kernel issues them before its state loads, so both latencies overlap): this lane's body, joint,
+// the body's first three hinges, its geom / site frame constants and its dof (lane & 31).
+struct KinPre {
+  BodyRec br;       // brec[lane < nbody ? lane : 0]: kinematics, com_pos_crb, velocity_stage
+  JntRec jown;      // jrec[lane < njnt ? lane : 0]
+  HingeRec bh[3];   // the body's first three hinges
+  FrameRec fr;      // geom lane (< 32) or site lane (32 + s)
+  DofRec dr;        // drec[(lane & 31) < nv ? lane & 31 : 0]: com_pos_crb (cdof, M column), velocity_stage
+};
+INL KinPre kin_prefetch(MP m_, int lane) {
+  MP m = uniform_ptr(m_);
+  KinPre k;
+  const int b = lane < m->nbody ? lane : 0;
+  k.br = ldrec(&m->brec[b]);
+  k.jown = ldrec(&m->jrec[lane < m->njnt ? lane : 0]);
+#pragma unroll
+  for (int i = 0; i < 3; i++) k.bh[i] = ldrec(&m->bhinge[b][i]);
+  k.fr = ldrec(&m->frec[lane]);
+  k.dr = ldrec(&m->drec[(lane & 31) < m->nv ? (lane & 31) : 0]);
+  return k;
+}
+
+template <class D> PHASE void kinematics(MP m_, LDSA WS<D>* W, int lane, const KinPre& kp) {
   MP m = uniform_ptr(m_);
   const int maxlevel = m->maxlevel, nbody = m->nbody, ngeom = m->ngeom, nsite = m->nsite, njnt = m->njnt;
   TSTART(tk);
-  // model records of this lane, loaded once: body `lane`, geom `lane`, site `lane - 32`, joint `lane`
+  // model records of this lane (kin_prefetch): body `lane`, geom `lane`, site `lane - 32`, joint `lane`
   const bool isb = lane > 0 && lane < nbody;
-  BodyRec br = ldrec(&m->brec[isb ? lane : 0]);
+  const BodyRec& br = kp.br;
   const bool isg = lane < ngeom, iss = lane >= 32 && lane - 32 < nsite, isj = lane < njnt;
-  const int gb = isg ? m->geom_bodyid[lane] : 0, sb = iss ? m->site_bodyid[lane - 32] : 0;
-  float gp[3] = {0.f, 0.f, 0.f}, gz[3] = {0.f, 0.f, 0.f}, sp[3] = {0.f, 0.f, 0.f}, sm[9];
-  if (isg) for (int i = 0; i < 3; i++) { gp[i] = m->geom_pos[lane][i]; gz[i] = m->geom_zaxis[lane][i]; }
-  if (iss) {
-    for (int i = 0; i < 3; i++) sp[i] = m->site_pos[lane - 32][i];
-    for (int i = 0; i < 9; i++) sm[i] = m->site_mat[lane - 32][i];
-  }
-  const JntRec jown = ldrec(&m->jrec[isj ? lane : 0]);
+  const int gb = isg ? kp.fr.body : 0, sb = iss ? kp.fr.body : 0;
+  const float* gp = kp.fr.pos;
+  const float* gz = kp.fr.mat;
+  const float* sp = kp.fr.pos;
+  const float* sm = kp.fr.mat;
+  const JntRec& jown = kp.jown;
   const int jpar = jown.parent, jfree = isj ? jown.isfree : 1;
   TACC(16, tk, lane);
   if (lane == 0) {
@@ -629,14 +666,12 @@ template <class D> PHASE void kinematics(MP m_, LDSA WS<D>* W, int lane) {
     sincosf(0.5f * (W->qpos[jown.qadr] - jown.qpos0), &s, &c);
     jq[0] = c; jq[1] = jown.axis[0] * s; jq[2] = jown.axis[1] * s; jq[3] = jown.axis[2] * s;
   }
-  // a body's first three joints: records loaded together up front, rotations from the joint lanes
+  // a body's first three joints: hinge records from kin_prefetch, rotations from the joint lanes
   constexpr int KJ = 3;
-  JntRec jr3[KJ];
   float ql3[KJ][4];
 #pragma unroll
   for (int k = 0; k < KJ; k++) {
     const int j = (isb && k < br.jntnum) ? br.jntadr + k : 0;
-    jr3[k] = ldrec(&m->jrec[j]);
 #pragma unroll
     for (int e = 0; e < 4; e++) ql3[k][e] = __shfl(jq[e], j);
   }
@@ -656,7 +691,7 @@ template <class D> PHASE void kinematics(MP m_, LDSA WS<D>* W, int lane) {
       for (int k = 0; k < KJ; k++) {
         if (k >= br.jntnum) break;
         const int j = br.jntadr + k;
-        const JntRec& jr = jr3[k];
+        const HingeRec& jr = kp.bh[k];
         float mat[9], anc[3], ax[3];
         q2m(mat, lq);
         mv3(anc, mat, jr.pos);
@@ -807,16 +842,15 @@ template <int NC, class Src, class Dst> INL void subtree_sums16(Src in, Dst out,
 }
 
 // cinert (lane = body) and cdof (lane 32 + dof); crb (lane = body); M columns (lane = dof)
-template <class D> PHASE void com_pos_crb(MP m_, LDSA WS<D>* W, int lane) {
+template <class D> PHASE void com_pos_crb(MP m_, LDSA WS<D>* W, int lane, const KinPre& kp) {
   MP m = uniform_ptr(m_);
   constexpr int LD = D::LD;
   const int nbody = m->nbody, nv = m->nv;
   const bool isb = lane < nbody, iscd = lane >= 32 && lane - 32 < nv;
-  const BodyRec br = ldrec(&m->brec[isb ? lane : 0]);
-  const DofRec dcd = ldrec(&m->drec[iscd ? lane - 32 : 0]), dcol = ldrec(&m->drec[(lane & 31) < nv ? (lane & 31) : 0]);
+  const BodyRec& br = kp.br;
+  const DofRec &dcd = kp.dr, &dcol = kp.dr;  // lanes 32 + d (cdof of dof d) and lane & 31 (M column)
   TSTART(tc);
-  float t[6];
-  for (int i = 0; i < 6; i++) t[i] = isb ? m->body_inertia[lane][i] : 0.f;
+  const float* t = br.inertia;
   if (isb) {
     const int b = lane;
     LDSA float* ci = W->cinert[b];
@@ -913,12 +947,12 @@ template <class D> PHASE void com_pos_crb(MP m_, LDSA WS<D>* W, int lane) {
 // velocity stage: com_vel + rne forward pass by levels, backward by subtree ranges; passive
 // forces and actuation   [smooth.com_vel / smooth.rne / passive.passive / forward.fwd_actuation]
 // ---------------------------------------------------------------------------------------------
-template <class D> PHASE void velocity_stage(MP m_, LDSA WS<D>* W, int lane) {
+template <class D> PHASE void velocity_stage(MP m_, LDSA WS<D>* W, int lane, const KinPre& kp) {
   MP m = uniform_ptr(m_);
   const int maxlevel = m->maxlevel, nbody = m->nbody, nv = m->nv, nu = m->nu;
   const bool isb = lane > 0 && lane < nbody, isd = lane < nv, isu = lane < nu;
-  const BodyRec br = ldrec(&m->brec[isb ? lane : 0]);
-  const DofRec dr = ldrec(&m->drec[isd ? lane : 0]);
+  const BodyRec& br = kp.br;
+  const DofRec& dr = kp.dr;
   int udof = 0, ulim = 0;
   TSTART(tv);
   float ugear = 0.f, ulo = 0.f, uhi = 0.f;
@@ -1013,6 +1047,14 @@ template <class D> PHASE void velocity_stage(MP m_, LDSA WS<D>* W, int lane) {
   SYNC();
   if (isd) W->frc_smooth[lane] = W->frc_passive[lane] - W->frc_bias[lane] + W->frc_act[lane];
   SYNC();
+}
+
+// row . v over LD entries as four interleaved partial sums (four 7-long FMA chains, not one 28-long)
+template <int LD, class RowF, class VF> INL float rowdot(RowF* a, VF* v) {
+  float s[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int k = 0; k < LD; k++) s[k & 3] = fmaf(a[k], v[k], s[k & 3]);
+  return (s[0] + s[1]) + (s[2] + s[3]);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -1126,8 +1168,7 @@ template <class D> INL bool collide(const PairRec& pr, LDSA WS<D>* W, int k, flo
 // ---------------------------------------------------------------------------------------------
 // constraint rows: limits, contacts; then per-row D / aref   [constraint.make_constraint]
 // ---------------------------------------------------------------------------------------------
-INL void kbi(float tstep, const CSTA float* solref, const CSTA float* solimp, float pos, float& k, float& b,
-             float& imp) {
+template <class P> INL void kbi(float tstep, P solref, P solimp, float pos, float& k, float& b, float& imp) {
   float timeconst = fmaxf(solref[0], 2.f * tstep), dampratio = solref[1];
   float dmin = fminf(fmaxf(solimp[0], kMinImp), kMaxImp);
   float dmax = fminf(fmaxf(solimp[1], kMinImp), kMaxImp);
@@ -1160,87 +1201,165 @@ template <class D, bool G> PHASE bool build_rows(MP m_, LDSA WS<D>* W, Rows<G> R
   const int nv = m->nv, cap = R.cap, capc = R.capc;
   int nl = 0;
   TSTART(tr);
-  PairRec pr_next = ldrec(&m->prec[lane < m->npair ? lane : 0]);  // in flight during the limit rows
+  // every model record of the pass issues here, before the first wait: the first trip's pair
+  // records (the next trip's load while a trip collides) and the limit records
+  PairRec pr_next = ldrec(&m->prec[lane < m->npair ? lane : 0]);
+  const LimRec jl = ldrec(&m->jlim[lane < m->njnt ? lane : 0]);
+  const LimRec tl = ldrec(&m->tlim[lane < m->ntendon ? lane : 0]);
+  const float tstep = m->timestep;
+  // A limit row's impedance is known at creation (its pos and parameters are in the creating lane's
+  // registers): D is written there, and k imp / b wait in aref / Jv for the row loop below, which
+  // forms aref once J is built (the same expression as before, so the same rounding).
+  auto row_imp = [&](int r, float pos, float invw, const float* sr, const float* si) {
+    float k, b, imp;
+    kbi(tstep, sr, si, pos, k, b, imp);
+    R.D[r] = 1.f / fmaxf(invw * (1.f - imp) / imp, kMinVal);
+    R.aref[r] = k * imp;
+    R.Jv[r] = b;
+  };
   {  // joint limits (lane = joint), then tendon limits (lane = tendon), ballot-compacted
     bool act = false;
     float dist = 0.f, sgn = 0.f;
-    if (lane < m->njnt && m->jnt_limited[lane] && m->jnt_type[lane] == MJL_JNT_HINGE) {
-      float q = W->qpos[m->jnt_qposadr[lane]];
-      float dmin = q - m->jnt_range[lane][0], dmax = m->jnt_range[lane][1] - q;
+    if (lane < m->njnt && jl.on) {
+      float q = W->qpos[jl.qadr];
+      float dmin = q - jl.lo, dmax = jl.hi - q;
       dist = fminf(dmin, dmax);
       sgn = dmin < dmax ? 1.f : -1.f;
-      act = dist - m->jnt_margin[lane] < 0.f;
+      act = dist - jl.margin < 0.f;
     }
     unsigned long long bal = __ballot(act);
     int r = __popcll(bal & lanes_below(lane));
     if (act && r < cap) {
       RF* Jr = R.J + r * LD;
       for (int k = 0; k < LD; k++) Jr[k] = 0.f;
-      Jr[m->jnt_dofadr[lane]] = sgn;
-      R.epos[r] = dist - m->jnt_margin[lane];
-      R.einvw[r] = m->dof_invweight0[m->jnt_dofadr[lane]];
+      Jr[jl.dofadr] = sgn;
+      R.epos[r] = dist - jl.margin;
+      R.einvw[r] = jl.invweight;
       R.emeta[r] = (0 << 16) | lane;
+      row_imp(r, dist - jl.margin, jl.invweight, jl.solref, jl.solimp);
     }
     nl = __popcll(bal);
     act = false;
-    if (lane < m->ntendon && m->tendon_limited[lane]) {
+    if (lane < m->ntendon && tl.on) {
       float len = W->tenlen[lane];
-      float dmin = len - m->tendon_range[lane][0], dmax = m->tendon_range[lane][1] - len;
+      float dmin = len - tl.lo, dmax = tl.hi - len;
       dist = fminf(dmin, dmax);
       sgn = dmin < dmax ? 1.f : -1.f;
-      act = dist - m->tendon_margin[lane] < 0.f;
+      act = dist - tl.margin < 0.f;
     }
     bal = __ballot(act);
     r = nl + __popcll(bal & lanes_below(lane));
     if (act && r < cap) {
       RF* Jr = R.J + r * LD;
       for (int k = 0; k < LD; k++) Jr[k] = (k < nv) ? sgn * W->tenJ[lane][k] : 0.f;
-      R.epos[r] = dist - m->tendon_margin[lane];
-      R.einvw[r] = m->tendon_invweight0[lane];
+      R.epos[r] = dist - tl.margin;
+      R.einvw[r] = tl.invweight;
       R.emeta[r] = (1 << 16) | lane;
+      row_imp(r, dist - tl.margin, tl.invweight, tl.solref, tl.solimp);
     }
     nl += __popcll(bal);
   }
-  // contacts: one pass over candidate pairs (lane = pair), active ones compacted in pair order
+  // contacts, emitted in (trip, k, pair) order: trip = 64 consecutive candidate pairs, k = which of a
+  // pair's contacts (only plane-capsule pairs have a second). One (pair, k) item per lane; active
+  // items compacted by ballots, rows per contact 1 (condim 1) or 4 (condim 3, pyramidal).
   int nc = 0, nr = nl;
   const int npair = m->npair;
   TACC(20, tr, lane);
-  for (int base = 0; base < npair; base += 64) {
-    const int p = base + lane;
-    const bool isp = p < npair;
-    const PairRec pr = pr_next;
-    {  // the next trip's records load while this trip collides
-      const int pn = p + 64;
-      pr_next = ldrec(&m->prec[pn < npair ? pn : 0]);
-    }
-    for (int k = 0; k < 2; k++) {
-      bool act = false;
-      float dist = 0.f, pos[3], fr[9];
-      if (isp && collide(pr, W, k, dist, pos, fr)) act = dist - pr.includemargin < 0.f;
-      // rows per contact are 1 (condim 1) or 4 (condim 3, pyramidal): prefix sums from ballots
-      unsigned long long b1 = __ballot(act && pr.condim == 1), b4 = __ballot(act && pr.condim != 1);
-      unsigned long long below = lanes_below(lane);
-      int slot = __popcll((b1 | b4) & below);
-      int rbefore = __popcll(b1 & below) + 4 * __popcll(b4 & below);
-      int rows = pr.condim == 1 ? 1 : 4;
-      int c = nc + slot, r0 = nr + rbefore;
-      if (act && c < capc && r0 + rows <= cap) {
-        RF* cr = R.con + c * CONW;
-        cr[0] = pos[0]; cr[1] = pos[1]; cr[2] = pos[2];
-        for (int i = 0; i < 9; i++) cr[3 + i] = fr[i];
-        cr[12] = __uint_as_float(pr.mask1); cr[13] = __uint_as_float(pr.mask2); cr[14] = pr.mu;
-        cr[15] = __int_as_float(pr.b1 | (pr.b2 << 8) | (pr.condim << 16) | (k << 24));
-        R.con_pair[c] = p;
-        R.con_efc[c] = r0;
-        float ep = dist - pr.includemargin, iw = pr.invweight;
-        for (int q = 0; q < rows; q++) {
-          R.epos[r0 + q] = ep;
-          R.einvw[r0 + q] = iw;
-          R.emeta[r0 + q] = (2 << 16) | p;
-        }
+  auto emit = [&](const PairRec& pr, int p, int k, bool isp) {
+    bool act = false;
+    float dist = 0.f, pos[3], fr[9];
+    if (isp && collide(pr, W, k, dist, pos, fr)) act = dist - pr.includemargin < 0.f;
+    unsigned long long b1 = __ballot(act && pr.condim == 1), b4 = __ballot(act && pr.condim != 1);
+    unsigned long long below = lanes_below(lane);
+    int slot = __popcll((b1 | b4) & below);
+    int rbefore = __popcll(b1 & below) + 4 * __popcll(b4 & below);
+    int rows = pr.condim == 1 ? 1 : 4;
+    int c = nc + slot, r0 = nr + rbefore;
+    if (act && c < capc && r0 + rows <= cap) {
+      RF* cr = R.con + c * CONW;
+      cr[0] = pos[0]; cr[1] = pos[1]; cr[2] = pos[2];
+      for (int i = 0; i < 9; i++) cr[3 + i] = fr[i];
+      cr[12] = __uint_as_float(pr.mask1); cr[13] = __uint_as_float(pr.mask2); cr[14] = pr.mu;
+      cr[15] = __int_as_float(pr.b1 | (pr.b2 << 8) | (pr.condim << 16) | (k << 24));
+      R.con_pair[c] = p;
+      R.con_efc[c] = r0;
+      float ep = dist - pr.includemargin, iw = pr.invweight;
+      for (int q = 0; q < rows; q++) {
+        R.epos[r0 + q] = ep;
+        R.einvw[r0 + q] = iw;
+        R.emeta[r0 + q] = (2 << 16) | p;
       }
-      nc += __popcll(b1 | b4);
-      nr += __popcll(b1) + 4 * __popcll(b4);
+    }
+    nc += __popcll(b1 | b4);
+    nr += __popcll(b1) + 4 * __popcll(b4);
+  };
+  // Broadphase: a lower bound of every (pair, k)'s distance from the geom centres (exact for the
+  // plane pairs; |x1 - x2| - r1 - r2 - h1 - h2 otherwise, the capsules' half lengths h). Items whose
+  // bound clears the pair's margin by kSlack (far above fp32 rounding) cannot touch; the rest,
+  // usually far fewer than 64, run the exact tests in ONE compacted pass, lane j = the j-th item in
+  // emission order, so contacts, rows and every computed value are those of the full pass.
+  constexpr float kSlack = 1e-4f;
+  constexpr int kMaxTrip = (MJL_MAXPAIR + 63) / 64;
+  const int ntrip = (npair + 63) / 64;
+  unsigned long long cm[2 * kMaxTrip];  // candidate items per (trip, k), uniform
+  int ncand = 0;
+#pragma unroll
+  for (int t = 0; t < kMaxTrip; t++) {
+    cm[2 * t] = cm[2 * t + 1] = 0ull;
+    if (t < ntrip) {
+      const int p = 64 * t + lane;
+      const PairRec pr = pr_next;
+      if (t + 1 < ntrip) pr_next = ldrec(&m->prec[p + 64 < npair ? p + 64 : 0]);
+      const LDSA float* x1 = W->gpos[pr.g1];
+      const LDSA float* x2 = W->gpos[pr.g2];
+      const LDSA float* z1 = W->gaxis[pr.g1];
+      const LDSA float* z2 = W->gaxis[pr.g2];
+      const float d[3] = {x2[0] - x1[0], x2[1] - x1[1], x2[2] - x1[2]};
+      float lb0, lb1 = 1e30f;
+      if (pr.kind == MJL_COL_PLANE_SPHERE || pr.kind == MJL_COL_PLANE_CAPSULE) {
+        const float c = dot3(d, z1) - pr.r2, e = pr.h2 * dot3(z2, z1);
+        lb0 = c + e;  // the exact plane distances of the (capsule end) points
+        lb1 = pr.kind == MJL_COL_PLANE_CAPSULE ? c - e : 1e30f;
+      } else {
+        lb0 = sqrtf(dot3(d, d)) - pr.r1 - pr.r2 - pr.h1 - pr.h2;
+      }
+      const bool isp = p < npair;
+      cm[2 * t] = __ballot(isp && lb0 - pr.includemargin < kSlack);
+      cm[2 * t + 1] = __ballot(isp && lb1 - pr.includemargin < kSlack);
+      ncand += __popcll(cm[2 * t]) + __popcll(cm[2 * t + 1]);
+    }
+  }
+  if (ncand <= 64) {
+    // lane j -> the j-th set bit of the concatenated masks (group g = 2 trip + k, then bit order)
+    int g = 0, pre_g = 0, pre = 0;
+#pragma unroll
+    for (int q = 0; q < 2 * kMaxTrip; q++) {
+      const int c = __popcll(cm[q]);
+      if (q < 2 * ntrip && lane >= pre + c) { g = q + 1; pre_g = pre + c; }
+      pre += c;
+    }
+    int r = lane - pre_g;
+    unsigned long long mk = 0ull;
+#pragma unroll
+    for (int q = 0; q < 2 * kMaxTrip; q++) mk = (g == q) ? cm[q] : mk;
+    // r-th set bit of mk (binary search on popcounts)
+    unsigned w = (unsigned)mk;
+    int pos = 0, cnt = __popc(w);
+    if (r >= cnt) { r -= cnt; pos = 32; w = (unsigned)(mk >> 32); }
+#pragma unroll
+    for (int sh = 16; sh >= 1; sh >>= 1) {
+      cnt = __popc(w & ((1u << sh) - 1u));
+      if (r >= cnt) { r -= cnt; pos += sh; w >>= sh; }
+    }
+    const bool has = lane < ncand;
+    const int p = has ? 64 * (g >> 1) + pos : 0, k = g & 1;
+    const PairRec pr = ldrec(&m->prec[p]);
+    emit(pr, p, k, has);
+  } else {  // every item, trip by trip (records reloaded: the rare crowded state)
+    for (int base = 0; base < npair; base += 64) {
+      const int p = base + lane;
+      const PairRec pr = ldrec(&m->prec[p < npair ? p : 0]);
+      for (int k = 0; k < 2; k++) emit(pr, p, k, p < npair);
     }
   }
   if (lane == 0) { W->ncon = nc; W->nefc = nr; W->nlim = nl; }
@@ -1285,21 +1404,25 @@ template <class D, bool G> PHASE bool build_rows(MP m_, LDSA WS<D>* W, Rows<G> R
   }
   SYNC();
   TACC(22, tr, lane);
-  // per-row impedance, D and reference acceleration (lane = row)
+  // reference acceleration (lane = row): aref = -b J qvel - k imp pos; a limit row's b and k imp
+  // from row_imp, a contact row's impedance here (lane = row: one pass for all contact rows)
   for (int r = lane; r < nr; r += 64) {
-    int meta = R.emeta[r], type = meta >> 16, id = meta & 0xffff;
-    const CSTA float *sr, *si;
-    if (type == 0) { sr = m->jnt_solref[id]; si = m->jnt_solimp[id]; }
-    else if (type == 1) { sr = m->tendon_solref[id]; si = m->tendon_solimp[id]; }
-    else { sr = m->pair_solref[id]; si = m->pair_solimp[id]; }
-    float k, b, imp, pos = R.epos[r];
-    kbi(m->timestep, sr, si, pos, k, b, imp);
-    float rr = fmaxf(R.einvw[r] * (1.f - imp) / imp, kMinVal);
-    R.D[r] = 1.f / rr;
+    const float pos = R.epos[r];
+    float b, kimp;
+    if (r >= nl) {
+      const int id = R.emeta[r] & 0xffff;
+      float k, imp;
+      kbi(tstep, m->pair_solref[id], m->pair_solimp[id], pos, k, b, imp);
+      R.D[r] = 1.f / fmaxf(R.einvw[r] * (1.f - imp) / imp, kMinVal);
+      kimp = k * imp;
+    } else {
+      b = R.Jv[r];
+      kimp = R.aref[r];
+    }
     float vel = 0.f;
 #pragma unroll
     for (int kk = 0; kk < LD; kk++) vel += R.J[r * LD + kk] * W->qvel[kk];
-    R.aref[r] = -b * vel - k * imp * pos;
+    R.aref[r] = -b * vel - kimp * pos;
   }
   SYNC();
   return true;
@@ -1308,13 +1431,6 @@ template <class D, bool G> PHASE bool build_rows(MP m_, LDSA WS<D>* W, Rows<G> R
 // ---------------------------------------------------------------------------------------------
 // primal solver (Newton with exact line search; CG with Polak-Ribiere)   [solver.solve]
 // ---------------------------------------------------------------------------------------------
-// row . v over LD entries as four interleaved partial sums (four 7-long FMA chains, not one 28-long)
-template <int LD, class RowF, class VF> INL float rowdot(RowF* a, VF* v) {
-  float s[4] = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-  for (int k = 0; k < LD; k++) s[k & 3] = fmaf(a[k], v[k], s[k & 3]);
-  return (s[0] + s[1]) + (s[2] + s[3]);
-}
 template <class D> INL float mrow(LDSA WS<D>* W, LDSA float* v, int lane) {  // (M v)[lane]
   return rowdot<D::LD>(W->M + lane * D::LD, v);
 }
@@ -1813,15 +1929,15 @@ template <class D> NOINL void global_rows_path(MP m, LDSA WS<D>* W, float* scrat
 
 // full forward pass (mjx.forward)
 template <class D> PHASE void forward(MP m_, LDSA WS<D>* W, float* scratch_env, int gmax_efc, int gmax_con,
-                                      int force_global, int lane) {
+                                      int force_global, int lane, const KinPre& kp) {
   MP m = uniform_ptr(m_);
   constexpr int LD = D::LD;
   STAMP(0, lane);
-  kinematics<D>(m, W, lane);
+  kinematics<D>(m, W, lane, kp);
   STAMP(1, lane);
-  com_pos_crb<D>(m, W, lane);
+  com_pos_crb<D>(m, W, lane, kp);
   STAMP(2, lane);
-  velocity_stage<D>(m, W, lane);
+  velocity_stage<D>(m, W, lane, kp);
   STAMP(3, lane);
   // factor M into H: qacc_smooth now, CG preconditioner later
   float x = chol_factor_solve<D>(W->M, W->H, W->invd, m->nv, W->frc_smooth, lane);
@@ -1850,13 +1966,16 @@ template <class D> PHASE void integrate(MP m_, LDSA WS<D>* W, int lane, LDSA flo
   constexpr int LD = D::LD;
   const int nv = m->nv;
   const float dt = m->timestep;
+  // this lane's joint record and dof damping, issued before the first wait
+  const JntRec jr = ldrec(&m->jrec[lane < m->njnt ? lane : 0]);
+  const float dmp = m->dof_damping[lane < nv ? lane : 0];
   float qa = (lane < nv) ? W->qacc[lane] : 0.f;
   bool damp = (m->integrator == MJL_INT_IMPLICITFAST || m->eulerdamp) && m->any_damping;
   if (damp) {  // (M + dt*diag(damping)) qacc' = qfrc_smooth + qfrc_constraint
     for (int i = lane; i < D::NV * LD; i += 64) W->H[i] = W->M[i];
     SYNC();
     if (lane < nv) {
-      W->H[lane * LD + lane] += dt * m->dof_damping[lane];
+      W->H[lane * LD + lane] += dt * dmp;
       W->Mv[lane] = W->frc_smooth[lane] + W->frc_con[lane];  // Mv: solver scratch, free now
     }
     SYNC();
@@ -1866,8 +1985,8 @@ template <class D> PHASE void integrate(MP m_, LDSA WS<D>* W, int lane, LDSA flo
   if (lane < nv) W->qvel[lane] += dt * qa;
   SYNC();
   if (lane < m->njnt) {
-    int j = lane, q = m->jnt_qposadr[j], d = m->jnt_dofadr[j];
-    if (m->jnt_type[j] == MJL_JNT_FREE) {
+    const int q = jr.qadr, d = jr.dofadr;
+    if (jr.isfree) {
       W->qpos[q] += dt * W->qvel[d];
       W->qpos[q + 1] += dt * W->qvel[d + 1];
       W->qpos[q + 2] += dt * W->qvel[d + 2];
@@ -2022,6 +2141,7 @@ template <class D> NOINL void env_reset(MP m_, LDSA WS<D>* W, const EnvArgs* Ap,
       u = uniform01(A.s0, A.s1, A.c0, A.c1, env, lane);
     }
   }
+  const KinPre kp = kin_prefetch(m, lane);
   if (lane < m->nq) W->qpos[lane] = m->qpos0[lane];
   if (lane < 32) W->ctrl[lane] = 0.f;
   if (lane < D::LD) { W->qacc_ws[lane] = 0.f; W->qvel[lane] = 0.f; }
@@ -2035,7 +2155,7 @@ template <class D> NOINL void env_reset(MP m_, LDSA WS<D>* W, const EnvArgs* Ap,
   }
   SYNC();
   if (c->initial_velocity_max > 0.f) {
-    kinematics<D>(m, W, lane);  // the first forward's pelvis position (positions depend on qpos only)
+    kinematics<D>(m, W, lane, kp);  // the first forward's pelvis position (positions depend on qpos only)
     LDSA float* bp = W->xpos[c->pelvis_body_id];
     float tx = bp[0] + c->target_dist, ty = bp[1];
     float dx = tx - bp[0], dy = ty - bp[1];
@@ -2047,7 +2167,7 @@ template <class D> NOINL void env_reset(MP m_, LDSA WS<D>* W, const EnvArgs* Ap,
     if (lane == 0) { W->qvel[0] = vx; W->qvel[1] = vy; }
     SYNC();
   }
-  forward<D>(m, W, A.scratch_env, A.gmax_efc, A.gmax_con, A.force_global, lane);
+  forward<D>(m, W, A.scratch_env, A.gmax_efc, A.gmax_con, A.force_global, lane, kp);
   if (lane == 0) {
     LDSA float* bp = W->xpos[c->pelvis_body_id];
     float tx = bp[0] + c->target_dist, ty = bp[1], tz = bp[2];
@@ -2169,6 +2289,7 @@ template <class D, int MODE> __global__ __launch_bounds__(64, MJL_MINWAVES) void
   if (MODE == MODE_ENV_RESET) {
     env_reset<D>(m, W, &A, env, lane, aux, P.obs ? P.obs + (size_t)env * P.env->obs_dim : nullptr);
   } else {
+    const KinPre kp = kin_prefetch(m, lane);  // issued before the state loads: the latencies overlap
     if (MODE == MODE_SPEEDTEST) {  // fresh make_data, qvel[0] = vel (mjx_humanoid_speed_test.py:50-55)
       if (lane < nq) W->qpos[lane] = m->qpos0[lane];
       if (lane < nv) W->qvel[lane] = (lane == 0) ? P.vel[env] : 0.f;
@@ -2194,7 +2315,7 @@ template <class D, int MODE> __global__ __launch_bounds__(64, MJL_MINWAVES) void
       if (lane == 0) W->sc[SC_FLIP] = aux[0];
       SYNC();
     }
-    forward<D>(m, W, A.scratch_env, A.gmax_efc, A.gmax_con, A.force_global, lane);
+    forward<D>(m, W, A.scratch_env, A.gmax_efc, A.gmax_con, A.force_global, lane, kp);
     if (MODE != MODE_FORWARD) integrate<D>(m, W, lane);
     STAMP(8, lane);
     if (MODE == MODE_ENV_STEP) {

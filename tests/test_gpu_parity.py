@@ -390,3 +390,42 @@ def test_env_config_rejects_non_permutation_flip_tables():
     cfg_c.obs_perm[5] = cfg_c.obs_perm[6]
     with pytest.raises(MjlError, match="obs_perm is not a permutation"):
         check(lib().mjl_env_config(env.data.handle, C.byref(cfg_c)))
+
+
+@pytest.mark.parametrize("spread", [0.25, 2.5])
+def test_crowded_broadphase_parity(spread):
+    """The contact pass runs the exact pair tests only on the items the distance bound cannot rule
+    out, compacted into one pass when there are at most 64 of them. A crowded cluster (4 free bodies
+    x 4 capsules within `spread` of each other: up to 96 candidate items, so the full pass) and a
+    sparse one (the compacted pass) give the oracle's contact / row counts and constrained
+    accelerations."""
+    from mjx_amd import mjcf
+    rng = np.random.default_rng(11)
+    bodies = []
+    for b in range(4):
+        geoms = "".join(
+            f'<geom type="capsule" size="0.06" fromto="{" ".join(f"{x:.4f}" for x in rng.uniform(-0.15, 0.15, 6))}" condim="1"/>'
+            for _ in range(4))
+        c = rng.uniform(-spread, spread, 3) * [1, 1, 0.02] + [0, 0, 0.3 if spread < 1 else 0.1]
+        bodies.append(f'<body pos="{c[0]:.4f} {c[1]:.4f} {c[2]:.4f}"><freejoint/>{geoms}</body>')
+    m = mjcf.compile_xml_string(f"""<mujoco><option timestep="0.002"/><worldbody>
+      <geom type="plane" size="0 0 1" condim="1"/>{''.join(bodies)}</worldbody></mujoco>""")
+    sys_ = mjx.put_model(m)
+    states = []
+    for i in range(6):
+        q = m.qpos0.copy()
+        q[:: 7] += rng.uniform(-0.02, 0.02, 4)
+        states.append((q, rng.uniform(-0.3, 0.3, m.nv), np.zeros(m.nv), np.zeros(m.nu)))
+    states = [tuple(np.float32(x).astype(np.float64) for x in st) for st in states]
+    d = mjx.make_data(sys_, len(states))  # no actuators: no ctrl to set
+    for i, f in enumerate(("qpos", "qvel", "qacc_warmstart")):
+        d.set(f, torch.tensor(np.array([st[i] for st in states]), dtype=torch.float32))
+    mjx.forward(sys_, d)
+    st, qacc = d.get("stats").cpu().numpy(), d.get("qacc").cpu().numpy()
+    orc = Oracle(m)
+    for i, (q, v, w, c) in enumerate(states):
+        a = state_arrays(m, orc.forward(orc.new_state(q, v, w, c)))
+        assert (st[i][0], st[i][1]) == (a["ncon"], a["nefc"]), f"state {i}: counts"
+        _close(qacc[i], a["qacc"], 2e-3, f"state {i} qacc")
+    if spread < 1:
+        assert st[:, 0].max() > 10   # crowded enough to exercise many contacts
