@@ -339,33 +339,20 @@ template <class D> INL void chol_factor(LDSA float* A, LDSA float* invd_out, int
 // B operands are the lane's own registers. The MFMA result C has row r of C in column r of the C
 // layout, i.e. C[i][j] sits in lane i (half (j >> 2) & 1) register (j & 3) + 4 (j >> 3); one
 // v_permlane32_swap of a register with itself hands each lane both halves' values.
-#ifndef MJL_CHOL_PANEL
-#define MJL_CHOL_PANEL 8
-#endif
 template <int LD, int NV, int P0, int P1> INL void chol_panel(float (&a)[LD], int kh) {
   static_assert(P0 % 2 == 0 && P1 <= NV && NV <= 32, "panels start on a K = 2 boundary");
 #pragma unroll
   for (int k = P0; k < P1; k++) {
     // the column's broadcasts read the unscaled a_jk (they do not wait for the pivot's rsq) and
-    // each lane's multiplier is L_ik / L_kk instead; fminf after v_rsq is the 1e-30 pivot floor
-    // (rsq(1e-30)) off the readlane -> rsq chain (an fmaxf before it needs a canonicalising v_max)
-    const float piv = rdlane(a[k], k);
-    const float inv = fminf(__builtin_amdgcn_rsqf(piv), 1e15f);
-#ifdef MJL_CHOL_RCP
-    // the multiplier L_ik / L_kk = a_ik / pivot from v_rcp beside the v_rsq: one multiply on the
-    // column-to-column chain instead of two (a_ik * inv * inv)
-    const float rp = fminf(__builtin_amdgcn_rcpf(piv), 1e30f);
-#endif
+    // each lane's multiplier is L_ik / L_kk instead. No pivot floor: like MJX's cho_factor (and the
+    // oracle), a non-SPD pivot is not patched; its NaN reaches the env's non-finite guard. (A floor
+    // on the rsq was one more dependent op per column: ~8 cycles x 27 on the factor's chain.)
+    const float inv = __builtin_amdgcn_rsqf(rdlane(a[k], k));
     float s[P1];
 #pragma unroll
     for (int j = k + 1; j < P1; j++) s[j] = rdlane(a[k], j);
-#ifdef MJL_CHOL_RCP
-    const float t = a[k] * rp;
-    a[k] *= inv;  // lane k: sqrt of its pivot
-#else
     a[k] *= inv;  // lane k: sqrt of its pivot
     const float t = a[k] * inv;
-#endif
 #pragma unroll
     for (int j = k + 1; j < P1; j++) a[j] = fmaf(-t, s[j], a[j]);
   }
@@ -420,7 +407,6 @@ template <class D, bool ADD> INL float chol_aug_factor_solve(const LDSA float* s
                                                              int lane, f32x16 C = {}) {
   constexpr int NV = D::NV, LD = D::LD, R = NV;
   static_assert(NV < 32 && LD % 4 == 0 && LD > NV, "augmented factor needs a spare row and 16-B rows");
-  constexpr int B1 = NV > 16 ? 16 : NV;
   const int i = lane & 31, kh = lane >> 5;
   (void)n;
   float a[LD];
@@ -445,15 +431,11 @@ template <class D, bool ADD> INL float chol_aug_factor_solve(const LDSA float* s
   }
   TACC(32, tch, lane);
 
-#if MJL_CHOL_PANEL == 8
+  // panels [0, 8), [8, 16), [16, NV): a last MFMA update for the final few columns cost more than
+  // it saved (tools/chol_micro.hip: boundaries 8/16 beat 8/16/24 by 5 %, 10/20 by 3 %)
   chol_panel<LD, NV, 0, (NV < 8 ? NV : 8)>(a, kh);
   if constexpr (NV > 8) chol_panel<LD, NV, 8, (NV < 16 ? NV : 16)>(a, kh);
-  if constexpr (NV > 16) chol_panel<LD, NV, 16, (NV < 24 ? NV : 24)>(a, kh);
-  if constexpr (NV > 24) chol_panel<LD, NV, 24, NV>(a, kh);
-#else
-  chol_panel<LD, NV, 0, B1>(a, kh);
-  if constexpr (NV > B1) chol_panel<LD, NV, B1, NV>(a, kh);
-#endif
+  if constexpr (NV > 16) chol_panel<LD, NV, 16, NV>(a, kh);
   // rows of L to dst, y = L[R][0..NV) to invd_out (scratch until the reads below)
   TACC(33, tch, lane);
   if (lane <= R) {
@@ -1791,7 +1773,9 @@ template <class D, bool G, class TP> PHASE void solver_t(MP m_, LDSA WS<D>* W, R
   for (bool first = true;; first = false) {
     if (!first) {
       float alpha = solver_linesearch<D, G>(m, W, R, lane, tp);
+#ifndef MJL_DIAG_FIXIT
       if (!(alpha != 0.f)) { iter++; break; }  // no improvement: MJX's next cond stops (also on NaN)
+#endif
       // (the line search applied the step to qacc, Ma and jar)
       if (!newton && lane < nv) { W->gradold[lane] = W->grad[lane]; W->Mgradold[lane] = W->Mgrad[lane]; }
       SYNC();
@@ -1802,18 +1786,27 @@ template <class D, bool G, class TP> PHASE void solver_t(MP m_, LDSA WS<D>* W, R
     if constexpr (TP::on) tp.update(W, R, lane);
     if (first && maxit != 1) {  // MJX cond before the first body (iterations == 1 runs one body)
       float gp = (lane < nv) ? W->grad[lane] * W->grad[lane] : 0.f;
+#ifndef MJL_DIAG_FIXIT
       if (maxit <= 0 || scale * sqrtf(wsum(gp)) < m->tolerance) break;
+#endif
     }
     if (!first) {
       iter++;
       float gp = (lane < nv) ? W->grad[lane] * W->grad[lane] : 0.f;
       float gnorm = scale * sqrtf(wsum(gp));
       float improvement = scale * (oldcost - cost);
+#ifdef MJL_DIAG_FIXIT  // diagnostic: exactly `iterations` iterations (cost attribution by knockouts)
+      if (iter >= maxit) break;
+      (void)gnorm; (void)improvement;
+#else
       if (improvement < m->tolerance || gnorm < m->tolerance || iter >= maxit) break;
+#endif
       if (exact_exit) {
         unsigned long long am[4];
         active_masks(am);
+#ifndef MJL_DIAG_FIXIT
         if (am[0] == hm[0] && am[1] == hm[1] && am[2] == hm[2] && am[3] == hm[3]) break;
+#endif
       }
     }
     TACC(11, ts, lane);
@@ -1825,9 +1818,17 @@ template <class D, bool G, class TP> PHASE void solver_t(MP m_, LDSA WS<D>* W, R
       }
       float x;
       if constexpr (D::NV < 32) {  // J'DJ goes from the MFMA accumulator straight into the factor's rows
+#ifdef MJL_DIAG_KO_HESS
+        f32x16 acc = {};
+#else
         const f32x16 acc = solver_hessian_acc<D, G>(m, W, R, lane);
+#endif
         TACC(12, ts, lane);
+#ifdef MJL_DIAG_KO_CHOL
+        x = W->grad[lane & 31] + acc[0] * 1e-30f;
+#else
         x = chol_aug_factor_solve<D, true>(W->M, W->H, W->invd, nv, W->grad, lane, acc);
+#endif
       } else {
         solver_hessian<D, G>(m, W, R, lane);
         TACC(12, ts, lane);
