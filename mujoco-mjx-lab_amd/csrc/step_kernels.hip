@@ -1420,8 +1420,9 @@ template <class D, class RowF> INL float jrow(RowF* J, LDSA float* v, int r) {  
   return rowdot<D::LD>(J + r * D::LD, v);
 }
 
-// forces, cost, qfrc_constraint and gradient at the current qacc / Ma / jar; returns the cost
-template <class D, bool G> INL float solver_update(MP m_, LDSA WS<D>* W, Rows<G> R, int lane) {
+// forces, cost, qfrc_constraint and gradient at the current qacc / Ma / jar; returns the cost and
+// |grad|^2 (two wave sums issued together)
+template <class D, bool G> INL float solver_update(MP m_, LDSA WS<D>* W, Rows<G> R, int lane, float& gsq) {
   MP m = uniform_ptr(m_);
   constexpr int LD = D::LD;
   const int nv = m->nv, nefc = W->nefc;
@@ -1453,13 +1454,15 @@ template <class D, bool G> INL float solver_update(MP m_, LDSA WS<D>* W, Rows<G>
     for (; r < nefc; r += 2) s += R.J[r * LD + d] * R.force[r];
   }
   s += __shfl_xor(s, 32);
-  float g = 0.f;
+  float g = 0.f, gr = 0.f;
   if (lane < nv) {
     W->frc_con[lane] = s;
     g = 0.5f * (ma - fs) * (qa - qsm);
-    W->grad[lane] = ma - fs - s;
+    gr = ma - fs - s;
+    W->grad[lane] = gr;
   }
   float cost = wsum(g + c);
+  gsq = wsum(gr * gr);
   SYNC();
   return cost;
 }
@@ -1781,19 +1784,17 @@ template <class D, bool G, class TP> PHASE void solver_t(MP m_, LDSA WS<D>* W, R
       SYNC();
       TACC(10, ts, lane);
     }
-    float oldcost = cost;
-    cost = solver_update<D, G>(m, W, R, lane);
+    float oldcost = cost, gsq;
+    cost = solver_update<D, G>(m, W, R, lane, gsq);
     if constexpr (TP::on) tp.update(W, R, lane);
     if (first && maxit != 1) {  // MJX cond before the first body (iterations == 1 runs one body)
-      float gp = (lane < nv) ? W->grad[lane] * W->grad[lane] : 0.f;
 #ifndef MJL_DIAG_FIXIT
-      if (maxit <= 0 || scale * sqrtf(wsum(gp)) < m->tolerance) break;
+      if (maxit <= 0 || scale * sqrtf(gsq) < m->tolerance) break;
 #endif
     }
     if (!first) {
       iter++;
-      float gp = (lane < nv) ? W->grad[lane] * W->grad[lane] : 0.f;
-      float gnorm = scale * sqrtf(wsum(gp));
+      float gnorm = scale * sqrtf(gsq);
       float improvement = scale * (oldcost - cost);
 #ifdef MJL_DIAG_FIXIT  // diagnostic: exactly `iterations` iterations (cost attribution by knockouts)
       if (iter >= maxit) break;
@@ -1969,18 +1970,30 @@ template <class D> PHASE void integrate(MP m_, LDSA WS<D>* W, int lane, LDSA flo
   const float dt = m->timestep;
   // this lane's joint record and dof damping, issued before the first wait
   const JntRec jr = ldrec(&m->jrec[lane < m->njnt ? lane : 0]);
-  const float dmp = m->dof_damping[lane < nv ? lane : 0];
+  const float dmp = m->dof_damping[(lane & 31) < nv ? (lane & 31) : 0];
   float qa = (lane < nv) ? W->qacc[lane] : 0.f;
   bool damp = (m->integrator == MJL_INT_IMPLICITFAST || m->eulerdamp) && m->any_damping;
   if (damp) {  // (M + dt*diag(damping)) qacc' = qfrc_smooth + qfrc_constraint
-    for (int i = lane; i < D::NV * LD; i += 64) W->H[i] = W->M[i];
-    SYNC();
-    if (lane < nv) {
-      W->H[lane * LD + lane] += dt * dmp;
-      W->Mv[lane] = W->frc_smooth[lane] + W->frc_con[lane];  // Mv: solver scratch, free now
+    if constexpr (D::NV < 32) {
+      // dt*diag(damping) enters the factor as its MFMA-layout addend (register v of lane l holds
+      // row (v&3) + 8(v>>2) + 4(l>>5) of column l&31): no copy of M into H and no barrier for it
+      if (lane < nv) W->Mv[lane] = W->frc_smooth[lane] + W->frc_con[lane];  // Mv: solver scratch, free now
+      f32x16 C;
+      const int c = lane & 31, h = lane >> 5;
+#pragma unroll
+      for (int v = 0; v < 16; v++) C[v] = ((v & 3) + 8 * (v >> 2) + 4 * h == c && c < nv) ? dt * dmp : 0.f;
+      SYNC();
+      qa = chol_aug_factor_solve<D, true>(W->M, W->H, W->invd, nv, W->Mv, lane, C);
+    } else {
+      for (int i = lane; i < D::NV * LD; i += 64) W->H[i] = W->M[i];
+      SYNC();
+      if (lane < nv) {
+        W->H[lane * LD + lane] += dt * dmp;
+        W->Mv[lane] = W->frc_smooth[lane] + W->frc_con[lane];
+      }
+      SYNC();
+      qa = chol_factor_solve<D>(W->H, W->H, W->invd, nv, W->Mv, lane);
     }
-    SYNC();
-    qa = chol_factor_solve<D>(W->H, W->H, W->invd, nv, W->Mv, lane);
   }
   if (ap_out && lane < D::LD) ap_out[lane] = (lane < nv) ? qa : 0.f;  // a' for the step adjoint
   if (lane < nv) W->qvel[lane] += dt * qa;
