@@ -707,7 +707,8 @@ template <class D> PHASE void kinematics(MP m_, LDSA WS<D>* W, int lane, const K
       }
     }
   }
-  SYNC();
+  // (no barrier: the level pass below works in registers; the anchors / axes written above are read
+  // after the next barrier)
   TACC(17, tk, lane);
   // tree pass: compose with the parent's world frame, one level at a time  [smooth.kinematics].
   // A body's frame stays in its lane's registers; children read it with ds_bpermute (no LDS
@@ -970,7 +971,8 @@ template <class D> PHASE void velocity_stage(MP m_, LDSA WS<D>* W, int lane, con
       }
     }
   }
-  SYNC();
+  // (no barrier: the level pass works in registers, and the world rows written above are read only
+  // after the next one)
   TACC(25, tv, lane);
   // cvel / cacc by levels in registers, the parent's read with ds_bpermute (lane 0: the world,
   // cvel 0 and cacc = -gravity)
@@ -1568,7 +1570,8 @@ template <class D, bool G, class TP> INL float solver_linesearch(MP m_, LDSA WS<
     jv1 = jrow<D>(R.J, W->search, lane + 64); ja1 = R.jar[lane + 64]; dd1 = R.D[lane + 64]; R.Jv[lane + 64] = jv1;
   }
   for (int r = lane + 128; r < nefc; r += 64) R.Jv[r] = jrow<D>(R.J, W->search, r);
-  SYNC();
+  // (Mv / Jv entries are read back only by the lanes that wrote them: no barrier in the primal)
+  if constexpr (TP::on) SYNC();
   if constexpr (TP::on) tp.ls_begin(W, lane);
   TACC(28, tl, lane);
   // the step qacc += a s, Ma += a M s, jar += a J s from the registers the search already holds
@@ -1751,7 +1754,8 @@ template <class D, bool G, class TP> PHASE void solver_t(MP m_, LDSA WS<D>* W, R
   if (lane < nv) W->Ma[lane] = mq[wsel];
   if (lane < nefc) R.jar[lane] = jq[wsel] - ar;
   for (int r = lane + 64; r < nefc; r += 64) R.jar[r] = jrow<D>(R.J, q0, r) - R.aref[r];
-  SYNC();
+  // (qacc, Ma and jar entries are read next by the lanes that wrote them: no barrier in the primal)
+  if constexpr (TP::on) SYNC();
   if constexpr (TP::on) tp.warm(wsel, lane);
   TACC(9, ts, lane);
   // Newton / CG iterations, written so that each helper appears once in the loop body.
@@ -1779,9 +1783,10 @@ template <class D, bool G, class TP> PHASE void solver_t(MP m_, LDSA WS<D>* W, R
 #ifndef MJL_DIAG_FIXIT
       if (!(alpha != 0.f)) { iter++; break; }  // no improvement: MJX's next cond stops (also on NaN)
 #endif
-      // (the line search applied the step to qacc, Ma and jar)
+      // (the line search applied the step to qacc, Ma and jar, each entry by the lane that reads it
+      // next, so the primal needs no barrier here; the tape's hooks read across lanes)
       if (!newton && lane < nv) { W->gradold[lane] = W->grad[lane]; W->Mgradold[lane] = W->Mgrad[lane]; }
-      SYNC();
+      if constexpr (TP::on) SYNC();
       TACC(10, ts, lane);
     }
     float oldcost = cost, gsq;
@@ -1835,9 +1840,7 @@ template <class D, bool G, class TP> PHASE void solver_t(MP m_, LDSA WS<D>* W, R
         TACC(12, ts, lane);
         x = chol_factor_solve<D>(W->H, W->H, W->invd, nv, W->grad, lane);
       }
-      if (lane < nv) W->Mgrad[lane] = x;
-      SYNC();
-      TACC(13, ts, lane);
+      TACC(13, ts, lane);  // (Mgrad is CG's: Newton does not store it)
       if constexpr (TP::on) tp.direction(x, 0.f, 0.f, 0.f, lane);
       if (lane < LD) W->search[lane] = (lane < nv) ? -x : 0.f;
     } else {
@@ -1943,8 +1946,7 @@ template <class D> PHASE void forward(MP m_, LDSA WS<D>* W, float* scratch_env, 
   STAMP(3, lane);
   // factor M into H: qacc_smooth now, CG preconditioner later
   float x = chol_factor_solve<D>(W->M, W->H, W->invd, m->nv, W->frc_smooth, lane);
-  if (lane < LD) W->qacc_smooth[lane] = (lane < m->nv) ? x : 0.f;
-  SYNC();
+  if (lane < LD) W->qacc_smooth[lane] = (lane < m->nv) ? x : 0.f;  // first read after build_rows' barriers
   STAMP(4, lane);
   bool ok = false;
   if (!force_global) ok = build_rows<D, false>(m, W, lds_rows<D>(W), lane);
