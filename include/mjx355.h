@@ -299,6 +299,20 @@ int mjl_obs_normalize(const float* x, const float* mean, const float* var, int n
 int mjl_policy_head(const float* z, const float* log_std, const float* eps, int B, int A, float* act, float* logp,
                     void* stream);
 
+/* The rollout step's whole policy forward in one launch (train_ppo.py:134-139 with
+ * src/networks.py:22-61,82-112: normalize_obs + clip, the GaussianPolicy MLP with tanh hidden
+ * layers and a linear last layer, the tanh head, sampling and gaussian_logprob), on the matrix
+ * cores: replaces mjl_obs_normalize + the MLP's GEMMs / activations + mjl_policy_head.
+ * dims[0..nlayer] = obs_dim, hidden sizes..., act_dim (each <= 256, nlayer <= 6). params: per layer
+ * WP[K/4][N][4] = W^T (K = in, N = out, both zero-padded to multiples of 16; WP[k/4][n][k%4] =
+ * weight[n][k] of the torch / flax Dense) followed by the padded bias [N];
+ * mjl_policy_param_floats(nlayer, dims) = its length. obs [B, obs_dim], eps [B, act_dim] -> act
+ * [B, act_dim], logp [B]; device pointers, float32, row-major. */
+long long mjl_policy_param_floats(int nlayer, const int* dims);
+int mjl_policy_fwd(const float* obs, const float* mean, const float* var, float clip, const float* params, int nlayer,
+                   const int* dims, const float* log_std, const float* eps, int B, float* act, float* logp,
+                   void* stream);
+
 /* PPO update (train_ppo.py:233-252, the bias-gradient column sums of every dense layer's backward
  * in value_and_grad of ppo_loss_fn / value_loss_fn, and the split-K weight-gradient sum):
  * out[d] = sum over rows of x[n, d] (row-major, float32, device), in a fixed order (two launches

@@ -756,6 +756,44 @@ extern "C" int mjl_policy_head(const float* z, const float* log_std, const float
   return MJL_OK;
 }
 
+static int policy_dims(int nlayer, const int* dims, PolicyDims& pd) {
+  if (nlayer < 1 || nlayer > kPolMaxLayers || !dims) return fail(MJL_ERR_ARG, "policy: 1..%d layers", kPolMaxLayers);
+  pd.nlayer = nlayer;
+  pd.obs_dim = dims[0];
+  pd.act_dim = dims[nlayer];
+  long long off = 0;
+  for (int l = 0; l < nlayer; l++) {
+    if (dims[l] <= 0 || dims[l + 1] <= 0) return fail(MJL_ERR_ARG, "policy: layer sizes must be positive");
+    pd.K[l] = (dims[l] + 15) & ~15;
+    pd.N[l] = (dims[l + 1] + 15) & ~15;
+    if (pd.K[l] > 256 || pd.N[l] > 256) return fail(MJL_ERR_ARG, "policy: layer sizes above 256 not supported");
+    pd.off[l] = off;
+    off += (long long)pd.K[l] * pd.N[l] + pd.N[l];
+  }
+  return MJL_OK;
+}
+
+extern "C" long long mjl_policy_param_floats(int nlayer, const int* dims) {
+  PolicyDims pd;
+  if (policy_dims(nlayer, dims, pd) != MJL_OK) return -1;
+  const int l = nlayer - 1;
+  return pd.off[l] + (long long)pd.K[l] * pd.N[l] + pd.N[l];
+}
+
+extern "C" int mjl_policy_fwd(const float* obs, const float* mean, const float* var, float clip, const float* params,
+                              int nlayer, const int* dims, const float* log_std, const float* eps, int B, float* act,
+                              float* logp, void* stream) {
+  if (!obs || !mean || !var || !params || !log_std || !eps || !act || !logp || B < 0)
+    return fail(MJL_ERR_ARG, "bad argument");
+  PolicyDims pd;
+  if (int rc = policy_dims(nlayer, dims, pd)) return rc;
+  if (B == 0) return MJL_OK;
+  hipLaunchKernelGGL(policy_rollout_kernel, dim3((B + 15) / 16), dim3(64 * kPolWaves), 0, (hipStream_t)stream, obs, mean, var,
+                     clip, params, pd, log_std, eps, B, act, logp);
+  HIPCHK(hipGetLastError());
+  return MJL_OK;
+}
+
 extern "C" long long mjl_colsum_scratch(int n, int d) {
   if (n <= 0 || d <= 0) return 0;
   const ColsumPlan p(n, d);

@@ -24,6 +24,7 @@ EXPORTS = [
     "mjl_step_vjp", "mjl_env_step_vjp", "mjl_gae", "mjl_batch_set_counter_base",
     "mjl_env_set_reset_keys", "mjl_prng_split", "mjl_env_step_vjp_guarded", "mjl_state_size", "mjl_get_state",
     "mjl_set_state", "mjl_obs_normalize", "mjl_policy_head", "mjl_colsum_scratch", "mjl_colsum",
+    "mjl_policy_param_floats", "mjl_policy_fwd",
     "mjl_step_vjp_full", "mjl_env_step_vjp_full",
 ]
 
@@ -92,6 +93,9 @@ def lib() -> C.CDLL:
     L.mjl_gae.argtypes = [f32p, f32p, f32p, f32p, i32, i32, C.c_double, C.c_double, f32p, f32p, vp]
     L.mjl_obs_normalize.argtypes = [f32p, f32p, f32p, i32, i32, C.c_float, f32p, vp]
     L.mjl_policy_head.argtypes = [f32p, f32p, f32p, i32, i32, f32p, f32p, vp]
+    L.mjl_policy_param_floats.argtypes = [i32, C.POINTER(i32)]
+    L.mjl_policy_param_floats.restype = C.c_longlong
+    L.mjl_policy_fwd.argtypes = [f32p, f32p, f32p, C.c_float, f32p, i32, C.POINTER(i32), f32p, f32p, i32, f32p, f32p, vp]
     L.mjl_colsum_scratch.argtypes = [i32, i32]
     L.mjl_colsum_scratch.restype = C.c_longlong
     L.mjl_colsum.argtypes = [f32p, i32, i32, f32p, f32p, vp]

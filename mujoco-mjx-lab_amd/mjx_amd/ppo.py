@@ -211,6 +211,54 @@ def policy_head_native(z, log_std, eps, act_out, logp_out):
                                 act_out.data_ptr(), logp_out.data_ptr(), torch.cuda.current_stream(z.device).cuda_stream))
 
 
+def _ceil16(x: int) -> int:
+    return (x + 15) // 16 * 16
+
+
+def policy_fused_dims(policy) -> Optional[List[int]]:
+    """[obs_dim, hidden..., act_dim] when the policy fits mjl_policy_fwd (tanh hidden layers, a linear
+    last layer, every size <= 256, at most 6 layers), else None (the rollout keeps the torch MLP)."""
+    mlp = policy.mlp
+    if len(mlp.layers) > 6 or any(a not in ("tanh",) for a in mlp.acts[:-1]) or mlp.acts[-1] != "linear":
+        return None
+    dims = [mlp.layers[0].in_features] + [lin.out_features for lin in mlp.layers]
+    return dims if max(dims) <= 256 else None
+
+
+def pack_policy_params(policy, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """mjl_policy_fwd's parameter layout: per layer WP[K/4][N][4] = W^T zero-padded to K, N multiples
+    of 16 (WP[k // 4, n, k % 4] = weight[n, k]), then the padded bias [N]."""
+    parts = []
+    for lin in policy.mlp.layers:
+        w = lin.weight.detach()
+        n, k = w.shape
+        kp, np_ = _ceil16(k), _ceil16(n)
+        wt = torch.zeros((kp, np_), device=w.device, dtype=torch.float32)
+        wt[:k, :n] = w.t()
+        parts.append(wt.reshape(kp // 4, 4, np_).permute(0, 2, 1).reshape(-1))
+        b = torch.zeros(np_, device=w.device, dtype=torch.float32)
+        b[:n] = lin.bias.detach()
+        parts.append(b)
+    flat = torch.cat(parts)
+    if out is None:
+        return flat
+    out.copy_(flat)
+    return out
+
+
+def policy_fwd_native(obs, mean, var, clip, params, dims, log_std, eps, act_out, logp_out):
+    """The rollout step's normalisation + policy MLP + head + sampling + log-prob as one launch
+    (mjl_policy_fwd); same results as obs_normalize_native -> policy.mlp -> policy_head_native up to
+    the GEMMs' accumulation order."""
+    import ctypes as C
+    from ._lib import check, lib
+    B = obs.shape[0]
+    d = (C.c_int * len(dims))(*dims)
+    check(lib().mjl_policy_fwd(obs.data_ptr(), mean.data_ptr(), var.data_ptr(), float(clip), params.data_ptr(),
+                               len(dims) - 1, d, log_std.detach().contiguous().data_ptr(), eps.data_ptr(), B,
+                               act_out.data_ptr(), logp_out.data_ptr(), torch.cuda.current_stream(obs.device).cuda_stream))
+
+
 class _GaussianLogprob(torch.autograd.Function):
     """gaussian_logprob for the update's [65,536, 21] minibatch with a hand-written backward:
     d logp / d mean = (act - mean) e^(-2 s), d logp / d s_j = sum_i g_i (q_ij - 1) with
@@ -368,10 +416,12 @@ class PPOTrainer:
     with auto-reset (HumanoidEnv, or a stand-in in CPU tests), obs_dim, act_dim, num_envs."""
 
     def __init__(self, cfg, env, eval_env=None, device="cuda", dist=None, out_dir: Optional[str] = None,
-                 use_graph: bool = True, jax_keys: bool = False):
+                 use_graph: bool = True, jax_keys: bool = False, fused_policy: bool = True):
         """jax_keys: draw every env reset (initial, auto-reset, eval) from the jax.random key chain
         train_ppo.py derives from cfg.seed (:88-118, :132/:150-151 per rollout step, :325, :359,
-        :419, eval :268-293), so the reset stream equals the reference's for the same seed."""
+        :419, eval :268-293), so the reset stream equals the reference's for the same seed.
+        fused_policy: the rollout's normalisation + policy MLP + head as one launch (mjl_policy_fwd)
+        when the network fits it; False keeps normalisation launch + torch MLP + head launch."""
         self.cfg, self.env, self.eval_env, self.dist = cfg, env, eval_env, dist
         self.rank = dist.get_rank() if dist is not None else 0
         self.world = dist.get_world_size() if dist is not None else 1
@@ -398,6 +448,8 @@ class PPOTrainer:
         self.obs = env.reset().clone()
         self.use_graph = bool(use_graph)
         self._buf, self._graph, self._rollouts = None, None, 0
+        self.fused_policy = bool(fused_policy)
+        self._pol_dims, self._pol_params = None, None
         self.allreduce_events = None  # a list to time the per-minibatch all-reduce (bench.py --workload ppo)
         self.total_env_steps = 0.0
         self.start = time.time()
@@ -458,10 +510,15 @@ class PPOTrainer:
         relative to the env's device counter base (the body is being captured)."""
         bf, env = self._buf, self.env
         native = bf["obs"].is_cuda  # normalisation and the policy head as two native launches
+        fused = native and self._pol_dims is not None  # ... or the whole policy as one (mjl_policy_fwd)
         for t in range(self.cfg.rollout_length):
             if self.jax_keys:
                 self._jax_step_keys()
-            if native:
+            if fused:
+                policy_fwd_native(bf["obs"][t], self.rms.mean, self.rms.var, 10.0, self._pol_params, self._pol_dims,
+                                  self.policy.log_std, bf["eps"][t], bf["act"][t], bf["logp"][t])
+                act = bf["act"][t]
+            elif native:
                 obs_normalize_native(bf["obs"][t], self.rms.mean, self.rms.var, 10.0, bf["xn"])
                 act = bf["act"][t]
                 policy_head_native(self.policy.mlp(bf["xn"]), self.policy.log_std, bf["eps"][t], act, bf["logp"][t])
@@ -486,6 +543,13 @@ class PPOTrainer:
         otherwise): the sampling noise for all T steps is drawn before it, and the env RNG counters
         come from the env's device counter base, so a replay is bit-identical to the eager loop."""
         bf, env, T = self._rollout_buffers(), self.env, self.cfg.rollout_length
+        if self._pol_dims is None and self.fused_policy and bf["obs"].is_cuda:
+            self._pol_dims = policy_fused_dims(self.policy)
+        if self._pol_dims is not None:  # the policy changed in the update: repack into the static buffer
+            if self._pol_params is None:
+                self._pol_params = pack_policy_params(self.policy)
+            else:
+                pack_policy_params(self.policy, out=self._pol_params)
         bf["eps"].normal_(generator=self.gen)
         bf["obs"][0].copy_(self.obs)
         if self.jax_keys:

@@ -275,6 +275,73 @@ def test_native_rollout_head_matches_formulas():
         torch.testing.assert_close(lp, ppo.gaussian_logprob(mean, s, act), rtol=1e-5, atol=1e-3)
 
 
+def test_policy_pack_layout():
+    """mjl_policy_fwd's parameter layout (pack_policy_params): WP[k // 4, n, k % 4] = weight[n, k]
+    zero-padded to multiples of 16, bias after each layer; length = mjl_policy_param_floats."""
+    import ctypes as C
+    from mjx_amd._lib import lib
+    g = torch.Generator().manual_seed(9)
+    pol = ppo.GaussianPolicy(54, 21, [(256, "tanh"), (256, "tanh"), (256, "tanh")], 0.0, g)
+    for lin in pol.mlp.layers:
+        with torch.no_grad():
+            lin.bias.normal_(generator=g)
+    dims = ppo.policy_fused_dims(pol)
+    assert dims == [54, 256, 256, 256, 21]
+    flat = ppo.pack_policy_params(pol)
+    assert flat.numel() == lib().mjl_policy_param_floats(len(dims) - 1, (C.c_int * len(dims))(*dims))
+    off = 0
+    for lin in pol.mlp.layers:
+        n, k = lin.weight.shape
+        kp, np_ = -(-k // 16) * 16, -(-n // 16) * 16
+        wp = flat[off:off + kp * np_].reshape(kp // 4, np_, 4)
+        w = torch.zeros(kp, np_)
+        w[:k, :n] = lin.weight.detach().t()
+        for kk in (0, 1, k - 1):
+            for nn_ in (0, 7, n - 1):
+                assert wp[kk // 4, nn_, kk % 4] == lin.weight[nn_, kk]
+        assert torch.equal(wp.permute(0, 2, 1).reshape(kp, np_), w)
+        b = flat[off + kp * np_:off + kp * np_ + np_]
+        assert torch.equal(b[:n], lin.bias.detach()) and torch.all(b[n:] == 0)
+        off += kp * np_ + np_
+    assert ppo.policy_fused_dims(ppo.GaussianPolicy(54, 21, [(300, "tanh")], 0.0, g)) is None   # > 256
+    assert ppo.policy_fused_dims(ppo.GaussianPolicy(54, 21, [(64, "relu")], 0.0, g)) is None    # not tanh
+
+
+@pytest.mark.gpu
+def test_fused_rollout_policy_matches_torch_path():
+    """mjl_policy_fwd (normalisation + MLP on the matrix cores + head + sampling + log-prob, one
+    launch) = obs_normalize_native -> policy.mlp (torch GEMMs) -> policy_head_native up to the GEMMs'
+    fp32 accumulation order; the reference-size policy at 2048 envs, a ragged batch, and a
+    different shape (obs 17, hidden 64 / 48, act 6)."""
+    g = torch.Generator().manual_seed(4)
+    gd = torch.Generator(device="cuda").manual_seed(4)
+    for obs_dim, hid, act_dim, B in ((54, [256, 256, 256], 21, 2048), (54, [256, 256, 256], 21, 37),
+                                     (17, [64, 48], 6, 100)):
+        pol = ppo.GaussianPolicy(obs_dim, act_dim, [(h, "tanh") for h in hid], 0.0, g)
+        with torch.no_grad():
+            for lin in pol.mlp.layers:
+                lin.bias.normal_(0.0, 0.3, generator=g)
+            pol.log_std.copy_(torch.linspace(-1.0, 0.5, act_dim))
+        pol = pol.cuda()
+        x = torch.randn((B, obs_dim), generator=gd, device="cuda") * 3
+        rms = ppo.RunningMeanStd(obs_dim, "cuda")
+        rms.mean.copy_(torch.randn(obs_dim, generator=gd, device="cuda"))
+        rms.var.copy_(torch.rand(obs_dim, generator=gd, device="cuda") + 0.5)
+        eps = torch.randn((B, act_dim), generator=gd, device="cuda")
+        dims = ppo.policy_fused_dims(pol)
+        params = ppo.pack_policy_params(pol)
+        act, lp = torch.empty((B, act_dim), device="cuda"), torch.empty(B, device="cuda")
+        ppo.policy_fwd_native(x, rms.mean, rms.var, 10.0, params, dims, pol.log_std, eps, act, lp)
+        xn = torch.empty_like(x)
+        ppo.obs_normalize_native(x, rms.mean, rms.var, 10.0, xn)
+        with torch.no_grad():
+            z = pol.mlp(xn)
+        act_ref, lp_ref = torch.empty_like(act), torch.empty_like(lp)
+        ppo.policy_head_native(z, pol.log_std, eps, act_ref, lp_ref)
+        torch.testing.assert_close(act, act_ref, rtol=0, atol=2e-5)
+        torch.testing.assert_close(lp, lp_ref, rtol=1e-5, atol=1e-4)
+
+
 @pytest.mark.gpu
 def test_native_colsum_matches_torch():
     """mjl_colsum (bias gradients, split-K sums of the update) equals x.sum(0) in fp64 to fp32
