@@ -173,8 +173,10 @@ int mjl_batch_nenv(const mjlBatch* batch);
  * as executed (what jax.grad through MJX's fixed-count solver computes; reference train_apg.py:
  * 101-105,187-189 runs CG 4/4) instead of the implicit derivative at the converged active set; the
  * integrator's input is then qfrc_smooth + qfrc_constraint of the stopped solve. The VJP must see
- * the pre-step qacc_warmstart the forward step saw (the recompute replays that solve). */
-enum { MJL_OPT_STORE_DERIVED = 0, MJL_OPT_FORCE_GLOBAL_ROWS = 1, MJL_OPT_VJP_UNROLLED = 2 };
+ * the pre-step qacc_warmstart the forward step saw (the recompute replays that solve).
+ * MJL_OPT_RESET_POOL (default 0): value = slots per env (<= 64) of the reset pool that
+ * mjl_env_fill_reset_pool fills (call outside stream capture; 0 frees it). */
+enum { MJL_OPT_STORE_DERIVED = 0, MJL_OPT_FORCE_GLOBAL_ROWS = 1, MJL_OPT_VJP_UNROLLED = 2, MJL_OPT_RESET_POOL = 3 };
 int mjl_batch_set_option(mjlBatch* batch, int option, int value);
 
 /* Copy a per-env field to / from a device buffer [nenv, dim] (async on stream). `mask` (device,
@@ -205,6 +207,16 @@ int mjl_env_config(mjlBatch* batch, const mjlEnvConfig* cfg);
  * the post-reset observation, exactly as merge_if_done does; rew/term/trunc stay the step's. */
 int mjl_env_step(mjlBatch* batch, const float* act, float* obs, float* rew, float* term,
                  float* trunc, int auto_reset, uint64_t seed, uint64_t counter, void* stream);
+
+/* Reset pool: the v_reset half of train_ppo.py:147-161's merge_if_done, moved off the step's
+ * critical path. A reset does not depend on the state it replaces, so resets can be computed in bulk
+ * (full-occupancy launches) instead of one wave at a time at the end of a finishing env's step:
+ * this fills slots 0..n-1 of every env (n = min(*dev_n, slots), device int read at execution
+ * time), slot j drawn from (seed, (counter + j) ^ 2^63, env) with the same single_reset semantics
+ * (src/envs.py:115-202). Each later mjl_env_step(auto_reset=1) merges a finished env's next unused
+ * slot; an env whose slots are used up resets in place from (seed, step counter, env) as before.
+ * Requires MJL_OPT_RESET_POOL; not for key-drawn resets (mjl_env_set_reset_keys). */
+int mjl_env_fill_reset_pool(mjlBatch* batch, const int* dev_n, uint64_t seed, uint64_t counter, void* stream);
 
 /* RNG counter base for hipGraph capture of env steps / resets: if dev_counter_base (a device
  * uint64, may be NULL to detach) is set, the kernels draw with counter = the call's `counter` +

@@ -64,6 +64,11 @@ struct mjlBatch {
   const unsigned long long* ctr_base;  // device RNG counter base (mjl_batch_set_counter_base), or null
   const uint32_t* reset_keys;           // per-env jax.random reset keys (mjl_env_set_reset_keys), or null
   int key_mode;
+  float* d_rs;     // MJL_OPT_RESET_POOL: pool slots (the state fields again, [slots * nenv] rows) + obs
+  int* d_pool_ctl;  // [nenv, 2] next slot, filled slots
+  int pool_slots;
+  StateBuf rs;
+  float* rs_obs;
 };
 
 extern "C" {
@@ -395,6 +400,7 @@ void mjl_batch_destroy(mjlBatch* B) {
   (void)hipFree(B->d_state); (void)hipFree(B->d_model); (void)hipFree(B->d_env); (void)hipFree(B->d_scratch);
   (void)hipFree(B->d_adj_scratch);
   (void)hipFree(B->d_unr);
+  (void)hipFree(B->d_rs); (void)hipFree(B->d_pool_ctl);
   delete B;
 }
 
@@ -408,6 +414,38 @@ int mjl_batch_set_option(mjlBatch* B, int option, int value) {
     if (value && B->model->desc.iterations > 256)
       return fail(MJL_ERR_ARG, "unrolled VJP: %d solver iterations (at most 256 are taped)", B->model->desc.iterations);
     B->vjp_unrolled = value != 0;
+    return MJL_OK;
+  }
+  if (option == MJL_OPT_RESET_POOL) {
+    if (value < 0 || value > 64) return fail(MJL_ERR_ARG, "reset pool: 0..64 slots per env");
+    HIPCHK(hipSetDevice(B->device));
+    (void)hipFree(B->d_rs); (void)hipFree(B->d_pool_ctl);
+    B->d_rs = nullptr; B->d_pool_ctl = nullptr; B->pool_slots = 0;
+    if (!value) return MJL_OK;
+    const size_t rows = (size_t)value * B->nenv;
+    size_t total = 0;
+    for (int f = 0; f < MJL_NFIELD; f++) total += (size_t)B->dim[f] * rows;
+    const size_t obs_floats = (size_t)64 * rows;  // obs_dim <= 64 (mjl_env_config)
+    hipError_t e = hipMalloc(&B->d_rs, (total + obs_floats) * sizeof(float));
+    if (e == hipSuccess) e = hipMalloc(&B->d_pool_ctl, (size_t)B->nenv * 2 * sizeof(int));
+    if (e == hipSuccess) e = hipMemset(B->d_pool_ctl, 0, (size_t)B->nenv * 2 * sizeof(int));  // empty
+    if (e != hipSuccess) {
+      (void)hipFree(B->d_rs); (void)hipFree(B->d_pool_ctl);
+      B->d_rs = nullptr; B->d_pool_ctl = nullptr;
+      return fail(MJL_ERR_HIP, "reset pool: %s", hipGetErrorString(e));
+    }
+    float* f[MJL_NFIELD];
+    size_t off = 0;
+    for (int k = 0; k < MJL_NFIELD; k++) { f[k] = B->d_rs + off; off += (size_t)B->dim[k] * rows; }
+    StateBuf& r = B->rs;
+    r.qpos = f[MJL_FIELD_QPOS]; r.qvel = f[MJL_FIELD_QVEL]; r.qacc_warmstart = f[MJL_FIELD_QACC_WARMSTART];
+    r.time = f[MJL_FIELD_TIME]; r.ctrl = f[MJL_FIELD_CTRL]; r.aux = f[MJL_FIELD_AUX]; r.qacc = f[MJL_FIELD_QACC];
+    r.xpos = f[MJL_FIELD_XPOS]; r.xquat = f[MJL_FIELD_XQUAT]; r.qfrc_actuator = f[MJL_FIELD_QFRC_ACTUATOR];
+    r.sensordata = f[MJL_FIELD_SENSORDATA]; r.stats = f[MJL_FIELD_STATS]; r.qfrc_bias = f[MJL_FIELD_QFRC_BIAS];
+    r.qfrc_passive = f[MJL_FIELD_QFRC_PASSIVE]; r.qfrc_constraint = f[MJL_FIELD_QFRC_CONSTRAINT];
+    r.qacc_smooth = f[MJL_FIELD_QACC_SMOOTH];
+    B->rs_obs = B->d_rs + total;
+    B->pool_slots = value;
     return MJL_OK;
   }
   return fail(MJL_ERR_ARG, "unknown option %d", option);
@@ -505,6 +543,7 @@ extern "C" int mjl_set_state(mjlBatch* B, const float* src, const float* ws_src,
 static KParams make_params(mjlBatch* B) {
   KParams P;
   std::memset(&P, 0, sizeof(P));
+  P.pool_slot = -1;
   P.m = B->d_model;
   P.env = B->d_env;
   P.s = B->s;
@@ -586,6 +625,7 @@ int mjl_env_config(mjlBatch* B, const mjlEnvConfig* cfg) {
     return fail(MJL_ERR_ARG, "obs_perm is not a permutation");
   HIPCHK(hipSetDevice(B->device));
   HIPCHK(hipMemcpy(B->d_env, cfg, sizeof(mjlEnvConfig), hipMemcpyHostToDevice));
+  if (B->d_pool_ctl) HIPCHK(hipMemset(B->d_pool_ctl, 0, (size_t)B->nenv * 2 * sizeof(int)));  // drawn under the old config
   B->has_env = 1;
   B->obs_dim = cfg->obs_dim;
   return MJL_OK;
@@ -600,7 +640,39 @@ int mjl_env_step(mjlBatch* B, const float* act, float* obs, float* rew, float* t
   P.auto_reset = auto_reset;
   P.seed_lo = (uint32_t)seed; P.seed_hi = (uint32_t)(seed >> 32);
   P.ctr_lo = (uint32_t)counter; P.ctr_hi = (uint32_t)(counter >> 32);
+  if (B->d_pool_ctl && auto_reset) { P.rs = B->rs; P.rs_obs = B->rs_obs; P.pool_ctl = B->d_pool_ctl; }
   return launch<MODE_ENV_STEP>(B, P, stream);
+}
+
+int mjl_env_fill_reset_pool(mjlBatch* B, const int* dev_n, uint64_t seed, uint64_t counter, void* stream) {
+  if (!B || !dev_n) return fail(MJL_ERR_ARG, "bad argument");
+  if (!B->has_env) return fail(MJL_ERR_ARG, "mjl_env_config not called");
+  if (!B->d_pool_ctl) return fail(MJL_ERR_ARG, "MJL_OPT_RESET_POOL not set");
+  if (B->reset_keys) return fail(MJL_ERR_ARG, "resets drawn from jax.random keys are not pooled");
+  for (int j = 0; j < B->pool_slots; j++) {  // one launch per slot: each uses the batch's per-env scratch
+    KParams P = make_params(B);
+    const size_t rows = (size_t)j * B->nenv;
+    StateBuf& r = P.s;
+    r = B->rs;
+    r.qpos += rows * B->dim[MJL_FIELD_QPOS]; r.qvel += rows * B->dim[MJL_FIELD_QVEL];
+    r.qacc_warmstart += rows * B->dim[MJL_FIELD_QACC_WARMSTART]; r.time += rows * B->dim[MJL_FIELD_TIME];
+    r.ctrl += rows * B->dim[MJL_FIELD_CTRL]; r.aux += rows * B->dim[MJL_FIELD_AUX];
+    r.qacc += rows * B->dim[MJL_FIELD_QACC]; r.xpos += rows * B->dim[MJL_FIELD_XPOS];
+    r.xquat += rows * B->dim[MJL_FIELD_XQUAT]; r.qfrc_actuator += rows * B->dim[MJL_FIELD_QFRC_ACTUATOR];
+    r.sensordata += rows * B->dim[MJL_FIELD_SENSORDATA]; r.stats += rows * B->dim[MJL_FIELD_STATS];
+    r.qfrc_bias += rows * B->dim[MJL_FIELD_QFRC_BIAS]; r.qfrc_passive += rows * B->dim[MJL_FIELD_QFRC_PASSIVE];
+    r.qfrc_constraint += rows * B->dim[MJL_FIELD_QFRC_CONSTRAINT];
+    r.qacc_smooth += rows * B->dim[MJL_FIELD_QACC_SMOOTH];
+    P.obs = B->rs_obs + rows * B->obs_dim;
+    P.pool_ctl = B->d_pool_ctl; P.pool_n = dev_n; P.pool_slot = j; P.pool_slots = B->pool_slots;
+    P.store_derived = 1;  // the consuming step may store derived fields
+    const uint64_t c = (counter + (uint64_t)j) ^ (1ull << 63);  // a counter domain of its own
+    P.seed_lo = (uint32_t)seed; P.seed_hi = (uint32_t)(seed >> 32);
+    P.ctr_lo = (uint32_t)c; P.ctr_hi = (uint32_t)(c >> 32);
+    int rc = launch<MODE_ENV_RESET>(B, P, stream);
+    if (rc != MJL_OK) return rc;
+  }
+  return MJL_OK;
 }
 
 int mjl_batch_set_counter_base(mjlBatch* B, const uint64_t* dev_counter_base) {

@@ -143,6 +143,13 @@ struct KParams {
   const unsigned long long* ctr_base;  // device counter base added to (ctr_hi, ctr_lo), or null
   const uint32_t* keys;                // per-env jax.random reset keys [nenv, 2], or null
   int key_mode;                        // MJL_RNG_* of `keys`
+  // reset pool (mjl_env_fill_reset_pool): slot j of env e is row j * nenv + e of `rs` / rs_obs
+  StateBuf rs;
+  float* rs_obs;    // [slots * nenv, obs_dim]
+  int* pool_ctl;    // [nenv, 2]: next unused slot, filled slots; null = no pool
+  const int* pool_n;  // fill: slots to fill (device int, read at execution time)
+  int pool_slot;    // fill: the slot this launch draws (-1: not a fill)
+  int pool_slots;   // fill: pool capacity (slots per env)
 };
 
 }  // namespace mjl

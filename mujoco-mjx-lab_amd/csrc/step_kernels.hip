@@ -2205,8 +2205,9 @@ template <class D> NOINL void env_reset(MP m_, LDSA WS<D>* W, const EnvArgs* Ap,
 }
 
 // post-step part of single_step (envs.py:347-492): reward, termination, aux, obs
+// (skip_done_obs: finished envs' observations are replaced by the auto-reset's, so not written)
 template <class D> PHASE void env_post(MP m_, LDSA WS<D>* W, const mjlEnvConfig* cfg, LDSA float* aux, float* obs,
-                                       int lane) {
+                                       int lane, bool skip_done_obs) {
   MP m = uniform_ptr(m_);
   CP c = (CP)cfg;
   float pw = 0.f, st = 0.f;  // energy terms over the actuated hinge dofs (mean over nv - 6)
@@ -2264,7 +2265,44 @@ template <class D> PHASE void env_post(MP m_, LDSA WS<D>* W, const mjlEnvConfig*
     for (int i = 0; i < MJL_AUX_DIM; i++) aux[i] = a[i];
   }
   SYNC();
-  write_obs<D>(m, W, c, obs, lane);
+  if (!(skip_done_obs && W->sc[SC_DONE] > 0.5f)) write_obs<D>(m, W, c, obs, lane);
+}
+
+// merge a pooled reset (mjl_env_fill_reset_pool, row = slot * nenv + env) into the wave: the
+// state, aux, observation and (store_derived) the derived fields an in-place env_reset leaves
+template <class D> INL void rs_load(MP m, const KParams& P, LDSA WS<D>* W, LDSA float* aux, float* obs, size_t env,
+                                    int lane) {
+  const StateBuf& R = P.rs;
+  const int nq = m->nq, nv = m->nv, nu = m->nu, nb = m->nbody;
+  if (lane < nq) W->qpos[lane] = R.qpos[(size_t)env * nq + lane];
+  if (lane < nv) {
+    const size_t o = (size_t)env * nv + lane;
+    W->qvel[lane] = R.qvel[o]; W->qacc_ws[lane] = R.qacc_warmstart[o];
+    if (P.store_derived) {
+      W->qacc[lane] = R.qacc[o]; W->frc_act[lane] = R.qfrc_actuator[o]; W->frc_bias[lane] = R.qfrc_bias[o];
+      W->frc_passive[lane] = R.qfrc_passive[o]; W->frc_con[lane] = R.qfrc_constraint[o];
+      W->qacc_smooth[lane] = R.qacc_smooth[o];
+    }
+  }
+  if (lane < nu) W->ctrl[lane] = R.ctrl[(size_t)env * nu + lane];
+  if (lane < MJL_AUX_DIM) aux[lane] = R.aux[(size_t)env * MJL_AUX_DIM + lane];
+  const int od = P.env->obs_dim;
+  if (lane < od) obs[lane] = P.rs_obs[(size_t)env * od + lane];
+  if (P.store_derived) {
+    for (int i = lane; i < nb * 3; i += 64) W->xpos[i / 3][i % 3] = R.xpos[(size_t)env * nb * 3 + i];
+    for (int i = lane; i < nb * 4; i += 64) W->xquat[i / 4][i % 4] = R.xquat[(size_t)env * nb * 4 + i];
+    if (lane < m->nsensordata) W->sens[lane] = R.sensordata[(size_t)env * m->nsensordata + lane];
+  }
+  if (lane == 0) {
+    W->sc[SC_TIME] = R.time[env];
+    W->sc[SC_HEIGHT] = R.stats[(size_t)env * 4 + 3];  // a pool slot keeps the pelvis height there
+    if (P.store_derived) {
+      W->ncon = (int)R.stats[(size_t)env * 4 + 0];
+      W->nefc = (int)R.stats[(size_t)env * 4 + 1];
+      W->niter = (int)R.stats[(size_t)env * 4 + 2];
+    }
+  }
+  SYNC();
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -2281,6 +2319,11 @@ template <class D, int MODE> __global__ __launch_bounds__(64, MJL_MINWAVES) void
   const int lane = threadIdx.x;
   if (env >= P.nenv) return;
   if ((MODE == MODE_FORWARD || MODE == MODE_ENV_RESET) && P.mask && !(P.mask[env] > 0.5f)) return;
+  if (MODE == MODE_ENV_RESET && P.pool_slot >= 0) {  // reset-pool fill: slot pool_slot of this env
+    const int n = min(*P.pool_n, P.pool_slots);
+    if (P.pool_slot == 0 && lane == 0) { P.pool_ctl[2 * env] = 0; P.pool_ctl[2 * env + 1] = n; }
+    if (P.pool_slot >= n) return;
+  }
   const int nq = m->nq, nv = m->nv, nu = m->nu;
   const StateBuf& S = P.s;
   EnvArgs A;
@@ -2336,14 +2379,25 @@ template <class D, int MODE> __global__ __launch_bounds__(64, MJL_MINWAVES) void
     STAMP(8, lane);
     if (MODE == MODE_ENV_STEP) {
       float* obs = P.obs + (size_t)env * P.env->obs_dim;
-      env_post<D>(m, W, P.env, aux, obs, lane);
+      env_post<D>(m, W, P.env, aux, obs, lane, P.auto_reset != 0);
       if (lane == 0) { P.rew[env] = W->sc[SC_REW]; P.term[env] = W->sc[SC_TERM]; P.trunc[env] = W->sc[SC_TRUNC]; }
       bool bad = (lane < nq && !isfinite(W->qpos[lane])) || (lane < nv && !isfinite(W->qvel[lane]));
       bool anybad = __ballot(bad) != 0ull;
       if (lane == 0) W->sc[SC_NAN] = anybad ? 1.f : 0.f;
       SYNC();
-      if (P.auto_reset && W->sc[SC_DONE] > 0.5f)  // merge_if_done (train_ppo.py:154-161)
-        env_reset<D>(m, W, &A, env, lane, aux, obs);
+      if (P.auto_reset && W->sc[SC_DONE] > 0.5f) {  // merge_if_done (train_ppo.py:154-161)
+        int slot = -1;  // the env's next pooled reset, if one is left (key-drawn resets are never pooled)
+        if (P.pool_ctl && !P.keys) {
+          const int cur = P.pool_ctl[2 * env], lim = P.pool_ctl[2 * env + 1];
+          slot = __builtin_amdgcn_readfirstlane(cur < lim ? cur : -1);
+        }
+        if (slot >= 0) {
+          rs_load<D>(m, P, W, aux, obs, (size_t)slot * P.nenv + env, lane);
+          if (lane == 0) P.pool_ctl[2 * env] = slot + 1;
+        } else {
+          env_reset<D>(m, W, &A, env, lane, aux, obs);
+        }
+      }
     }
   }
   SYNC();
@@ -2382,6 +2436,7 @@ template <class D, int MODE> __global__ __launch_bounds__(64, MJL_MINWAVES) void
       S.stats[(size_t)env * 4 + 3] = (MODE == MODE_ENV_STEP) ? W->sc[SC_NAN] : W->sc[SC_NACT];
     }
   }
+  if (MODE == MODE_ENV_RESET && P.pool_slot >= 0 && lane == 0) S.stats[(size_t)env * 4 + 3] = W->sc[SC_HEIGHT];
 }
 
 }  // namespace mjl

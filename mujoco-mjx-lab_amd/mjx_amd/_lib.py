@@ -25,7 +25,7 @@ EXPORTS = [
     "mjl_env_set_reset_keys", "mjl_prng_split", "mjl_env_step_vjp_guarded", "mjl_state_size", "mjl_get_state",
     "mjl_set_state", "mjl_obs_normalize", "mjl_policy_head", "mjl_colsum_scratch", "mjl_colsum",
     "mjl_policy_param_floats", "mjl_policy_fwd",
-    "mjl_step_vjp_full", "mjl_env_step_vjp_full",
+    "mjl_step_vjp_full", "mjl_env_step_vjp_full", "mjl_env_fill_reset_pool",
 ]
 
 _lib = None
@@ -83,6 +83,7 @@ def lib() -> C.CDLL:
     L.mjl_env_config.argtypes = [vp, P(abi.EnvConfigC)]
     L.mjl_env_step.argtypes = [vp, f32p, f32p, f32p, f32p, f32p, i32, u64, u64, vp]
     L.mjl_env_reset.argtypes = [vp, f32p, u64, u64, f32p, f32p, vp]
+    L.mjl_env_fill_reset_pool.argtypes = [vp, vp, u64, u64, vp]
     L.mjl_batch_set_counter_base.argtypes = [vp, vp]
     L.mjl_env_set_reset_keys.argtypes = [vp, vp, i32]
     L.mjl_env_step_vjp_guarded.argtypes = [vp] + [vp] * 10 + [vp]

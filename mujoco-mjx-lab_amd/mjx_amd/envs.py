@@ -87,6 +87,19 @@ class HumanoidEnv:
                                   _ptr(self.obs), _stream()))
         return self.obs
 
+    def enable_reset_pool(self, slots: int = 16):
+        """Allocate `slots` pooled resets per env (MJL_OPT_RESET_POOL); outside stream capture."""
+        self.data.set_option(abi.OPT_RESET_POOL, int(slots))
+        self.pool_slots = int(slots)
+
+    def fill_reset_pool(self, n: torch.Tensor, counter: Optional[int] = None):
+        """Compute min(n, slots) resets per env in bulk (mjl_env_fill_reset_pool; n: device int32 [1],
+        read at execution time); the next auto-resets of step() merge them in order. `counter`:
+        the draw's counter (relative to ctr_base under graph capture); default the current counter,
+        which the pool's own counter domain keeps apart from the steps' draws."""
+        check(lib().mjl_env_fill_reset_pool(self.data.handle, C.c_void_p(n.data_ptr()), self.seed,
+                                            self.counter if counter is None else int(counter), _stream()))
+
     def step(self, act: torch.Tensor, auto_reset: bool = True,
              out: Optional[Tuple[torch.Tensor, ...]] = None, counter: Optional[int] = None) -> Tuple[torch.Tensor, ...]:
         """v_step (src/envs.py:333-495) fused with merge_if_done (train_ppo.py:147-161).

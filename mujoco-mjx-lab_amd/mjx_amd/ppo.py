@@ -416,12 +416,17 @@ class PPOTrainer:
     with auto-reset (HumanoidEnv, or a stand-in in CPU tests), obs_dim, act_dim, num_envs."""
 
     def __init__(self, cfg, env, eval_env=None, device="cuda", dist=None, out_dir: Optional[str] = None,
-                 use_graph: bool = True, jax_keys: bool = False, fused_policy: bool = True):
+                 use_graph: bool = True, jax_keys: bool = False, fused_policy: bool = True,
+                 reset_pool: int = 16):
         """jax_keys: draw every env reset (initial, auto-reset, eval) from the jax.random key chain
         train_ppo.py derives from cfg.seed (:88-118, :132/:150-151 per rollout step, :325, :359,
         :419, eval :268-293), so the reset stream equals the reference's for the same seed.
         fused_policy: the rollout's normalisation + policy MLP + head as one launch (mjl_policy_fwd)
-        when the network fits it; False keeps normalisation launch + torch MLP + head launch."""
+        when the network fits it; False keeps normalisation launch + torch MLP + head launch.
+        reset_pool: up to this many auto-resets per env and rollout are computed in bulk before the
+        rollout (mjl_env_fill_reset_pool; as many as the busiest env used last rollout, + 1) and
+        merged by the env steps, instead of each finishing env resetting at the end of its step;
+        0 = in place only. Not with jax_keys (those resets are drawn per step)."""
         self.cfg, self.env, self.eval_env, self.dist = cfg, env, eval_env, dist
         self.rank = dist.get_rank() if dist is not None else 0
         self.world = dist.get_world_size() if dist is not None else 1
@@ -450,6 +455,10 @@ class PPOTrainer:
         self._buf, self._graph, self._rollouts = None, None, 0
         self.fused_policy = bool(fused_policy)
         self._pol_dims, self._pol_params = None, None
+        self._pool_n = None  # device int: pooled resets per env for the next rollout
+        if reset_pool > 0 and not self.jax_keys and self.device.type == "cuda" and hasattr(env, "enable_reset_pool"):
+            env.enable_reset_pool(int(reset_pool))
+            self._pool_n = torch.full((1,), min(4, int(reset_pool)), dtype=torch.int32, device=self.device)
         self.allreduce_events = None  # a list to time the per-minibatch all-reduce (bench.py --workload ppo)
         self.total_env_steps = 0.0
         self.start = time.time()
@@ -509,6 +518,8 @@ class PPOTrainer:
         obs[t + 1], rew / term / trunc [t] in place (no copies). With graph=True the RNG counters are
         relative to the env's device counter base (the body is being captured)."""
         bf, env = self._buf, self.env
+        if self._pool_n is not None:  # this rollout's auto-resets, in bulk (counter 0: see fill_reset_pool)
+            env.fill_reset_pool(self._pool_n, counter=0 if graph else None)
         native = bf["obs"].is_cuda  # normalisation and the policy head as two native launches
         fused = native and self._pol_dims is not None  # ... or the whole policy as one (mjl_policy_fwd)
         for t in range(self.cfg.rollout_length):
@@ -567,6 +578,9 @@ class PPOTrainer:
         else:
             self._rollout_body(graph=False)
         self._rollouts += 1
+        if self._pool_n is not None:  # next rollout's pool: the busiest env's auto-resets + 1 (no host sync)
+            busiest = (torch.maximum(bf["term"], bf["trunc"]) > 0.5).sum(0).max()
+            self._pool_n.copy_(torch.clamp(busiest + 1, max=self.env.pool_slots))
         self.obs = bf["obs"][T]
         return bf["obs"][:T], bf["act"], bf["logp"], bf["rew"], bf["term"], bf["trunc"]
 

@@ -410,6 +410,10 @@ def test_graph_rollout_bit_identical_to_eager():
                           use_graph=g, jax_keys=jk) for g, jk in ((False, False), (True, False))]
     trs += [ppo.PPOTrainer(cfg, HumanoidEnv(mjx.put_model(m), ecfg, cfg.num_envs, seed=11), None, device="cuda",
                            use_graph=g, jax_keys=True) for g in (False, True)]
+    # the first two pool their auto-resets (reset_pool, default 16); these two reset in place only
+    trs += [ppo.PPOTrainer(cfg, HumanoidEnv(mjx.put_model(m), ecfg, cfg.num_envs, seed=11), None, device="cuda",
+                           use_graph=g, jax_keys=False, reset_pool=0) for g in (False, True)]
+    assert trs[0]._pool_n is not None and trs[2]._pool_n is None and trs[4]._pool_n is None
     for it in range(3):
         outs = []
         for tr in trs:
@@ -421,6 +425,8 @@ def test_graph_rollout_bit_identical_to_eager():
             assert torch.equal(a, b), f"rollout {it}"
         for a, b in zip(outs[2], outs[3]):  # jax-key resets: keys split inside the captured steps
             assert torch.equal(a, b), f"rollout {it} (jax keys)"
+        for a, b in zip(outs[4], outs[5]):
+            assert torch.equal(a, b), f"rollout {it} (in-place resets)"
         assert outs[0][5].sum() > 0  # truncations happened
 
 

@@ -27,6 +27,7 @@ def main():
     ap.add_argument("--iters", type=int, default=3)
     ap.add_argument("--seed", type=int, default=42)
     ap.add_argument("--no-fused-policy", action="store_true", help="rollout policy as normalise + torch MLP + head")
+    ap.add_argument("--reset-pool", type=int, default=16, help="pooled auto-resets per env (0: in place only)")
     a = ap.parse_args()
     cfg = reference_ppo_config()
     cfg.num_envs, cfg.rollout_length, cfg.seed = a.envs, a.rollout, a.seed
@@ -34,7 +35,8 @@ def main():
     sys_ = mjx.put_model(m)
     ecfg = resolve_ids(m, cfg.env_config)
     env = HumanoidEnv(sys_, ecfg, cfg.num_envs, seed=cfg.seed)
-    tr = ppo.PPOTrainer(cfg, env, None, device="cuda", fused_policy=not a.no_fused_policy)
+    tr = ppo.PPOTrainer(cfg, env, None, device="cuda", fused_policy=not a.no_fused_policy,
+                        reset_pool=a.reset_pool)
     tr.iteration(0)  # warm-up (GEMM heuristics, allocator)
     tr.iteration(0)  # second rollout captures the rollout hipGraph
     res, t_roll = [], []
