@@ -325,6 +325,25 @@ int mjl_policy_fwd(const float* obs, const float* mean, const float* var, float 
                    const int* dims, const float* log_std, const float* eps, int B, float* act, float* logp,
                    void* stream);
 
+/* APG rollout bookkeeping (train_apg.py:161-209; the sweep of mjx_amd/apg.py), one launch each per
+ * rollout step. alive / alive_snap: uint8 [nenv] (0/1); device pointers, float32, row-major.
+ * mjl_apg_obs: o [nenv, nq + nv] = [qpos | qvel] of each env (the APG observation); on = the policy
+ *   input: x = alive ? o : 0, and with use_norm clip((x - mean) / (sqrt(var) + 1e-8), -10, 10)
+ *   (train_apg.py:171-176); alive_snap = alive (for the backward).
+ * mjl_apg_post: after the env step, per env: ok = rew, qpos, qvel finite (and max|qvel| <=
+ *   diverge_qvel if > 0); bad = alive && !ok; dropped += bad; alive &= !bad; d = alive ? disc : 0;
+ *   grew = -d / nenv (the reward's loss cotangent); ret += alive ? d rew : 0; rfin = rew if finite
+ *   else 0; disc = d gamma (1 - max(term, trunc)); alive &= disc != 0.
+ * mjl_apg_obs_vjp: g_qpos / g_qvel += (d on / d o)^T go at (o, alive_snap): zero where not alive,
+ *   outside the clip, else go / (sqrt(var) + 1e-8) (go itself without use_norm). */
+int mjl_apg_obs(mjlBatch* batch, const uint8_t* alive, const float* mean, const float* var, int use_norm, float* o,
+                float* on, uint8_t* alive_snap, void* stream);
+int mjl_apg_post(mjlBatch* batch, const float* rew, const float* term, const float* trunc, float gamma,
+                 float diverge_qvel, uint8_t* alive, float* disc, float* ret, float* dropped, float* grew, float* rfin,
+                 void* stream);
+int mjl_apg_obs_vjp(int nenv, int nq, int nv, const float* o, const uint8_t* alive_snap, const float* mean,
+                    const float* var, int use_norm, const float* go, float* g_qpos, float* g_qvel, void* stream);
+
 /* PPO update (train_ppo.py:233-252, the bias-gradient column sums of every dense layer's backward
  * in value_and_grad of ppo_loss_fn / value_loss_fn, and the split-K weight-gradient sum):
  * out[d] = sum over rows of x[n, d] (row-major, float32, device), in a fixed order (two launches

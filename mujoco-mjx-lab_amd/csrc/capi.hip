@@ -12,6 +12,7 @@
 #include "step_kernels.hip"
 #include "adjoint.hip"
 #include "ppo_kernels.hip"
+#include "apg_kernels.hip"
 
 using namespace mjl;
 
@@ -921,6 +922,45 @@ extern "C" int mjl_prng_split(const uint32_t* keys, int n, int num, int mode, ui
   if (n == 0) return MJL_OK;
   hipLaunchKernelGGL(prng_split_kernel, dim3((n * num + 255) / 256), dim3(256), 0, (hipStream_t)stream, keys, n, num,
                      mode, out);
+  HIPCHK(hipGetLastError());
+  return MJL_OK;
+}
+
+// ---------------------------------------------------------------- APG rollout bookkeeping
+extern "C" int mjl_apg_obs(mjlBatch* B, const uint8_t* alive, const float* mean, const float* var, int use_norm,
+                           float* o, float* on, uint8_t* alive_snap, void* stream) {
+  if (!B || !alive || !o || !on || !alive_snap || (use_norm && (!mean || !var))) return fail(MJL_ERR_ARG, "bad argument");
+  HIPCHK(hipSetDevice(B->device));
+  const int nq = B->model->desc.nq, nv = B->model->desc.nv;
+  const long n = (long)B->nenv * (nq + nv);
+  hipLaunchKernelGGL(apg_obs_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, (hipStream_t)stream, B->s,
+                     B->nenv, nq, nv, alive, mean, var, use_norm, o, on, alive_snap);
+  HIPCHK(hipGetLastError());
+  return MJL_OK;
+}
+
+extern "C" int mjl_apg_post(mjlBatch* B, const float* rew, const float* term, const float* trunc, float gamma,
+                            float diverge_qvel, uint8_t* alive, float* disc, float* ret, float* dropped, float* grew,
+                            float* rfin, void* stream) {
+  if (!B || !rew || !term || !trunc || !alive || !disc || !ret || !dropped || !grew || !rfin)
+    return fail(MJL_ERR_ARG, "bad argument");
+  HIPCHK(hipSetDevice(B->device));
+  hipLaunchKernelGGL(apg_post_kernel, dim3((B->nenv + 255) / 256), dim3(256), 0, (hipStream_t)stream, B->s, B->nenv,
+                     B->model->desc.nq, B->model->desc.nv, rew, term, trunc, gamma, diverge_qvel, alive, disc, ret,
+                     dropped, grew, rfin);
+  HIPCHK(hipGetLastError());
+  return MJL_OK;
+}
+
+extern "C" int mjl_apg_obs_vjp(int B, int nq, int nv, const float* o, const uint8_t* alive_snap, const float* mean,
+                               const float* var, int use_norm, const float* go, float* g_qpos, float* g_qvel,
+                               void* stream) {
+  if (B < 0 || nq < 0 || nv < 0 || !o || !alive_snap || !go || !g_qpos || !g_qvel || (use_norm && (!mean || !var)))
+    return fail(MJL_ERR_ARG, "bad argument");
+  const long n = (long)B * (nq + nv);
+  if (n == 0) return MJL_OK;
+  hipLaunchKernelGGL(apg_obs_vjp_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, (hipStream_t)stream, B, nq,
+                     nv, o, alive_snap, mean, var, use_norm, go, g_qpos, g_qvel);
   HIPCHK(hipGetLastError());
   return MJL_OK;
 }

@@ -16,6 +16,7 @@ rank rolls out its own envs; gradients (one all-reduce) and observation statisti
 """
 from __future__ import annotations
 
+import ctypes
 import json
 import os
 import time
@@ -24,6 +25,13 @@ from typing import Optional
 import torch
 
 from .ppo import APGPolicy, RunningMeanStd, _flat_grads, _jsonable, _set_grads
+
+
+def _u8(t: torch.Tensor):
+    """Device pointer of a contiguous uint8 CUDA tensor (alive flags of the native bookkeeping)."""
+    if not t.is_cuda or t.dtype != torch.uint8 or not t.is_contiguous():
+        raise ValueError("alive flags must be a contiguous uint8 CUDA tensor")
+    return ctypes.c_void_p(t.data_ptr())
 
 
 def apg_normalize(rms: RunningMeanStd, x: torch.Tensor) -> torch.Tensor:
@@ -36,8 +44,10 @@ class APGTrainer:
     get_state() / set_state(tape entry), qpos_qvel() and num_envs, act_dim, nq, nv (HumanoidEnv
     through `HumanoidAPGEnv`, or the differentiable stand-in of the CPU tests)."""
 
-    def __init__(self, cfg, env, device="cuda", dist=None, out_dir: Optional[str] = None):
+    def __init__(self, cfg, env, device="cuda", dist=None, out_dir: Optional[str] = None, use_graph: bool = True):
         self.cfg, self.env, self.dist = cfg, env, dist
+        self.use_graph = bool(use_graph)
+        self._graphs, self._warm = {}, set()
         self.rank = dist.get_rank() if dist is not None else 0
         self.world = dist.get_world_size() if dist is not None else 1
         self.device = torch.device(device)
@@ -66,6 +76,92 @@ class APGTrainer:
         return o, (apg_normalize(self.rms, x) if use_norm else x)
 
     def loss_and_grad(self, use_norm: bool, per_step_param_grad: bool = False):
+        """One rollout + backward (see _loss_and_grad). On the GPU the second and later calls per
+        `use_norm` replay one hipGraph of the whole thing: ~60 launches per rollout step (env step,
+        VJP, the policy's forward and backward, the guard's elementwise ops) with no host in between;
+        the env's reset counter comes from its device counter base, so a replay is bit-identical to
+        the eager call (tests/test_apg.py)."""
+        env = self.env
+        if per_step_param_grad or not self.use_graph or self.device.type != "cuda" or not hasattr(env, "ctr_base"):
+            return self._loss_and_grad(use_norm, per_step_param_grad)
+        key = bool(use_norm)
+        if key not in self._graphs:
+            if key not in self._warm:  # first call eager: library handles, allocator pools, GEMM choices
+                self._warm.add(key)
+                return self._loss_and_grad(use_norm, False)
+            graph = torch.cuda.CUDAGraph()
+            c0 = env.counter
+            self.opt.zero_grad(set_to_none=True)
+            with torch.cuda.graph(graph):
+                out = self._loss_and_grad(use_norm, False, graph=True)
+            env.counter = c0  # capture ran nothing; the replay below draws the reset
+            self._graphs[key] = (graph, out, [p.grad for p in self.policy.parameters()])
+        graph, out, grads = self._graphs[key]
+        env.ctr_base.fill_(env.counter)
+        graph.replay()
+        env.counter += 1 + self.cfg.horizon  # what the eager call consumes (reset + steps)
+        env.ctr_base.zero_()
+        for p, g in zip(self.policy.parameters(), grads):  # the graph's gradient buffers
+            p.grad = g
+        return out
+
+    def _loss_and_grad(self, use_norm: bool, per_step_param_grad: bool = False, graph: bool = False):
+        if getattr(self.env, "native_apg", False) and not per_step_param_grad:
+            return self._loss_and_grad_native(use_norm, graph)
+        return self._loss_and_grad_torch(use_norm, per_step_param_grad, graph)
+
+    def _loss_and_grad_native(self, use_norm: bool, graph: bool = False):
+        """_loss_and_grad_torch with its per-step bookkeeping as three native launches
+        (mjl_apg_obs / mjl_apg_post / mjl_apg_obs_vjp, include/mjx355.h: the same guard, discount,
+        return and observation derivative): ~50 torch ops per rollout step become 2, and the
+        reverse sweep's observation backward 1. The policy input `on` is the autograd leaf."""
+        cfg, env = self.cfg, self.env
+        H, B, gamma, dev = cfg.horizon, env.num_envs, cfg.gamma, self.device
+        w = env.nq + env.nv
+        if graph:
+            env.reset(counter=1)  # relative to ctr_base = the counter before the call
+        else:
+            env.reset()
+        o_all, on_all = torch.empty((H, B, w), device=dev), torch.empty((H, B, w), device=dev)
+        snap = torch.empty((H, B), dtype=torch.uint8, device=dev)
+        grew_all, rfin = torch.empty((H, B), device=dev), torch.empty((H, B), device=dev)
+        alive = torch.ones(B, dtype=torch.uint8, device=dev)
+        disc, ret = torch.ones(B, device=dev), torch.zeros(B, device=dev)
+        dropped_e = torch.zeros(B, device=dev)
+        dq = float(getattr(cfg, "diverge_qvel", None) or 0.0)
+        tape, acts, leaves = [], [], []
+        for t in range(H):
+            tape.append(env.get_state())
+            env.apg_obs(alive, self.rms, use_norm, o_all[t], on_all[t], snap[t])
+            on = on_all[t].detach().requires_grad_(True)
+            a = self.policy(on)
+            acts.append(a)
+            leaves.append(on)
+            _, r, te, tr = env.step(a.detach(), auto_reset=False)
+            env.apg_post(r, te, tr, gamma, dq, alive, disc, ret, dropped_e, grew_all[t], rfin[t])
+        loss = -ret.mean()
+        final = env.get_state()
+        self.opt.zero_grad(set_to_none=True)
+        gq = torch.zeros((B, env.nq), device=dev)
+        gv = torch.zeros((B, env.nv), device=dev)
+        gaux = None
+        nonfinite = torch.zeros(1, device=dev)
+        gws = torch.zeros((B, env.nv), device=dev) if getattr(env, "vjp_carries_ws", False) else None
+        gas = [None] * H
+        for t in range(H - 1, -1, -1):
+            env.set_state(tape[t], tape[t + 1] if t + 1 < H else final)
+            if gws is not None:
+                gq, gv, gws, ga, gaux = env.step_vjp_full(acts[t].detach(), gq, gv, gws, grew_all[t], gaux, nonfinite)
+            else:
+                gq, gv, ga, gaux = env.step_vjp(acts[t].detach(), gq, gv, grew_all[t], gaux, nonfinite)
+            og, = torch.autograd.grad(acts[t], leaves[t], grad_outputs=ga)
+            env.apg_obs_vjp(o_all[t], snap[t], self.rms, use_norm, og, gq, gv)
+            gas[t] = ga
+        torch.autograd.backward(self.policy(on_all.reshape(H * B, w)), grad_tensors=torch.cat(gas))
+        dropped = dropped_e.sum() + nonfinite[0]
+        return loss.detach(), (rfin.mean(1).sum() / H).detach(), o_all, dropped
+
+    def _loss_and_grad_torch(self, use_norm: bool, per_step_param_grad: bool = False, graph: bool = False):
         """One rollout + backward. Returns (loss, mean reward, obs trajectory, envs dropped as
         non-finite); grads in .grad.
 
@@ -76,7 +172,10 @@ class APGTrainer:
         dropped envs is reported."""
         cfg, env = self.cfg, self.env
         H, B, gamma = cfg.horizon, env.num_envs, cfg.gamma
-        env.reset()
+        if graph:
+            env.reset(counter=1)  # relative to ctr_base = the counter before the call
+        else:
+            env.reset()
         tape, obs_leaves, acts, discs, pol_in = [], [], [], [], []
         disc = ret = rsum = None  # created from the first reward (dtype follows the env)
         alive = torch.ones(B, dtype=torch.bool, device=self.device)
@@ -222,6 +321,7 @@ class HumanoidAPGEnv:
     the MJCF's Newton 10/20); the recompute is seeded with the forward's solution (~1 iteration)."""
 
     guarded_vjp = True
+    native_apg = True  # APGTrainer's bookkeeping as native launches (apg_obs / apg_post / apg_obs_vjp)
 
     def __init__(self, env, vjp: str = "implicit"):
         from . import abi
@@ -234,8 +334,20 @@ class HumanoidAPGEnv:
         self.num_envs, self.act_dim = env.num_envs, env.act_dim
         self.nq, self.nv = env.sys.nq, env.sys.nv
 
-    def reset(self):
-        return self.env.reset()
+    def reset(self, counter=None):
+        return self.env.reset(counter=counter)
+
+    @property
+    def ctr_base(self):
+        return self.env.ctr_base
+
+    @property
+    def counter(self):
+        return self.env.counter
+
+    @counter.setter
+    def counter(self, v):
+        self.env.counter = v
 
     def step(self, act, auto_reset=False):
         return self.env.step(act, auto_reset=auto_reset)
@@ -253,6 +365,24 @@ class HumanoidAPGEnv:
 
     def step_vjp(self, act, gq, gv, grew, gaux, nonfinite=None):
         return self.env.step_vjp(act, gq, gv, grew, gaux, nonfinite)
+
+    def apg_obs(self, alive, rms, use_norm, o, on, snap):
+        from ._lib import check, lib
+        from .mjx import _ptr, _stream
+        check(lib().mjl_apg_obs(self.env.data.handle, _u8(alive), _ptr(rms.mean), _ptr(rms.var), int(use_norm),
+                                _ptr(o), _ptr(on), _u8(snap), _stream()))
+
+    def apg_post(self, r, te, tr, gamma, diverge_qvel, alive, disc, ret, dropped, grew, rfin):
+        from ._lib import check, lib
+        from .mjx import _ptr, _stream
+        check(lib().mjl_apg_post(self.env.data.handle, _ptr(r), _ptr(te), _ptr(tr), float(gamma), float(diverge_qvel),
+                                 _u8(alive), _ptr(disc), _ptr(ret), _ptr(dropped), _ptr(grew), _ptr(rfin), _stream()))
+
+    def apg_obs_vjp(self, o, snap, rms, use_norm, go, gq, gv):
+        from ._lib import check, lib
+        from .mjx import _ptr, _stream
+        check(lib().mjl_apg_obs_vjp(self.num_envs, self.nq, self.nv, _ptr(o), _u8(snap), _ptr(rms.mean),
+                                    _ptr(rms.var), int(use_norm), _ptr(go.contiguous()), _ptr(gq), _ptr(gv), _stream()))
 
     def step_vjp_full(self, act, gq, gv, gws, grew, gaux, nonfinite=None):
         return self.env.step_vjp_full(act, gq, gv, gws, grew, gaux, nonfinite)

@@ -78,12 +78,15 @@ class HumanoidEnv:
         self.counter += 1
         return self.counter
 
-    def reset(self, mask: Optional[torch.Tensor] = None, noise: Optional[torch.Tensor] = None) -> torch.Tensor:
+    def reset(self, mask: Optional[torch.Tensor] = None, noise: Optional[torch.Tensor] = None,
+              counter: Optional[int] = None) -> torch.Tensor:
         """v_reset (src/envs.py:115-202,494) on all envs, or on envs with mask > 0.5.
-        `noise` [num_envs, nq-7+nv+2] of uniforms replaces the on-device RNG (parity tests)."""
+        `noise` [num_envs, nq-7+nv+2] of uniforms replaces the on-device RNG (parity tests).
+        `counter` (graph capture) is the RNG counter relative to `ctr_base`; default: the next one."""
         mk = None if mask is None else mask.to(self.obs.device, torch.float32).contiguous()
         nz = None if noise is None else noise.to(self.obs.device, torch.float32).contiguous()
-        check(lib().mjl_env_reset(self.data.handle, _ptr(mk), self.seed, self._next_counter(), _ptr(nz),
+        check(lib().mjl_env_reset(self.data.handle, _ptr(mk), self.seed,
+                                  self._next_counter() if counter is None else int(counter), _ptr(nz),
                                   _ptr(self.obs), _stream()))
         return self.obs
 

@@ -279,3 +279,58 @@ def test_packed_state_roundtrip_and_guarded_vjp():
     keep = torch.arange(B, device="cuda") != 3
     for a, b in zip(out, ref):
         assert torch.all(a[3] == 0) and torch.equal(a[keep], b[keep])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("solver,vjp", [("model", "implicit"), ("cg44", "unrolled")])
+def test_apg_graph_replay_bit_identical_to_eager(solver, vjp):
+    """The hipGraph replay of the APG rollout + reverse sweep (APGTrainer use_graph) gives the eager
+    call's loss, gradient and parameters bit for bit, update after update, through both
+    observation-normalisation graphs (warm-up call, capture, replays) and the per-update reset draws
+    (device counter base)."""
+    import mjx_amd
+    from mjx_amd import mjcf, mjx
+    from mjx_amd.config import reference_ppo_config
+    from mjx_amd.envs import HumanoidEnv, resolve_ids
+    m = mjx_amd.load_model("humanoid_mjx")
+    if solver == "cg44":
+        m.solver, m.iterations, m.ls_iterations = mjcf.SOLVER_CG, 4, 4
+    ecfg = resolve_ids(m, reference_ppo_config().env_config)
+    cfg = _cfg(batch_size=64, horizon=8, hidden_size=32)
+    trs = [apg.APGTrainer(cfg, apg.HumanoidAPGEnv(HumanoidEnv(mjx.put_model(m), ecfg, cfg.batch_size, seed=3), vjp),
+                          device="cuda", use_graph=g) for g in (False, True)]
+    for step in range(6):
+        ms = [tr.update(step) for tr in trs]
+        for k in ("loss", "grad_norm", "mean_reward", "nonfinite_envs"):
+            assert ms[0][k] == ms[1][k] or (ms[0][k] != ms[0][k] and ms[1][k] != ms[1][k]), f"update {step}: {k}"
+        for p, q in zip(trs[0].policy.parameters(), trs[1].policy.parameters()):
+            assert torch.equal(p, q), f"update {step}: parameters"
+        assert torch.equal(trs[0].rms.mean, trs[1].rms.mean)
+    assert set(trs[1]._graphs) == {True} and trs[0]._graphs == {}
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("solver,vjp", [("model", "implicit"), ("cg44", "unrolled")])
+def test_apg_native_bookkeeping_matches_torch_ops(solver, vjp):
+    """The native per-step bookkeeping (mjl_apg_obs / mjl_apg_post / mjl_apg_obs_vjp) gives the same
+    loss, gradient, dropped-env count and parameters as the torch-op restatement of the same sweep
+    (_loss_and_grad_torch), with and without observation normalisation."""
+    import mjx_amd
+    from mjx_amd import mjcf, mjx
+    from mjx_amd.config import reference_ppo_config
+    from mjx_amd.envs import HumanoidEnv, resolve_ids
+    m = mjx_amd.load_model("humanoid_mjx")
+    if solver == "cg44":
+        m.solver, m.iterations, m.ls_iterations = mjcf.SOLVER_CG, 4, 4
+    ecfg = resolve_ids(m, reference_ppo_config().env_config)
+    cfg = _cfg(batch_size=64, horizon=8, hidden_size=32)
+    envs = [apg.HumanoidAPGEnv(HumanoidEnv(mjx.put_model(m), ecfg, cfg.batch_size, seed=3), vjp) for _ in range(2)]
+    envs[1].native_apg = False
+    trs = [apg.APGTrainer(cfg, e, device="cuda", use_graph=False) for e in envs]
+    for step in range(3):
+        ms = [tr.update(step) for tr in trs]
+        assert ms[0]["nonfinite_envs"] == ms[1]["nonfinite_envs"]
+        for k in ("loss", "grad_norm", "mean_reward"):
+            assert ms[0][k] == pytest.approx(ms[1][k], rel=1e-5, abs=1e-6), f"update {step}: {k}"
+        for p, q in zip(trs[0].policy.parameters(), trs[1].policy.parameters()):
+            torch.testing.assert_close(p, q, rtol=1e-5, atol=1e-6)

@@ -101,6 +101,7 @@ def test_ppo_c3_iterations_at_full_size(tmp_path):
     env2.counter = env.counter
     tr2.obs = tr.obs.clone()
     tr2.gen.set_state(tr.gen.get_state())
+    tr2._pool_n.copy_(tr._pool_n)  # the reset pool's size adapts per rollout
     a = [x.clone() for x in tr.collect_rollout()]
     b = tr2.collect_rollout()
     assert tr._graph is not None and tr2._graph is None

@@ -37,8 +37,9 @@ def main():
     m = apg_model(cfg, solver=a.solver)
     env = HumanoidEnv(mjx.put_model(m), resolve_ids(m, EnvConfig()), cfg.batch_size, seed=cfg.seed)
     tr = APGTrainer(cfg, HumanoidAPGEnv(env, vjp), device="cuda")
-    tr.update(0)  # warm-up
-    res = [tr.update(i) for i in range(1, a.updates + 1)]
+    tr.update(0)  # warm-up (eager: library handles, GEMM choices)
+    tr.update(1)  # captures the rollout + reverse sweep hipGraph (one-time)
+    res = [tr.update(i) for i in range(2, a.updates + 2)]
     sps = sum(r["env_steps_per_sec"] for r in res) / len(res)
     # forward-only rollout time for the split (no tape, no backward)
     torch.cuda.synchronize()
