@@ -730,7 +730,7 @@ template <bool ENV> static int launch_vjp(mjlBatch* B, const VjpArgs& V0, void* 
   V.row_floats = B->adj_row_floats;
   dim3 grid(B->nenv), block(64);
   if (B->model->nvc == 0)
-    hipLaunchKernelGGL((vjp_kernel<DHum, ENV>), grid, block, 0, (hipStream_t)stream, P, V);
+    hipLaunchKernelGGL((vjp_kernel<DHumV, ENV>), grid, block, 0, (hipStream_t)stream, P, V);
   else
     hipLaunchKernelGGL((vjp_kernel<DGen, ENV>), grid, block, 0, (hipStream_t)stream, P, V);
   HIPCHK(hipGetLastError());

@@ -97,6 +97,9 @@ template <int NV_, int NB_, int NJ_, int NG_, int CAP_, int CAPC_> struct Dims {
 };
 using DHum = Dims<27, 17, 22, 20, MJL_CAP, MJL_CAPC>;  // both reference humanoids (nv 27, 17 bodies, 22 joints, 20 geoms)
 using DGen = Dims<32, 32, 32, 32, 32, 16>;               // any model within the MJL_MAX* capacities
+// the step VJP keeps its rows in the global slab, so its workspace drops the LDS row arrays (which
+// share a union with the smooth-dynamics scratch): 6.4 KB less LDS, 5 instead of 4 waves per CU
+using DHumV = Dims<27, 17, 22, 20, 4, 4>;
 
 // ---------------------------------------------------------------------------------------------
 // wave primitives
