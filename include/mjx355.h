@@ -174,9 +174,13 @@ int mjl_batch_nenv(const mjlBatch* batch);
  * 101-105,187-189 runs CG 4/4) instead of the implicit derivative at the converged active set; the
  * integrator's input is then qfrc_smooth + qfrc_constraint of the stopped solve. The VJP must see
  * the pre-step qacc_warmstart the forward step saw (the recompute replays that solve).
+ * MJL_OPT_VJP_TAPE (default 0): value = slots of the VJP tape (mjl_env_step_record /
+ * mjl_env_step_vjp_replay), each holding one env step's forward workspace for every env
+ * (~50 KB per env and slot for the humanoid; call outside stream capture; 0 frees it).
  * MJL_OPT_RESET_POOL (default 0): value = slots per env (<= 64) of the reset pool that
  * mjl_env_fill_reset_pool fills (call outside stream capture; 0 frees it). */
-enum { MJL_OPT_STORE_DERIVED = 0, MJL_OPT_FORCE_GLOBAL_ROWS = 1, MJL_OPT_VJP_UNROLLED = 2, MJL_OPT_RESET_POOL = 3 };
+enum { MJL_OPT_STORE_DERIVED = 0, MJL_OPT_FORCE_GLOBAL_ROWS = 1, MJL_OPT_VJP_UNROLLED = 2, MJL_OPT_RESET_POOL = 3,
+       MJL_OPT_VJP_TAPE = 4 };
 int mjl_batch_set_option(mjlBatch* batch, int option, int value);
 
 /* Copy a per-env field to / from a device buffer [nenv, dim] (async on stream). `mask` (device,
@@ -324,6 +328,21 @@ long long mjl_policy_param_floats(int nlayer, const int* dims);
 int mjl_policy_fwd(const float* obs, const float* mean, const float* var, float clip, const float* params, int nlayer,
                    const int* dims, const float* log_std, const float* eps, int B, float* act, float* logp,
                    void* stream);
+
+/* APG with a stored forward instead of a recomputed one (train_apg.py:187-189 takes jax.grad with
+ * per-step remat; HBM holds the forward instead): mjl_env_step_record is mjl_env_step without
+ * auto-reset (same outputs and state update; derived fields are not stored) that also leaves in tape
+ * slot `slot` what the step VJP's reverse passes read (workspace after integration, constraint rows,
+ * the pre-step qpos / qvel / aux, the factor of the converged Hessian, the unrolled solve's tape);
+ * mjl_env_step_vjp_replay is mjl_env_step_vjp_full of that step from the slot, without the
+ * recompute and without restoring the pre-step state first. Requires MJL_OPT_VJP_TAPE; the VJP mode
+ * (MJL_OPT_VJP_UNROLLED) must be the same at record and replay. */
+int mjl_env_step_record(mjlBatch* batch, int slot, const float* act, float* obs, float* rew, float* term,
+                        float* trunc, void* stream);
+int mjl_env_step_vjp_replay(mjlBatch* batch, int slot, const float* act, const float* g_qpos, const float* g_qvel,
+                            const float* g_qacc_ws, const float* g_rew, const float* g_aux, float* out_qpos,
+                            float* out_qvel, float* out_qacc_ws, float* out_act, float* out_aux,
+                            float* nonfinite_count, void* stream);
 
 /* APG rollout bookkeeping (train_apg.py:161-209; the sweep of mjx_amd/apg.py), one launch each per
  * rollout step. alive / alive_snap: uint8 [nenv] (0/1); device pointers, float32, row-major.

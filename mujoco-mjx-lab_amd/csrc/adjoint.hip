@@ -173,6 +173,7 @@ struct TapeDims {
 struct SolveTape {
   static constexpr bool on = true;
   GLBA float* t;
+  GLBA float* acc;  // the reverse sweep's row accumulators (t + d.tape, or the env's own scratch)
   TapeDims d;
   int nup, nls, nsets, overflow;
   INL GLBA float* upd(int k) const { return t + 4 + k * d.US; }
@@ -500,7 +501,7 @@ template <class D> INL void adj_solver_unrolled(MP m, LDSA WS<D>* W, LDSA WSA<D>
   const int nv = m->nv, nefc = W->nefc;
   const bool cg = m->solver != MJL_SOLVER_NEWTON;
   const TapeDims& d = tp.d;
-  GLBA float* arefb = tp.t + d.tape;
+  GLBA float* arefb = tp.acc;
   GLBA float* Dbar = arefb + nefc_max;
   GLBA float* ca = arefb + 2 * nefc_max;
   GLBA float* cb = arefb + 3 * nefc_max;
@@ -1475,16 +1476,54 @@ struct VjpArgs {
   TapeDims td;
   const float* g_ws; // optional: cotangent of the output qacc_warmstart (= qacc)
   float* o_ws;       // optional: cotangent of the input qacc_warmstart (unrolled mode, warm start taken)
+  // VJP tape (record / replay): this step's slot, per env `slot_stride` floats: the workspace after
+  // integrate [s_w], the pre-step qpos / qvel / aux and the forward's a', factor of Hc [s_a], the
+  // constraint rows [s_r], the solve tape (unrolled) [s_t]
+  float* slot;
+  long long slot_stride;
+  int s_w, s_a, s_r, s_t;
 };
+
+// record mode's share of WSA: what the forward leaves there for the reverse passes
+template <class DM> struct WSAR {
+  static constexpr int NV = DM::NV, LD = DM::LD;
+  float qpos0[MJL_MAXQ], qvel0[LD];
+  alignas(16) float Lc[NV * LD];
+  alignas(16) float invdc[LD];
+  float ap[LD];
+};
+// slot layout of the A part: qpos0 [MAXQ], qvel0 [LD], aux [12], ap [LD], invdc [LD], Lc [NV * LD]
+template <class DM> __host__ __device__ constexpr int slot_a_floats() {
+  return MJL_MAXQ + DM::LD + 12 + 2 * DM::LD + DM::NV * DM::LD;
+}
+template <class DM> __host__ __device__ constexpr int slot_w_floats() { return (int)(sizeof(WS<DM>) / 4); }
+
+// record / replay of the A part (lanes stride the arrays)
+template <class DM, class AT> INL void slot_a_io(GLBA float* sa, AT* A, LDSA float* aux, int lane, bool store) {
+  constexpr int LD = DM::LD, NV = DM::NV;
+  auto mv = [&](LDSA float* l, GLBA float* g, int n) {
+    for (int i = lane; i < n; i += 64) { if (store) g[i] = l[i]; else l[i] = g[i]; }
+  };
+  mv((LDSA float*)A->qpos0, sa, MJL_MAXQ);
+  mv((LDSA float*)A->qvel0, sa + MJL_MAXQ, LD);
+  mv(aux, sa + MJL_MAXQ + LD, MJL_AUX_DIM);
+  mv((LDSA float*)A->ap, sa + MJL_MAXQ + LD + 12, LD);
+  mv((LDSA float*)A->invdc, sa + MJL_MAXQ + 2 * LD + 12, LD);
+  mv((LDSA float*)A->Lc, sa + MJL_MAXQ + 3 * LD + 12, NV * LD);
+}
 
 // One wave per env: recompute the step from the batch state (not modified), then run the reverse
 // passes. ENV: the env step of envs.py (action flip / clip, reward, aux) without the reset merge.
-template <class D, bool ENV> __global__ __launch_bounds__(64, 1) void vjp_kernel(KParams P, VjpArgs V) {
+// TM (VJP tape): 0 recompute, as above; 1 record: the forward only — the env step itself (outputs
+// and state write-back as mjl_env_step without auto-reset) — leaving in the step's tape slot what
+// the reverse passes read; 2 replay: the reverse passes from the slot, no recompute.
+template <class D, bool ENV, int TM> __global__ __launch_bounds__(64, 1) void vjp_kernel(KParams P, VjpArgs V) {
+  typedef typename std::conditional<TM == 1, WSAR<D>, WSA<D>>::type AT;
   __shared__ WS<D> Ws;
-  __shared__ WSA<D> As;
+  __shared__ AT As;
   __shared__ float aux_s[MJL_AUX_DIM + 3];
   LDSA WS<D>* W = (LDSA WS<D>*)&Ws;
-  LDSA WSA<D>* A = (LDSA WSA<D>*)&As;
+  LDSA AT* A = (LDSA AT*)&As;
   LDSA float* aux = (LDSA float*)aux_s;
   constexpr int LD = D::LD;
   MP m = (MP)P.m;
@@ -1492,8 +1531,8 @@ template <class D, bool ENV> __global__ __launch_bounds__(64, 1) void vjp_kernel
   if (env >= P.nenv) return;
   const int nq = m->nq, nv = m->nv, nu = m->nu;
   const StateBuf& S = P.s;
-  {  // the VJP is linear in the cotangents: all-zero in -> all-zero out, without the recompute
-     // (envs past termination in an APG rollout; also keeps 0 * non-finite out of their outputs)
+  if constexpr (TM != 1) {  // the VJP is linear in the cotangents: all-zero in -> all-zero out, without
+     // the recompute (envs past termination in an APG rollout; also keeps 0 * non-finite out of their outputs)
     bool nz = false;
     if (lane < nq) nz |= V.g_qpos[(size_t)env * nq + lane] != 0.f;
     if (lane < nv) nz |= V.g_qvel[(size_t)env * nv + lane] != 0.f;
@@ -1513,9 +1552,10 @@ template <class D, bool ENV> __global__ __launch_bounds__(64, 1) void vjp_kernel
   }
   float* scr_env = V.scratch + (size_t)env * (size_t)V.scratch_stride;
   GLBA float* scr_adj = (GLBA float*)(scr_env + V.row_floats);
+  GLBA float* slot = TM ? (GLBA float*)(V.slot + (size_t)env * (size_t)V.slot_stride) : nullptr;
   {  // zero the adjoint workspace and the LD-wide vectors of the forward one
     LDSA float* a = (LDSA float*)A;
-    for (int i = lane; i < (int)(sizeof(WSA<D>) / 4); i += 64) a[i] = 0.f;
+    for (int i = lane; i < (int)(sizeof(AT) / 4); i += 64) a[i] = 0.f;
     for (int i = lane; i < LD; i += 64) {
       W->qvel[i] = 0.f; W->qacc_ws[i] = 0.f;
       W->frc_bias[i] = W->frc_passive[i] = W->frc_act[i] = W->frc_smooth[i] = W->qacc_smooth[i] = 0.f;
@@ -1524,6 +1564,20 @@ template <class D, bool ENV> __global__ __launch_bounds__(64, 1) void vjp_kernel
     }
   }
   SYNC();
+  const bool unr = V.unr != nullptr;
+  SolveTape tp;
+  tp.t = unr ? (TM ? slot + V.s_t : (GLBA float*)(V.unr + (size_t)env * V.td.stride)) : nullptr;
+  tp.acc = unr ? (GLBA float*)(V.unr + (size_t)env * V.td.stride) + V.td.tape : nullptr;
+  tp.d = V.td;
+  tp.nup = tp.nls = tp.nsets = tp.overflow = 0;
+  Rows<true> R = global_rows<D>(TM ? (float*)(slot + V.s_r) : scr_env, P.gmax_efc, P.gmax_con);
+  if constexpr (TM == 2) {  // replay: the forward's workspace, pre-step state and factors from the slot
+    const GLBA f32x4* src = (const GLBA f32x4*)(slot + V.s_w);
+    LDSA f32x4* dst = (LDSA f32x4*)W;
+    for (int i = lane; i < (int)(sizeof(WS<D>) / 16); i += 64) dst[i] = src[i];
+    slot_a_io<D>(slot + V.s_a, A, aux, lane, false);
+    SYNC();
+  } else {
   if (lane < nq) { W->qpos[lane] = S.qpos[(size_t)env * nq + lane]; A->qpos0[lane] = W->qpos[lane]; }
   if (lane < nv) {
     W->qvel[lane] = S.qvel[(size_t)env * nv + lane]; A->qvel0[lane] = W->qvel[lane];
@@ -1539,6 +1593,7 @@ template <class D, bool ENV> __global__ __launch_bounds__(64, 1) void vjp_kernel
       const float a = flip ? V.act[(size_t)env * nu + c->act_perm[lane]] * c->act_sign[lane] : V.act[(size_t)env * nu + lane];
       W->ctrl[lane] = fminf(fmaxf(a, -1.f), 1.f);
     }
+    if (TM == 1 && lane == 0) W->sc[SC_FLIP] = aux[0];
   } else if (lane < nu) {
     W->ctrl[lane] = S.ctrl[(size_t)env * nu + lane];
   }
@@ -1556,13 +1611,7 @@ template <class D, bool ENV> __global__ __launch_bounds__(64, 1) void vjp_kernel
     if (lane < LD) W->qacc_smooth[lane] = (lane < nv) ? x : 0.f;
     SYNC();
   }
-  Rows<true> R = global_rows<D>(scr_env, P.gmax_efc, P.gmax_con);
   build_rows<D, true>(m, W, R, lane);
-  const bool unr = V.unr != nullptr;
-  SolveTape tp;
-  tp.t = unr ? (GLBA float*)(V.unr + (size_t)env * V.td.stride) : nullptr;
-  tp.d = V.td;
-  tp.nup = tp.nls = tp.nsets = tp.overflow = 0;
   if (unr) {
     solver_t<D, true>(m, W, R, lane, tp);  // the same solve, recording its tape
     tp.finish(lane);
@@ -1578,6 +1627,29 @@ template <class D, bool ENV> __global__ __launch_bounds__(64, 1) void vjp_kernel
   }
   integrate<D>(m, W, lane, A->ap);
   STAMP(1, lane);
+  if constexpr (TM == 1) {  // record: the workspace as the reverse passes find it, then the env step
+    {
+      const LDSA f32x4* src = (const LDSA f32x4*)W;
+      GLBA f32x4* dst = (GLBA f32x4*)(slot + V.s_w);
+      for (int i = lane; i < (int)(sizeof(WS<D>) / 16); i += 64) dst[i] = src[i];
+      slot_a_io<D>(slot + V.s_a, A, aux, lane, true);
+    }
+    float* obs = P.obs + (size_t)env * P.env->obs_dim;
+    env_post<D>(m, W, P.env, aux, obs, lane, false);
+    if (lane == 0) { P.rew[env] = W->sc[SC_REW]; P.term[env] = W->sc[SC_TERM]; P.trunc[env] = W->sc[SC_TRUNC]; }
+    SYNC();
+    if (lane < nq) S.qpos[(size_t)env * nq + lane] = W->qpos[lane];
+    if (lane < nv) {
+      S.qvel[(size_t)env * nv + lane] = W->qvel[lane];
+      S.qacc_warmstart[(size_t)env * nv + lane] = W->qacc_ws[lane];
+    }
+    if (lane < nu) S.ctrl[(size_t)env * nu + lane] = W->ctrl[lane];
+    if (lane == 0) S.time[env] = W->sc[SC_TIME];
+    if (lane < MJL_AUX_DIM) S.aux[(size_t)env * MJL_AUX_DIM + lane] = aux[lane];
+    return;
+  }
+  }
+  if constexpr (TM != 1) {
   // ---- reverse
   const float* gq = V.g_qpos + (size_t)env * nq;
   if (lane < nv) A->vtmp[lane] = V.g_qvel[(size_t)env * nv + lane];
@@ -1590,7 +1662,7 @@ template <class D, bool ENV> __global__ __launch_bounds__(64, 1) void vjp_kernel
   if (unr) adj_solver_unrolled<D>(m, W, A, R, scr_adj, P.gmax_efc, tp, lane);
   else adj_solver_rows<D>(m, W, A, R, scr_adj, P.gmax_efc, lane);
   STAMP(3, lane);
-  adj_contact_jac<D>(m, W, A, R, scr_adj, P.gmax_efc, unr ? (GLBA const float*)(tp.t + V.td.tape + 4 * P.gmax_efc) : nullptr,
+  adj_contact_jac<D>(m, W, A, R, scr_adj, P.gmax_efc, unr ? (GLBA const float*)(tp.acc + 4 * P.gmax_efc) : nullptr,
                      lane);
   STAMP(4, lane);
   adj_collision<D>(m, W, A, R, scr_adj, P.gmax_efc, lane);
@@ -1642,6 +1714,7 @@ template <class D, bool ENV> __global__ __launch_bounds__(64, 1) void vjp_kernel
     }
   }
   if (ENV && lane < MJL_AUX_DIM) V.o_aux[(size_t)env * MJL_AUX_DIM + lane] = A->auxb[lane];
+  }
 }
 
 }  // namespace mjl

@@ -65,6 +65,9 @@ struct mjlBatch {
   const unsigned long long* ctr_base;  // device RNG counter base (mjl_batch_set_counter_base), or null
   const uint32_t* reset_keys;           // per-env jax.random reset keys (mjl_env_set_reset_keys), or null
   int key_mode;
+  float* d_vtape;  // MJL_OPT_VJP_TAPE: slots x nenv x vtape_stride floats (record / replay), or null
+  int vtape_slots, vt_w, vt_a, vt_r, vt_t;
+  long long vtape_stride;
   float* d_rs;     // MJL_OPT_RESET_POOL: pool slots (the state fields again, [slots * nenv] rows) + obs
   int* d_pool_ctl;  // [nenv, 2] next slot, filled slots
   int pool_slots;
@@ -401,7 +404,7 @@ void mjl_batch_destroy(mjlBatch* B) {
   (void)hipFree(B->d_state); (void)hipFree(B->d_model); (void)hipFree(B->d_env); (void)hipFree(B->d_scratch);
   (void)hipFree(B->d_adj_scratch);
   (void)hipFree(B->d_unr);
-  (void)hipFree(B->d_rs); (void)hipFree(B->d_pool_ctl);
+  (void)hipFree(B->d_rs); (void)hipFree(B->d_pool_ctl); (void)hipFree(B->d_vtape);
   delete B;
 }
 
@@ -415,6 +418,29 @@ int mjl_batch_set_option(mjlBatch* B, int option, int value) {
     if (value && B->model->desc.iterations > 256)
       return fail(MJL_ERR_ARG, "unrolled VJP: %d solver iterations (at most 256 are taped)", B->model->desc.iterations);
     B->vjp_unrolled = value != 0;
+    return MJL_OK;
+  }
+  if (option == MJL_OPT_VJP_TAPE) {
+    if (value < 0) return fail(MJL_ERR_ARG, "VJP tape: slots must be >= 0");
+    HIPCHK(hipSetDevice(B->device));
+    (void)hipFree(B->d_vtape);
+    B->d_vtape = nullptr; B->vtape_slots = 0;
+    if (!value) return MJL_OK;
+    const bool gen = B->model->nvc != 0;
+    const int LD = gen ? DGen::LD : DHumV::LD;
+    TapeDims td;
+    td.init(LD, B->gmax_efc, B->model->desc.iterations);
+    const long long r4 = 3;
+    B->vt_w = 0;
+    B->vt_a = (int)((gen ? slot_w_floats<DGen>() : slot_w_floats<DHumV>()) + r4) & ~3;
+    B->vt_r = (int)((B->vt_a + (gen ? slot_a_floats<DGen>() : slot_a_floats<DHumV>()) + r4) & ~3);
+    const long long rows = ((long long)B->gmax_efc * (LD + 8) + (long long)B->gmax_con * (CONW + 2) + r4) & ~r4;
+    B->vt_t = (int)(B->vt_r + rows);
+    B->vtape_stride = ((long long)B->vt_t + td.tape + r4) & ~r4;
+    const size_t bytes = (size_t)value * B->nenv * (size_t)B->vtape_stride * sizeof(float);
+    hipError_t e = hipMalloc(&B->d_vtape, bytes);
+    if (e != hipSuccess) { B->d_vtape = nullptr; return fail(MJL_ERR_HIP, "VJP tape (%zu bytes): %s", bytes, hipGetErrorString(e)); }
+    B->vtape_slots = value;
     return MJL_OK;
   }
   if (option == MJL_OPT_RESET_POOL) {
@@ -705,7 +731,8 @@ int mjl_env_reset(mjlBatch* B, const float* mask, uint64_t seed, uint64_t counte
 }  // extern "C"
 
 // ---------------------------------------------------------------- step VJP (APG backward)
-template <bool ENV> static int launch_vjp(mjlBatch* B, const VjpArgs& V0, void* stream) {
+template <bool ENV, int TM = 0> static int launch_vjp(mjlBatch* B, const VjpArgs& V0, void* stream,
+                                                     const KParams* P0 = nullptr) {
   HIPCHK(hipSetDevice(B->device));
   if (!B->d_adj_scratch) {
     const int LD = B->model->nvc == 0 ? DHum::LD : DGen::LD;
@@ -721,18 +748,20 @@ template <bool ENV> static int launch_vjp(mjlBatch* B, const VjpArgs& V0, void* 
     hipError_t e = hipMalloc(&B->d_unr, (size_t)B->unr_dims.stride * B->nenv * sizeof(float));
     if (e != hipSuccess) { B->d_unr = nullptr; return fail(MJL_ERR_HIP, "unrolled VJP tape: %s", hipGetErrorString(e)); }
   }
-  KParams P = make_params(B);
+  KParams P = P0 ? *P0 : make_params(B);
   VjpArgs V = V0;
   V.unr = B->vjp_unrolled ? B->d_unr : nullptr;
+  V.slot_stride = B->vtape_stride;
+  V.s_w = B->vt_w; V.s_a = B->vt_a; V.s_r = B->vt_r; V.s_t = B->vt_t;
   V.td = B->unr_dims;
   V.scratch = B->d_adj_scratch;
   V.scratch_stride = B->adj_stride;
   V.row_floats = B->adj_row_floats;
   dim3 grid(B->nenv), block(64);
   if (B->model->nvc == 0)
-    hipLaunchKernelGGL((vjp_kernel<DHumV, ENV>), grid, block, 0, (hipStream_t)stream, P, V);
+    hipLaunchKernelGGL((vjp_kernel<DHumV, ENV, TM>), grid, block, 0, (hipStream_t)stream, P, V);
   else
-    hipLaunchKernelGGL((vjp_kernel<DGen, ENV>), grid, block, 0, (hipStream_t)stream, P, V);
+    hipLaunchKernelGGL((vjp_kernel<DGen, ENV, TM>), grid, block, 0, (hipStream_t)stream, P, V);
   HIPCHK(hipGetLastError());
   return MJL_OK;
 }
@@ -793,6 +822,38 @@ int mjl_env_step_vjp_full(mjlBatch* B, const float* act, const float* g_qpos, co
   V.g_ws = g_qacc_ws; V.o_ws = out_qacc_ws;
   V.nonfinite = nonfinite_count;
   return launch_vjp<true>(B, V, stream);
+}
+
+int mjl_env_step_record(mjlBatch* B, int slot, const float* act, float* obs, float* rew, float* term, float* trunc,
+                        void* stream) {
+  if (!B || !act || !obs || !rew || !term || !trunc) return fail(MJL_ERR_ARG, "bad argument");
+  if (!B->has_env) return fail(MJL_ERR_ARG, "mjl_env_config not called");
+  if (!B->d_vtape || slot < 0 || slot >= B->vtape_slots) return fail(MJL_ERR_ARG, "VJP tape slot %d not allocated", slot);
+  KParams P = make_params(B);
+  P.obs = obs; P.rew = rew; P.term = term; P.trunc = trunc;
+  VjpArgs V;
+  std::memset(&V, 0, sizeof(V));
+  V.act = act;
+  V.slot = B->d_vtape + (size_t)slot * B->nenv * (size_t)B->vtape_stride;
+  return launch_vjp<true, 1>(B, V, stream, &P);
+}
+
+int mjl_env_step_vjp_replay(mjlBatch* B, int slot, const float* act, const float* g_qpos, const float* g_qvel,
+                            const float* g_qacc_ws, const float* g_rew, const float* g_aux, float* out_qpos,
+                            float* out_qvel, float* out_qacc_ws, float* out_act, float* out_aux,
+                            float* nonfinite_count, void* stream) {
+  if (!B || !act || !g_qpos || !g_qvel || !g_rew || !g_aux || !out_qpos || !out_qvel || !out_act || !out_aux)
+    return fail(MJL_ERR_ARG, "bad argument");
+  if (!B->has_env) return fail(MJL_ERR_ARG, "mjl_env_config not called");
+  if (!B->d_vtape || slot < 0 || slot >= B->vtape_slots) return fail(MJL_ERR_ARG, "VJP tape slot %d not allocated", slot);
+  VjpArgs V;
+  std::memset(&V, 0, sizeof(V));
+  V.act = act; V.g_qpos = g_qpos; V.g_qvel = g_qvel; V.g_rew = g_rew; V.g_aux = g_aux;
+  V.o_qpos = out_qpos; V.o_qvel = out_qvel; V.o_ctrl = out_act; V.o_aux = out_aux;
+  V.g_ws = g_qacc_ws; V.o_ws = out_qacc_ws;
+  V.nonfinite = nonfinite_count;
+  V.slot = B->d_vtape + (size_t)slot * B->nenv * (size_t)B->vtape_stride;
+  return launch_vjp<true, 2>(B, V, stream);
 }
 
 }  // extern "C"

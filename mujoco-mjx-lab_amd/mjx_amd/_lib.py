@@ -26,7 +26,7 @@ EXPORTS = [
     "mjl_set_state", "mjl_obs_normalize", "mjl_policy_head", "mjl_colsum_scratch", "mjl_colsum",
     "mjl_policy_param_floats", "mjl_policy_fwd",
     "mjl_step_vjp_full", "mjl_env_step_vjp_full", "mjl_env_fill_reset_pool",
-    "mjl_apg_obs", "mjl_apg_post", "mjl_apg_obs_vjp",
+    "mjl_apg_obs", "mjl_apg_post", "mjl_apg_obs_vjp", "mjl_env_step_record", "mjl_env_step_vjp_replay",
 ]
 
 _lib = None
@@ -85,6 +85,8 @@ def lib() -> C.CDLL:
     L.mjl_env_step.argtypes = [vp, f32p, f32p, f32p, f32p, f32p, i32, u64, u64, vp]
     L.mjl_env_reset.argtypes = [vp, f32p, u64, u64, f32p, f32p, vp]
     L.mjl_env_fill_reset_pool.argtypes = [vp, vp, u64, u64, vp]
+    L.mjl_env_step_record.argtypes = [vp, i32, vp, vp, vp, vp, vp, vp]
+    L.mjl_env_step_vjp_replay.argtypes = [vp, i32] + [vp] * 12 + [vp]
     L.mjl_apg_obs.argtypes = [vp, vp, vp, vp, i32, vp, vp, vp, vp]
     L.mjl_apg_post.argtypes = [vp, vp, vp, vp, C.c_float, C.c_float, vp, vp, vp, vp, vp, vp, vp]
     L.mjl_apg_obs_vjp.argtypes = [i32, i32, i32, vp, vp, vp, vp, i32, vp, vp, vp, vp]

@@ -16,6 +16,7 @@ AUX_DIM = 9
 OPT_STORE_DERIVED = 0
 OPT_FORCE_GLOBAL_ROWS = 1
 OPT_RESET_POOL = 3  # slots per env of the reset pool (mjl_env_fill_reset_pool)
+OPT_VJP_TAPE = 4  # slots of the APG VJP tape (mjl_env_step_record / mjl_env_step_vjp_replay)
 OPT_VJP_UNROLLED = 2  # step VJPs differentiate the solver iterations as executed (jax.grad semantics)
 
 FIELD = {

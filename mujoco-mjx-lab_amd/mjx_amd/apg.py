@@ -44,9 +44,14 @@ class APGTrainer:
     get_state() / set_state(tape entry), qpos_qvel() and num_envs, act_dim, nq, nv (HumanoidEnv
     through `HumanoidAPGEnv`, or the differentiable stand-in of the CPU tests)."""
 
-    def __init__(self, cfg, env, device="cuda", dist=None, out_dir: Optional[str] = None, use_graph: bool = True):
+    def __init__(self, cfg, env, device="cuda", dist=None, out_dir: Optional[str] = None, use_graph: bool = True,
+                 vjp_tape: bool = True):
+        """vjp_tape: the forward rollout records each step's workspace in HBM (mjl_env_step_record,
+        ~50 KB per env-step: 6 GB at 2048 x 128) and the reverse sweep replays it
+        (mjl_env_step_vjp_replay) instead of restoring the state and recomputing the step."""
         self.cfg, self.env, self.dist = cfg, env, dist
         self.use_graph = bool(use_graph)
+        self.vjp_tape = bool(vjp_tape)
         self._graphs, self._warm = {}, set()
         self.rank = dist.get_rank() if dist is not None else 0
         self.world = dist.get_world_size() if dist is not None else 1
@@ -94,12 +99,15 @@ class APGTrainer:
             self.opt.zero_grad(set_to_none=True)
             with torch.cuda.graph(graph):
                 out = self._loss_and_grad(use_norm, False, graph=True)
+            # the counters the eager call takes: the host code's during capture, plus the reset's own
+            # (passed explicitly, relative to the base, under capture)
+            used = env.counter - c0 + 1
             env.counter = c0  # capture ran nothing; the replay below draws the reset
-            self._graphs[key] = (graph, out, [p.grad for p in self.policy.parameters()])
-        graph, out, grads = self._graphs[key]
+            self._graphs[key] = (graph, out, [p.grad for p in self.policy.parameters()], used)
+        graph, out, grads, used = self._graphs[key]
         env.ctr_base.fill_(env.counter)
         graph.replay()
-        env.counter += 1 + self.cfg.horizon  # what the eager call consumes (reset + steps)
+        env.counter += used
         env.ctr_base.zero_()
         for p, g in zip(self.policy.parameters(), grads):  # the graph's gradient buffers
             p.grad = g
@@ -129,18 +137,25 @@ class APGTrainer:
         disc, ret = torch.ones(B, device=dev), torch.zeros(B, device=dev)
         dropped_e = torch.zeros(B, device=dev)
         dq = float(getattr(cfg, "diverge_qvel", None) or 0.0)
+        taped = self.vjp_tape and hasattr(env, "step_record")
+        if taped and getattr(env, "tape_slots", 0) < H:
+            env.enable_vjp_tape(H)
         tape, acts, leaves = [], [], []
         for t in range(H):
-            tape.append(env.get_state())
+            if not taped:
+                tape.append(env.get_state())
             env.apg_obs(alive, self.rms, use_norm, o_all[t], on_all[t], snap[t])
             on = on_all[t].detach().requires_grad_(True)
             a = self.policy(on)
             acts.append(a)
             leaves.append(on)
-            _, r, te, tr = env.step(a.detach(), auto_reset=False)
+            if taped:  # the step, leaving its forward workspace in tape slot t
+                _, r, te, tr = env.step_record(t, a.detach())
+            else:
+                _, r, te, tr = env.step(a.detach(), auto_reset=False)
             env.apg_post(r, te, tr, gamma, dq, alive, disc, ret, dropped_e, grew_all[t], rfin[t])
         loss = -ret.mean()
-        final = env.get_state()
+        final = None if taped else env.get_state()
         self.opt.zero_grad(set_to_none=True)
         gq = torch.zeros((B, env.nq), device=dev)
         gv = torch.zeros((B, env.nv), device=dev)
@@ -149,11 +164,16 @@ class APGTrainer:
         gws = torch.zeros((B, env.nv), device=dev) if getattr(env, "vjp_carries_ws", False) else None
         gas = [None] * H
         for t in range(H - 1, -1, -1):
-            env.set_state(tape[t], tape[t + 1] if t + 1 < H else final)
-            if gws is not None:
-                gq, gv, gws, ga, gaux = env.step_vjp_full(acts[t].detach(), gq, gv, gws, grew_all[t], gaux, nonfinite)
+            if taped:  # the reverse passes from slot t: no state restore, no recompute
+                gq, gv, gws, ga, gaux = env.step_vjp_replay(t, acts[t].detach(), gq, gv, gws, grew_all[t], gaux,
+                                                            nonfinite)
             else:
-                gq, gv, ga, gaux = env.step_vjp(acts[t].detach(), gq, gv, grew_all[t], gaux, nonfinite)
+                env.set_state(tape[t], tape[t + 1] if t + 1 < H else final)
+                if gws is not None:
+                    gq, gv, gws, ga, gaux = env.step_vjp_full(acts[t].detach(), gq, gv, gws, grew_all[t], gaux,
+                                                              nonfinite)
+                else:
+                    gq, gv, ga, gaux = env.step_vjp(acts[t].detach(), gq, gv, grew_all[t], gaux, nonfinite)
             og, = torch.autograd.grad(acts[t], leaves[t], grad_outputs=ga)
             env.apg_obs_vjp(o_all[t], snap[t], self.rms, use_norm, og, gq, gv)
             gas[t] = ga
@@ -365,6 +385,40 @@ class HumanoidAPGEnv:
 
     def step_vjp(self, act, gq, gv, grew, gaux, nonfinite=None):
         return self.env.step_vjp(act, gq, gv, grew, gaux, nonfinite)
+
+    def enable_vjp_tape(self, slots: int):
+        """Allocate `slots` VJP tape slots (MJL_OPT_VJP_TAPE; outside stream capture)."""
+        from . import abi
+        self.env.data.set_option(abi.OPT_VJP_TAPE, int(slots))
+        self.tape_slots = int(slots)
+
+    def step_record(self, slot: int, act):
+        """The env step (no reset merge) that also records slot `slot` of the VJP tape."""
+        from ._lib import check, lib
+        from .mjx import _ptr, _stream
+        e = self.env
+        act = act.to(e.obs.device, torch.float32).contiguous()
+        check(lib().mjl_env_step_record(e.data.handle, int(slot), _ptr(act), _ptr(e.obs), _ptr(e.rew), _ptr(e.term),
+                                        _ptr(e.trunc), _stream()))
+        return e.obs, e.rew, e.term, e.trunc
+
+    def step_vjp_replay(self, slot: int, act, gq, gv, gws, grew, gaux, nonfinite=None):
+        """VJP of the step recorded in `slot` (mjl_env_step_vjp_replay): returns the cotangents of
+        (qpos, qvel, qacc_warmstart or None, action, aux)."""
+        from . import abi
+        from ._lib import check, lib
+        from .mjx import _ptr, _stream
+        B, dev = self.num_envs, self.env.obs.device
+        f = lambda x, *shape: x.to(dev, torch.float32).reshape(B, *shape).contiguous()  # noqa: E731
+        act, gq, gv, gr = f(act, self.act_dim), f(gq, self.nq), f(gv, self.nv), f(grew)
+        ga = torch.zeros((B, abi.AUX_DIM), device=dev) if gaux is None else f(gaux, abi.AUX_DIM)
+        gw = None if gws is None else f(gws, self.nv)
+        oq, ov, oa, oaux = torch.empty_like(gq), torch.empty_like(gv), torch.empty_like(act), torch.empty_like(ga)
+        ow = None if gws is None else torch.empty_like(gw)
+        check(lib().mjl_env_step_vjp_replay(self.env.data.handle, int(slot), _ptr(act), _ptr(gq), _ptr(gv), _ptr(gw),
+                                            _ptr(gr), _ptr(ga), _ptr(oq), _ptr(ov), _ptr(ow), _ptr(oa), _ptr(oaux),
+                                            _ptr(nonfinite), _stream()))
+        return oq, ov, ow, oa, oaux
 
     def apg_obs(self, alive, rms, use_norm, o, on, snap):
         from ._lib import check, lib

@@ -1,0 +1,75 @@
+"""VJP tape (mjl_env_step_record / mjl_env_step_vjp_replay): the recorded step is the env step, and
+the replayed VJP is the recomputing one (train_apg.py:187-189's jax.grad through the step)."""
+import pytest
+import torch
+
+import mjx_amd
+from mjx_amd import abi, apg, mjcf, mjx
+from mjx_amd.config import reference_ppo_config
+from mjx_amd.envs import HumanoidEnv, resolve_ids
+
+pytestmark = pytest.mark.gpu
+
+STATE = ("qpos", "qvel", "qacc_warmstart", "ctrl", "time", "aux")
+
+
+def _pair(solver, vjp, B=64):
+    m = mjx_amd.load_model("humanoid_mjx")
+    if solver == "cg44":
+        m.solver, m.iterations, m.ls_iterations = mjcf.SOLVER_CG, 4, 4
+    ecfg = resolve_ids(m, reference_ppo_config().env_config)
+    return m, [apg.HumanoidAPGEnv(HumanoidEnv(mjx.put_model(m), ecfg, B, seed=9), vjp) for _ in range(2)]
+
+
+@pytest.mark.parametrize("solver,vjp", [("model", "implicit"), ("cg44", "unrolled")])
+def test_record_and_replay_equal_step_and_recompute(solver, vjp):
+    """Over 12 steps of random actions: the recorded step's outputs and state are the env step's;
+    the replayed VJP's cotangents (state, warm start, action, aux) are those of the VJP that restores
+    the pre-step state and recomputes (same warm start), bit for bit."""
+    m, (plain, taped) = _pair(solver, vjp)
+    B, H = plain.num_envs, 12
+    taped.enable_vjp_tape(H)
+    for e in (plain, taped):
+        e.reset()
+    g = torch.Generator(device="cuda").manual_seed(1)
+    acts, pre = [], []
+    for t in range(H):
+        a = torch.rand((B, m.nu), generator=g, device="cuda") * 2 - 1
+        acts.append(a)
+        pre.append(plain.get_state())
+        o1 = [x.clone() for x in plain.step(a)]
+        o2 = [x.clone() for x in taped.step_record(t, a)]
+        for x, y, k in zip(o1, o2, ("obs", "rew", "term", "trunc")):
+            assert torch.equal(x, y), f"step {t}: {k}"
+        for f in STATE:
+            assert torch.equal(plain.env.data.get(f), taped.env.data.get(f)), f"step {t}: {f}"
+    gws_on = vjp == "unrolled"
+    for t in range(H - 1, -1, -1):
+        gq = torch.randn((B, m.nq), generator=g, device="cuda")
+        gv = torch.randn((B, m.nv), generator=g, device="cuda")
+        gw = torch.randn((B, m.nv), generator=g, device="cuda") if gws_on else None
+        gr = torch.randn(B, generator=g, device="cuda")
+        gx = torch.randn((B, abi.AUX_DIM), generator=g, device="cuda")
+        plain.env.set_state(pre[t])  # the forward's own warm start
+        if gws_on:
+            r1 = plain.step_vjp_full(acts[t], gq, gv, gw, gr, gx)
+        else:
+            oq, ov, oa, ox = plain.step_vjp(acts[t], gq, gv, gr, gx)
+            r1 = (oq, ov, None, oa, ox)
+        r2 = taped.step_vjp_replay(t, acts[t], gq, gv, gw, gr, gx)
+        for x, y, k in zip(r1, r2, ("qpos", "qvel", "ws", "act", "aux")):
+            if x is None:
+                assert y is None
+                continue
+            assert torch.equal(x, y), f"step {t}: {k} cotangent ({(x - y).abs().max().item():.3g})"
+
+
+def test_tape_slot_bounds():
+    m, (env, _) = _pair("model", "implicit", B=4)
+    a = torch.zeros((4, m.nu), device="cuda")
+    with pytest.raises(Exception, match="slot"):
+        env.step_record(0, a)
+    env.enable_vjp_tape(2)
+    env.step_record(1, a)
+    with pytest.raises(Exception, match="slot"):
+        env.step_record(2, a)
