@@ -1045,8 +1045,11 @@ template <class D> INL void adj_rne(MP m, LDSA WS<D>* W, LDSA WSA<D>* A, int lan
   SYNC();
   if (isb) {  // cfrc-bar_c = sum over ancestors-or-self b of cfsub-bar_b
     float s[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-    for (int b = lane; b > 0; b = ldrec(&m->brec[b]).parent)
+    for (uint32_t mk = m->body_ancmask[lane]; mk;) {  // self, then up the chain
+      const int b = 31 - __clz(mk);
+      mk &= ~(1u << b);
       for (int k = 0; k < 6; k++) s[k] += A->cfsubb[b][k];
+    }
     for (int k = 0; k < 6; k++) A->cfrcb[lane][k] = s[k];
   }
   // recompute cvel / cacc (tree pass of velocity_stage)
@@ -1092,9 +1095,8 @@ template <class D> INL void adj_rne(MP m, LDSA WS<D>* W, LDSA WSA<D>* A, int lan
     }
     SYNC();
     if (isb && br.level == L - 1) {
-      for (int c = lane + 1; c < br.subtree_end; c++) {
-        const BodyRec cb = ldrec(&m->brec[c]);
-        if (cb.parent != lane) continue;
+      for (uint32_t mk = m->body_childmask[lane]; mk; mk &= mk - 1) {
+        const int c = __ffs(mk) - 1;
         for (int i = 0; i < 6; i++) { A->cvelb[lane][i] += A->cfsubb[c][i]; A->caccb[lane][i] += A->cfrcb[c][i]; }
       }
     }
@@ -1194,8 +1196,11 @@ template <class D> INL void adj_mass(MP m, LDSA WS<D>* W, LDSA WSA<D>* A, int la
 template <class D> INL void adj_crb(MP m, LDSA WSA<D>* A, int lane) {
   if (lane > 0 && lane < m->nbody) {
     float s[10] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-    for (int b = lane; b > 0; b = ldrec(&m->brec[b]).parent)
+    for (uint32_t mk = m->body_ancmask[lane]; mk;) {  // self, then up the chain
+      const int b = 31 - __clz(mk);
+      mk &= ~(1u << b);
       for (int k = 0; k < 10; k++) s[k] += A->crbb[b][k];
+    }
     for (int k = 0; k < 10; k++) A->cinertb[lane][k] += s[k];
   }
   SYNC();
@@ -1284,9 +1289,7 @@ template <class D> INL void adj_kinematics(MP m, LDSA WS<D>* W, LDSA WSA<D>* A, 
   // scom_r = sum_c m_c xipos_c / sum_c m_c over the root's subtree
   if (isb) {
     const int r = br.rootid;
-    float mr = 0.f;
-    const BodyRec rr = ldrec(&m->brec[r]);
-    for (int c = r; c < rr.subtree_end; c++) mr += m->body_mass[c];
+    const float mr = m->body_rootmass[r];
     if (mr >= kMinVal) for (int i = 0; i < 3; i++) A->xiposb[lane][i] += br.mass / mr * A->scomb[r][i];
   }
   SYNC();
@@ -1304,11 +1307,12 @@ template <class D> INL void adj_kinematics(MP m, LDSA WS<D>* W, LDSA WSA<D>* A, 
   SYNC();
   if (lane < nbody) {  // gather: free joint -> its body; hinge -> its parent frame (la, lx in local)
     float pb[3] = {0.f, 0.f, 0.f}, mb[9] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-    for (int j = 0; j < njnt; j++) {
+    for (uint32_t mk = m->body_jgather[lane]; mk; mk &= mk - 1) {
+      const int j = __ffs(mk) - 1;
       const JntRec jr = ldrec(&m->jrec[j]);
-      if (jr.isfree && jr.body == lane) {
+      if (jr.isfree) {
         for (int i = 0; i < 3; i++) { pb[i] += A->xanchorb[j][i]; mb[3 * i + 2] += A->xaxisb[j][i]; }
-      } else if (!jr.isfree && jr.parent == lane) {
+      } else {
         // anc = xpos_p + xmat_p la, ax = xmat_p lx with la, lx the local values stored in xanchor/xaxis?
         // (the forward overwrote them with world values: recover local = xmat_p^T (world - xpos_p))
         float la[3], lx[3], wa[3] = {W->xanchor[j][0] - W->xpos[lane][0], W->xanchor[j][1] - W->xpos[lane][1],
@@ -1392,9 +1396,8 @@ template <class D> INL void adj_kinematics(MP m, LDSA WS<D>* W, LDSA WSA<D>* A, 
     }
     SYNC();
     if (isb && br.level == L - 1) {
-      for (int c = lane + 1; c < br.subtree_end; c++) {
-        const BodyRec cb = ldrec(&m->brec[c]);
-        if (cb.parent != lane || cb.isfree) continue;
+      for (uint32_t mk = m->body_childmask_nf[lane]; mk; mk &= mk - 1) {
+        const int c = __ffs(mk) - 1;
         for (int i = 0; i < 4; i++) A->xquatb[lane][i] += A->Sb[c][i];
         A->xposb[lane][0] += A->Sb[c][4]; A->xposb[lane][1] += A->Sb[c][5]; A->xposb[lane][2] += A->Ub[c][0];
         for (int i = 0; i < 6; i++) A->xmatb[lane][i] += A->Tb[c][i];

@@ -145,6 +145,24 @@ int mjl_model_create(const mjlModelDesc* d, mjlModel** out) {
       for (int k = d->body_dofadr[bb]; k < d->body_dofadr[bb] + d->body_dofnum[bb]; k++) mask |= 1u << k;
     f.body_dofmask[b] = mask;
   }
+  for (int b = 1; b < d->nbody; b++) {
+    uint32_t anc = 0;
+    for (int bb = b; bb > 0; bb = d->body_parentid[bb]) anc |= 1u << bb;
+    f.body_ancmask[b] = anc;
+    const int p = d->body_parentid[b];
+    const bool bfree = d->body_jntnum[b] > 0 && d->jnt_type[d->body_jntadr[b]] == MJL_JNT_FREE;
+    if (p > 0) {
+      f.body_childmask[p] |= 1u << b;
+      if (!bfree) f.body_childmask_nf[p] |= 1u << b;
+    }
+    float mr = 0.f;  // the same float sum, in the same order, as a loop over the subtree would take
+    for (int c = b; c < d->body_subtree_end[b]; c++) mr += f.body_mass[c];
+    f.body_rootmass[b] = mr;
+  }
+  for (int j = 0; j < d->njnt; j++) {
+    const int b = d->jnt_bodyid[j];
+    f.body_jgather[d->jnt_type[j] == MJL_JNT_FREE ? b : d->body_parentid[b]] |= 1u << j;
+  }
   int nlim = 0;
   for (int j = 0; j < d->njnt; j++) {
     if (d->jnt_type[j] != MJL_JNT_FREE && d->jnt_type[j] != MJL_JNT_HINGE) {

@@ -70,6 +70,13 @@ struct ModelF {
   int body_jntnum[MJL_MAXBODY], body_dofadr[MJL_MAXBODY], body_dofnum[MJL_MAXBODY];
   int body_subtree_end[MJL_MAXBODY], body_level[MJL_MAXBODY];
   uint32_t body_dofmask[MJL_MAXBODY];  // bit d set <=> dof d moves body b (ancestor chain)
+  // tree walks of the reverse passes as bit loops (no record loads in the loop): ancestors-or-self
+  // (world excluded), children, children without a free joint, joints whose world anchor / axis
+  // cotangents gather into b (b's free joint, hinges of b's children); the float sum of the masses
+  // of root r's subtree in body order
+  uint32_t body_ancmask[MJL_MAXBODY], body_childmask[MJL_MAXBODY], body_childmask_nf[MJL_MAXBODY];
+  uint32_t body_jgather[MJL_MAXBODY];
+  float body_rootmass[MJL_MAXBODY];
   float body_pos[MJL_MAXBODY][3], body_quat[MJL_MAXBODY][4], body_ipos[MJL_MAXBODY][3];
   float body_inertia[MJL_MAXBODY][6], body_mass[MJL_MAXBODY], body_invweight0[MJL_MAXBODY][2];
 
