@@ -13,6 +13,7 @@
 #include "adjoint.hip"
 #include "ppo_kernels.hip"
 #include "apg_kernels.hip"
+#include "ppo_loss_kernels.hip"
 
 using namespace mjl;
 
@@ -1040,6 +1041,62 @@ extern "C" int mjl_apg_obs_vjp(int B, int nq, int nv, const float* o, const uint
   if (n == 0) return MJL_OK;
   hipLaunchKernelGGL(apg_obs_vjp_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, (hipStream_t)stream, B, nq,
                      nv, o, alive_snap, mean, var, use_norm, go, g_qpos, g_qvel);
+  HIPCHK(hipGetLastError());
+  return MJL_OK;
+}
+
+// ---------------------------------------------------------------- PPO update losses
+extern "C" long long mjl_ppo_loss_scratch(int n, int A) {
+  if (n <= 0 || A <= 0) return 0;
+  const long long nb = (n + kLossT - 1) / kLossT;
+  return 3 * nb + nb * (A + 1);
+}
+
+extern "C" int mjl_ppo_surrogate(const float* mean, const float* log_std, const float* act, const float* old_logp,
+                                 const float* adv, int n, int A, float clip_eps, float ent_coef, float* scratch,
+                                 float* loss, float* g_mean, float* g_log_std, void* stream) {
+  if (!mean || !log_std || !act || !old_logp || !adv || !scratch || !loss || !g_mean || !g_log_std || n <= 0 || A <= 0)
+    return fail(MJL_ERR_ARG, "bad argument");
+  if (A > kLossMaxA) return fail(MJL_ERR_UNSUPPORTED, "ppo surrogate: at most %d action columns", kLossMaxA);
+  hipStream_t s = (hipStream_t)stream;
+  const int nb = (n + kLossT - 1) / kLossT;
+  float* adv_part = scratch;
+  float* part = scratch + 3 * (size_t)nb;
+  hipLaunchKernelGGL(adv_stats_kernel, dim3(nb), dim3(kLossT), 0, s, adv, n, adv_part);
+  hipLaunchKernelGGL(ppo_surrogate_kernel, dim3(nb), dim3(kLossT), 0, s, mean, log_std, act, old_logp, adv, n, A,
+                     clip_eps, adv_part, nb, g_mean, part);
+  hipLaunchKernelGGL(ppo_surrogate_final_kernel, dim3(1), dim3(64), 0, s, part, nb, n, A, log_std, ent_coef, loss,
+                     g_log_std);
+  HIPCHK(hipGetLastError());
+  return MJL_OK;
+}
+
+extern "C" int mjl_mse(const float* v, const float* r, int n, float* scratch, float* loss, float* g_v, void* stream) {
+  if (!v || !r || !scratch || !loss || !g_v || n <= 0) return fail(MJL_ERR_ARG, "bad argument");
+  hipStream_t s = (hipStream_t)stream;
+  const int nb = (n + kLossT - 1) / kLossT;
+  hipLaunchKernelGGL(mse_kernel, dim3(nb), dim3(kLossT), 0, s, v, r, n, g_v, scratch);
+  hipLaunchKernelGGL(mse_final_kernel, dim3(1), dim3(64), 0, s, scratch, nb, n, loss);
+  HIPCHK(hipGetLastError());
+  return MJL_OK;
+}
+
+extern "C" int mjl_gather_rows(const long long* idx, int n, int narr, const float* const* src, float* const* dst,
+                               const int* cols, void* stream) {
+  if (!idx || n < 0 || narr < 1 || narr > 5 || !src || !dst || !cols) return fail(MJL_ERR_ARG, "bad argument");
+  GatherArgs g;
+  std::memset(&g, 0, sizeof(g));
+  g.narr = narr;
+  long long tot = 0;
+  for (int k = 0; k < narr; k++) {
+    if (!src[k] || !dst[k] || cols[k] <= 0) return fail(MJL_ERR_ARG, "bad argument");
+    g.src[k] = src[k]; g.dst[k] = dst[k]; g.cols[k] = cols[k];
+    tot += cols[k];
+  }
+  const long long work = (long long)n * tot;
+  if (work == 0) return MJL_OK;
+  hipLaunchKernelGGL(gather_rows_kernel, dim3((unsigned)((work + 255) / 256)), dim3(256), 0, (hipStream_t)stream, idx,
+                     n, g);
   HIPCHK(hipGetLastError());
   return MJL_OK;
 }

@@ -1,0 +1,171 @@
+// PPO update losses as native launches (reference train_ppo.py:204-220): the clipped surrogate with
+// the advantage normalisation, the Gaussian log-prob and the entropy bonus, and the value MSE, each
+// returning the loss and its gradients in one forward pass (the backward is a scale by the incoming
+// gradient). Deterministic: block partials reduced in a fixed order, no float atomics.
+#pragma once
+#include <hip/hip_runtime.h>
+
+namespace mjl {
+
+constexpr int kLossT = 256;       // threads per block = rows per block
+constexpr int kLossMaxA = 32;     // action columns
+constexpr float kLog2Pi = 1.8378770664093453f;
+
+// block sum of v over kLossT threads (fixed tree), result valid in thread 0
+__device__ __forceinline__ float block_sum(float v, float* red) {
+  const int t = threadIdx.x;
+  red[t] = v;
+  __syncthreads();
+  for (int s = kLossT / 2; s > 0; s >>= 1) {
+    if (t < s) red[t] += red[t + s];
+    __syncthreads();
+  }
+  const float r = red[0];
+  __syncthreads();
+  return r;
+}
+
+// per-block advantage statistics (count, mean, M2: two passes over the block's rows) for Chan's merge
+__global__ __launch_bounds__(kLossT) void adv_stats_kernel(const float* __restrict__ adv, int n, float* __restrict__ part) {
+  __shared__ float red[kLossT];
+  const int i = blockIdx.x * kLossT + threadIdx.x;
+  const bool in = i < n;
+  const float x = in ? adv[i] : 0.f;
+  const float cnt = (float)min(kLossT, n - blockIdx.x * kLossT);
+  const float mu = block_sum(x, red) / cnt;
+  const float dx = in ? x - mu : 0.f;
+  const float m2 = block_sum(dx * dx, red);
+  if (threadIdx.x == 0) { part[3 * blockIdx.x] = cnt; part[3 * blockIdx.x + 1] = mu; part[3 * blockIdx.x + 2] = m2; }
+}
+
+// the minibatch's advantage mean and population std from the block partials (Chan et al. pairwise
+// merge in block order; every caller reduces the same partials the same way)
+__device__ __forceinline__ void adv_merge(const float* __restrict__ part, int nb, float& mu, float& sd) {
+  float c = 0.f, m = 0.f, M2 = 0.f;
+  for (int b = 0; b < nb; b++) {
+    const float cb = part[3 * b], mb = part[3 * b + 1], M2b = part[3 * b + 2];
+    const float tot = c + cb, d = mb - m;
+    m = m + d * (cb / tot);
+    M2 = M2 + M2b + d * d * (c * cb / tot);
+    c = tot;
+  }
+  mu = m;
+  sd = sqrtf(M2 / c);
+}
+
+// per row: logp = -1/2 (sum_j (a - m)^2 e^(-2 s_j) + sum_j (2 s_j + log 2 pi)), ratio = exp(logp -
+// old), surr = min(ratio an, clip(ratio, 1 - eps, 1 + eps) an) with an the normalised advantage;
+// d(-mean surr)/d mean written per row, block partials of sum surr and of d/d s_j
+__global__ __launch_bounds__(kLossT) void ppo_surrogate_kernel(
+    const float* __restrict__ mean, const float* __restrict__ log_std, const float* __restrict__ act,
+    const float* __restrict__ old_logp, const float* __restrict__ adv, int n, int A, float clip_eps,
+    const float* __restrict__ adv_part, int nb, float* __restrict__ gmean, float* __restrict__ part) {
+  __shared__ float red[kLossT];
+  __shared__ float ivs[kLossMaxA], lss;
+  __shared__ float mu_s, sd_s;
+  const int t = threadIdx.x, i = blockIdx.x * kLossT + t;
+  if (t < A) ivs[t] = expf(-2.f * log_std[t]);
+  if (t == 0) {
+    float s = 0.f;
+    for (int j = 0; j < A; j++) s += 2.f * log_std[j] + kLog2Pi;
+    lss = s;
+    float mu, sd;
+    adv_merge(adv_part, nb, mu, sd);
+    mu_s = mu; sd_s = sd;
+  }
+  __syncthreads();
+  const bool in = i < n;
+  const float* ar = act + (size_t)(in ? i : 0) * A;
+  const float* mr = mean + (size_t)(in ? i : 0) * A;
+  float qs = 0.f;
+  for (int j = 0; j < A; j++) {
+    const float d = ar[j] - mr[j];
+    qs += d * d * ivs[j];
+  }
+  float surr = 0.f, dlogp = 0.f;
+  if (in) {
+    const float logp = -0.5f * (qs + lss);
+    const float ratio = expf(logp - old_logp[i]);
+    const float an = (adv[i] - mu_s) / (sd_s + 1e-8f);
+    const float lo = 1.f - clip_eps, hi = 1.f + clip_eps;
+    const float rc = fminf(fmaxf(ratio, lo), hi);
+    const float t1 = ratio * an, t2 = rc * an;
+    surr = fminf(t1, t2);
+    // torch.minimum's gradient: the smaller argument, half each on a tie; the clip passes it inside
+    // [lo, hi] (bounds included)
+    const float w1 = t1 < t2 ? 1.f : (t1 == t2 ? 0.5f : 0.f);
+    const float w2 = t2 < t1 ? 1.f : (t1 == t2 ? 0.5f : 0.f);
+    const float dratio = (-1.f / (float)n) * (w1 * an + ((ratio >= lo && ratio <= hi) ? w2 * an : 0.f));
+    dlogp = dratio * ratio;
+    for (int j = 0; j < A; j++) gmean[(size_t)i * A + j] = dlogp * (ar[j] - mr[j]) * ivs[j];
+  }
+  const float ssum = block_sum(surr, red);
+  if (t == 0) part[(size_t)blockIdx.x * (A + 1)] = ssum;
+  for (int j = 0; j < A; j++) {  // d logp / d s_j = q_j - 1
+    const float d = ar[j] - mr[j];
+    const float c = block_sum(in ? dlogp * (d * d * ivs[j] - 1.f) : 0.f, red);
+    if (t == 0) part[(size_t)blockIdx.x * (A + 1) + 1 + j] = c;
+  }
+}
+
+// loss = -sum surr / n - ent_coef * entropy; d loss / d s_j = sum of the partials - ent_coef / A
+// (entropy = 0.5 sum_j (1 + log 2 pi + 2 s_j) / A, train_ppo.py:215)
+__global__ __launch_bounds__(64) void ppo_surrogate_final_kernel(const float* __restrict__ part, int nb, int n, int A,
+                                                                 const float* __restrict__ log_std, float ent_coef,
+                                                                 float* __restrict__ loss, float* __restrict__ glog_std) {
+  const int t = threadIdx.x;
+  if (t <= A) {
+    float s = 0.f;
+    for (int b = 0; b < nb; b++) s += part[(size_t)b * (A + 1) + t];
+    if (t == 0) {
+      float e = 0.f;
+      for (int j = 0; j < A; j++) e += 1.f + kLog2Pi + 2.f * log_std[j];
+      loss[0] = -s / (float)n - ent_coef * (0.5f * e / (float)A);
+    } else {
+      glog_std[t - 1] = s - ent_coef / (float)A;
+    }
+  }
+}
+
+// value MSE: per block sum of (v - r)^2 and d/dv = 2 (v - r) / n
+__global__ __launch_bounds__(kLossT) void mse_kernel(const float* __restrict__ v, const float* __restrict__ r, int n,
+                                                     float* __restrict__ gv, float* __restrict__ part) {
+  __shared__ float red[kLossT];
+  const int i = blockIdx.x * kLossT + threadIdx.x;
+  float e = 0.f;
+  if (i < n) {
+    const float d = v[i] - r[i];
+    e = d * d;
+    gv[i] = 2.f * d / (float)n;
+  }
+  const float s = block_sum(e, red);
+  if (threadIdx.x == 0) part[blockIdx.x] = s;
+}
+__global__ __launch_bounds__(64) void mse_final_kernel(const float* __restrict__ part, int nb, int n, float* __restrict__ loss) {
+  if (threadIdx.x == 0) {
+    float s = 0.f;
+    for (int b = 0; b < nb; b++) s += part[b];
+    loss[0] = s / (float)n;
+  }
+}
+
+// minibatch gather: dst_k[r] = src_k[idx[r]] for up to 5 row-major arrays of `cols_k` columns
+struct GatherArgs {
+  const float* src[5];
+  float* dst[5];
+  int cols[5];
+  int narr;
+};
+__global__ __launch_bounds__(256) void gather_rows_kernel(const long long* __restrict__ idx, int n, GatherArgs g) {
+  const long long tid = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  int tot = 0;
+  for (int k = 0; k < g.narr; k++) tot += g.cols[k];
+  if (tid >= (long long)n * tot) return;
+  const int r = (int)(tid / tot);
+  int c = (int)(tid % tot), k = 0;
+  while (c >= g.cols[k]) { c -= g.cols[k]; k++; }
+  const long long s = idx[r];
+  g.dst[k][(size_t)r * g.cols[k] + c] = g.src[k][(size_t)s * g.cols[k] + c];
+}
+
+}  // namespace mjl

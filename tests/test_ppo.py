@@ -477,3 +477,46 @@ def test_jax_key_chain_follows_train_ppo():
         roll = roll[0]
     np.testing.assert_array_equal(tr._env_keys.cpu().numpy().view(np.uint32), keys)
     np.testing.assert_array_equal(tr._jax_rng.cpu().numpy().view(np.uint32), rng)
+
+
+@pytest.mark.gpu
+def test_native_update_losses_match_torch_ops():
+    """mjl_ppo_surrogate / mjl_mse / mjl_gather_rows against the torch restatement of
+    train_ppo.py:204-220 on a 65,536-row minibatch: losses and every parameter gradient of both nets,
+    with ratios spread across the clip range (ties, both sides of the bounds)."""
+    cfg = reference_ppo_config()
+    g = torch.Generator().manual_seed(0)
+    pol = ppo.GaussianPolicy(54, 21, cfg.policy_hidden_layer_specs, cfg.log_std_init, g).cuda()
+    val = ppo.ValueNet(54, cfg.value_hidden_layer_specs, g).cuda()
+    gd = torch.Generator(device="cuda").manual_seed(3)
+    N, n = 131072, 65536
+    obs = torch.randn((N, 54), generator=gd, device="cuda")
+    idx = torch.randperm(N, generator=gd, device="cuda")[:n]
+    with torch.no_grad():
+        mean, log_std = pol(obs)
+        acts = (mean + torch.exp(log_std) * torch.randn((N, 21), generator=gd, device="cuda")).contiguous()
+        from mjx_amd.ppo import gaussian_logprob
+        logp = gaussian_logprob(mean, log_std, acts) + 0.3 * torch.randn(N, generator=gd, device="cuda")
+    ret = torch.randn(N, generator=gd, device="cuda")
+    adv = 2.0 * torch.randn(N, generator=gd, device="cuda") + 0.5
+    res = []
+    for native in (True, False):
+        ppo.NATIVE_LOSSES = native
+        try:
+            o, a, ol, r, ad = (ppo._gather_minibatch(idx, obs, acts, logp, ret, adv) if native else
+                               (obs[idx], acts[idx], logp[idx], ret[idx], adv[idx]))
+            for p in list(pol.parameters()) + list(val.parameters()):
+                p.grad = None
+            lp = ppo.ppo_policy_loss(pol, o, a, ol, ad, cfg.clip_eps, cfg.ent_coef)
+            lv = ppo.value_loss(val, o, r)
+            (lp + lv).backward()
+            res.append((float(lp), float(lv), [p.grad.clone() for p in list(pol.parameters()) + list(val.parameters())],
+                        (o, a, ol, r, ad)))
+        finally:
+            ppo.NATIVE_LOSSES = True
+    (lp1, lv1, g1, d1), (lp2, lv2, g2, d2) = res
+    for x, y in zip(d1, d2):
+        assert torch.equal(x, y)
+    assert lp1 == pytest.approx(lp2, rel=1e-5, abs=1e-6) and lv1 == pytest.approx(lv2, rel=1e-5)
+    for x, y in zip(g1, g2):
+        torch.testing.assert_close(x, y, rtol=1e-4, atol=1e-6)
