@@ -388,6 +388,11 @@ int mjl_ppo_surrogate(const float* mean, const float* log_std, const float* act,
 int mjl_mse(const float* v, const float* r, int n, float* scratch, float* loss, float* g_v, void* stream);
 int mjl_gather_rows(const long long* idx, int n, int narr, const float* const* src, float* const* dst,
                     const int* cols, void* stream);
+/* Adam (optax.adam defaults as train_ppo.py:84-85 build them; torch.optim.Adam's fused update) over
+ * nt <= 16 float32 tensors in one launch: m = b1 m + (1 - b1) g, v = b2 v + (1 - b2) g^2,
+ * p -= lr / (1 - b1^step) m / (sqrt(v) / sqrt(1 - b2^step) + eps); g[k] NULL skips tensor k. */
+int mjl_adam(int nt, float* const* p, const float* const* g, float* const* m, float* const* v,
+             const long long* numel, float lr, float beta1, float beta2, float eps, int step, void* stream);
 
 #ifdef __cplusplus
 }

@@ -1100,3 +1100,25 @@ extern "C" int mjl_gather_rows(const long long* idx, int n, int narr, const floa
   HIPCHK(hipGetLastError());
   return MJL_OK;
 }
+
+extern "C" int mjl_adam(int nt, float* const* p, const float* const* g, float* const* m, float* const* v,
+                        const long long* numel, float lr, float beta1, float beta2, float eps, int step, void* stream) {
+  if (nt < 1 || nt > kAdamMaxT || !p || !g || !m || !v || !numel || step < 1) return fail(MJL_ERR_ARG, "bad argument");
+  AdamArgs a;
+  std::memset(&a, 0, sizeof(a));
+  a.nt = nt;
+  for (int k = 0; k < nt; k++) {
+    if (!p[k] || !m[k] || !v[k] || numel[k] < 0) return fail(MJL_ERR_ARG, "bad argument");
+    a.p[k] = p[k]; a.g[k] = g[k]; a.m[k] = m[k]; a.v[k] = v[k];
+    a.off[k + 1] = a.off[k] + numel[k];
+  }
+  const float bc1 = 1.f - powf(beta1, (float)step), bc2 = 1.f - powf(beta2, (float)step);
+  a.step_size = lr / bc1;
+  a.bc2_sqrt = sqrtf(bc2);
+  a.b1 = beta1; a.b2 = beta2; a.eps = eps;
+  const long long n = a.off[nt];
+  if (n == 0) return MJL_OK;
+  hipLaunchKernelGGL(adam_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, (hipStream_t)stream, a);
+  HIPCHK(hipGetLastError());
+  return MJL_OK;
+}

@@ -168,4 +168,33 @@ __global__ __launch_bounds__(256) void gather_rows_kernel(const long long* __res
   g.dst[k][(size_t)r * g.cols[k] + c] = g.src[k][(size_t)s * g.cols[k] + c];
 }
 
+// Adam over up to 16 tensors in one launch (torch.optim.Adam's fused update, fp32): m = b1 m +
+// (1 - b1) g; v = b2 v + (1 - b2) g^2; p -= step_size m / (sqrt(v) / bc2_sqrt + eps), step_size =
+// lr / (1 - b1^t), bc2_sqrt = sqrt(1 - b2^t); tensors without a gradient are skipped
+constexpr int kAdamMaxT = 16;
+struct AdamArgs {
+  float* p[kAdamMaxT];
+  const float* g[kAdamMaxT];
+  float* m[kAdamMaxT];
+  float* v[kAdamMaxT];
+  long long off[kAdamMaxT + 1];
+  int nt;
+  float step_size, bc2_sqrt, b1, b2, eps;
+};
+__global__ __launch_bounds__(256) void adam_kernel(AdamArgs a) {
+  const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= a.off[a.nt]) return;
+  int k = 0;
+  while (i >= a.off[k + 1]) k++;
+  if (!a.g[k]) return;
+  const long long j = i - a.off[k];
+  const float g = a.g[k][j];
+  const float m = a.b1 * a.m[k][j] + (1.f - a.b1) * g;
+  const float v = a.b2 * a.v[k][j] + (1.f - a.b2) * g * g;
+  a.m[k][j] = m;
+  a.v[k][j] = v;
+  const float denom = sqrtf(v) / a.bc2_sqrt + a.eps;
+  a.p[k][j] = a.p[k][j] - a.step_size * m / denom;
+}
+
 }  // namespace mjl

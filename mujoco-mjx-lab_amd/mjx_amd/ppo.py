@@ -455,6 +455,63 @@ def make_index_batches(total: int, minibatch: int, epochs: int, generator: torch
     return torch.cat(out, 0).to(device)
 
 
+class NativeAdam:
+    """torch.optim.Adam (betas, eps; no weight decay) for CUDA float32 parameters as one native
+    launch per step (mjl_adam: the fused update of every tensor), where torch's fused Adam took
+    ≈42 µs for the 151K-parameter policy. zero_grad / step / state_dict / load_state_dict as torch's."""
+
+    def __init__(self, params, lr: float, betas=(0.9, 0.999), eps: float = 1e-8):
+        self.params = [p for p in params]
+        if len(self.params) > 16 or any((not p.is_cuda) or p.dtype != torch.float32 or not p.is_contiguous()
+                                        for p in self.params):
+            raise ValueError("NativeAdam: at most 16 contiguous float32 CUDA tensors")
+        self.lr, self.betas, self.eps = float(lr), (float(betas[0]), float(betas[1])), float(eps)
+        self.m = [torch.zeros_like(p) for p in self.params]
+        self.v = [torch.zeros_like(p) for p in self.params]
+        self.t = 0
+
+    def zero_grad(self, set_to_none: bool = True):
+        for p in self.params:
+            if set_to_none:
+                p.grad = None
+            elif p.grad is not None:
+                p.grad.zero_()
+
+    @torch.no_grad()
+    def step(self):
+        import ctypes
+        from ._lib import check, lib
+        self.t += 1
+        k = len(self.params)
+        grads = [p.grad if p.grad is None else p.grad.contiguous() for p in self.params]
+        vp = ctypes.c_void_p * k
+        check(lib().mjl_adam(k, vp(*[p.data_ptr() for p in self.params]),
+                             vp(*[None if g is None else g.data_ptr() for g in grads]),
+                             vp(*[x.data_ptr() for x in self.m]), vp(*[x.data_ptr() for x in self.v]),
+                             (ctypes.c_longlong * k)(*[p.numel() for p in self.params]), self.lr, self.betas[0],
+                             self.betas[1], self.eps, self.t, torch.cuda.current_stream(self.params[0].device).cuda_stream))
+        self._keep = grads  # the launch reads them asynchronously
+
+    def state_dict(self):
+        return {"t": self.t, "lr": self.lr, "betas": list(self.betas), "eps": self.eps,
+                "m": [x.detach().clone() for x in self.m], "v": [x.detach().clone() for x in self.v]}
+
+    def load_state_dict(self, d):
+        self.t, self.lr, self.eps = int(d["t"]), float(d["lr"]), float(d["eps"])
+        self.betas = (float(d["betas"][0]), float(d["betas"][1]))
+        for dst, src in zip(self.m + self.v, list(d["m"]) + list(d["v"])):
+            dst.copy_(src)
+
+
+def _adam(params, lr):
+    """optax.adam defaults (b1 .9, b2 .999, eps 1e-8) = torch.optim.Adam defaults; on the GPU one
+    native launch per step (NativeAdam), on the CPU torch's."""
+    params = list(params)
+    if params and all(p.is_cuda for p in params) and len(params) <= 16:
+        return NativeAdam(params, lr=lr, betas=(0.9, 0.999), eps=1e-8)
+    return torch.optim.Adam(params, lr=lr, betas=(0.9, 0.999), eps=1e-8)
+
+
 def _flat_grads(params: List[torch.Tensor]) -> torch.Tensor:
     return torch.cat([(p.grad if p.grad is not None else torch.zeros_like(p)).reshape(-1) for p in params])
 
@@ -527,11 +584,8 @@ class PPOTrainer:
         if dist is not None:
             for p in list(self.policy.parameters()) + list(self.value.parameters()):
                 dist.broadcast(p.data, 0)
-        # optax.adam defaults (b1 .9, b2 .999, eps 1e-8) = torch.optim.Adam defaults
-        # (fused: one multi-tensor kernel per step on the GPU, the same update formula)
-        fused = {"fused": True} if self.device.type == "cuda" else {}
-        self.opt_p = torch.optim.Adam(self.policy.parameters(), lr=cfg.lr_policy, betas=(0.9, 0.999), eps=1e-8, **fused)
-        self.opt_v = torch.optim.Adam(self.value.parameters(), lr=cfg.lr_value, betas=(0.9, 0.999), eps=1e-8, **fused)
+        self.opt_p = _adam(self.policy.parameters(), cfg.lr_policy)
+        self.opt_v = _adam(self.value.parameters(), cfg.lr_value)
         self.rms = RunningMeanStd(env.obs_dim, self.device)
         self.gen = torch.Generator(device=self.device).manual_seed(int(cfg.seed) * 1000 + self.rank)
         # minibatch permutations drawn on the device they index (4 host randperms of T*B took ~30 ms)
