@@ -375,7 +375,8 @@ int mjl_colsum(const float* x, int n, int d, float* scratch, float* out, void* s
  * mjl_ppo_surrogate: loss = -mean_i min(r_i an_i, clip(r_i, 1 - clip_eps, 1 + clip_eps) an_i)
  *   - ent_coef 0.5 sum_j (1 + log 2 pi + 2 log_std_j) / A, with r_i = exp(logp_i - old_logp_i),
  *   logp the diagonal Gaussian log-density of act under (mean, exp(log_std)) and an the advantage
- *   normalised over the n rows, (adv - mean) / (population std + 1e-8); g_mean [n, A] and
+ *   normalised over the n rows, (adv - mean) / (population std + 1e-8) — or by adv_stats = (mean,
+ *   std) when given (device, the data-parallel minibatch's global statistics); g_mean [n, A] and
  *   g_log_std [A] are d loss / d mean and d loss / d log_std (torch.minimum / clamp conventions for
  *   ties and bounds). mjl_mse: loss = mean (v - r)^2, g_v = 2 (v - r) / n. scratch:
  *   mjl_ppo_loss_scratch(n, A) floats (mjl_mse needs n / 256 + 1). A <= 32.
@@ -383,8 +384,8 @@ int mjl_colsum(const float* x, int n, int d, float* scratch, float* out, void* s
  *   columns (the minibatch gather of train_ppo.py:237-241), idx int64 [n]; one launch. */
 long long mjl_ppo_loss_scratch(int n, int A);
 int mjl_ppo_surrogate(const float* mean, const float* log_std, const float* act, const float* old_logp,
-                      const float* adv, int n, int A, float clip_eps, float ent_coef, float* scratch, float* loss,
-                      float* g_mean, float* g_log_std, void* stream);
+                      const float* adv, const float* adv_stats, int n, int A, float clip_eps, float ent_coef,
+                      float* scratch, float* loss, float* g_mean, float* g_log_std, void* stream);
 int mjl_mse(const float* v, const float* r, int n, float* scratch, float* loss, float* g_v, void* stream);
 int mjl_gather_rows(const long long* idx, int n, int narr, const float* const* src, float* const* dst,
                     const int* cols, void* stream);

@@ -1053,8 +1053,9 @@ extern "C" long long mjl_ppo_loss_scratch(int n, int A) {
 }
 
 extern "C" int mjl_ppo_surrogate(const float* mean, const float* log_std, const float* act, const float* old_logp,
-                                 const float* adv, int n, int A, float clip_eps, float ent_coef, float* scratch,
-                                 float* loss, float* g_mean, float* g_log_std, void* stream) {
+                                 const float* adv, const float* adv_stats, int n, int A, float clip_eps,
+                                 float ent_coef, float* scratch, float* loss, float* g_mean, float* g_log_std,
+                                 void* stream) {
   if (!mean || !log_std || !act || !old_logp || !adv || !scratch || !loss || !g_mean || !g_log_std || n <= 0 || A <= 0)
     return fail(MJL_ERR_ARG, "bad argument");
   if (A > kLossMaxA) return fail(MJL_ERR_UNSUPPORTED, "ppo surrogate: at most %d action columns", kLossMaxA);
@@ -1062,9 +1063,9 @@ extern "C" int mjl_ppo_surrogate(const float* mean, const float* log_std, const 
   const int nb = (n + kLossT - 1) / kLossT;
   float* adv_part = scratch;
   float* part = scratch + 3 * (size_t)nb;
-  hipLaunchKernelGGL(adv_stats_kernel, dim3(nb), dim3(kLossT), 0, s, adv, n, adv_part);
+  if (!adv_stats) hipLaunchKernelGGL(adv_stats_kernel, dim3(nb), dim3(kLossT), 0, s, adv, n, adv_part);
   hipLaunchKernelGGL(ppo_surrogate_kernel, dim3(nb), dim3(kLossT), 0, s, mean, log_std, act, old_logp, adv, n, A,
-                     clip_eps, adv_part, nb, g_mean, part);
+                     clip_eps, adv_part, nb, adv_stats, g_mean, part);
   hipLaunchKernelGGL(ppo_surrogate_final_kernel, dim3(1), dim3(64), 0, s, part, nb, n, A, log_std, ent_coef, loss,
                      g_log_std);
   HIPCHK(hipGetLastError());

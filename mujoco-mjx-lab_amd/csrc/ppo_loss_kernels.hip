@@ -59,7 +59,8 @@ __device__ __forceinline__ void adv_merge(const float* __restrict__ part, int nb
 __global__ __launch_bounds__(kLossT) void ppo_surrogate_kernel(
     const float* __restrict__ mean, const float* __restrict__ log_std, const float* __restrict__ act,
     const float* __restrict__ old_logp, const float* __restrict__ adv, int n, int A, float clip_eps,
-    const float* __restrict__ adv_part, int nb, float* __restrict__ gmean, float* __restrict__ part) {
+    const float* __restrict__ adv_part, int nb, const float* __restrict__ adv_stats, float* __restrict__ gmean,
+    float* __restrict__ part) {
   __shared__ float red[kLossT];
   __shared__ float ivs[kLossMaxA], lss;
   __shared__ float mu_s, sd_s;
@@ -70,7 +71,8 @@ __global__ __launch_bounds__(kLossT) void ppo_surrogate_kernel(
     for (int j = 0; j < A; j++) s += 2.f * log_std[j] + kLog2Pi;
     lss = s;
     float mu, sd;
-    adv_merge(adv_part, nb, mu, sd);
+    if (adv_stats) { mu = adv_stats[0]; sd = adv_stats[1]; }  // global statistics (data-parallel)
+    else adv_merge(adv_part, nb, mu, sd);
     mu_s = mu; sd_s = sd;
   }
   __syncthreads();

@@ -88,7 +88,7 @@ def lib() -> C.CDLL:
     L.mjl_env_fill_reset_pool.argtypes = [vp, vp, u64, u64, vp]
     L.mjl_ppo_loss_scratch.restype = C.c_longlong
     L.mjl_ppo_loss_scratch.argtypes = [i32, i32]
-    L.mjl_ppo_surrogate.argtypes = [vp, vp, vp, vp, vp, i32, i32, C.c_float, C.c_float, vp, vp, vp, vp, vp]
+    L.mjl_ppo_surrogate.argtypes = [vp, vp, vp, vp, vp, vp, i32, i32, C.c_float, C.c_float, vp, vp, vp, vp, vp]
     L.mjl_mse.argtypes = [vp, vp, i32, vp, vp, vp, vp]
     L.mjl_gather_rows.argtypes = [vp, i32, i32, vp, vp, vp, vp]
     L.mjl_adam.argtypes = [i32, vp, vp, vp, vp, vp, C.c_float, C.c_float, C.c_float, C.c_float, i32, vp]

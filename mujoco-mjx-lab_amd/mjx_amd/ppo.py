@@ -337,10 +337,7 @@ def normalize_adv(adv, dist=None):
     std); over the global minibatch when data-parallel."""
     if dist is None:
         return (adv - adv.mean()) / (adv.std(unbiased=False) + 1e-8)
-    buf = torch.stack([adv.sum(), (adv * adv).sum(), torch.tensor(float(adv.numel()), device=adv.device)])
-    dist.all_reduce(buf)
-    mu = buf[0] / buf[2]
-    sd = torch.sqrt(torch.clamp(buf[1] / buf[2] - mu * mu, min=0.0))
+    mu, sd = _global_adv_stats(adv, dist)
     return (adv - mu) / (sd + 1e-8)
 
 
@@ -361,14 +358,14 @@ class _PPOSurrogate(torch.autograd.Function):
     three launches, where the torch ops were ~60 small kernels per minibatch)."""
 
     @staticmethod
-    def forward(ctx, mean, log_std, act, old_logp, adv, clip_eps, ent_coef):
+    def forward(ctx, mean, log_std, act, old_logp, adv, clip_eps, ent_coef, adv_stats=None):
         from ._lib import check, lib
         n, A = mean.shape
         loss = torch.empty((), dtype=torch.float32, device=mean.device)
         gm, gs = torch.empty_like(mean), torch.empty_like(log_std)
         scr = _loss_scratch(mean.device, int(lib().mjl_ppo_loss_scratch(n, A)))
         check(lib().mjl_ppo_surrogate(mean.data_ptr(), log_std.data_ptr(), act.data_ptr(), old_logp.data_ptr(),
-                                      adv.data_ptr(), n, A, float(clip_eps), float(ent_coef), scr.data_ptr(),
+                                      adv.data_ptr(), None if adv_stats is None else adv_stats.data_ptr(), n, A, float(clip_eps), float(ent_coef), scr.data_ptr(),
                                       loss.data_ptr(), gm.data_ptr(), gs.data_ptr(),
                                       torch.cuda.current_stream(mean.device).cuda_stream))
         ctx.save_for_backward(gm, gs)
@@ -377,7 +374,7 @@ class _PPOSurrogate(torch.autograd.Function):
     @staticmethod
     def backward(ctx, g):
         gm, gs = ctx.saved_tensors
-        return gm * g, gs * g, None, None, None, None, None
+        return gm * g, gs * g, None, None, None, None, None, None
 
 
 class _MSE(torch.autograd.Function):
@@ -404,17 +401,26 @@ class _MSE(torch.autograd.Function):
 NATIVE_LOSSES = True  # tests switch the torch restatement back on
 
 
-def _native_loss_ok(x: torch.Tensor, dist) -> bool:
-    return NATIVE_LOSSES and dist is None and x.is_cuda and torch.is_grad_enabled() and x.shape[0] >= 16384
+def _native_loss_ok(x: torch.Tensor) -> bool:
+    return NATIVE_LOSSES and x.is_cuda and torch.is_grad_enabled() and x.shape[0] >= 16384
+
+
+def _global_adv_stats(adv, dist) -> torch.Tensor:
+    """(mean, population std) of the advantages over every rank's share of the minibatch."""
+    buf = torch.stack([adv.sum(), (adv * adv).sum(), torch.tensor(float(adv.numel()), device=adv.device)])
+    dist.all_reduce(buf)
+    mu = buf[0] / buf[2]
+    return torch.stack([mu, torch.sqrt(torch.clamp(buf[1] / buf[2] - mu * mu, min=0.0))]).contiguous()
 
 
 def ppo_policy_loss(policy, obs, acts, old_logp, adv, clip_eps, ent_coef, dist=None):
     """train_ppo.py:204-216."""
     mean, log_std = policy(obs)
-    if _native_loss_ok(mean, dist) and mean.dim() == 2 and log_std.dim() == 1 and mean.shape[1] <= 32:
+    if _native_loss_ok(mean) and mean.dim() == 2 and log_std.dim() == 1 and mean.shape[1] <= 32:
         f = lambda x: x.float().contiguous()  # noqa: E731
+        st = None if dist is None else _global_adv_stats(f(adv), dist)
         return _PPOSurrogate.apply(f(mean), log_std.contiguous(), f(acts), f(old_logp), f(adv), float(clip_eps),
-                                   float(ent_coef))
+                                   float(ent_coef), st)
     ratio = torch.exp(gaussian_logprob(mean, log_std, acts) - old_logp)
     adv_n = normalize_adv(adv, dist)
     surr = torch.minimum(ratio * adv_n, torch.clamp(ratio, 1.0 - clip_eps, 1.0 + clip_eps) * adv_n)
@@ -424,7 +430,7 @@ def ppo_policy_loss(policy, obs, acts, old_logp, adv, clip_eps, ent_coef, dist=N
 def value_loss(value, obs, returns):
     """train_ppo.py:218-220 (vf_coef is unused by the reference)."""
     v = value(obs)
-    if _native_loss_ok(v, None) and v.shape == returns.shape:
+    if _native_loss_ok(v) and v.shape == returns.shape:
         return _MSE.apply(v.contiguous(), returns.float().contiguous())
     return torch.mean((v - returns) ** 2)
 

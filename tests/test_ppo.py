@@ -545,3 +545,37 @@ def test_native_adam_matches_torch_adam():
     oc = ppo.NativeAdam([x.clone() for x in a], lr=1.0)
     oc.load_state_dict(sd)
     assert oc.t == 6 and oc.lr == pytest.approx(3e-4) and all(torch.equal(x, y) for x, y in zip(oc.m, oa.m))
+
+
+@pytest.mark.gpu
+def test_native_surrogate_with_global_advantage_stats():
+    """The data-parallel form of the native surrogate (advantage statistics all-reduced over the
+    ranks, passed in) equals the single-process form on a one-rank group (gloo over 127.0.0.1)."""
+    import os
+    cfg = reference_ppo_config()
+    g = torch.Generator().manual_seed(0)
+    pol = ppo.GaussianPolicy(54, 21, cfg.policy_hidden_layer_specs, cfg.log_std_init, g).cuda()
+    gd = torch.Generator(device="cuda").manual_seed(5)
+    n = 65536
+    o = torch.randn((n, 54), generator=gd, device="cuda")
+    with torch.no_grad():
+        m, s = pol(o)
+        a = (m + torch.exp(s) * torch.randn((n, 21), generator=gd, device="cuda")).contiguous()
+        from mjx_amd.ppo import gaussian_logprob
+        lp = gaussian_logprob(m, s, a) + 0.3 * torch.randn(n, generator=gd, device="cuda")
+    adv = 1.5 * torch.randn(n, generator=gd, device="cuda") - 0.4
+    port = _free_port()
+    tdist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=0, world_size=1)
+    try:
+        out = []
+        for dist in (None, tdist):
+            for p in pol.parameters():
+                p.grad = None
+            loss = ppo.ppo_policy_loss(pol, o, a, lp, adv, cfg.clip_eps, cfg.ent_coef, dist)
+            loss.backward()
+            out.append((float(loss), [p.grad.clone() for p in pol.parameters()]))
+    finally:
+        tdist.destroy_process_group()
+    assert out[0][0] == pytest.approx(out[1][0], rel=1e-5)
+    for x, y in zip(out[0][1], out[1][1]):
+        torch.testing.assert_close(x, y, rtol=1e-4, atol=1e-6)
