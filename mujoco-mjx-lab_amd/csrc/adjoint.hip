@@ -971,8 +971,8 @@ template <class D> INL void adj_collision(MP m, LDSA WS<D>* W, LDSA WSA<D>* A, R
 // geom frames (kinematics): gpos = xpos_b + xmat_b geom_pos, gaxis = xmat_b zaxis; lane = body
 template <class D> INL void adj_geom_frames(MP m, LDSA WSA<D>* A, int lane) {
   if (lane > 0 && lane < m->nbody) {
-    for (int g = 0; g < m->ngeom; g++) {
-      if (m->geom_bodyid[g] != lane) continue;
+    for (uint32_t gm = m->body_geommask[lane]; gm; gm &= gm - 1) {
+      const int g = __ffs(gm) - 1;
       for (int i = 0; i < 3; i++) {
         const float pb = A->gposb[g][i], ab = A->gaxisb[g][i];
         A->xposb[lane][i] += pb;
@@ -1165,8 +1165,8 @@ template <class D> INL void adj_mass(MP m, LDSA WS<D>* W, LDSA WSA<D>* A, int la
     }
     const int j = lane;  // cdof-bar_j += sum over descendants i of vbar_ij f_i
     float cb[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-    for (int ii = j; ii < nv; ii++) {
-      if (!((ldrec(&m->drec[ii]).ancmask >> j) & 1u)) continue;
+    for (uint32_t dm = m->dof_descmask[j]; dm; dm &= dm - 1) {
+      const int ii = __ffs(dm) - 1;
       const float vb = (ii == j) ? A->Mb[j * LD + j] : A->Mb[ii * LD + j] + A->Mb[j * LD + ii];
       for (int k = 0; k < 6; k++) cb[k] += vb * A->ftmp[ii][k];
     }

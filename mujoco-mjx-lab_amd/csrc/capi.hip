@@ -318,6 +318,9 @@ int mjl_model_create(const mjlModelDesc* d, mjlModel** out) {
     r.qpos_spring = r.qadr_spring >= 0 ? f.qpos_spring[r.qadr_spring] : 0.f;
     r.invweight0 = f.dof_invweight0[k];
   }
+  for (int g = 0; g < d->ngeom; g++) f.body_geommask[d->geom_bodyid[g]] |= 1u << g;
+  for (int k = 0; k < d->nv; k++)  // descendants-or-self of each dof
+    for (int a = k; a >= 0; a = d->dof_parentid[a]) f.dof_descmask[a] |= 1u << k;
   for (int p = 0; p < d->npair; p++) {
     PairRec& r = f.prec[p];
     r.g1 = f.pair_geom1[p]; r.g2 = f.pair_geom2[p]; r.kind = f.pair_kind[p]; r.condim = f.pair_condim[p];

@@ -76,6 +76,8 @@ struct ModelF {
   // of root r's subtree in body order
   uint32_t body_ancmask[MJL_MAXBODY], body_childmask[MJL_MAXBODY], body_childmask_nf[MJL_MAXBODY];
   uint32_t body_jgather[MJL_MAXBODY];
+  uint32_t dof_descmask[MJL_MAXV];  // bit i set <=> dof i is this dof or one of its descendants
+  uint32_t body_geommask[MJL_MAXBODY];  // bit g set <=> geom g belongs to body b
   float body_rootmass[MJL_MAXBODY];
   float body_pos[MJL_MAXBODY][3], body_quat[MJL_MAXBODY][4], body_ipos[MJL_MAXBODY][3];
   float body_inertia[MJL_MAXBODY][6], body_mass[MJL_MAXBODY], body_invweight0[MJL_MAXBODY][2];
