@@ -13,20 +13,22 @@ pytestmark = pytest.mark.gpu
 STATE = ("qpos", "qvel", "qacc_warmstart", "ctrl", "time", "aux")
 
 
-def _pair(solver, vjp, B=64):
-    m = mjx_amd.load_model("humanoid_mjx")
+def _pair(solver, vjp, B=64, model="humanoid_mjx"):
+    m = mjx_amd.load_model(model)
     if solver == "cg44":
         m.solver, m.iterations, m.ls_iterations = mjcf.SOLVER_CG, 4, 4
     ecfg = resolve_ids(m, reference_ppo_config().env_config)
     return m, [apg.HumanoidAPGEnv(HumanoidEnv(mjx.put_model(m), ecfg, B, seed=9), vjp) for _ in range(2)]
 
 
-@pytest.mark.parametrize("solver,vjp", [("model", "implicit"), ("cg44", "unrolled")])
-def test_record_and_replay_equal_step_and_recompute(solver, vjp):
-    """Over 12 steps of random actions: the recorded step's outputs and state are the env step's;
+@pytest.mark.parametrize("model,solver,vjp", [("humanoid_mjx", "model", "implicit"), ("humanoid_mjx", "cg44", "unrolled"),
+                                              ("humanoid", "model", "implicit"), ("humanoid", "cg44", "unrolled")])
+def test_record_and_replay_equal_step_and_recompute(model, solver, vjp):
+    """Over 12 steps of random actions (humanoid_mjx: implicitfast; humanoid.xml: Euler with
+    eulerdamp): the recorded step's outputs and state are the env step's;
     the replayed VJP's cotangents (state, warm start, action, aux) are those of the VJP that restores
     the pre-step state and recomputes (same warm start), bit for bit."""
-    m, (plain, taped) = _pair(solver, vjp)
+    m, (plain, taped) = _pair(solver, vjp, model=model)
     B, H = plain.num_envs, 12
     taped.enable_vjp_tape(H)
     for e in (plain, taped):
