@@ -516,23 +516,52 @@ template <class D> INL void adj_solver_unrolled(MP m, LDSA WS<D>* W, LDSA WSA<D>
     const uint32_t w = __float_as_uint(mk[2 * (r >> 6) + ((r >> 5) & 1)]);
     return (w >> (r & 31)) & 1u;
   };
-  // J-bar rows += ca (x) va + cb (x) vb (ca, cb per row in scratch; va, vb in LDS)
+  // J-bar rows += ca (x) va + cb (x) vb (ca, cb per row in scratch; va, vb in LDS); four rows per
+  // step with every load issued before the stores (a loop of single global read-modify-writes
+  // waited for each one)
   auto jbar_add = [&](LDSA const float* va, LDSA const float* vb) {
     SYNC();
     if (isd) {
       const float a = va[lane], b = vb[lane];
-      for (int r = 0; r < nefc; r++) Jbar[r * LD + lane] += ca[r] * a + cb[r] * b;
+      int r = 0;
+      for (; r + 4 <= nefc; r += 4) {
+        float c0[4], c1[4], jb[4];
+#pragma unroll
+        for (int e = 0; e < 4; e++) { c0[e] = ca[r + e]; c1[e] = cb[r + e]; jb[e] = Jbar[(r + e) * LD + lane]; }
+#pragma unroll
+        for (int e = 0; e < 4; e++) Jbar[(r + e) * LD + lane] = jb[e] + (c0[e] * a + c1[e] * b);
+      }
+      for (; r < nefc; r++) Jbar[r * LD + lane] += ca[r] * a + cb[r] * b;
     }
   };
-  auto jt = [&](GLBA const float* c) -> float {  // (J' c)[lane]
+  auto jt = [&](GLBA const float* c) -> float {  // (J' c)[lane], four rows' loads per step
     float x = 0.f;
-    if (isd)
-      for (int r = 0; r < nefc; r++) x += R.J[r * LD + lane] * c[r];
+    if (isd) {
+      int r = 0;
+      for (; r + 4 <= nefc; r += 4) {
+        float jv[4], cv[4];
+#pragma unroll
+        for (int e = 0; e < 4; e++) { jv[e] = R.J[(r + e) * LD + lane]; cv[e] = c[r + e]; }
+#pragma unroll
+        for (int e = 0; e < 4; e++) x += jv[e] * cv[e];
+      }
+      for (; r < nefc; r++) x += R.J[r * LD + lane] * c[r];
+    }
     return x;
   };
-  auto mb_outer = [&](float a, LDSA const float* v) {  // Mb[lane][:] += a v'
-    if (isd)
-      for (int k = 0; k < nv; k++) A->Mb[lane * LD + k] += a * v[k];
+  auto mb_outer = [&](float a, LDSA const float* v) {  // Mb[lane][:] += a v' (v zero beyond nv)
+    if (isd) {
+      LDSA f32x4* row = (LDSA f32x4*)(A->Mb + lane * LD);
+      const LDSA f32x4* vv = (const LDSA f32x4*)v;
+#pragma unroll
+      for (int q = 0; q < LD / 4; q++) {
+        f32x4 x = row[q];
+        const f32x4 y = vv[q];
+#pragma unroll
+        for (int e = 0; e < 4; e++) x[e] += a * y[e];
+        row[q] = x;
+      }
+    }
   };
   for (int r = lane; r < nefc; r += 64) { arefb[r] = 0.f; Dbar[r] = 0.f; }
   if (isd)

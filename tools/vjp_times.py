@@ -19,8 +19,14 @@ names = ["forward recompute", "adj env + integrate", "adj solver rows", "adj con
 L = _lib.lib()
 L.mjl_debug_set_stamps.argtypes = [C.c_void_p]
 m = mjx_amd.load_model("humanoid_mjx")
+if os.environ.get("SOLVER") == "cg44":  # train_apg.py's override
+    from mjx_amd import mjcf
+    m.solver, m.iterations, m.ls_iterations = mjcf.SOLVER_CG, 4, 4
 B = 2048
 env = HumanoidEnv(mjx.put_model(m), resolve_ids(m, EnvConfig()), B, seed=3)
+if os.environ.get("VJP") == "unrolled":
+    from mjx_amd import abi
+    env.data.set_option(abi.OPT_VJP_UNROLLED, 1)
 buf = torch.zeros((B, 16), dtype=torch.int64, device="cuda")
 env.reset()
 g = torch.Generator(device="cuda").manual_seed(0)
