@@ -380,14 +380,15 @@ int mjl_colsum(const float* x, int n, int d, float* scratch, float* out, void* s
  *   g_log_std [A] are d loss / d mean and d loss / d log_std (torch.minimum / clamp conventions for
  *   ties and bounds). mjl_mse: loss = mean (v - r)^2, g_v = 2 (v - r) / n. scratch:
  *   mjl_ppo_loss_scratch(n, A) floats (mjl_mse needs n / 256 + 1). A <= 32.
- * mjl_gather_rows: dst_k[r, :] = src_k[idx[r], :] for narr <= 5 row-major float arrays of cols[k]
- *   columns (the minibatch gather of train_ppo.py:237-241), idx int64 [n]; one launch. */
+ * mjl_gather_rows: dst_k[r, :] = src_k[idx[r], :] for narr <= 5 row-major float arrays of nsrc rows
+ *   and cols[k] columns (the minibatch gather of train_ppo.py:237-241), idx int64 [n]; one launch;
+ *   an index outside [0, nsrc) gives a NaN row. */
 long long mjl_ppo_loss_scratch(int n, int A);
 int mjl_ppo_surrogate(const float* mean, const float* log_std, const float* act, const float* old_logp,
                       const float* adv, const float* adv_stats, int n, int A, float clip_eps, float ent_coef,
                       float* scratch, float* loss, float* g_mean, float* g_log_std, void* stream);
 int mjl_mse(const float* v, const float* r, int n, float* scratch, float* loss, float* g_v, void* stream);
-int mjl_gather_rows(const long long* idx, int n, int narr, const float* const* src, float* const* dst,
+int mjl_gather_rows(const long long* idx, int n, long long nsrc, int narr, const float* const* src, float* const* dst,
                     const int* cols, void* stream);
 /* Adam (optax.adam defaults as train_ppo.py:84-85 build them; torch.optim.Adam's fused update) over
  * nt <= 16 float32 tensors in one launch: m = b1 m + (1 - b1) g, v = b2 v + (1 - b2) g^2,

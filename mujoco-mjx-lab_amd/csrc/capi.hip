@@ -1085,9 +1085,9 @@ extern "C" int mjl_mse(const float* v, const float* r, int n, float* scratch, fl
   return MJL_OK;
 }
 
-extern "C" int mjl_gather_rows(const long long* idx, int n, int narr, const float* const* src, float* const* dst,
-                               const int* cols, void* stream) {
-  if (!idx || n < 0 || narr < 1 || narr > 5 || !src || !dst || !cols) return fail(MJL_ERR_ARG, "bad argument");
+extern "C" int mjl_gather_rows(const long long* idx, int n, long long nsrc, int narr, const float* const* src,
+                               float* const* dst, const int* cols, void* stream) {
+  if (!idx || n < 0 || nsrc < 0 || narr < 1 || narr > 5 || !src || !dst || !cols) return fail(MJL_ERR_ARG, "bad argument");
   GatherArgs g;
   std::memset(&g, 0, sizeof(g));
   g.narr = narr;
@@ -1100,7 +1100,7 @@ extern "C" int mjl_gather_rows(const long long* idx, int n, int narr, const floa
   const long long work = (long long)n * tot;
   if (work == 0) return MJL_OK;
   hipLaunchKernelGGL(gather_rows_kernel, dim3((unsigned)((work + 255) / 256)), dim3(256), 0, (hipStream_t)stream, idx,
-                     n, g);
+                     n, nsrc, g);
   HIPCHK(hipGetLastError());
   return MJL_OK;
 }

@@ -158,7 +158,8 @@ struct GatherArgs {
   int cols[5];
   int narr;
 };
-__global__ __launch_bounds__(256) void gather_rows_kernel(const long long* __restrict__ idx, int n, GatherArgs g) {
+__global__ __launch_bounds__(256) void gather_rows_kernel(const long long* __restrict__ idx, int n, long long nsrc,
+                                                          GatherArgs g) {
   const long long tid = (long long)blockIdx.x * blockDim.x + threadIdx.x;
   int tot = 0;
   for (int k = 0; k < g.narr; k++) tot += g.cols[k];
@@ -166,8 +167,8 @@ __global__ __launch_bounds__(256) void gather_rows_kernel(const long long* __res
   const int r = (int)(tid / tot);
   int c = (int)(tid % tot), k = 0;
   while (c >= g.cols[k]) { c -= g.cols[k]; k++; }
-  const long long s = idx[r];
-  g.dst[k][(size_t)r * g.cols[k] + c] = g.src[k][(size_t)s * g.cols[k] + c];
+  const long long s = idx[r];  // an index outside [0, nsrc) yields NaN rows, not an out-of-bounds read
+  g.dst[k][(size_t)r * g.cols[k] + c] = (s >= 0 && s < nsrc) ? g.src[k][(size_t)s * g.cols[k] + c] : __builtin_nanf("");
 }
 
 // Adam over up to 16 tensors in one launch (torch.optim.Adam's fused update, fp32): m = b1 m +

@@ -90,7 +90,7 @@ def lib() -> C.CDLL:
     L.mjl_ppo_loss_scratch.argtypes = [i32, i32]
     L.mjl_ppo_surrogate.argtypes = [vp, vp, vp, vp, vp, vp, i32, i32, C.c_float, C.c_float, vp, vp, vp, vp, vp]
     L.mjl_mse.argtypes = [vp, vp, i32, vp, vp, vp, vp]
-    L.mjl_gather_rows.argtypes = [vp, i32, i32, vp, vp, vp, vp]
+    L.mjl_gather_rows.argtypes = [vp, i32, C.c_longlong, i32, vp, vp, vp, vp]
     L.mjl_adam.argtypes = [i32, vp, vp, vp, vp, vp, C.c_float, C.c_float, C.c_float, C.c_float, i32, vp]
     L.mjl_env_step_record.argtypes = [vp, i32, vp, vp, vp, vp, vp, vp]
     L.mjl_env_step_vjp_replay.argtypes = [vp, i32] + [vp] * 12 + [vp]

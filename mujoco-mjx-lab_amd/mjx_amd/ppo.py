@@ -449,7 +449,9 @@ def _gather_minibatch(idx, *arrays):
     src = (ctypes.c_void_p * k)(*[a.data_ptr() for a in arrays])
     dst = (ctypes.c_void_p * k)(*[o.data_ptr() for o in outs])
     cols = (ctypes.c_int * k)(*[max(1, a[0].numel()) for a in arrays])
-    check(lib().mjl_gather_rows(idx.data_ptr(), n, k, src, dst, cols, torch.cuda.current_stream(idx.device).cuda_stream))
+    nsrc = min(a.shape[0] for a in arrays)
+    check(lib().mjl_gather_rows(idx.data_ptr(), n, nsrc, k, src, dst, cols,
+                                torch.cuda.current_stream(idx.device).cuda_stream))
     return outs
 
 

@@ -579,3 +579,16 @@ def test_native_surrogate_with_global_advantage_stats():
     assert out[0][0] == pytest.approx(out[1][0], rel=1e-5)
     for x, y in zip(out[0][1], out[1][1]):
         torch.testing.assert_close(x, y, rtol=1e-4, atol=1e-6)
+
+
+@pytest.mark.gpu
+def test_gather_rows_bounds():
+    """mjl_gather_rows: rows gathered exactly; an index outside the source rows gives a NaN row
+    instead of an out-of-bounds read."""
+    g = torch.Generator(device="cuda").manual_seed(0)
+    a, b = torch.randn((100, 7), generator=g, device="cuda"), torch.randn(100, generator=g, device="cuda")
+    idx = torch.tensor([3, 99, 0, 100, -1, 50], dtype=torch.int64, device="cuda")
+    oa, ob = ppo._gather_minibatch(idx, a, b)
+    ok = torch.tensor([True, True, True, False, False, True], device="cuda")
+    assert torch.equal(oa[ok], a[idx[ok]]) and torch.equal(ob[ok], b[idx[ok]])
+    assert bool(torch.isnan(oa[~ok]).all()) and bool(torch.isnan(ob[~ok]).all())
