@@ -99,7 +99,7 @@ __global__ __launch_bounds__(256) void policy_head_kernel(const float* __restric
 constexpr int kPolMaxLayers = 6;
 constexpr int kPolLdx = 260;  // LDS row stride (floats): rows 4 banks apart, conflict-free b128
 #ifndef MJL_POL_WAVES
-#define MJL_POL_WAVES 8
+#define MJL_POL_WAVES 16
 #endif
 constexpr int kPolWaves = MJL_POL_WAVES;        // waves per 16-env workgroup
 constexpr int kPolBpw = 16 / kPolWaves;         // 16-column blocks per wave per pass (256 columns)
@@ -158,13 +158,12 @@ __global__ __launch_bounds__(64 * MJL_POL_WAVES) void policy_rollout_kernel(cons
           b[q] = *(const f4*)&WP[((size_t)((c >> 2) + g) * N + nb * 16 + c16) * 4];
         }
       };
-      auto mac = [&](const f4& a, const f4 (&b)[kPolBpw]) {
+      auto mac = [&](const f4& a, const f4 (&b)[kPolBpw]) {  // the blocks' accumulators alternate
 #pragma unroll
-        for (int q = 0; q < kPolBpw; q++) {
-          if (nbs[q] < nblk) {
+        for (int t = 0; t < 4; t++) {
 #pragma unroll
-            for (int t = 0; t < 4; t++) acc[q] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[t], b[q][t], acc[q], 0, 0, 0);
-          }
+          for (int q = 0; q < kPolBpw; q++)
+            if (nbs[q] < nblk) acc[q] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[t], b[q][t], acc[q], 0, 0, 0);
         }
       };
       f4 a0, a1, b0[kPolBpw], b1[kPolBpw];
@@ -192,21 +191,30 @@ __global__ __launch_bounds__(64 * MJL_POL_WAVES) void policy_rollout_kernel(cons
     __syncthreads();
     cur ^= 1;
   }
-  // head (policy_head_kernel's arithmetic): one thread per env
-  if (tid < 16 && row0 + tid < B) {
-    const int b = row0 + tid, A = pd.act_dim;
+  // head (policy_head_kernel's arithmetic): one thread per (env, action) for the action and its
+  // log-density term, then one thread per env sums its terms in action order
+  {
+    const int A = pd.act_dim;
     const float log2pi = 1.8378770664093453f;
-    float accl = 0.f;
-    for (int j = 0; j < A; j++) {
-      const size_t o = (size_t)b * A + j;
-      const float s = fminf(fmaxf(log_std[j], -20.f), 2.f);
-      const float mu = tanhf(X[cur][tid * kPolLdx + j]);
-      const float a = mu + expf(s) * eps[o];
-      act[o] = a;
-      const float d = a - mu;
-      accl += __fdiv_rn(d * d, expf(2.f * s)) + 2.f * s + log2pi;
+    float* term = &X[cur ^ 1][0];  // the other activation buffer is free now
+    for (int e = tid; e < 16 * A; e += 64 * kPolWaves) {
+      const int r = e / A, j = e - r * A, b = row0 + r;
+      if (b < B) {
+        const size_t o = (size_t)b * A + j;
+        const float s = fminf(fmaxf(log_std[j], -20.f), 2.f);
+        const float mu = tanhf(X[cur][r * kPolLdx + j]);
+        const float a = mu + expf(s) * eps[o];
+        act[o] = a;
+        const float d = a - mu;
+        term[r * kPolLdx + j] = __fdiv_rn(d * d, expf(2.f * s)) + 2.f * s + log2pi;
+      }
     }
-    logp[b] = -0.5f * accl;
+    __syncthreads();
+    if (tid < 16 && row0 + tid < B) {
+      float accl = 0.f;
+      for (int j = 0; j < A; j++) accl += term[tid * kPolLdx + j];
+      logp[row0 + tid] = -0.5f * accl;
+    }
   }
 }
 #pragma clang fp contract(on)
