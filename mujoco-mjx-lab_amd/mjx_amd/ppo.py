@@ -41,7 +41,7 @@ def colsum_native(x: torch.Tensor) -> torch.Tensor:
     ns = int(lib().mjl_colsum_scratch(n, d))
     scratch = None
     if ns:
-        key = (x.device, ns)
+        key = (x.device, ns, torch.cuda.current_stream(x.device).cuda_stream)  # one per stream (two-stream update)
         scratch = _COLSUM_SCRATCH.get(key)
         if scratch is None:
             scratch = _COLSUM_SCRATCH[key] = torch.empty(ns, dtype=torch.float32, device=x.device)
@@ -345,7 +345,7 @@ _LOSS_SCRATCH = {}
 
 
 def _loss_scratch(dev, floats: int) -> torch.Tensor:
-    key = (dev, floats)
+    key = (dev, floats, torch.cuda.current_stream(dev).cuda_stream)  # one per stream (two-stream update)
     t = _LOSS_SCRATCH.get(key)
     if t is None:
         t = _LOSS_SCRATCH[key] = torch.empty(max(floats, 1), dtype=torch.float32, device=dev)
@@ -532,14 +532,43 @@ def _set_grads(params: List[torch.Tensor], flat: torch.Tensor):
         o += n
 
 
+TWO_STREAM_UPDATE = os.environ.get("MJL_TWO_STREAM", "1") != "0"  # value net on a side stream in ppo_update
+_SIDE_STREAMS = {}
+
+
+def _side_stream(dev):
+    s = _SIDE_STREAMS.get(dev)
+    if s is None:
+        s = _SIDE_STREAMS[dev] = torch.cuda.Stream(dev)
+    return s
+
+
 def ppo_update(policy, value, opt_p, opt_v, obs, acts, logp, ret, adv, index_batches, cfg, dist=None, world=1,
                events: Optional[list] = None):
     """train_ppo.py:233-252: per minibatch, a policy Adam step then a value Adam step. Data-parallel:
     each rank takes its share of every minibatch; gradients of both nets travel in one all-reduce.
     `events` (a list) collects a (start, end) CUDA event pair around each all-reduce (bench.py)."""
     pp, vp = list(policy.parameters()), list(value.parameters())
+    # single-process on the GPU: the value net's step runs on a second stream beside the policy's
+    # (the two are independent within a minibatch; one 65,536 x 256 x 256 GEMM leaves each CU one
+    # 256-thread workgroup, so two at once hide each other's latency)
+    side = _side_stream(obs.device) if (dist is None and obs.is_cuda and TWO_STREAM_UPDATE) else None
     for idx in index_batches:
         o, a, ol, r, ad = _gather_minibatch(idx, obs, acts, logp, ret, adv)
+        if side is not None:
+            cur = torch.cuda.current_stream(obs.device)
+            side.wait_stream(cur)
+            # o and r (allocated on cur, read on side) are released at the next gather, after the
+            # cur.wait_stream(side) below, so their blocks are not reused early (no record_stream)
+            with torch.cuda.stream(side):
+                opt_v.zero_grad(set_to_none=True)
+                value_loss(value, o, r).backward()
+                opt_v.step()
+            opt_p.zero_grad(set_to_none=True)
+            ppo_policy_loss(policy, o, a, ol, ad, cfg.clip_eps, cfg.ent_coef, dist).backward()
+            opt_p.step()
+            cur.wait_stream(side)
+            continue
         opt_p.zero_grad(set_to_none=True)
         opt_v.zero_grad(set_to_none=True)
         ppo_policy_loss(policy, o, a, ol, ad, cfg.clip_eps, cfg.ent_coef, dist).backward()

@@ -63,7 +63,42 @@ def enqueue_vs_wall():
         print(f"enqueue {1e3 * (t1 - t0):.1f} ms, wall {1e3 * (t2 - t0):.1f} ms", flush=True)
 
 
+def two_stream(envs: int, reps: int = 8):
+    """Synced wall time of one update with the value net on a side stream vs sequential,
+    interleaved, with the trainer's NativeAdam."""
+    cfg = reference_ppo_config()
+    g = torch.Generator().manual_seed(0)
+    pol = ppo.GaussianPolicy(54, 21, cfg.policy_hidden_layer_specs, cfg.log_std_init, g).cuda()
+    val = ppo.ValueNet(54, cfg.value_hidden_layer_specs, g).cuda()
+    op, ov = ppo._adam(pol.parameters(), 3e-4), ppo._adam(val.parameters(), 3e-4)
+    N = envs * 256
+    gd = torch.Generator(device="cuda").manual_seed(1)
+    obs, act = torch.randn((N, 54), generator=gd, device="cuda"), torch.randn((N, 21), generator=gd, device="cuda").clamp(-1, 1)
+    logp, ret, adv = (torch.randn(N, generator=gd, device="cuda") for _ in range(3))
+    ts = {True: [], False: []}
+    for r in range(reps + 1):
+        for mode in (True, False):
+            ppo.TWO_STREAM_UPDATE = mode
+            idx = ppo.make_index_batches(N, cfg.minibatch_size, cfg.epochs, torch.Generator().manual_seed(r), "cuda")
+            torch.cuda.synchronize()
+            t0 = time.time()
+            ppo.ppo_update(pol, val, op, ov, obs, act, logp, ret, adv, idx, cfg)
+            t1 = time.time()
+            torch.cuda.synchronize()
+            t2 = time.time()
+            if r:
+                ts[mode].append((t1 - t0, t2 - t0))
+    for mode in (True, False):
+        e = sorted(x[0] for x in ts[mode]); w = sorted(x[1] for x in ts[mode])
+        print(f"envs={envs} two_stream={mode}: wall median {1e3 * w[len(w) // 2]:.2f} ms min {1e3 * w[0]:.2f} "
+              f"max {1e3 * w[-1]:.2f}; enqueue median {1e3 * e[len(e) // 2]:.2f} ms", flush=True)
+
+
 if __name__ == "__main__":
+    if len(sys.argv) > 1 and sys.argv[1] == "two":
+        two_stream(2048)
+        two_stream(1024)
+        sys.exit(0)
     if len(sys.argv) > 1 and sys.argv[1] == "enqueue":
         enqueue_vs_wall()
         sys.exit(0)
