@@ -206,6 +206,68 @@ template <int LD, int NV, int P0, int P1, int CV> INL void chol_panel_cv(float (
   }
 }
 
+// ---- candidate: 2x2 block pivots. Columns k and k + 1 from one set of broadcasts of the panel's
+// state before column k: column k + 1's pivot and broadcasts after column k's update are formed
+// from the uniform values (the same fma / mul sequence the column step runs in the lanes, so the
+// result is bit-identical), which takes one readlane off the dependent chain per two columns.
+template <int LD, int NV, int P0, int P1> INL void chol_panel_b2(float (&a)[LD], int kh) {
+#pragma unroll
+  for (int k = P0; k + 1 < P1; k += 2) {
+    const float p = rdlane(a[k], k), b = rdlane(a[k], k + 1), c = rdlane(a[k + 1], k + 1);
+    float s1[P1], s1b[P1], s2[P1];
+#pragma unroll
+    for (int j = k + 2; j < P1; j++) { s1[j] = rdlane(a[k], j); s1b[j] = rdlane(a[k + 1], j); }
+    const float inv1 = __builtin_amdgcn_rsqf(p);
+    const float tb = (b * inv1) * inv1;
+    const float p2 = fmaf(-tb, b, c);
+    const float inv2 = __builtin_amdgcn_rsqf(p2);
+    a[k] *= inv1;
+    const float t1 = a[k] * inv1;
+    a[k + 1] = fmaf(-t1, b, a[k + 1]);
+#pragma unroll
+    for (int j = k + 2; j < P1; j++) {
+      a[j] = fmaf(-t1, s1[j], a[j]);
+      s2[j] = fmaf(-((s1[j] * inv1) * inv1), b, s1b[j]);
+    }
+    a[k + 1] *= inv2;
+    const float t2 = a[k + 1] * inv2;
+#pragma unroll
+    for (int j = k + 2; j < P1; j++) a[j] = fmaf(-t2, s2[j], a[j]);
+  }
+  if constexpr ((P1 - P0) & 1) {
+    constexpr int k = P1 - 1;
+    const float inv = __builtin_amdgcn_rsqf(rdlane(a[k], k));
+    a[k] *= inv;
+  }
+  if constexpr (P1 < NV) {
+    f32x16 acc;
+#pragma unroll
+    for (int v = 0; v < 16; v++) acc[v] = 0.f;
+#pragma unroll
+    for (int t = P0 / 2; t < P1 / 2; t++) {
+      const float op = kh ? a[2 * t + 1] : a[2 * t];
+      acc = __builtin_amdgcn_mfma_f32_32x32x2f32(op, op, acc, 0, 0, 0);
+    }
+    float lo[16], hi[16];
+#pragma unroll
+    for (int v = 0; v < 16; v++) {
+      bool used = false;
+#pragma unroll
+      for (int j = P1; j < NV; j++) used |= ((j & 3) + 4 * (j >> 3)) == v;
+      if (used) {
+        auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(acc[v]), __float_as_uint(acc[v]), false, false);
+        lo[v] = __uint_as_float(r[0]);
+        hi[v] = __uint_as_float(r[1]);
+      }
+    }
+#pragma unroll
+    for (int j = P1; j < NV; j++) {
+      const int v = (j & 3) + 4 * (j >> 3);
+      a[j] -= ((j >> 2) & 1) ? hi[v] : lo[v];
+    }
+  }
+}
+
 // the product's factor + solve with a pluggable panel and optional stop after the factor
 template <int PV, int SOLVE> INL float aug_variant(const LDSA float* src, LDSA float* dst, LDSA float* invd_out,
                                                    const LDSA float* rhs, int lane) {
@@ -261,6 +323,15 @@ template <int PV, int SOLVE> INL float aug_variant(const LDSA float* src, LDSA f
     chol_panel_cv<LD, NV, 0, 10, 2>(a, kh); chol_panel_cv<LD, NV, 10, 16, 2>(a, kh); chol_panel_cv<LD, NV, 16, NV, 2>(a, kh);
   } else if constexpr (PV == 48) {
     chol_panel_cv<LD, NV, 0, 8, 2>(a, kh); chol_panel_cv<LD, NV, 8, 14, 2>(a, kh); chol_panel_cv<LD, NV, 14, 20, 2>(a, kh); chol_panel_cv<LD, NV, 20, NV, 2>(a, kh);
+  } else if constexpr (PV == 50) {
+    chol_panel_b2<LD, NV, 0, 8>(a, kh); chol_panel_b2<LD, NV, 8, 16>(a, kh); chol_panel_b2<LD, NV, 16, NV>(a, kh);
+  } else if constexpr (PV == 51) {
+    chol_panel_b2<LD, NV, 0, 10>(a, kh); chol_panel_b2<LD, NV, 10, 20>(a, kh); chol_panel_b2<LD, NV, 20, NV>(a, kh);
+  } else if constexpr (PV == 52) {
+    chol_panel_b2<LD, NV, 0, 6>(a, kh); chol_panel_b2<LD, NV, 6, 16>(a, kh); chol_panel_b2<LD, NV, 16, NV>(a, kh);
+  } else if constexpr (PV == 53) {
+    chol_panel_b2<LD, NV, 0, 8>(a, kh); chol_panel_b2<LD, NV, 8, 16>(a, kh); chol_panel_b2<LD, NV, 16, 24>(a, kh);
+    chol_panel_b2<LD, NV, 24, NV>(a, kh);
   } else if constexpr (PV == 9) {  // no factor: load + store (+ solve) overhead only
   } else if constexpr (PV == 4) {
     chol_panel<LD, NV, 0, 4>(a, kh); chol_panel<LD, NV, 4, 8>(a, kh); chol_panel<LD, NV, 8, 12>(a, kh);
@@ -347,6 +418,10 @@ template <int V> __global__ __launch_bounds__(64, 2) void kern(unsigned long lon
     else if constexpr (V == 46) x = aug_variant<46, 1>(W.S, W.L, W.invd, W.rhs, lane);
     else if constexpr (V == 47) x = aug_variant<47, 1>(W.S, W.L, W.invd, W.rhs, lane);
     else if constexpr (V == 48) x = aug_variant<48, 1>(W.S, W.L, W.invd, W.rhs, lane);
+    else if constexpr (V == 50) x = aug_variant<50, 1>(W.S, W.L, W.invd, W.rhs, lane);
+    else if constexpr (V == 51) x = aug_variant<51, 1>(W.S, W.L, W.invd, W.rhs, lane);
+    else if constexpr (V == 52) x = aug_variant<52, 1>(W.S, W.L, W.invd, W.rhs, lane);
+    else if constexpr (V == 53) x = aug_variant<53, 1>(W.S, W.L, W.invd, W.rhs, lane);
     else if constexpr (V == 15) x = aug_variant<0, 1>(W.S, W.L, W.invd, W.rhs, lane);
     else if constexpr (V == 16) x = aug_variant<0, 2>(W.S, W.L, W.invd, W.rhs, lane);
     else if constexpr (V == 17) x = aug_variant<9, 0>(W.S, W.L, W.invd, W.rhs, lane);
@@ -419,6 +494,10 @@ int main(int argc, char** argv) {
   run<46>(B, "no clamp, panels 6/14", &ref);
   run<47>(B, "no clamp, panels 10/16", &ref);
   run<48>(B, "no clamp, panels 8/14/20", &ref);
+  run<50>(B, "2x2 block pivots, panels 8/16", &ref);
+  run<51>(B, "2x2 block pivots, panels 10/20", &ref);
+  run<52>(B, "2x2 block pivots, panels 6/16", &ref);
+  run<53>(B, "2x2 block pivots, panels 8/16/24", &ref);
   run<0>(B, "product again", &ref);
   return 0;
 }
