@@ -75,6 +75,12 @@ def dist_setup(args):
                          f"torch.distributed.run --nproc-per-node {args.gpus}, or without WORLD_SIZE")
     if world > 1:
         import torch.distributed as dist
+        if os.environ.get("MJL_BENCH_REHEARSAL") == "1":
+            # rehearsal of the N-rank path on a one-GPU box: every rank on cuda:0 over gloo (RCCL
+            # refuses two ranks on one device); its numbers are not scaling measurements
+            torch.cuda.set_device(0)
+            dist.init_process_group("gloo")
+            return dist, rank, world, 0
         torch.cuda.set_device(local)
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
         return dist, rank, world, local
@@ -234,9 +240,11 @@ def run_ppo(args, dist, rank, world, local):
         "config": {"workload": f"PPO src/config.json: {args.envs} envs per GPU x {cfg.rollout_length} rollout x "
                                f"{cfg.epochs} epochs, global minibatch {cfg.minibatch_size}",
                    "envs_per_gpu": args.envs, "global_envs": args.envs * world,
-                   "parallelism": f"env-sharded x{world}, RCCL all-reduce per minibatch" if world > 1 else "1 GPU"},
+                   "parallelism": (f"env-sharded x{world}, {'RCCL' if dist.get_backend() == 'nccl' else 'gloo'} all-reduce "
+                                   f"per minibatch") if world > 1 else "1 GPU"},
         "step": "one PPO iteration (rollout + GAE + updates), synced",
-        "rccl_ranks": world if dist is not None else 0,
+        "rccl_ranks": world if dist is not None and dist.get_backend() == "nccl" else 0,
+        "rehearsal": os.environ.get("MJL_BENCH_REHEARSAL") == "1",
         "allreduce_ms_per_minibatch": ar_ms if dist is not None else None,
         "minibatches_per_iteration": nmb if dist is not None else cfg.epochs * (args.envs * cfg.rollout_length // cfg.minibatch_size),
         "allreduce_bytes": 4 * grad_numel,
@@ -356,6 +364,8 @@ def main():
             "cpu_baseline": cpu,
         }
         line.update(extras)
+        if os.environ.get("MJL_BENCH_REHEARSAL") == "1":
+            line["rehearsal"] = True
         print(json.dumps(line), flush=True)
     if dist is not None:
         dist.destroy_process_group()
