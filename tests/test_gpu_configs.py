@@ -3,7 +3,9 @@ the reference-shaped env functions, evaluation and the qpos-history dump.
 
 * C3: PPOTrainer iterations at src/config.json values with 1024 envs x 256 steps x 4 epochs x
   minibatch 65,536 (train_ppo.py:320-441): finite metrics, metrics.jsonl keys, and the captured
-  rollout graph replays the eager rollout bit for bit at that size.
+  rollout graph replays the eager rollout bit for bit at that size, and its first 25 steps of six
+  envs that do not finish match the oracle env (rewards, done flags, observations) from the state
+  each env entered the rollout with, under the rollout's sampled actions.
 * C4: one APG update at 2048 envs x 128 steps with train_apg.py's CG 4/4 override and the unrolled
   VJP (jax.grad semantics): finite loss and gradient (diverging envs leave the loss, DESIGN.md
   "Truncated solves"); the batched parameter gradient equals the per-step accumulation.
@@ -102,11 +104,30 @@ def test_ppo_c3_iterations_at_full_size(tmp_path):
     tr2.obs = tr.obs.clone()
     tr2.gen.set_state(tr.gen.get_state())
     tr2._pool_n.copy_(tr._pool_n)  # the reset pool's size adapts per rollout
+    st = env.get_state().cpu().numpy().astype(np.float64)
     a = [x.clone() for x in tr.collect_rollout()]
     b = tr2.collect_rollout()
     assert tr._graph is not None and tr2._graph is None
     for x, y in zip(a, b):
         assert torch.equal(x, y)
+    # the replayed rollout against the oracle env: envs that run 25 steps without finishing, from
+    # the state they entered the rollout with, under the rollout's own (unclipped) actions
+    obs_b, act_b, _, rew_b, te_b, tr_b = (x.cpu().numpy().astype(np.float64) for x in a)
+    cfg_c = abi.env_config_c(ecfg, m, obs_size(m.nq, m.nv))
+    nq, nv, S = m.nq, m.nv, 25
+    alive = np.nonzero((np.maximum(te_b[:S], tr_b[:S]) < 0.5).all(0))[0]
+    assert len(alive) >= 4
+    o = Oracle(m)
+    for i in alive[:: max(1, len(alive) // 6)][:6]:
+        row = st[i]
+        s_ = o.new_state(row[:nq], row[nq:nq + nv], row[nq + nv:nq + 2 * nv], time=row[-1])
+        aux = row[nq + 2 * nv:nq + 2 * nv + abi.AUX_DIM]
+        for t in range(S):
+            s_, aux, oo, ro, te, trn = o.env_step(cfg_c, s_, aux, act_b[t, i])
+            assert rew_b[t, i] == pytest.approx(ro, abs=5e-3 * (1 + abs(ro))), (i, t)
+            assert (te_b[t, i], tr_b[t, i]) == (te, trn)
+            if t + 1 < S:
+                np.testing.assert_allclose(obs_b[t + 1, i], oo[:obs_b.shape[2]], atol=5e-3 * (1 + np.abs(oo).max()))
 
 
 def _apg_trainer(B, H, seed=0):
