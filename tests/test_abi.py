@@ -53,3 +53,18 @@ def test_no_silent_cpu_fallback():
     sys_ = mjx.put_model(mjx_amd.load_model("humanoid_mjx"))
     with pytest.raises(_lib.MjlError):
         mjx.make_data(sys_, 4)
+
+
+def test_batch_create_rejects_empty_and_null_without_gpu():
+    """An empty or negative batch and a null model are argument errors, reported before any device
+    call (so also on a host without a GPU)."""
+    L = _lib.lib()
+    m = mjx_amd.load_model("humanoid_mjx")
+    d = abi.model_desc(m)
+    h, b = C.c_void_p(), C.c_void_p()
+    assert L.mjl_model_create(C.byref(d), C.byref(h)) == 0
+    for n in (0, -1):
+        assert L.mjl_batch_create(h, n, 0, C.byref(b)) == 1  # MJL_ERR_ARG
+        assert b"bad argument" in L.mjl_last_error()
+    assert L.mjl_batch_create(None, 4, 0, C.byref(b)) == 1
+    L.mjl_model_destroy(h)

@@ -429,3 +429,30 @@ def test_crowded_broadphase_parity(spread):
         _close(qacc[i], a["qacc"], 2e-3, f"state {i} qacc")
     if spread < 1:
         assert st[:, 0].max() > 10   # crowded enough to exercise many contacts
+
+
+def test_ragged_and_single_env_batches():
+    """Batch sizes are not tiled: one env, a ragged 37 and 4097 (one past the README's 4096). Each env's
+    speed-test output depends only on its own input, so a 37-env slice of the 4097-env launch equals
+    a 37-env launch bit for bit; one env of the env step matches the oracle env step for 5 steps."""
+    m = mjx_amd.load_model("humanoid_mjx")
+    sys_ = mjx.put_model(m)
+    big = torch.linspace(0.0, 1.0, 4097, device="cuda")
+    ob = mjx.speedtest_step(sys_, mjx.make_data(sys_, 4097), big).clone()
+    sl = big[1000:1037].contiguous()
+    os_ = mjx.speedtest_step(sys_, mjx.make_data(sys_, 37), sl)
+    assert torch.equal(ob[1000:1037], os_) and torch.isfinite(ob).all()
+    m1, env, cfg_c = _env(1)
+    orc = Oracle(m1)
+    env.reset()
+    st = env.get_state().cpu().numpy().astype(np.float64)[0]
+    nq, nv = m1.nq, m1.nv
+    s = orc.new_state(st[:nq], st[nq:nq + nv], st[nq + nv:nq + 2 * nv], time=st[-1])
+    aux = st[nq + 2 * nv:nq + 2 * nv + abi.AUX_DIM]
+    rng = np.random.default_rng(3)
+    for _ in range(5):
+        a = rng.uniform(-1, 1, m1.nu).astype(np.float32)
+        o, r, te, trn = env.step(torch.tensor(a[None], device="cuda"))
+        s, aux, oo, ro, te_o, tr_o = orc.env_step(cfg_c, s, aux, a.astype(np.float64))
+        assert float(r[0]) == pytest.approx(ro, abs=5e-3 * (1 + abs(ro)))
+        np.testing.assert_allclose(o[0].cpu().numpy(), oo[:o.shape[1]], atol=5e-3 * (1 + np.abs(oo).max()))
