@@ -456,3 +456,27 @@ def test_ragged_and_single_env_batches():
         s, aux, oo, ro, te_o, tr_o = orc.env_step(cfg_c, s, aux, a.astype(np.float64))
         assert float(r[0]) == pytest.approx(ro, abs=5e-3 * (1 + abs(ro)))
         np.testing.assert_allclose(o[0].cpu().numpy(), oo[:o.shape[1]], atol=5e-3 * (1 + np.abs(oo).max()))
+
+
+def test_non_finite_env_is_flagged_and_isolated():
+    """no abort on NaN — a non-finite state in one env raises that env's nan_flag
+    (stats[:, 3]) after the fused env step, and every other env's outputs are bit for bit those of
+    the same batch without the bad env (envs share nothing)."""
+    B, bad = 8, 3
+    m, env, _ = _env(B, seed=5)
+    _, env2, _ = _env(B, seed=5)
+    env.reset()
+    env2.set_state(env.get_state())
+    qv = env.data.get("qvel").clone()
+    qv[bad, 0] = float("nan")
+    env.data.set("qvel", qv)
+    act = torch.zeros((B, m.nu), device="cuda")
+    o1, r1, te1, tr1 = (x.clone() for x in env.step(act, auto_reset=False))
+    o2, r2, te2, tr2 = (x.clone() for x in env2.step(act, auto_reset=False))
+    flags = env.data.get("stats")[:, 3].cpu().numpy()
+    assert flags[bad] == 1.0 and (np.delete(flags, bad) == 0.0).all()
+    assert (env2.data.get("stats")[:, 3] == 0).all()
+    keep = [i for i in range(B) if i != bad]
+    for x, y in ((o1, o2), (r1, r2), (te1, te2), (tr1, tr2), (env.data.get("qpos"), env2.data.get("qpos"))):
+        assert torch.equal(x[keep], y[keep])
+    assert not torch.isfinite(env.data.get("qpos")[bad]).all() or not torch.isfinite(env.data.get("qvel")[bad]).all()
