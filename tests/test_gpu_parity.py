@@ -480,3 +480,17 @@ def test_non_finite_env_is_flagged_and_isolated():
     for x, y in ((o1, o2), (r1, r2), (te1, te2), (tr1, tr2), (env.data.get("qpos"), env2.data.get("qpos"))):
         assert torch.equal(x[keep], y[keep])
     assert not torch.isfinite(env.data.get("qpos")[bad]).all() or not torch.isfinite(env.data.get("qvel")[bad]).all()
+
+
+def test_large_batch_speedtest():
+    """65,536 envs in one launch (32 envs per LDS slot; ~2 GB of per-env row scratch): every output
+    finite, and a 64-env slice near the end equals a 64-env launch of the same inputs bit for bit
+    (64-bit offsets into the state and scratch slabs)."""
+    m = mjx_amd.load_model("humanoid_mjx")
+    sys_ = mjx.put_model(m)
+    B = 65536
+    vel = torch.linspace(0.0, 1.0, B, device="cuda")
+    out = mjx.speedtest_step(sys_, mjx.make_data(sys_, B), vel).clone()
+    assert torch.isfinite(out).all()
+    sl = vel[B - 100:B - 36].contiguous()
+    assert torch.equal(out[B - 100:B - 36], mjx.speedtest_step(sys_, mjx.make_data(sys_, 64), sl))
