@@ -139,13 +139,32 @@ def test_cg_solver_parity():
     assert np.median(errs) <= 1e-4, f"median step {np.median(errs):.2e}"
 
 
-def test_speedtest_parity():
-    m = mjx_amd.load_model("humanoid_mjx")
+@pytest.mark.parametrize("name,B", [("humanoid_mjx", 64), ("humanoid_mjx", 2048), ("humanoid", 2048)])
+def test_speedtest_parity(name, B):
+    """The speed-test step (mjx_humanoid_speed_test.py:48-57) against the oracle at the bench's own
+    size (B = 2048, BASELINE configs[1]): every env's qpos[0] to 1e-6."""
+    m = mjx_amd.load_model(name)
     sys_ = mjx.put_model(m)
-    vel = torch.linspace(0, 1, 64, device="cuda")
-    out = mjx.speedtest_step(sys_, mjx.make_data(sys_, 64), vel).cpu().numpy()
+    vel = torch.linspace(0, 1, B, device="cuda")
+    out = mjx.speedtest_step(sys_, mjx.make_data(sys_, B), vel).cpu().numpy()
     ref = Oracle(m).speedtest(vel.cpu().numpy().astype(np.float64))
     np.testing.assert_allclose(out, ref, atol=1e-6)
+    if B < 2048:
+        return
+    # the whole post-step state of the same 2048 states (mjx.step from qpos0, qvel[0] = vel)
+    d = mjx.make_data(sys_, B)
+    qv = torch.zeros((B, m.nv))
+    qv[:, 0] = vel.cpu()
+    d.set("qvel", qv)
+    mjx.step(sys_, d)
+    q1, v1 = (d.get(f).cpu().numpy() for f in ("qpos", "qvel"))
+    o = Oracle(m)
+    for i in range(B):
+        v0 = np.zeros(m.nv)
+        v0[0] = np.float32(vel[i].item())
+        a = state_arrays(m, o.step(o.new_state(m.qpos0.copy(), v0)))
+        np.testing.assert_allclose(q1[i], a["qpos"], atol=2e-5)
+        _close(v1[i], a["qvel"], 2e-3, f"env {i} qvel")
 
 
 def test_global_row_storage_matches_lds(setup):
