@@ -1,11 +1,20 @@
 """Benchmark: humanoid env-steps/s on MI355X (BASELINE.json metric), one process per GPU.
 
-Workload (BASELINE.json configs[1], the reference's speed-test row, mjx_humanoid_speed_test.py:
-48-108): models/humanoid_mjx.xml, 2048 envs per GPU; every step starts from a fresh make_data state
-at qpos0 with qvel[0] = linspace(0, 1, B) and runs one full mjx.step (collision, constraints, Newton
-solve, implicitfast integration), output qpos[0]. One "step" = one launch over the batch. The state
-is re-initialised inside the kernel each launch, so every launch does the full work (nothing is
-hoisted the way XLA may hoist the reference's loop-invariant fori_loop body).
+Headline (`value`, BASELINE.json configs[1], the reference's speed-test row,
+mjx_humanoid_speed_test.py:48-108): models/humanoid_mjx.xml, 2048 envs per GPU; every step starts
+from a fresh make_data state at qpos0 with qvel[0] = linspace(0, 1, B) and runs one full mjx.step
+(collision, constraints, Newton solve, implicitfast integration), output qpos[0]. One "step" = one
+launch over the batch. The state is re-initialised inside the kernel each launch, so every launch does
+the full work (nothing is hoisted the way XLA may hoist the reference's loop-invariant fori_loop body).
+
+The same line carries the metric's other half and the other BASELINE configs, each timed in this run:
+  * N = 1: the fused PPO env step with its roofline; C3 PPO (src/config.json, 1024 envs x 256 x 4
+    epochs x 65,536) throughput and its return@iteration (train_return_avg at iterations 0/25/50/100
+    and eval_return at 100, train_ppo.py:321-424); C4 APG (2048 x 128, CG 4/4, backward through the
+    simulator, train_apg.py:258-315) under both solve derivatives, with the replay VJP kernel's
+    roofline; the CPU legs (C1 humanoid.xml carried steps, and the speed-test states themselves).
+  * N > 1: C5, PPO with 1024 envs per rank and the per-minibatch RCCL all-reduce of both nets'
+    gradients timed (train_ppo.py:233-252), next to the sharded speed test.
 
 Usage:  python bench.py [--gpus N] [--steps K] [--warmup W] [--envs B]
         python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
@@ -14,6 +23,7 @@ Prints ONE JSON line on rank 0.
 from __future__ import annotations
 
 import argparse
+import gc
 import json
 import os
 import sys
@@ -29,19 +39,32 @@ REF_DEVICE_STEPS_PER_S = 72618.0  # HUMANOID_MJX device steps/s (RE
 HBM_PEAK_GBS = 8000.0             # MI355X_MICROARCH.md: HBM3E peak 8.0 TB/s (spec)
 F32_PEAK_TFLOPS = 157.3           # MI355X_MICROARCH.md: peak FP32 matrix (dense) = FP32 vector
 SPEEDTEST_KERNEL = "step_kernel<mjl::Dims<27, 17, 22, 20, 48, 16>, 2>"  # rocprofv3 kernel name
+ENV_STEP_BYTES = 1048             # 113 floats in + 149 out per fused env step
+PPO_CURVE_ITERS = (0, 25, 50, 100)
 
 
 def parse(argv=None):
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
-    p.add_argument("--workload", default="speedtest", choices=["speedtest", "ppo"])
+    p.add_argument("--workload", default="all", choices=["all", "speedtest", "ppo"],
+                   help="all: the headline speed test plus every leg; speedtest: the headline only; "
+                        "ppo: the PPO leg alone as the headline (C3 / C5)")
     p.add_argument("--steps", type=int, default=None, help="timed steps (speedtest launches: 50; ppo iterations: 3)")
     p.add_argument("--warmup", type=int, default=None, help="untimed steps (speedtest: 5; ppo: 2, graph capture)")
     p.add_argument("--envs", type=int, default=None, help="envs per GPU (speedtest: 2048; ppo: 1024)")
     p.add_argument("--model", default="humanoid_mjx")
+    p.add_argument("--ppo-envs", type=int, default=1024, help="PPO leg: envs per GPU (C3 / C5: 1024)")
+    p.add_argument("--ppo-iters", type=int, default=3, help="PPO leg: timed iterations")
+    p.add_argument("--ppo-curve", type=int, default=PPO_CURVE_ITERS[-1],
+                   help="PPO leg (N = 1): train to this iteration for return@iter (0: no curve)")
+    p.add_argument("--apg-envs", type=int, default=2048)
+    p.add_argument("--apg-horizon", type=int, default=128)
+    p.add_argument("--apg-updates", type=int, default=3, help="APG leg: timed updates per solve derivative")
     p.add_argument("--cpu-steps", type=int, default=10000, help="CPU baseline: steps per env (C1: 10,000)")
     p.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline")
-    p.add_argument("--no-extras", action="store_true", help="skip the secondary measurements")
+    p.add_argument("--no-extras", action="store_true", help="skip the secondary speed-test measurements")
+    p.add_argument("--no-ppo", action="store_true", help="skip the PPO leg")
+    p.add_argument("--no-apg", action="store_true", help="skip the APG leg")
     a = p.parse_args(argv)
     ppo = a.workload == "ppo"
     if a.steps is None:
@@ -93,6 +116,11 @@ def barrier(dist):
         dist.barrier()
 
 
+def sync(device):
+    if torch.device(device).type == "cuda":
+        torch.cuda.synchronize(device)
+
+
 def timed_launches(fn, steps, warmup, dist):
     """W untimed + K timed launches. Returns (wall seconds, mean kernel ms from HIP events on the
     launch stream)."""
@@ -116,17 +144,17 @@ def timed_launches(fn, steps, warmup, dist):
     return wall, e0.elapsed_time(e1) / steps
 
 
-def max_over_ranks(x, dist, local):
+def max_over_ranks(x, dist, device="cuda"):
     if dist is None:
         return x
-    t = torch.tensor([x], dtype=torch.float64, device=torch.device("cuda", local))
+    t = torch.tensor([x], dtype=torch.float64, device=torch.device(device))
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     return float(t.item())
 
 
-def pmc_traffic(B: int):
-    """HBM bytes per speed-test launch from the committed rocprofv3 PMC passes (tools/profile_round.sh),
-    used only when they were taken on the current kernel sources and this batch size."""
+def pmc_traffic(B: int, key: str = "bytes_per_launch"):
+    """HBM bytes per launch from the committed rocprofv3 PMC passes (tools/profile_round.sh), used only
+    when they were taken on the current kernel sources and this batch size."""
     from mjx_amd import _lib
     path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     try:
@@ -136,9 +164,17 @@ def pmc_traffic(B: int):
         return None
     if t.get("src_hash") != _lib.source_hash() or int(t.get("envs", -1)) != B:
         return None
-    return t.get("bytes_per_launch")
+    return t.get(key)
 
 
+def free_gpu():
+    gc.collect()
+    if torch.cuda.is_available():
+        torch.cuda.synchronize()
+        torch.cuda.empty_cache()
+
+
+# ------------------------------------------------------------------------------------ CPU legs
 def cpu_model_name() -> str:
     try:
         with open("/proc/cpuinfo") as f:
@@ -151,23 +187,48 @@ def cpu_model_name() -> str:
     return platform.processor() or "unknown"
 
 
-def cpu_baseline(steps: int):
+def physical_cores(cpus=None) -> int:
+    """Distinct (package, core) pairs among `cpus` (default: every online CPU), from sysfs topology;
+    the logical count when the topology is unreadable."""
+    cpus = sorted(cpus) if cpus is not None else list(range(os.cpu_count() or 1))
+    seen = set()
+    for c in cpus:
+        base = f"/sys/devices/system/cpu/cpu{c}/topology/"
+        try:
+            with open(base + "physical_package_id") as f:
+                pkg = f.read().strip()
+            with open(base + "core_id") as f:
+                core = f.read().strip()
+        except OSError:
+            return len(cpus)
+        seen.add((pkg, core))
+    return len(seen)
+
+
+def cpu_threads():
+    """(threads, affinity CPUs): the CPUs in this process's affinity mask, capped by OMP_NUM_THREADS when
+    set (the pool's CPU share per GPU, 16; os.cpu_count() shows the host)."""
+    aff = sorted(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else list(range(os.cpu_count() or 1))
+    share = int(os.environ.get("OMP_NUM_THREADS", "0") or 0)
+    return max(1, min(len(aff), share) if share > 0 else len(aff)), aff
+
+
+def cpu_baseline(steps: int, speedtest_envs: int = 2048):
     """BASELINE config C1 (mjx_humanoid_speed_test.py:140 HUMANOID row): humanoid.xml,
     1 env x `steps` carried steps from qpos0, ctrl = 0 and ctrl ~ U[-1,1] (seed 0); single thread,
-    best of 3, then one env per core on every core this process may use, best of 3; warm-up run
-    excluded. MuJoCo is not importable on the box (plan B), so the timed CPU path is this
-    build's serial C++ restatement (oracle/, kind "port") in its fp32 instantiation, the GPU's
-    arithmetic type. `cores` = the threads used: the CPUs in this process's affinity mask, capped by
-    OMP_NUM_THREADS when set (the pool's CPU share per GPU, 16; os.cpu_count() shows the host)."""
+    best of 3, then one env per thread on the threads this process may use, best of 3; warm-up run
+    excluded. Beside it, the headline's own workload on the CPU (`speedtest`): the humanoid_mjx
+    speed-test step from the same fresh states (qvel[0] = linspace(0, 1, speedtest_envs)), split over
+    the threads, best of 3. MuJoCo is not importable on the box (plan B), so the timed CPU
+    path is this build's serial C++ restatement (oracle/, kind "port") in its fp32 instantiation, the
+    GPU's arithmetic type; ctypes releases the GIL, so the threads run in parallel."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     from concurrent.futures import ThreadPoolExecutor
 
     import mjx_amd
     from oracle import Oracle
     m = mjx_amd.load_model("humanoid")
-    avail = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
-    share = int(os.environ.get("OMP_NUM_THREADS", "0") or 0)
-    threads = max(1, min(avail, share) if share > 0 else avail)
+    threads, aff = cpu_threads()
     rng = np.random.default_rng(0)
     ctrls = {"ctrl0": np.zeros((steps, m.nu)), "ctrlU": rng.uniform(-1.0, 1.0, (steps, m.nu))}
 
@@ -191,101 +252,55 @@ def cpu_baseline(steps: int):
                 dt = time.perf_counter() - t
                 best = dt if best is None else min(best, dt)
         res[name] = (steps / single, threads * steps / best)
-    total_s = time.perf_counter() - t_all
+    c1_s = time.perf_counter() - t_all
+
+    # the headline workload on the CPU: 2048 fresh speed-test states, split over the threads
+    mj = mjx_amd.load_model("humanoid_mjx")
+    vel = np.linspace(0.0, 1.0, speedtest_envs)
+    chunks = np.array_split(vel, threads)
+    orcs = [Oracle(mj, use_float=True) for _ in range(threads)]
+    orcs[0].speedtest(vel[:8])  # warm-up
+    t1 = time.perf_counter()
+    s1 = min((lambda t: (orcs[0].speedtest(vel[:256]), time.perf_counter() - t)[1])(time.perf_counter())
+             for _ in range(3))
+    best = None
+    with ThreadPoolExecutor(threads) as ex:
+        for _ in range(3):
+            t = time.perf_counter()
+            list(ex.map(lambda k: orcs[k].speedtest(chunks[k]), range(threads)))
+            dt = time.perf_counter() - t
+            best = dt if best is None else min(best, dt)
+    st_s = time.perf_counter() - t1
     return {"value": res["ctrlU"][1], "unit": "env-steps/s", "cores": threads, "kind": "port",
-            "cpu_model": cpu_model_name(), "host_cpus": os.cpu_count(), "affinity_cpus": avail,
+            "cpu_model": cpu_model_name(), "host_cpus": os.cpu_count(), "host_physical_cores": physical_cores(),
+            "affinity_cpus": len(aff), "affinity_physical_cores": physical_cores(aff),
             "single_thread": {k: v[0] for k, v in res.items()}, "all_cores": {k: v[1] for k, v in res.items()},
+            "speedtest": {"steps_per_s": speedtest_envs / best, "single_thread_steps_per_s": 256 / s1,
+                          "envs": speedtest_envs, "threads": threads},
             "sample": f"C1: humanoid.xml (Newton 100/50, Euler + eulerdamp), 1 env x {steps} carried steps "
                       f"from qpos0 per thread, ctrl U[-1,1] seed 0 (value) and ctrl 0; oracle/ C++ "
-                      f"restatement, fp32; single thread best of 3, then {threads} threads x 1 env, best of 3; "
-                      f"{total_s:.1f} s in all"}
+                      f"restatement, fp32; single thread best of 3, then {threads} threads x 1 env, best of 3 "
+                      f"({c1_s:.1f} s). speedtest: humanoid_mjx speed-test step from the headline's "
+                      f"{speedtest_envs} fresh states over {threads} threads, best of 3 ({st_s:.1f} s)"}
 
 
-def run_ppo(args, dist, rank, world, local):
-    """BASELINE config C5 (C3 at N = 1): PPO with src/config.json values, args.envs envs per rank,
-    T = 256, 4 epochs, global minibatch 65,536 (each rank takes its share of every minibatch), one
-    RCCL all-reduce of the flattened policy + value gradients per minibatch (train_ppo.py:233-252)."""
-    from mjx_amd import mjx, ppo
-    from mjx_amd.config import reference_ppo_config
-    from mjx_amd.envs import HumanoidEnv, resolve_ids
+# ---------------------------------------------------------------------------------- GPU legs
+def speedtest(args, dist, world, local):
+    """The headline: K speed-test launches over B envs per GPU, with the kernel's roofline."""
     import mjx_amd
-    cfg = reference_ppo_config()
-    cfg.num_envs, cfg.rollout_length = args.envs * world, 256
-    m = mjx_amd.load_model(args.model)
-    env = HumanoidEnv(mjx.put_model(m), resolve_ids(m, cfg.env_config), args.envs, device=local,
-                      seed=cfg.seed * 7919 + rank)
-    tr = ppo.PPOTrainer(cfg, env, None, device=f"cuda:{local}", dist=dist)
-    for it in range(max(2, args.warmup)):  # >= 2: the second rollout captures the rollout graph
-        tr.iteration(it)
-    tr.allreduce_events = []
-    torch.cuda.synchronize()
-    barrier(dist)
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    res = [tr.iteration(it) for it in range(args.steps)]
-    torch.cuda.synchronize()
-    barrier(dist)
-    torch.cuda.synchronize()
-    wall = max_over_ranks(time.perf_counter() - t0, dist, local)
-    ar = [a.elapsed_time(b) for a, b in tr.allreduce_events]
-    ar_ms = max_over_ranks(sum(ar) / len(ar) if ar else 0.0, dist, local)
-    nmb = len(ar) // max(1, args.steps)
-    total = float(args.envs * world * cfg.rollout_length * args.steps)
-    grad_numel = sum(p.numel() for p in list(tr.policy.parameters()) + list(tr.value.parameters()))
-    return {
-        "metric": "humanoid PPO env-steps/sec (whole node)", "value": total / wall, "unit": "env-steps/s",
-        "n_gpus": world, "steps": args.steps, "warmup": max(2, args.warmup), "ms_per_step": wall / args.steps * 1e3,
-        "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f32",
-        "data": "synthetic (env resets drawn on the device; random-init policy / value nets)",
-        "config": {"workload": f"PPO src/config.json: {args.envs} envs per GPU x {cfg.rollout_length} rollout x "
-                               f"{cfg.epochs} epochs, global minibatch {cfg.minibatch_size}",
-                   "envs_per_gpu": args.envs, "global_envs": args.envs * world,
-                   "parallelism": (f"env-sharded x{world}, {'RCCL' if dist.get_backend() == 'nccl' else 'gloo'} all-reduce "
-                                   f"per minibatch") if world > 1 else "1 GPU"},
-        "step": "one PPO iteration (rollout + GAE + updates), synced",
-        "rccl_ranks": world if dist is not None and dist.get_backend() == "nccl" else 0,
-        "rehearsal": os.environ.get("MJL_BENCH_REHEARSAL") == "1",
-        "allreduce_ms_per_minibatch": ar_ms if dist is not None else None,
-        "minibatches_per_iteration": nmb if dist is not None else cfg.epochs * (args.envs * cfg.rollout_length // cfg.minibatch_size),
-        "allreduce_bytes": 4 * grad_numel,
-        "train_return_avg": [r["train_return_avg"] for r in res],
-        "roofline": None, "cpu_baseline": None,
-    }
-
-
-def main():
-    args = parse()
-    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
-        # launch the N ranks as a child process (nothing here has touched the GPU yet) and pass
-        # its status through; rank 0 of the child prints the JSON line
-        import subprocess
-        sys.exit(subprocess.run(launch_cmd(sys.argv[1:], args.gpus, free_port())).returncode)
-    dist, rank, world, local = dist_setup(args)
-    if args.workload == "ppo":
-        line = run_ppo(args, dist, rank, world, local)
-        if rank == 0:
-            print(json.dumps(line), flush=True)
-        if dist is not None:
-            dist.destroy_process_group()
-        return
-    import mjx_amd
+    from mjx_amd import flops as flops_mod
     from mjx_amd import mjx
-
     model = mjx_amd.load_model(args.model)
     sys_ = mjx.put_model(model)
     B = args.envs
     d = mjx.make_data(sys_, B, device=local)
     vel = torch.linspace(0.0, 1.0, B, device=f"cuda:{local}")
     out = torch.empty_like(vel)
-
     wall, kern_ms = timed_launches(lambda: mjx.speedtest_step(sys_, d, vel, out), args.steps, args.warmup, dist)
-    wall = max_over_ranks(wall, dist, local)
+    wall = max_over_ranks(wall, dist)
     value = B * args.steps * world / wall
-    ms_per_step = wall / args.steps * 1e3
-
     # solver statistics of exactly these states (a forward pass from the same fresh state), for the
     # algorithmic FLOP count of one env-step (mjx_amd/flops.py, DESIGN.md "Roofline")
-    from mjx_amd import flops as flops_mod
     ds = mjx.make_data(sys_, B, device=local)
     qv = torch.zeros((B, sys_.nv), device=f"cuda:{local}")
     qv[:, 0] = vel
@@ -296,74 +311,305 @@ def main():
     achieved_tflops = fl["total"] * B / (kern_ms * 1e-3) / 1e12
     bytes_per_env = 8  # speed test: 4 B vel in + 4 B qpos[0] out; the state never leaves LDS
     achieved_gbs = bytes_per_env * B / (kern_ms * 1e-3) / 1e9
-    traffic = pmc_traffic(B)
+    line = {
+        "metric": "humanoid env-steps/sec (whole node)",
+        "value": value,
+        "unit": "env-steps/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": wall / args.steps * 1e3,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": value / REF_DEVICE_STEPS_PER_S,
+        "dtype": "f32",
+        "data": "synthetic (speed-test states: qpos0, qvel[0]=linspace(0,1,B); PPO / APG legs: env resets drawn "
+                "on the device, random-init networks)",
+        "config": {"workload": f"{args.model}.xml speed-test step (fresh state per step), {B} envs per GPU",
+                   "envs_per_gpu": B, "parallelism": f"env-sharded x{world}, no collective in the speed test",
+                   "baseline_note": "vs_baseline divides by the README HUMANOID_MJX row (72,618 steps/s, batch 4096)"},
+        "roofline": {"bound": "mfma", "achieved": achieved_tflops, "peak": F32_PEAK_TFLOPS, "unit": "TFLOP/s",
+                     "frac": achieved_tflops / F32_PEAK_TFLOPS, "traffic": pmc_traffic(B),
+                     "kernel": SPEEDTEST_KERNEL, "kernel_ms": kern_ms,
+                     "flops_per_env_step": fl["total"],
+                     "workload_mean_ncon_nefc_iter": [float(x) for x in wst[:3]],
+                     "workload_mean_active_rows_per_hessian": float(wst[3]),
+                     "hbm_algorithmic_bytes_per_launch": bytes_per_env * B,
+                     "hbm_achieved_gbs": achieved_gbs, "hbm_frac": achieved_gbs / HBM_PEAK_GBS,
+                     "note": "FP32 roof (dense MFMA = vector peak); achieved = algorithmic FP32 FLOPs "
+                             "(mjx_amd/flops.py) / kernel time; traffic = HBM bytes per launch from the "
+                             "committed FETCH_SIZE/WRITE_SIZE passes (profiles/, DESIGN.md)"},
+    }
+    return line, (model, sys_)
 
-    extras = {}
-    if not args.no_extras and rank == 0:
-        # trajectory mode: carried state + random ctrl, full mjx.step with warm start (1048 B/env-step
-        # state traffic for the fused env step; mjl_step reads qpos/qvel/qacc_ws/ctrl/time, writes the same)
-        dd = mjx.make_data(sys_, B, device=local)
-        dd.set_option(0, 0)
-        g = torch.Generator(device=f"cuda:{local}").manual_seed(0)
-        ctrl = torch.rand((B, sys_.nu), generator=g, device=f"cuda:{local}") * 2 - 1
-        tw, tk = timed_launches(lambda: mjx.step(sys_, dd, ctrl), args.steps, args.warmup, None)
-        extras["trajectory_mode_steps_per_s"] = B * args.steps / tw
-        # fused PPO env step (physics + reward + obs + auto-reset) with random actions
-        from mjx_amd.config import reference_ppo_config
-        from mjx_amd.envs import HumanoidEnv, resolve_ids
-        cfg = reference_ppo_config().env_config
-        resolve_ids(model, cfg)
-        env = HumanoidEnv(sys_, cfg, B, device=local, seed=1)
-        env.reset()
-        act = torch.rand((B, sys_.nu), generator=g, device=f"cuda:{local}") * 2 - 1
-        ew, ek = timed_launches(lambda: env.step(act), args.steps, args.warmup, None)
-        extras["env_step_steps_per_s"] = B * args.steps / ew
-        extras["env_step_kernel_ms"] = ek
-        extras["env_step_hbm_gbs"] = 1048 * B / (ek * 1e-3) / 1e9
-        dd.set_option(0, 1)
-        mjx.step(sys_, dd, ctrl)
-        st = dd.get("stats").cpu().numpy()
-        extras["trajectory_mean_ncon_nefc_iter"] = [float(x) for x in st[:, :3].mean(0)]
-        # the reference's own batch size for the README row
-        d4 = mjx.make_data(sys_, 4096, device=local)
-        v4 = torch.linspace(0.0, 1.0, 4096, device=f"cuda:{local}")
-        o4 = torch.empty_like(v4)
-        w4, _ = timed_launches(lambda: mjx.speedtest_step(sys_, d4, v4, o4), args.steps, args.warmup, None)
-        extras["speedtest_b4096_steps_per_s"] = 4096 * args.steps / w4
-        extras["speedtest_b4096_vs_readme"] = extras["speedtest_b4096_steps_per_s"] / REF_DEVICE_STEPS_PER_S
 
+def speedtest_extras(args, model, sys_, local):
+    """Trajectory mode, the fused PPO env step (with its roofline) and the README's batch of 4096."""
+    from mjx_amd import flops as flops_mod
+    from mjx_amd import mjx
+    from mjx_amd.config import reference_ppo_config
+    from mjx_amd.envs import HumanoidEnv, resolve_ids
+    B = args.envs
+    ex = {}
+    dev = f"cuda:{local}"
+    # trajectory mode: carried state + random ctrl, full mjx.step with warm start
+    dd = mjx.make_data(sys_, B, device=local)
+    dd.set_option(0, 0)
+    g = torch.Generator(device=dev).manual_seed(0)
+    ctrl = torch.rand((B, sys_.nu), generator=g, device=dev) * 2 - 1
+    tw, tk = timed_launches(lambda: mjx.step(sys_, dd, ctrl), args.steps, args.warmup, None)
+    ex["trajectory_mode_steps_per_s"] = B * args.steps / tw
+    dd.set_option(0, 1)
+    mjx.step(sys_, dd, ctrl)
+    st = dd.get("stats").cpu().numpy()
+    ex["trajectory_mean_ncon_nefc_iter"] = [float(x) for x in st[:, :3].mean(0)]
+    # fused PPO env step (physics + reward + obs + auto-reset in place) with random actions
+    cfg = reference_ppo_config().env_config
+    resolve_ids(model, cfg)
+    env = HumanoidEnv(sys_, cfg, B, device=local, seed=1)
+    env.reset()
+    act = torch.rand((B, sys_.nu), generator=g, device=dev) * 2 - 1
+    for _ in range(50):  # off the all-standing reset states: a rollout's mix of contacts and resets
+        env.step(act)
+    ew, ek = timed_launches(lambda: env.step(act), args.steps, args.warmup, None)
+    ex["env_step_steps_per_s"] = B * args.steps / ew
+    ex["env_step_kernel_ms"] = ek
+    ex["env_step_hbm_gbs"] = ENV_STEP_BYTES * B / (ek * 1e-3) / 1e9
+    # the env step's solver statistics (a forward pass from the states it steps) and the share of envs
+    # that finish per step (their wave also runs the reset's forward pass)
+    done = 0.0
+    for _ in range(20):
+        _, _, te, tr = env.step(act)
+        done += float(torch.maximum(te, tr).sum())
+    reset_frac = done / (20 * B)
+    env.data.set_option(0, 1)
+    mjx.forward(sys_, env.data)
+    est = env.data.get("stats").double().mean(0).cpu().numpy()
+    fl = flops_mod.env_step_flops(model, float(est[0]), float(est[1]), float(est[2]), nact=float(est[3]),
+                                  reset_frac=reset_frac)
+    tf = fl["total"] * B / (ek * 1e-3) / 1e12
+    ex["env_step_roofline"] = {
+        "bound": "mfma", "achieved": tf, "peak": F32_PEAK_TFLOPS, "unit": "TFLOP/s", "frac": tf / F32_PEAK_TFLOPS,
+        "kernel": "step_kernel<mjl::Dims<27, 17, 22, 20, 48, 16>, 3>", "kernel_ms": ek,
+        "flops_per_env_step": fl["total"], "flops_by_stage": {k: v for k, v in fl.items() if k != "total"},
+        "workload_mean_ncon_nefc_iter": [float(x) for x in est[:3]],
+        "workload_mean_active_rows_per_hessian": float(est[3]), "reset_frac_per_step": reset_frac,
+        "traffic": pmc_traffic(B, "env_step_bytes_per_launch"),
+        "hbm_algorithmic_bytes_per_launch": ENV_STEP_BYTES * B,
+        "hbm_frac": ENV_STEP_BYTES * B / (ek * 1e-3) / 1e9 / HBM_PEAK_GBS}
+    del env, dd
+    # the reference's own batch size for the README row
+    d4 = mjx.make_data(sys_, 4096, device=local)
+    v4 = torch.linspace(0.0, 1.0, 4096, device=dev)
+    o4 = torch.empty_like(v4)
+    w4, _ = timed_launches(lambda: mjx.speedtest_step(sys_, d4, v4, o4), args.steps, args.warmup, None)
+    ex["speedtest_b4096_steps_per_s"] = 4096 * args.steps / w4
+    ex["speedtest_b4096_vs_readme"] = ex["speedtest_b4096_steps_per_s"] / REF_DEVICE_STEPS_PER_S
+    return ex
+
+
+def ppo_leg(tr, iters: int, warmup: int, dist, device, curve=()) -> dict:
+    """`warmup` untimed PPO iterations (>= 2 on the GPU: the second captures the rollout and update
+    hipGraphs), `iters` timed ones (barrier + sync on both sides, max over ranks), then untimed ones up
+    to max(curve) for train_return_avg at the iterations in `curve` (return@iter, train_ppo.py:379-380)."""
+    from mjx_amd.ppo import event_ms
+    returns, it = {}, [0]
+
+    def one():
+        r = tr.iteration(it[0])
+        if it[0] in curve:
+            returns[it[0]] = r["train_return_avg"]
+        it[0] += 1
+        return r
+
+    for _ in range(warmup):
+        one()
+    tr.allreduce_events = []
+    sync(device)
+    barrier(dist)
+    sync(device)
+    t0 = time.perf_counter()
+    res = [one() for _ in range(iters)]
+    sync(device)
+    barrier(dist)
+    sync(device)
+    wall = max_over_ranks(time.perf_counter() - t0, dist, device)
+    ar = [event_ms(e) for e in tr.allreduce_events]
+    tr.allreduce_events = None
+    ar_ms = max_over_ranks(sum(ar) / len(ar) if ar else 0.0, dist, device)
+    while curve and it[0] <= max(curve):
+        one()
+    world = 1 if dist is None else dist.get_world_size()
+    env_steps = float(tr.env.num_envs * world * tr.cfg.rollout_length * iters)
+    return {"env_steps_per_s": env_steps / wall, "ms_per_iter": wall / iters * 1e3, "iters": iters,
+            "warmup": warmup, "envs_per_rank": tr.env.num_envs, "ranks": world,
+            "allreduce_ms": ar_ms, "allreduces_per_iter": len(ar) // max(1, iters),
+            "train_return_avg": [r["train_return_avg"] for r in res], "return_at_iter": returns,
+            "next_iteration": it[0]}
+
+
+def c5_fields(res: dict, world: int, backend: str, grad_numel: int) -> dict:
+    """The C5 keys of the bench line (data-parallel PPO, BASELINE configs[4])."""
+    return {"ppo_c5_env_steps_per_s": res["env_steps_per_s"], "ppo_c5_ms_per_iter": res["ms_per_iter"],
+            "ppo_c5_envs_per_rank": res["envs_per_rank"], "ppo_c5_global_envs": res["envs_per_rank"] * world,
+            "allreduce_ms_per_minibatch": res["allreduce_ms"], "allreduces_per_iteration": res["allreduces_per_iter"],
+            "allreduce_bytes": 4 * grad_numel, "collective_backend": backend, "collective_ranks": world,
+            "rccl_ranks": world if backend == "nccl" else 0,
+            "ppo_c5_train_return_avg": res["train_return_avg"]}
+
+
+def ppo_trainer(args, envs, dist, rank, local, eval_envs=0):
+    import mjx_amd
+    from mjx_amd import mjx, ppo
+    from mjx_amd.config import reference_ppo_config
+    from mjx_amd.envs import HumanoidEnv, resolve_ids
+    world = 1 if dist is None else dist.get_world_size()
+    cfg = reference_ppo_config()
+    cfg.num_envs, cfg.rollout_length = envs * world, 256
+    m = mjx_amd.load_model(args.model)
+    sys_ = mjx.put_model(m)
+    ecfg = resolve_ids(m, cfg.env_config)
+    env = HumanoidEnv(sys_, ecfg, envs, device=local, seed=cfg.seed * 7919 + rank)
+    ev = HumanoidEnv(sys_, ecfg, eval_envs, device=local, seed=cfg.seed + 10000) if eval_envs else None
+    return ppo.PPOTrainer(cfg, env, ev, device=f"cuda:{local}", dist=dist)
+
+
+def grad_numel(tr) -> int:
+    return sum(p.numel() for p in list(tr.policy.parameters()) + list(tr.value.parameters()))
+
+
+def ppo_c3(args, local) -> dict:
+    """C3: src/config.json PPO at 1024 envs on one GPU, throughput and return@iter (seed 42)."""
+    tr = ppo_trainer(args, args.ppo_envs, None, 0, local, eval_envs=32)
+    curve = tuple(i for i in PPO_CURVE_ITERS if i <= args.ppo_curve) if args.ppo_curve > 0 else ()
+    t0 = time.perf_counter()
+    res = ppo_leg(tr, args.ppo_iters, 2, None, f"cuda:{local}", curve)
+    ev_it = res["next_iteration"] - 1
+    eval_ret = tr.evaluate(ev_it) if curve else None
+    out = {"ppo_c3_env_steps_per_s": res["env_steps_per_s"], "ppo_c3_ms_per_iter": res["ms_per_iter"],
+           "ppo_c3_config": f"src/config.json: {args.ppo_envs} envs x 256 rollout x 4 epochs, minibatch 65536, "
+                            f"seed 42; {res['iters']} timed iterations after 2 (graph capture)",
+           "ppo_return_at_iter": {str(k): v for k, v in sorted(res["return_at_iter"].items())},
+           "ppo_eval_return_at_iter": {str(ev_it): eval_ret} if eval_ret is not None else {},
+           "ppo_curve_wall_s": time.perf_counter() - t0}
+    del tr
+    free_gpu()
+    return out
+
+
+def apg_c4(args, local) -> dict:
+    """C4: train_apg.py at 2048 envs x 128 horizon, CG 4/4, under the reference's solve derivative
+    (unrolled: jax.grad through the iterations) and the implicit one; plus the replay VJP kernel's
+    roofline from standalone launches of the last update's first tape slot."""
+    from mjx_amd import flops as flops_mod
+    from mjx_amd import mjx
+    from mjx_amd.apg import APGTrainer, HumanoidAPGEnv
+    from mjx_amd.config import APGConfig, EnvConfig
+    from mjx_amd.envs import HumanoidEnv, resolve_ids
+    from train_apg import apg_model
+    out = {}
+    dev = f"cuda:{local}"
+    for vjp in ("unrolled", "implicit"):
+        cfg = APGConfig()
+        cfg.batch_size, cfg.horizon = args.apg_envs, args.apg_horizon
+        m = apg_model(cfg, solver="cg")
+        env = HumanoidEnv(mjx.put_model(m), resolve_ids(m, EnvConfig()), cfg.batch_size, device=local, seed=cfg.seed)
+        aenv = HumanoidAPGEnv(env, vjp)
+        tr = APGTrainer(cfg, aenv, device=dev)
+        tr.update(0)  # eager warm-up
+        tr.update(1)  # captures the rollout + reverse sweep hipGraph
+        sync(dev)
+        t0 = time.perf_counter()
+        res = [tr.update(i) for i in range(2, 2 + args.apg_updates)]
+        sync(dev)
+        wall = time.perf_counter() - t0
+        key = "apg_c4" if vjp == "unrolled" else "apg_c4_implicit"
+        out[f"{key}_env_steps_per_s"] = cfg.batch_size * cfg.horizon * len(res) / wall
+        out[f"{key}_ms_per_update"] = wall / len(res) * 1e3
+        out[f"{key}_returns"] = [r["return"] for r in res]
+        out[f"{key}_nonfinite_envs"] = [r["nonfinite_envs"] for r in res]
+        if vjp == "implicit":  # the replay VJP kernel alone: slot 0 of the last update's tape
+            B = cfg.batch_size
+            env.data.set_option(0, 1)
+            env.reset()  # slot 0 holds step 0 of the last rollout, which starts from resets:
+            mjx.forward(env.sys, env.data)  # solver statistics of (other) reset states
+            s = env.data.get("stats").double().mean(0).cpu().numpy()
+            act = torch.zeros((B, m.nu), device=dev)
+            gq, gv = torch.zeros((B, m.nq), device=dev), torch.zeros((B, m.nv), device=dev)
+            grew = torch.full((B,), -1.0 / B, device=dev)
+            nonf = torch.zeros(1, device=dev)
+            fn = lambda: aenv.step_vjp_replay(0, act, gq, gv, None, grew, None, nonf)  # noqa: E731
+            _, kms = timed_launches(fn, 20, 3, None)
+            fl = flops_mod.vjp_replay_flops(m, float(s[0]), float(s[1]), float(s[2]), nact=float(s[3]))
+            tf = fl["total"] * B / (kms * 1e-3) / 1e12
+            out["apg_vjp_roofline"] = {
+                "bound": "mfma", "achieved": tf, "peak": F32_PEAK_TFLOPS, "unit": "TFLOP/s",
+                "frac": tf / F32_PEAK_TFLOPS, "kernel": "vjp_kernel<..., true, 2> (mjl_env_step_vjp_replay, implicit)",
+                "kernel_ms": kms, "flops_per_env_step": fl["total"],
+                "flops_by_stage": {k: v for k, v in fl.items() if k != "total"},
+                "workload_mean_ncon_nefc_iter": [float(x) for x in s[:3]],
+                "workload_mean_active_rows_per_hessian": float(s[3])}
+        del tr, aenv, env
+        free_gpu()
+    out["apg_c4_config"] = (f"train_apg.py: {args.apg_envs} envs x {args.apg_horizon} horizon, CG 4/4, hidden 32x2, "
+                            f"lr 5e-5, clip 0.3; {args.apg_updates} timed updates after 2 (graph capture); "
+                            f"apg_c4 = unrolled VJP (jax.grad semantics), apg_c4_implicit = implicit VJP")
+    return out
+
+
+def main():
+    args = parse()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        # launch the N ranks as a child process (nothing here has touched the GPU yet) and pass
+        # its status through; rank 0 of the child prints the JSON line
+        import subprocess
+        sys.exit(subprocess.run(launch_cmd(sys.argv[1:], args.gpus, free_port())).returncode)
+    dist, rank, world, local = dist_setup(args)
+    backend = dist.get_backend() if dist is not None else None
+
+    if args.workload == "ppo":  # the PPO leg alone as the headline (C3 at N = 1, C5 at N > 1)
+        tr = ppo_trainer(args, args.envs, dist, rank, local)
+        res = ppo_leg(tr, args.steps, max(2, args.warmup), dist, f"cuda:{local}")
+        line = {"metric": "humanoid PPO env-steps/sec (whole node)", "value": res["env_steps_per_s"],
+                "unit": "env-steps/s", "n_gpus": world, "steps": args.steps, "warmup": max(2, args.warmup),
+                "ms_per_step": res["ms_per_iter"], "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+                "dtype": "f32", "data": "synthetic (env resets drawn on the device; random-init policy / value nets)",
+                "config": {"workload": f"PPO src/config.json: {args.envs} envs per GPU x 256 rollout x 4 epochs, "
+                                       f"global minibatch 65536", "envs_per_gpu": args.envs},
+                "step": "one PPO iteration (rollout + GAE + updates), synced", "roofline": None, "cpu_baseline": None,
+                "rehearsal": os.environ.get("MJL_BENCH_REHEARSAL") == "1"}
+        if dist is not None:
+            line.update(c5_fields(res, world, backend, grad_numel(tr)))
+        if rank == 0:
+            print(json.dumps(line), flush=True)
+        if dist is not None:
+            dist.destroy_process_group()
+        return
+
+    line, (model, sys_) = speedtest(args, dist, world, local)
+    legs = {}
+    full = args.workload == "all"
+    if world == 1:
+        if full and not args.no_extras:
+            legs.update(speedtest_extras(args, model, sys_, local))
+        if full and not args.no_ppo:
+            legs.update(ppo_c3(args, local))
+        if full and not args.no_apg:
+            legs.update(apg_c4(args, local))
+    elif full and not args.no_ppo:  # C5 on every rank: the one collective of the path, timed
+        tr = ppo_trainer(args, args.ppo_envs, dist, rank, local)
+        res = ppo_leg(tr, args.ppo_iters, 2, dist, f"cuda:{local}")
+        legs.update(c5_fields(res, world, backend, grad_numel(tr)))
+        legs["ppo_c5_config"] = (f"src/config.json PPO: {args.ppo_envs} envs per rank x 256 rollout x 4 epochs, "
+                                 f"global minibatch 65536 ({65536 // world} rows per rank); {res['iters']} timed "
+                                 f"iterations after 2 (graph capture)")
+        del tr
+        free_gpu()
     if rank == 0:
-        cpu = cpu_baseline(args.cpu_steps) if world == 1 and not args.no_cpu else None
-        line = {
-            "metric": "humanoid env-steps/sec (whole node)",
-            "value": value,
-            "unit": "env-steps/s",
-            "n_gpus": world,
-            "steps": args.steps,
-            "warmup": args.warmup,
-            "ms_per_step": ms_per_step,
-            "higher_is_better": True,
-            "scaling": "weak",
-            "vs_baseline": value / REF_DEVICE_STEPS_PER_S,
-            "dtype": "f32",
-            "data": "synthetic (speed-test states: qpos0, qvel[0]=linspace(0,1,B))",
-            "config": {"workload": f"{args.model}.xml speed-test step (fresh state per step), {B} envs per GPU",
-                       "envs_per_gpu": B, "parallelism": f"env-sharded x{world}, no collective",
-                       "baseline_note": "vs_baseline divides by the README HUMANOID_MJX row (72,618 steps/s, batch 4096)"},
-            "roofline": {"bound": "mfma", "achieved": achieved_tflops, "peak": F32_PEAK_TFLOPS, "unit": "TFLOP/s",
-                         "frac": achieved_tflops / F32_PEAK_TFLOPS, "traffic": traffic,
-                         "kernel": SPEEDTEST_KERNEL, "kernel_ms": kern_ms,
-                         "flops_per_env_step": fl["total"],
-                         "workload_mean_ncon_nefc_iter": [float(x) for x in wst[:3]],
-                         "workload_mean_active_rows_per_hessian": float(wst[3]),
-                         "hbm_algorithmic_bytes_per_launch": bytes_per_env * B,
-                         "hbm_achieved_gbs": achieved_gbs, "hbm_frac": achieved_gbs / HBM_PEAK_GBS,
-                         "note": "FP32 roof (dense MFMA = vector peak); achieved = algorithmic FP32 FLOPs "
-                                 "(mjx_amd/flops.py) / kernel time; traffic = HBM bytes per launch from the "
-                                 "committed FETCH_SIZE/WRITE_SIZE passes (profiles/, DESIGN.md)"},
-            "cpu_baseline": cpu,
-        }
-        line.update(extras)
+        line["cpu_baseline"] = cpu_baseline(args.cpu_steps, args.envs) if world == 1 and not args.no_cpu else None
+        if line["cpu_baseline"] is not None:
+            line["cpu_speedtest_steps_per_s"] = line["cpu_baseline"]["speedtest"]["steps_per_s"]
+        line.update(legs)
         if os.environ.get("MJL_BENCH_REHEARSAL") == "1":
             line["rehearsal"] = True
         print(json.dumps(line), flush=True)

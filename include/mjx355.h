@@ -173,7 +173,9 @@ int mjl_batch_nenv(const mjlBatch* batch);
  * as executed (what jax.grad through MJX's fixed-count solver computes; reference train_apg.py:
  * 101-105,187-189 runs CG 4/4) instead of the implicit derivative at the converged active set; the
  * integrator's input is then qfrc_smooth + qfrc_constraint of the stopped solve. The VJP must see
- * the pre-step qacc_warmstart the forward step saw (the recompute replays that solve).
+ * the pre-step qacc_warmstart the forward step saw (the recompute replays that solve). Rejected for
+ * models with iterations > 256 or ls_iterations > 31 (the tape's capacity); an env whose tape still
+ * overflows gets NaN cotangents, or is cut and counted by the guarded VJPs.
  * MJL_OPT_VJP_TAPE (default 0): value = slots of the VJP tape (mjl_env_step_record /
  * mjl_env_step_vjp_replay), each holding one env step's forward workspace for every env
  * (~50 KB per env and slot for the humanoid; call outside stream capture; 0 frees it).
@@ -216,7 +218,7 @@ int mjl_env_step(mjlBatch* batch, const float* act, float* obs, float* rew, floa
  * critical path. A reset does not depend on the state it replaces, so resets can be computed in bulk
  * (full-occupancy launches) instead of one wave at a time at the end of a finishing env's step:
  * this fills slots 0..n-1 of every env (n = min(*dev_n, slots), device int read at execution
- * time), slot j drawn from (seed, (counter + j) ^ 2^63, env) with the same single_reset semantics
+ * time), slot j drawn from (seed, (counter + j * 2^48) ^ 2^63, env) with the same single_reset semantics
  * (src/envs.py:115-202). Each later mjl_env_step(auto_reset=1) merges a finished env's next unused
  * slot; an env whose slots are used up resets in place from (seed, step counter, env) as before.
  * Requires MJL_OPT_RESET_POOL; not for key-drawn resets (mjl_env_set_reset_keys). */
@@ -395,6 +397,13 @@ int mjl_gather_rows(const long long* idx, int n, long long nsrc, int narr, const
  * p -= lr / (1 - b1^step) m / (sqrt(v) / sqrt(1 - b2^step) + eps); g[k] NULL skips tensor k. */
 int mjl_adam(int nt, float* const* p, const float* const* g, float* const* m, float* const* v,
              const long long* numel, float lr, float beta1, float beta2, float eps, int step, void* stream);
+/* mjl_adam with the step count read from device memory at execution time (step: device float, the
+ * step being taken, >= 1), so a hipGraph that captured the call takes the bias corrections of each
+ * replay's own step (the caller's captured increment advances it; train_ppo.py:233-252 runs the whole
+ * update as one compiled scan, optax keeping the count as device state). */
+int mjl_adam_dev(int nt, float* const* p, const float* const* g, float* const* m, float* const* v,
+                 const long long* numel, float lr, float beta1, float beta2, float eps, const float* step,
+                 void* stream);
 
 #ifdef __cplusplus
 }

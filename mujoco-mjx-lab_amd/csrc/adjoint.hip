@@ -1716,10 +1716,21 @@ template <class D, bool ENV, int TM> __global__ __launch_bounds__(64, 1) void vj
   adj_kinematics<D>(m, W, A, lane);
   STAMP(13, lane);
   // ---- outputs
+  // an unrolled solve whose tape overflowed (more line-search points or iterations than it holds;
+  // mjl_batch_set_option rejects the models that can) has no valid derivative: NaN, or cut by the guard
+  const bool tape_over = unr && tp.t[3] != 0.f;
+  if (tape_over && !V.nonfinite) {
+    const float nan = __builtin_nanf("");
+    if (lane < nq) A->qposb[lane] = nan;
+    if (lane < nv) { A->qvelb[lane] = nan; A->wsb[lane] = nan; }
+    if (lane < nu) A->ctrlb[lane] = nan;
+    if (ENV && lane < MJL_AUX_DIM) A->auxb[lane] = nan;
+    SYNC();
+  }
   if (V.nonfinite) {  // cut an env whose cotangents overflowed from the gradient (APG guard)
     bool bad = (lane < nq && !isfinite(A->qposb[lane])) || (lane < nv && !isfinite(A->qvelb[lane])) ||
                (lane < nu && !isfinite(A->ctrlb[lane])) || (ENV && lane < MJL_AUX_DIM && !isfinite(A->auxb[lane])) ||
-               (lane < nv && !isfinite(A->wsb[lane]));
+               (lane < nv && !isfinite(A->wsb[lane])) || tape_over;
     if (__ballot(bad) != 0ull) {
       if (lane < nq) V.o_qpos[(size_t)env * nq + lane] = 0.f;
       if (lane < nv) V.o_qvel[(size_t)env * nv + lane] = 0.f;

@@ -439,6 +439,10 @@ int mjl_batch_set_option(mjlBatch* B, int option, int value) {
   if (option == MJL_OPT_VJP_UNROLLED) {
     if (value && B->model->desc.iterations > 256)
       return fail(MJL_ERR_ARG, "unrolled VJP: %d solver iterations (at most 256 are taped)", B->model->desc.iterations);
+    // a zoom line search creates up to 1 + 2 ls_iterations Newton points; the tape holds 64 per search
+    if (value && 1 + 2 * B->model->desc.ls_iterations > 64)
+      return fail(MJL_ERR_ARG, "unrolled VJP: ls_iterations %d (at most 31: the tape holds 64 line-search points)",
+                  B->model->desc.ls_iterations);
     B->vjp_unrolled = value != 0;
     return MJL_OK;
   }
@@ -715,7 +719,9 @@ int mjl_env_fill_reset_pool(mjlBatch* B, const int* dev_n, uint64_t seed, uint64
     P.obs = B->rs_obs + rows * B->obs_dim;
     P.pool_ctl = B->d_pool_ctl; P.pool_n = dev_n; P.pool_slot = j; P.pool_slots = B->pool_slots;
     P.store_derived = 1;  // the consuming step may store derived fields
-    const uint64_t c = (counter + (uint64_t)j) ^ (1ull << 63);  // a counter domain of its own
+    // a counter domain of its own, the slot in bits 48..55: slot j + T of one rollout and slot j of the
+    // next (counter + T) stay distinct for any rollout length T
+    const uint64_t c = (counter + ((uint64_t)j << 48)) ^ (1ull << 63);
     P.seed_lo = (uint32_t)seed; P.seed_hi = (uint32_t)(seed >> 32);
     P.ctr_lo = (uint32_t)c; P.ctr_hi = (uint32_t)(c >> 32);
     int rc = launch<MODE_ENV_RESET>(B, P, stream);
@@ -1105,9 +1111,11 @@ extern "C" int mjl_gather_rows(const long long* idx, int n, long long nsrc, int 
   return MJL_OK;
 }
 
-extern "C" int mjl_adam(int nt, float* const* p, const float* const* g, float* const* m, float* const* v,
-                        const long long* numel, float lr, float beta1, float beta2, float eps, int step, void* stream) {
-  if (nt < 1 || nt > kAdamMaxT || !p || !g || !m || !v || !numel || step < 1) return fail(MJL_ERR_ARG, "bad argument");
+static int adam_launch(int nt, float* const* p, const float* const* g, float* const* m, float* const* v,
+                       const long long* numel, float lr, float beta1, float beta2, float eps, int step,
+                       const float* step_dev, void* stream) {
+  if (nt < 1 || nt > kAdamMaxT || !p || !g || !m || !v || !numel || (!step_dev && step < 1))
+    return fail(MJL_ERR_ARG, "bad argument");
   AdamArgs a;
   std::memset(&a, 0, sizeof(a));
   a.nt = nt;
@@ -1116,13 +1124,28 @@ extern "C" int mjl_adam(int nt, float* const* p, const float* const* g, float* c
     a.p[k] = p[k]; a.g[k] = g[k]; a.m[k] = m[k]; a.v[k] = v[k];
     a.off[k + 1] = a.off[k] + numel[k];
   }
-  const float bc1 = 1.f - powf(beta1, (float)step), bc2 = 1.f - powf(beta2, (float)step);
-  a.step_size = lr / bc1;
-  a.bc2_sqrt = sqrtf(bc2);
-  a.b1 = beta1; a.b2 = beta2; a.eps = eps;
+  if (!step_dev) {
+    const float bc1 = 1.f - powf(beta1, (float)step), bc2 = 1.f - powf(beta2, (float)step);
+    a.step_size = lr / bc1;
+    a.bc2_sqrt = sqrtf(bc2);
+  }
+  a.step_dev = step_dev;
+  a.lr = lr; a.b1 = beta1; a.b2 = beta2; a.eps = eps;
   const long long n = a.off[nt];
   if (n == 0) return MJL_OK;
   hipLaunchKernelGGL(adam_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, (hipStream_t)stream, a);
   HIPCHK(hipGetLastError());
   return MJL_OK;
+}
+
+extern "C" int mjl_adam(int nt, float* const* p, const float* const* g, float* const* m, float* const* v,
+                        const long long* numel, float lr, float beta1, float beta2, float eps, int step, void* stream) {
+  return adam_launch(nt, p, g, m, v, numel, lr, beta1, beta2, eps, step, nullptr, stream);
+}
+
+extern "C" int mjl_adam_dev(int nt, float* const* p, const float* const* g, float* const* m, float* const* v,
+                            const long long* numel, float lr, float beta1, float beta2, float eps, const float* step,
+                            void* stream) {
+  if (!step) return fail(MJL_ERR_ARG, "bad argument");
+  return adam_launch(nt, p, g, m, v, numel, lr, beta1, beta2, eps, 0, step, stream);
 }

@@ -182,7 +182,8 @@ struct AdamArgs {
   float* v[kAdamMaxT];
   long long off[kAdamMaxT + 1];
   int nt;
-  float step_size, bc2_sqrt, b1, b2, eps;
+  float step_size, bc2_sqrt, b1, b2, eps, lr;
+  const float* step_dev;  // device step count (hipGraph replays): the bias corrections from it at run time
 };
 __global__ __launch_bounds__(256) void adam_kernel(AdamArgs a) {
   const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
@@ -191,13 +192,19 @@ __global__ __launch_bounds__(256) void adam_kernel(AdamArgs a) {
   while (i >= a.off[k + 1]) k++;
   if (!a.g[k]) return;
   const long long j = i - a.off[k];
+  float step_size = a.step_size, bc2_sqrt = a.bc2_sqrt;
+  if (a.step_dev) {
+    const float t = *a.step_dev;
+    step_size = a.lr / (1.f - powf(a.b1, t));
+    bc2_sqrt = sqrtf(1.f - powf(a.b2, t));
+  }
   const float g = a.g[k][j];
   const float m = a.b1 * a.m[k][j] + (1.f - a.b1) * g;
   const float v = a.b2 * a.v[k][j] + (1.f - a.b2) * g * g;
   a.m[k][j] = m;
   a.v[k][j] = v;
-  const float denom = sqrtf(v) / a.bc2_sqrt + a.eps;
-  a.p[k][j] = a.p[k][j] - a.step_size * m / denom;
+  const float denom = sqrtf(v) / bc2_sqrt + a.eps;
+  a.p[k][j] = a.p[k][j] - step_size * m / denom;
 }
 
 }  // namespace mjl

@@ -45,3 +45,48 @@ def step_flops(m, ncon: float, nefc: float, iters: float, ls_evals: float = 3.0,
     f["solver"] = 2.0 * 2 * (nv * nv + nv * nefc) + iters * per_it
     f["total"] = sum(f.values())
     return f
+
+
+def env_post_flops(m) -> float:
+    """single_step's reward / termination / observation (src/envs.py:347-492): rpy from the pelvis
+    quaternion, the torso velocity rotated into the pelvis frame, distances, energy over the nu
+    actuated dofs, the target features; ~500 FMAs."""
+    return 2.0 * (60 + 2 * 9 + 30 + 4 * m.nu + 40 + 10 * 4 + m.nq + m.nv)
+
+
+def env_step_flops(m, ncon: float, nefc: float, iters: float, nact=None, reset_frac: float = 0.0) -> dict:
+    """FP32 FLOPs of one fused PPO env step (mjl_env_step, auto_reset = 1): the physics step at the
+    rollout's own solver statistics, the env's reward / obs, and for the fraction `reset_frac` of envs
+    that finish in a step, single_reset's forward pass (envs.py:108-113: a full forward without
+    integration, from a standing pose; counted with the same statistics)."""
+    f = dict(step_flops(m, ncon, nefc, iters, nact=nact))
+    phys = f.pop("total")
+    f["env_post"] = env_post_flops(m)
+    fwd = phys - f["integrate"]
+    f["auto_reset"] = reset_frac * (fwd + env_post_flops(m))
+    f["total"] = phys + f["env_post"] + f["auto_reset"]
+    return f
+
+
+def vjp_replay_flops(m, ncon: float, nefc: float, iters: float, nact=None, unrolled: bool = False) -> dict:
+    """FP32 FLOPs of one env-step VJP replayed from the tape (mjl_env_step_vjp_replay: reverse passes
+    only, the forward's workspace and factors read back). Reverse mode of a bilinear operation costs
+    two FMAs per forward FMA (a' += c' b, b' += c' a), so each smooth stage, the collision of the
+    active contacts, the row construction and the integrator's solve count twice their forward
+    (step_flops). The constraint solve: implicit, one solve with the taped factor of the converged
+    Hessian (2 substitutions) plus the cotangents of M (an nv x nv outer product), J (nact x nv), D and
+    aref, and the J^T products; unrolled (jax.grad through the iterations), twice each taped
+    iteration's forward arithmetic."""
+    nv = m.nv
+    fw = step_flops(m, ncon, nefc, iters, nact=nact)
+    nh = nefc if nact is None else nact
+    f = {k: 2.0 * fw[k] for k in ("kinematics", "crb_M", "rne", "rows", "integrate")}
+    f["collision"] = 2.0 * 2.0 * max(ncon, 1.0) * 120  # only active contacts carry cotangents
+    f["factor_M"] = 2.0 * (2.0 * nv * nv) + 2.0 * nv * nv  # M^-1 solve reverse + M' outer product
+    if unrolled:
+        f["solver"] = 2.0 * fw["solver"]
+    else:
+        f["solver"] = 2.0 * (2.0 * nv * nv) + 2.0 * (nv * nv + 3 * nh * nv + 4 * nefc)
+    f["env_post"] = 2.0 * env_post_flops(m)
+    f["total"] = sum(f.values())
+    return f

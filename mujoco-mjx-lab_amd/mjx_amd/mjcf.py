@@ -248,6 +248,62 @@ def _geom_inertia(gtype: int, size, density: float):
     raise MJCFError(f"inertia for geom type {gtype} not supported")
 
 
+def candidate_pairs(geoms, body_parentid, body_weldid, excludes, filterparent: bool = True) -> list:
+    """Candidate collision pairs by MuJoCo's filter (mj_collision's broadphase rules, as MJX's
+    collision_driver takes them from the model): geoms on one weld body never collide; a body's geoms
+    skip its weld parent's (filterparent, unless either is the world); `<exclude>` body pairs and
+    incompatible contype / conaffinity bits drop out; plane-plane is skipped. Contact parameters mix
+    as mj_contactParam does at equal priority: condim and friction by max, solref / solimp by the
+    solmix-weighted mean (solref by min when either is direct), margin and gap by max. `geoms`: dicts
+    with type, body, contype, conaffinity, condim, friction[3], solref[2], solimp[5], solmix, margin,
+    gap, priority (the MJCF compiler's, or mjmodel.py's from an MjModel)."""
+    ngeom = len(geoms)
+    pairs = []
+    for g1 in range(ngeom):
+        for g2 in range(g1 + 1, ngeom):
+            G1, G2 = geoms[g1], geoms[g2]
+            b1, b2 = G1["body"], G2["body"]
+            w1, w2 = body_weldid[b1], body_weldid[b2]
+            if w1 == w2:
+                continue
+            p1 = body_weldid[body_parentid[w1]] if w1 > 0 else 0
+            p2 = body_weldid[body_parentid[w2]] if w2 > 0 else 0
+            if filterparent and w1 != 0 and w2 != 0 and (w1 == p2 or w2 == p1):
+                continue  # filterparent
+            if (min(b1, b2), max(b1, b2)) in excludes:
+                continue
+            if not ((G1["contype"] & G2["conaffinity"]) or (G2["contype"] & G1["conaffinity"])):
+                continue
+            if G1["type"] == GEOM_PLANE and G2["type"] == GEOM_PLANE:
+                continue
+            ga, gb = (g1, g2) if G1["type"] <= G2["type"] else (g2, g1)
+            ta, tb = geoms[ga]["type"], geoms[gb]["type"]
+            kind = {(GEOM_PLANE, GEOM_SPHERE): COL_PLANE_SPHERE, (GEOM_PLANE, GEOM_CAPSULE): COL_PLANE_CAPSULE,
+                    (GEOM_SPHERE, GEOM_SPHERE): COL_SPHERE_SPHERE, (GEOM_SPHERE, GEOM_CAPSULE): COL_SPHERE_CAPSULE,
+                    (GEOM_CAPSULE, GEOM_CAPSULE): COL_CAPSULE_CAPSULE}.get((ta, tb))
+            if kind is None:
+                raise MJCFError(f"collision pair types {ta},{tb} not supported")
+            A, B = geoms[ga], geoms[gb]
+            # contact parameter mixing (MuJoCo mj_contactParam, equal priority)
+            if A["priority"] != B["priority"]:
+                raise MJCFError("geom priority not supported")
+            condim = max(A["condim"], B["condim"])
+            if condim not in (1, 3):
+                raise MJCFError(f"condim {condim} not supported")
+            fr = np.maximum(A["friction"], B["friction"])
+            mix = A["solmix"] / (A["solmix"] + B["solmix"]) if (A["solmix"] + B["solmix"]) > mjMINVAL else 0.5
+            if A["solref"][0] > 0 and B["solref"][0] > 0:
+                solref = [mix * A["solref"][i] + (1 - mix) * B["solref"][i] for i in range(2)]
+            else:
+                solref = [min(A["solref"][i], B["solref"][i]) for i in range(2)]
+            solimp = [mix * A["solimp"][i] + (1 - mix) * B["solimp"][i] for i in range(5)]
+            pairs.append({"g1": ga, "g2": gb, "kind": kind, "condim": condim,
+                          "friction": np.array([fr[0], fr[0], fr[1], fr[2], fr[2]]),
+                          "solref": solref, "solimp": solimp,
+                          "margin": max(A["margin"], B["margin"]), "gap": max(A["gap"], B["gap"])})
+    return pairs
+
+
 def compile_xml(path: str) -> CompiledModel:
     with open(path, "rb") as f:
         raw = f.read()
@@ -530,49 +586,7 @@ def compile_xml_string(text: str, name_hint: str = "", sha: str = "") -> Compile
                 excludes.add((min(b1, b2), max(b1, b2)))
             else:
                 raise MJCFError(f"<contact><{ex.tag}> not supported")
-    pairs = []
-    for g1 in range(ngeom):
-        for g2 in range(g1 + 1, ngeom):
-            G1, G2 = geoms[g1], geoms[g2]
-            b1, b2 = G1["body"], G2["body"]
-            w1, w2 = body_weldid[b1], body_weldid[b2]
-            if w1 == w2:
-                continue
-            p1 = body_weldid[bodies[w1]["parent"]] if w1 > 0 else 0
-            p2 = body_weldid[bodies[w2]["parent"]] if w2 > 0 else 0
-            if w1 != 0 and w2 != 0 and (w1 == p2 or w2 == p1):
-                continue  # filterparent
-            if (min(b1, b2), max(b1, b2)) in excludes:
-                continue
-            if not ((G1["contype"] & G2["conaffinity"]) or (G2["contype"] & G1["conaffinity"])):
-                continue
-            if G1["type"] == GEOM_PLANE and G2["type"] == GEOM_PLANE:
-                continue
-            ga, gb = (g1, g2) if G1["type"] <= G2["type"] else (g2, g1)
-            ta, tb = geoms[ga]["type"], geoms[gb]["type"]
-            kind = {(GEOM_PLANE, GEOM_SPHERE): COL_PLANE_SPHERE, (GEOM_PLANE, GEOM_CAPSULE): COL_PLANE_CAPSULE,
-                    (GEOM_SPHERE, GEOM_SPHERE): COL_SPHERE_SPHERE, (GEOM_SPHERE, GEOM_CAPSULE): COL_SPHERE_CAPSULE,
-                    (GEOM_CAPSULE, GEOM_CAPSULE): COL_CAPSULE_CAPSULE}.get((ta, tb))
-            if kind is None:
-                raise MJCFError(f"collision pair types {ta},{tb} not supported")
-            A, B = geoms[ga], geoms[gb]
-            # contact parameter mixing (MuJoCo mj_contactParam, equal priority)
-            if A["priority"] != B["priority"]:
-                raise MJCFError("geom priority not supported")
-            condim = max(A["condim"], B["condim"])
-            if condim not in (1, 3):
-                raise MJCFError(f"condim {condim} not supported")
-            fr = np.maximum(A["friction"], B["friction"])
-            mix = A["solmix"] / (A["solmix"] + B["solmix"]) if (A["solmix"] + B["solmix"]) > mjMINVAL else 0.5
-            if A["solref"][0] > 0 and B["solref"][0] > 0:
-                solref = [mix * A["solref"][i] + (1 - mix) * B["solref"][i] for i in range(2)]
-            else:
-                solref = [min(A["solref"][i], B["solref"][i]) for i in range(2)]
-            solimp = [mix * A["solimp"][i] + (1 - mix) * B["solimp"][i] for i in range(5)]
-            pairs.append({"g1": ga, "g2": gb, "kind": kind, "condim": condim,
-                          "friction": np.array([fr[0], fr[0], fr[1], fr[2], fr[2]]),
-                          "solref": solref, "solimp": solimp,
-                          "margin": max(A["margin"], B["margin"]), "gap": max(A["gap"], B["gap"])})
+    pairs = candidate_pairs(geoms, [b["parent"] for b in bodies], body_weldid, excludes)
 
     # ---- actuators ---------------------------------------------------------------------------
     act = root.find("actuator")
@@ -696,6 +710,13 @@ def compile_xml_string(text: str, name_hint: str = "", sha: str = "") -> Compile
     A["geom_quat"] = np.array([g["quat"] for g in geoms])
     A["geom_size"] = np.array([g["size"] for g in geoms])
     A["geom_friction"] = np.array([g["friction"] for g in geoms])
+    # per-geom contact parameters (MjModel's geom_solref ...; the pairs above hold their mixes)
+    A["geom_solref"] = np.array([g["solref"] for g in geoms]).reshape(-1, 2)
+    A["geom_solimp"] = np.array([g["solimp"] for g in geoms]).reshape(-1, 5)
+    A["geom_solmix"] = np.array([g["solmix"] for g in geoms])
+    A["geom_margin"] = np.array([g["margin"] for g in geoms])
+    A["geom_gap"] = np.array([g["gap"] for g in geoms])
+    A["geom_priority"] = np.array([g["priority"] for g in geoms], np.int32)
     A["pair_geom1"] = np.array([p["g1"] for p in pairs], np.int32)
     A["pair_geom2"] = np.array([p["g2"] for p in pairs], np.int32)
     A["pair_kind"] = np.array([p["kind"] for p in pairs], np.int32)
@@ -732,6 +753,7 @@ def compile_xml_string(text: str, name_hint: str = "", sha: str = "") -> Compile
     A["sensor_objid"] = np.array([s["objid"] for s in sensors], np.int32)
     A["sensor_adr"] = np.array([s["adr"] for s in sensors], np.int32)
     A["key_qpos"] = np.array(keys).reshape(-1, nq)
+    A["exclude_signature"] = np.array(sorted((b1 << 16) + b2 for b1, b2 in excludes), np.int64)  # MjModel's
 
     m.arrays = A
     m.names = {"body": body_names, "joint": jnt_names, "geom": geom_names, "site": site_names,

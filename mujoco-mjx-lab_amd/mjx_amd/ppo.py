@@ -413,16 +413,20 @@ def _global_adv_stats(adv, dist) -> torch.Tensor:
     return torch.stack([mu, torch.sqrt(torch.clamp(buf[1] / buf[2] - mu * mu, min=0.0))]).contiguous()
 
 
-def ppo_policy_loss(policy, obs, acts, old_logp, adv, clip_eps, ent_coef, dist=None):
-    """train_ppo.py:204-216."""
+def ppo_policy_loss(policy, obs, acts, old_logp, adv, clip_eps, ent_coef, dist=None, adv_stats=None):
+    """train_ppo.py:204-216. Data-parallel, the advantages are normalised by the global minibatch's
+    (mean, population std): `adv_stats` when given (a device [2]), else all-reduced here."""
     mean, log_std = policy(obs)
     if _native_loss_ok(mean) and mean.dim() == 2 and log_std.dim() == 1 and mean.shape[1] <= 32:
         f = lambda x: x.float().contiguous()  # noqa: E731
-        st = None if dist is None else _global_adv_stats(f(adv), dist)
+        st = adv_stats if adv_stats is not None else (None if dist is None else _global_adv_stats(f(adv), dist))
         return _PPOSurrogate.apply(f(mean), log_std.contiguous(), f(acts), f(old_logp), f(adv), float(clip_eps),
                                    float(ent_coef), st)
     ratio = torch.exp(gaussian_logprob(mean, log_std, acts) - old_logp)
-    adv_n = normalize_adv(adv, dist)
+    if adv_stats is not None:
+        adv_n = (adv - adv_stats[0]) / (adv_stats[1] + 1e-8)
+    else:
+        adv_n = normalize_adv(adv, dist)
     surr = torch.minimum(ratio * adv_n, torch.clamp(ratio, 1.0 - clip_eps, 1.0 + clip_eps) * adv_n)
     return -surr.mean() - ent_coef * gaussian_entropy(log_std, acts.shape[-1])
 
@@ -463,10 +467,57 @@ def make_index_batches(total: int, minibatch: int, epochs: int, generator: torch
     return torch.cat(out, 0).to(device)
 
 
+def _torch_adam_groups(n: int, lr: float, betas, eps: float) -> list:
+    """torch.optim.Adam's param_groups entry for n parameters with these hyper-parameters (taken from
+    a throwaway torch Adam, so the keys are exactly this torch version's)."""
+    dummy = torch.optim.Adam([torch.zeros(1, requires_grad=True) for _ in range(n)], lr=lr, betas=tuple(betas), eps=eps)
+    return dummy.state_dict()["param_groups"]
+
+
+def adam_state_to_torch(step: float, m: list, v: list, lr: float, betas, eps: float) -> dict:
+    """torch.optim.Adam.state_dict() layout: state[i] = {step, exp_avg, exp_avg_sq}, param_groups."""
+    state = {} if step <= 0 else {
+        i: {"step": torch.tensor(float(step)), "exp_avg": a.detach().clone(), "exp_avg_sq": b.detach().clone()}
+        for i, (a, b) in enumerate(zip(m, v))}
+    return {"state": state, "param_groups": _torch_adam_groups(len(m), lr, betas, eps)}
+
+
+def adam_state_from_torch(d: dict, shapes: list):
+    """(step, m list or None, v list or None, lr, betas, eps) from a torch.optim.Adam state dict (or a
+    round-2 NativeAdam one: t / m / v); raises ValueError when it does not fit `shapes`."""
+    if "t" in d:  # round-2 NativeAdam layout
+        m, v, step, lr, betas, eps = list(d["m"]), list(d["v"]), float(d["t"]), d["lr"], d["betas"], d["eps"]
+    else:
+        if "state" not in d or "param_groups" not in d or len(d["param_groups"]) != 1:
+            raise ValueError("Adam state dict: expected torch.optim.Adam's layout with one parameter group")
+        g = d["param_groups"][0]
+        if len(g["params"]) != len(shapes):
+            raise ValueError(f"Adam state dict: {len(g['params'])} parameters, optimiser has {len(shapes)}")
+        lr, betas, eps = g["lr"], g["betas"], g["eps"]
+        st = d["state"]
+        if not st:
+            return 0.0, None, None, float(lr), (float(betas[0]), float(betas[1])), float(eps)
+        ids = list(g["params"])
+        if any(i not in st for i in ids):
+            raise ValueError("Adam state dict: state missing for some parameters")
+        m = [st[i]["exp_avg"] for i in ids]
+        v = [st[i]["exp_avg_sq"] for i in ids]
+        step = float(st[ids[0]]["step"])
+    if len(m) != len(shapes) or len(v) != len(shapes):
+        raise ValueError(f"Adam state dict: {len(m)} moment tensors, optimiser has {len(shapes)} parameters")
+    for a, b, sh in zip(m, v, shapes):
+        if tuple(a.shape) != tuple(sh) or tuple(b.shape) != tuple(sh):
+            raise ValueError(f"Adam state dict: moment shape {tuple(a.shape)} does not match parameter {tuple(sh)}")
+    return step, m, v, float(lr), (float(betas[0]), float(betas[1])), float(eps)
+
+
 class NativeAdam:
     """torch.optim.Adam (betas, eps; no weight decay) for CUDA float32 parameters as one native
-    launch per step (mjl_adam: the fused update of every tensor), where torch's fused Adam took
-    ≈42 µs for the 151K-parameter policy. zero_grad / step / state_dict / load_state_dict as torch's."""
+    launch per step (mjl_adam_dev: the fused update of every tensor), where torch's fused Adam took
+    ≈42 µs for the 151K-parameter policy. The step count lives on the device and is advanced by a
+    launch inside step(), so a hipGraph that captured step() takes each replay's own bias
+    corrections (a host int baked into the capture made replays drift from eager).
+    state_dict / load_state_dict use torch.optim.Adam's layout (checkpoints interchange)."""
 
     def __init__(self, params, lr: float, betas=(0.9, 0.999), eps: float = 1e-8):
         self.params = [p for p in params]
@@ -476,7 +527,11 @@ class NativeAdam:
         self.lr, self.betas, self.eps = float(lr), (float(betas[0]), float(betas[1])), float(eps)
         self.m = [torch.zeros_like(p) for p in self.params]
         self.v = [torch.zeros_like(p) for p in self.params]
-        self.t = 0
+        self.step_t = torch.zeros(1, dtype=torch.float32, device=self.params[0].device)
+
+    @property
+    def t(self) -> int:
+        return int(self.step_t.item())
 
     def zero_grad(self, set_to_none: bool = True):
         for p in self.params:
@@ -486,28 +541,30 @@ class NativeAdam:
                 p.grad.zero_()
 
     @torch.no_grad()
-    def step(self):
+    def step(self, grads: Optional[List[torch.Tensor]] = None):
+        """One Adam step with `grads` (default: the parameters' .grad)."""
         import ctypes
         from ._lib import check, lib
-        self.t += 1
         k = len(self.params)
-        grads = [p.grad if p.grad is None else p.grad.contiguous() for p in self.params]
+        src = [p.grad for p in self.params] if grads is None else list(grads)
+        grads = [g if g is None else g.contiguous() for g in src]
+        self.step_t.add_(1.0)
         vp = ctypes.c_void_p * k
-        check(lib().mjl_adam(k, vp(*[p.data_ptr() for p in self.params]),
-                             vp(*[None if g is None else g.data_ptr() for g in grads]),
-                             vp(*[x.data_ptr() for x in self.m]), vp(*[x.data_ptr() for x in self.v]),
-                             (ctypes.c_longlong * k)(*[p.numel() for p in self.params]), self.lr, self.betas[0],
-                             self.betas[1], self.eps, self.t, torch.cuda.current_stream(self.params[0].device).cuda_stream))
+        check(lib().mjl_adam_dev(k, vp(*[p.data_ptr() for p in self.params]),
+                                 vp(*[None if g is None else g.data_ptr() for g in grads]),
+                                 vp(*[x.data_ptr() for x in self.m]), vp(*[x.data_ptr() for x in self.v]),
+                                 (ctypes.c_longlong * k)(*[p.numel() for p in self.params]), self.lr, self.betas[0],
+                                 self.betas[1], self.eps, ctypes.c_void_p(self.step_t.data_ptr()),
+                                 torch.cuda.current_stream(self.params[0].device).cuda_stream))
         self._keep = grads  # the launch reads them asynchronously
 
     def state_dict(self):
-        return {"t": self.t, "lr": self.lr, "betas": list(self.betas), "eps": self.eps,
-                "m": [x.detach().clone() for x in self.m], "v": [x.detach().clone() for x in self.v]}
+        return adam_state_to_torch(float(self.step_t.item()), self.m, self.v, self.lr, self.betas, self.eps)
 
     def load_state_dict(self, d):
-        self.t, self.lr, self.eps = int(d["t"]), float(d["lr"]), float(d["eps"])
-        self.betas = (float(d["betas"][0]), float(d["betas"][1]))
-        for dst, src in zip(self.m + self.v, list(d["m"]) + list(d["v"])):
+        step, m, v, self.lr, self.betas, self.eps = adam_state_from_torch(d, [p.shape for p in self.params])
+        self.step_t.fill_(step)
+        for dst, src in zip(self.m + self.v, (m + v) if m is not None else [torch.zeros_like(x) for x in self.m + self.v]):
             dst.copy_(src)
 
 
@@ -543,49 +600,186 @@ def _side_stream(dev):
     return s
 
 
-def ppo_update(policy, value, opt_p, opt_v, obs, acts, logp, ret, adv, index_batches, cfg, dist=None, world=1,
-               events: Optional[list] = None):
-    """train_ppo.py:233-252: per minibatch, a policy Adam step then a value Adam step. Data-parallel:
-    each rank takes its share of every minibatch; gradients of both nets travel in one all-reduce.
-    `events` (a list) collects a (start, end) CUDA event pair around each all-reduce (bench.py)."""
-    pp, vp = list(policy.parameters()), list(value.parameters())
-    # single-process on the GPU: the value net's step runs on a second stream beside the policy's
-    # (the two are independent within a minibatch; one 65,536 x 256 x 256 GEMM leaves each CU one
-    # 256-thread workgroup, so two at once hide each other's latency)
-    side = _side_stream(obs.device) if (dist is None and obs.is_cuda and TWO_STREAM_UPDATE) else None
-    for idx in index_batches:
-        o, a, ol, r, ad = _gather_minibatch(idx, obs, acts, logp, ret, adv)
-        if side is not None:
-            cur = torch.cuda.current_stream(obs.device)
-            side.wait_stream(cur)
+def minibatch_adv_stats(adv, index_batches, dist) -> torch.Tensor:
+    """(mean, population std) of the advantages of every minibatch over all ranks' shares, as
+    [n_minibatches, 2], with ONE all-reduce per update instead of one per minibatch (the reference
+    normalises per minibatch, train_ppo.py:209; data-parallel, the minibatch is the union of the
+    ranks' shares)."""
+    a = adv.reshape(-1)[index_batches]  # [nmb, mb]
+    loc = torch.stack([a.sum(1), (a * a).sum(1), torch.full((a.shape[0],), float(a.shape[1]), device=a.device,
+                                                              dtype=a.dtype)], 1)
+    dist.all_reduce(loc)
+    mu = loc[:, 0] / loc[:, 2]
+    return torch.stack([mu, torch.sqrt(torch.clamp(loc[:, 1] / loc[:, 2] - mu * mu, min=0.0))], 1).contiguous()
+
+
+class _HostTimer:
+    """A (start, end) pair like two CUDA events, for the all-reduce timing on CPU (gloo)."""
+
+    def __init__(self):
+        self.t = [0.0, 0.0]
+
+    def record(self, i):
+        self.t[i] = time.perf_counter()
+
+    def ms(self) -> float:
+        return (self.t[1] - self.t[0]) * 1e3
+
+
+def event_ms(ev) -> float:
+    """Milliseconds of one all-reduce timing pair collected by PPOUpdater (CUDA events or host)."""
+    if isinstance(ev, _HostTimer):
+        return ev.ms()
+    return ev[0].elapsed_time(ev[1])
+
+
+class PPOUpdater:
+    """run_ppo_updates (train_ppo.py:233-252): per minibatch a policy Adam step and a value Adam step
+    over 4 epochs of minibatches. The reference compiles the whole loop as one lax.scan; here:
+
+    * single process on the GPU: the minibatch step (gather, both nets' forward + backward through the
+      native losses, both Adam steps; the value net on a second stream) is captured once as a
+      hipGraph and replayed per minibatch, the minibatch's indices copied into the graph's static
+      index buffer before each replay;
+    * data-parallel: the advantage statistics of every minibatch in one all-reduce up front, then per
+      minibatch graph A (gather, forward, backward, both nets' gradients flattened into one buffer),
+      the RCCL all-reduce of that buffer (eager: the one exchange of the update), and
+      graph B (divide by the world size, both Adam steps);
+    * eager (CPU, torch optimisers, or use_graph=False): the same bodies without capture.
+
+    The graphs need NativeAdam (its step count is device state). The first run is eager (library
+    handles, allocator pools, GEMM choices); the second captures. Replays equal the eager bodies bit
+    for bit (tests/test_ppo_graph.py)."""
+
+    def __init__(self, policy, value, opt_p, opt_v, cfg, dist=None, world=1, use_graph=True):
+        self.policy, self.value, self.opt_p, self.opt_v, self.cfg = policy, value, opt_p, opt_v, cfg
+        self.dist, self.world = dist, world
+        self.pp, self.vp = list(policy.parameters()), list(value.parameters())
+        dev = self.pp[0].device
+        self.cuda = dev.type == "cuda"
+        self.graph_ok = (bool(use_graph) and self.cuda and isinstance(opt_p, NativeAdam)
+                         and isinstance(opt_v, NativeAdam))
+        self.side = _side_stream(dev) if (dist is None and self.cuda and TWO_STREAM_UPDATE) else None
+        self.flat = None
+        if dist is not None:
+            n = sum(p.numel() for p in self.pp + self.vp)
+            self.flat = torch.zeros(n, device=dev)
+            views, o = [], 0
+            for p in self.pp + self.vp:
+                views.append(self.flat[o:o + p.numel()].view_as(p))
+                o += p.numel()
+            self.views_p, self.views_v = views[:len(self.pp)], views[len(self.pp):]
+        self.runs = 0
+        self._src = self._idx = self._st = None
+        self._ga = self._gb = None
+
+    # ------------------------------------------------------------------ bodies
+    def _body_a(self, idx, src, st):
+        """Gather the minibatch; forward + backward of both nets (and, single-process, both Adam
+        steps). Data-parallel: leaves both nets' gradients in self.flat."""
+        cfg, opt_p, opt_v = self.cfg, self.opt_p, self.opt_v
+        o, a, ol, r, ad = _gather_minibatch(idx, *src)
+        if self.side is not None:
+            cur = torch.cuda.current_stream(o.device)
+            self.side.wait_stream(cur)
             # o and r (allocated on cur, read on side) are released at the next gather, after the
             # cur.wait_stream(side) below, so their blocks are not reused early (no record_stream)
-            with torch.cuda.stream(side):
+            with torch.cuda.stream(self.side):
                 opt_v.zero_grad(set_to_none=True)
-                value_loss(value, o, r).backward()
+                value_loss(self.value, o, r).backward()
                 opt_v.step()
             opt_p.zero_grad(set_to_none=True)
-            ppo_policy_loss(policy, o, a, ol, ad, cfg.clip_eps, cfg.ent_coef, dist).backward()
+            ppo_policy_loss(self.policy, o, a, ol, ad, cfg.clip_eps, cfg.ent_coef).backward()
             opt_p.step()
-            cur.wait_stream(side)
-            continue
+            cur.wait_stream(self.side)
+            return
         opt_p.zero_grad(set_to_none=True)
         opt_v.zero_grad(set_to_none=True)
-        ppo_policy_loss(policy, o, a, ol, ad, cfg.clip_eps, cfg.ent_coef, dist).backward()
-        value_loss(value, o, r).backward()
-        if dist is not None:
-            g = _flat_grads(pp + vp)
-            if events is not None:
+        ppo_policy_loss(self.policy, o, a, ol, ad, cfg.clip_eps, cfg.ent_coef, adv_stats=st).backward()
+        value_loss(self.value, o, r).backward()
+        if self.dist is not None:
+            torch.cat([(p.grad if p.grad is not None else torch.zeros_like(p)).reshape(-1) for p in self.pp + self.vp],
+                      out=self.flat)
+        else:
+            opt_p.step()
+            opt_v.step()
+
+    def _body_b(self):
+        """Data-parallel: the all-reduced gradient sum -> mean, then both Adam steps."""
+        self.flat.div_(self.world)
+        if isinstance(self.opt_p, NativeAdam):
+            self.opt_p.step(grads=self.views_p)
+            self.opt_v.step(grads=self.views_v)
+        else:
+            _set_grads(self.pp + self.vp, self.flat)
+            self.opt_p.step()
+            self.opt_v.step()
+
+    def _allreduce(self, events):
+        ev = None
+        if events is not None:
+            if self.cuda:
                 ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
                 ev[0].record()
-            dist.all_reduce(g)
-            if events is not None:
+            else:
+                ev = _HostTimer()
+                ev.record(0)
+        self.dist.all_reduce(self.flat)
+        if ev is not None:
+            if self.cuda:
                 ev[1].record()
-                events.append(ev)
-            g /= world
-            _set_grads(pp + vp, g)
-        opt_p.step()
-        opt_v.step()
+            else:
+                ev.record(1)
+            events.append(ev)
+
+    # ------------------------------------------------------------------ driver
+    def run(self, obs, acts, logp, ret, adv, index_batches, events: Optional[list] = None):
+        """One update over `index_batches` [n_minibatches, rows] of the flattened rollout arrays.
+        `events` (a list) collects one timing pair per all-reduce (event_ms)."""
+        src = (obs, acts, logp, ret, adv)
+        stats = minibatch_adv_stats(adv, index_batches, self.dist) if self.dist is not None else None
+        use_graph = self.graph_ok and self.runs > 0
+        self.runs += 1
+        if not use_graph:
+            for i in range(index_batches.shape[0]):
+                self._body_a(index_batches[i], src, None if stats is None else stats[i])
+                if self.dist is not None:
+                    self._allreduce(events)
+                    self._body_b()
+            return
+        mb = index_batches.shape[1]
+        if self._src is None or any(a.shape != b.shape for a, b in zip(self._src, src)) or self._idx.shape[0] != mb:
+            self._src = tuple(torch.empty_like(x, memory_format=torch.contiguous_format) for x in src)
+            self._idx = torch.empty(mb, dtype=index_batches.dtype, device=index_batches.device)
+            self._st = torch.zeros(2, device=adv.device)
+            self._ga = self._gb = None
+        for dst, x in zip(self._src, src):  # the graphs read the static copies
+            dst.copy_(x)
+        for i in range(index_batches.shape[0]):
+            self._idx.copy_(index_batches[i])
+            if stats is not None:
+                self._st.copy_(stats[i])
+            if self._ga is None:
+                self._ga = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(self._ga):
+                    self._body_a(self._idx, self._src, None if stats is None else self._st)
+                if self.dist is not None:
+                    self._gb = torch.cuda.CUDAGraph()
+                    with torch.cuda.graph(self._gb):
+                        self._body_b()
+            self._ga.replay()
+            if self.dist is not None:
+                self._allreduce(events)
+                self._gb.replay()
+
+
+def ppo_update(policy, value, opt_p, opt_v, obs, acts, logp, ret, adv, index_batches, cfg, dist=None, world=1,
+               events: Optional[list] = None):
+    """train_ppo.py:233-252 as one eager pass of PPOUpdater (no graphs): per minibatch, a policy Adam
+    step then a value Adam step; data-parallel, each rank takes its share of every minibatch and both
+    nets' gradients travel in one all-reduce."""
+    PPOUpdater(policy, value, opt_p, opt_v, cfg, dist, world, use_graph=False).run(obs, acts, logp, ret, adv,
+                                                                                  index_batches, events)
 
 
 # ----------------------------------------------------------------------------------------- trainer
@@ -600,7 +794,7 @@ class PPOTrainer:
 
     def __init__(self, cfg, env, eval_env=None, device="cuda", dist=None, out_dir: Optional[str] = None,
                  use_graph: bool = True, jax_keys: bool = False, fused_policy: bool = True,
-                 reset_pool: int = 16):
+                 reset_pool: int = 16, update_graph: bool = True):
         """jax_keys: draw every env reset (initial, auto-reset, eval) from the jax.random key chain
         train_ppo.py derives from cfg.seed (:88-118, :132/:150-151 per rollout step, :325, :359,
         :419, eval :268-293), so the reset stream equals the reference's for the same seed.
@@ -609,7 +803,9 @@ class PPOTrainer:
         reset_pool: up to this many auto-resets per env and rollout are computed in bulk before the
         rollout (mjl_env_fill_reset_pool; as many as the busiest env used last rollout, + 1) and
         merged by the env steps, instead of each finishing env resetting at the end of its step;
-        0 = in place only. Not with jax_keys (those resets are drawn per step)."""
+        0 = in place only. Not with jax_keys (those resets are drawn per step).
+        update_graph: the update's minibatch steps replay hipGraphs (PPOUpdater) from the second
+        iteration on."""
         self.cfg, self.env, self.eval_env, self.dist = cfg, env, eval_env, dist
         self.rank = dist.get_rank() if dist is not None else 0
         self.world = dist.get_world_size() if dist is not None else 1
@@ -623,6 +819,8 @@ class PPOTrainer:
                 dist.broadcast(p.data, 0)
         self.opt_p = _adam(self.policy.parameters(), cfg.lr_policy)
         self.opt_v = _adam(self.value.parameters(), cfg.lr_value)
+        self.updater = PPOUpdater(self.policy, self.value, self.opt_p, self.opt_v, cfg, dist, self.world,
+                                  use_graph=use_graph and update_graph)
         self.rms = RunningMeanStd(env.obs_dim, self.device)
         self.gen = torch.Generator(device=self.device).manual_seed(int(cfg.seed) * 1000 + self.rank)
         # minibatch permutations drawn on the device they index (4 host randperms of T*B took ~30 ms)
@@ -639,7 +837,7 @@ class PPOTrainer:
         if reset_pool > 0 and not self.jax_keys and self.device.type == "cuda" and hasattr(env, "enable_reset_pool"):
             env.enable_reset_pool(int(reset_pool))
             self._pool_n = torch.full((1,), min(4, int(reset_pool)), dtype=torch.int32, device=self.device)
-        self.allreduce_events = None  # a list to time the per-minibatch all-reduce (bench.py --workload ppo)
+        self.allreduce_events = None  # a list to time the per-minibatch all-reduce (bench.py, event_ms)
         self.total_env_steps = 0.0
         self.start = time.time()
         self.out_dir = out_dir if self.rank == 0 else None
@@ -781,9 +979,8 @@ class PPOTrainer:
             adv, ret = compute_gae(r_t, v, te_t, tr_t, cfg.gamma, cfg.lam)
         mb = cfg.minibatch_size // self.world
         idx = make_index_batches(T * B, mb, cfg.epochs, self.idx_gen, dev)
-        ppo_update(self.policy, self.value, self.opt_p, self.opt_v, obs_n.reshape(T * B, -1),
-                   act_t.reshape(T * B, -1), logp_t.reshape(-1), ret.reshape(-1), adv.reshape(-1), idx, cfg,
-                   self.dist, self.world, self.allreduce_events if self.device.type == "cuda" else None)
+        self.updater.run(obs_n.reshape(T * B, -1), act_t.reshape(T * B, -1), logp_t.reshape(-1), ret.reshape(-1),
+                         adv.reshape(-1), idx, self.allreduce_events)
         if dev.type == "cuda":
             torch.cuda.synchronize(dev)
         dt = max(time.time() - t0, 1e-9)

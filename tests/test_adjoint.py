@@ -258,3 +258,20 @@ def test_unrolled_env_step_vjp_matches_dual_jacobian_cg44():
     errs = np.array(errs)
     print("\nunrolled env-step VJP errors:", np.round(errs, 5))
     assert np.median(errs) <= 1e-3 and errs.max() <= 2e-2, errs
+
+
+@pytest.mark.gpu
+def test_unrolled_vjp_refused_beyond_tape_capacity():
+    """the unrolled solve's tape holds 64 line-search points per search (a zoom search
+    creates up to 1 + 2 ls_iterations); a model with more (humanoid.xml: Newton 100/50) is refused at
+    mjl_batch_set_option instead of overwriting tape entries (a silently wrong gradient)."""
+    from mjx_amd import mjx
+    from mjx_amd._lib import MjlError
+    m = mjx_amd.load_model("humanoid")
+    assert m.ls_iterations > 31
+    d = mjx.make_data(mjx.put_model(m), 4)
+    with pytest.raises(MjlError, match="ls_iterations"):
+        d.set_option(abi.OPT_VJP_UNROLLED, 1)
+    d.set_option(abi.OPT_VJP_UNROLLED, 0)  # the implicit VJP stays available
+    m2 = _truncated("humanoid", "cg", 4, 31)
+    mjx.make_data(mjx.put_model(m2), 4).set_option(abi.OPT_VJP_UNROLLED, 1)  # 63 points fit

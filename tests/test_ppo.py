@@ -140,6 +140,31 @@ def test_adam_matches_optax_formula():
     np.testing.assert_allclose(p.detach().numpy(), x.numpy(), rtol=1e-6)
 
 
+def test_adam_state_dict_conversion_round_trip():
+    """NativeAdam's checkpoint layout is torch.optim.Adam's: the conversion helpers
+    round-trip torch's own state dict, accept the round-2 layout, and refuse mismatched shapes."""
+    params = [torch.nn.Parameter(torch.randn(3, 2)), torch.nn.Parameter(torch.randn(4))]
+    opt = torch.optim.Adam(params, lr=1e-3, betas=(0.9, 0.99), eps=1e-7)
+    for _ in range(3):
+        for p in params:
+            p.grad = torch.randn_like(p)
+        opt.step()
+    sd = opt.state_dict()
+    step, m, v, lr, betas, eps = ppo.adam_state_from_torch(sd, [p.shape for p in params])
+    assert (step, lr, betas, eps) == (3.0, 1e-3, (0.9, 0.99), 1e-7)
+    back = ppo.adam_state_to_torch(step, m, v, lr, betas, eps)
+    opt2 = torch.optim.Adam([torch.nn.Parameter(p.detach().clone()) for p in params], lr=5.0)
+    opt2.load_state_dict(back)
+    for i in range(2):
+        assert torch.equal(opt2.state_dict()["state"][i]["exp_avg"], sd["state"][i]["exp_avg"])
+    old = {"t": 3, "lr": 1e-3, "betas": [0.9, 0.99], "eps": 1e-7, "m": m, "v": v}
+    assert ppo.adam_state_from_torch(old, [p.shape for p in params])[0] == 3.0
+    with pytest.raises(ValueError):
+        ppo.adam_state_from_torch(sd, [params[0].shape])
+    with pytest.raises(ValueError):
+        ppo.adam_state_from_torch(sd, [(3, 2), (5,)])
+
+
 def test_index_batches_drop_partial():
     idx = ppo.make_index_batches(100, 32, 2, torch.Generator().manual_seed(0), "cpu")
     assert idx.shape == (6, 32)

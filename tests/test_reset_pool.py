@@ -21,6 +21,11 @@ STATE = ("qpos", "qvel", "qacc_warmstart", "ctrl", "time", "aux", "xpos", "xquat
 DOMAIN = 1 << 63  # the pool's counter domain (include/mjx355.h)
 
 
+def slot_counter(c0, j):
+    """The RNG counter of pool slot j filled at counter c0: the slot index in bits 48..55."""
+    return ((c0 + (j << 48)) % (1 << 64)) ^ DOMAIN
+
+
 def _envs(B, max_steps, seed=5):
     m = mjx_amd.load_model("humanoid_mjx")
     cfg = resolve_ids(m, dataclasses.replace(reference_ppo_config().env_config, max_episode_steps=max_steps))
@@ -51,7 +56,7 @@ def test_pooled_resets_equal_slot_draws():
             assert float(trunc.sum()) == 0
             continue
         assert bool(torch.all(trunc == 1)) and float(term.sum()) == 0
-        want = _reset_at(ref, (c0 + t // 3 - 1) ^ DOMAIN if t < 9 else env.counter)
+        want = _reset_at(ref, slot_counter(c0, t // 3 - 1) if t < 9 else env.counter)
         assert torch.equal(obs, want), f"step {t}: obs"
         for f in STATE:
             assert torch.equal(env.data.get(f), ref.data.get(f)), f"step {t}: {f}"
@@ -70,7 +75,7 @@ def test_pool_fill_is_clamped_and_refilled():
         env.fill_reset_pool(torch.tensor([100], dtype=torch.int32, device="cuda"))
         for j in range(3):  # every step finishes (max_episode_steps 1): slots 0, 1, then in place
             obs = env.step(act)[0].clone()
-            want = _reset_at(ref, (c0 + j) ^ DOMAIN if j < 2 else env.counter)
+            want = _reset_at(ref, slot_counter(c0, j) if j < 2 else env.counter)
             assert torch.equal(obs, want), f"round {rnd} step {j}"
 
 
@@ -85,3 +90,21 @@ def test_pool_preconditions():
         env.fill_reset_pool(n)
     with pytest.raises(MjlError):
         env.data.set_option(3, 65)
+
+
+def test_consecutive_fills_never_share_a_draw():
+    """with the slot index added to the counter, slot j + T of one fill and slot j of the
+    next fill (counter + T, here T = 1 < the slot count) drew the same reset; with the slot in the
+    high bits every slot of both fills is a distinct draw."""
+    B = 8
+    m, (env, ref) = _envs(B, max_steps=1000)
+    env.enable_reset_pool(4)
+    env.reset()
+    c0 = env.counter
+    seen = []
+    for c in (c0, c0 + 1):
+        for j in range(4):
+            seen.append(_reset_at(ref, slot_counter(c, j)))
+    for a in range(len(seen)):
+        for b in range(a + 1, len(seen)):
+            assert not torch.equal(seen[a], seen[b]), (a, b)

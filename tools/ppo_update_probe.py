@@ -94,7 +94,60 @@ def two_stream(envs: int, reps: int = 8):
               f"max {1e3 * w[-1]:.2f}; enqueue median {1e3 * e[len(e) // 2]:.2f} ms", flush=True)
 
 
+class _NoComm:
+    """A one-rank stand-in for torch.distributed in the probe: all_reduce is the identity."""
+
+    @staticmethod
+    def all_reduce(t, op=None):
+        return t
+
+    @staticmethod
+    def get_world_size():
+        return 1
+
+
+def shard(reps: int = 5, minibatch: int = 8192, envs: int = 1024):
+    """One rank's update in the C5 configuration on 8 GPUs (1024 envs x 256 steps, 4 epochs of
+    8,192-row minibatches: 128 minibatch steps) through PPOUpdater's data-parallel bodies with the
+    collective replaced by the identity: eager vs hipGraph replays, interleaved; and the single-process
+    C3 update (65,536-row minibatches) eager vs graph."""
+    cfg = reference_ppo_config()
+    N = envs * 256
+    gd = torch.Generator(device="cuda").manual_seed(1)
+    obs, act = torch.randn((N, 54), generator=gd, device="cuda"), torch.randn((N, 21), generator=gd, device="cuda").clamp(-1, 1)
+    logp, ret, adv = (torch.randn(N, generator=gd, device="cuda") for _ in range(3))
+    for mb, dist in ((minibatch, _NoComm()), (cfg.minibatch_size, None)):
+        cfg.minibatch_size = mb
+        ups = {}
+        for mode in (False, True):
+            g = torch.Generator().manual_seed(0)
+            pol = ppo.GaussianPolicy(54, 21, cfg.policy_hidden_layer_specs, cfg.log_std_init, g).cuda()
+            val = ppo.ValueNet(54, cfg.value_hidden_layer_specs, g).cuda()
+            op, ov = ppo._adam(pol.parameters(), 3e-4), ppo._adam(val.parameters(), 3e-4)
+            ups[mode] = ppo.PPOUpdater(pol, val, op, ov, cfg, dist, 1, use_graph=mode)
+        ts = {False: [], True: []}
+        for r in range(reps + 2):
+            idx = ppo.make_index_batches(N, mb, cfg.epochs, torch.Generator(device="cuda").manual_seed(r), "cuda")
+            for mode in (False, True):
+                torch.cuda.synchronize()
+                t0 = time.time()
+                ups[mode].run(obs, act, logp, ret, adv, idx)
+                t1 = time.time()
+                torch.cuda.synchronize()
+                t2 = time.time()
+                if r >= 2:
+                    ts[mode].append((t1 - t0, t2 - t0))
+        for mode in (False, True):
+            w = sorted(x[1] for x in ts[mode]); e = sorted(x[0] for x in ts[mode])
+            print(f"{'dp-shard' if dist is not None else 'single'} minibatch={mb} steps={idx.shape[0]} "
+                  f"graph={mode}: wall median {1e3 * w[len(w) // 2]:.2f} ms (min {1e3 * w[0]:.2f}, max "
+                  f"{1e3 * w[-1]:.2f}); host enqueue median {1e3 * e[len(e) // 2]:.2f} ms", flush=True)
+
+
 if __name__ == "__main__":
+    if len(sys.argv) > 1 and sys.argv[1] == "shard":
+        shard()
+        sys.exit(0)
     if len(sys.argv) > 1 and sys.argv[1] == "two":
         two_stream(2048)
         two_stream(1024)
