@@ -385,8 +385,18 @@ def speedtest_extras(args, model, sys_, local):
     env.data.set_option(0, 1)
     mjx.forward(sys_, env.data)
     est = env.data.get("stats").double().mean(0).cpu().numpy()
+    env.data.set_option(0, 0)
     fl = flops_mod.env_step_flops(model, float(est[0]), float(est[1]), float(est[2]), nact=float(est[3]),
                                   reset_frac=reset_frac)
+    # where the launch's extra time goes: the same steps without the reset merge, and with the PPO
+    # trainer's reset pool (resets computed in bulk before the rollout, merged by the step)
+    env.enable_reset_pool(16)
+    npool = torch.tensor([16], dtype=torch.int32, device=dev)
+    env.fill_reset_pool(npool)
+    _, ex["env_step_pool_kernel_ms"] = timed_launches(lambda: env.step(act), args.steps, args.warmup, None)
+    env.enable_reset_pool(0)
+    _, ex["env_step_noreset_kernel_ms"] = timed_launches(lambda: env.step(act, auto_reset=False), args.steps,
+                                                         args.warmup, None)
     tf = fl["total"] * B / (ek * 1e-3) / 1e12
     ex["env_step_roofline"] = {
         "bound": "mfma", "achieved": tf, "peak": F32_PEAK_TFLOPS, "unit": "TFLOP/s", "frac": tf / F32_PEAK_TFLOPS,
@@ -528,27 +538,37 @@ def apg_c4(args, local) -> dict:
         out[f"{key}_ms_per_update"] = wall / len(res) * 1e3
         out[f"{key}_returns"] = [r["return"] for r in res]
         out[f"{key}_nonfinite_envs"] = [r["nonfinite_envs"] for r in res]
-        if vjp == "implicit":  # the replay VJP kernel alone: slot 0 of the last update's tape
-            B = cfg.batch_size
-            env.data.set_option(0, 1)
-            env.reset()  # slot 0 holds step 0 of the last rollout, which starts from resets:
-            mjx.forward(env.sys, env.data)  # solver statistics of (other) reset states
-            s = env.data.get("stats").double().mean(0).cpu().numpy()
+        if vjp == "implicit":  # the replay VJP kernel alone: one reverse sweep over the last update's tape
+            B, H = cfg.batch_size, cfg.horizon
             act = torch.zeros((B, m.nu), device=dev)
             gq, gv = torch.zeros((B, m.nq), device=dev), torch.zeros((B, m.nv), device=dev)
-            grew = torch.full((B,), -1.0 / B, device=dev)
+            grew = torch.full((B,), -1.0 / B, device=dev)  # the reward's cotangent: every env runs the reverse
             nonf = torch.zeros(1, device=dev)
-            fn = lambda: aenv.step_vjp_replay(0, act, gq, gv, None, grew, None, nonf)  # noqa: E731
-            _, kms = timed_launches(fn, 20, 3, None)
-            fl = flops_mod.vjp_replay_flops(m, float(s[0]), float(s[1]), float(s[2]), nact=float(s[3]))
+
+            def sweep():
+                for t in range(H - 1, -1, -1):
+                    aenv.step_vjp_replay(t, act, gq, gv, None, grew, None, nonf)
+            _, kms = timed_launches(sweep, 1, 1, None)
+            kms /= H
+            # the rollout's solver statistics (the same policy from fresh resets; CG reports no active-row
+            # count, so the implicit Hessian is counted over all rows)
+            env.data.set_option(0, 1)
+            env.reset()
+            acc = torch.zeros(3, dtype=torch.float64, device=dev)
+            with torch.no_grad():
+                for _ in range(H):
+                    env.step(tr.policy(aenv.qpos_qvel()), auto_reset=False)
+                    acc += env.data.get("stats")[:, :3].double().mean(0)
+            s = (acc / H).cpu().numpy()
+            fl = flops_mod.vjp_replay_flops(m, float(s[0]), float(s[1]), float(s[2]))
             tf = fl["total"] * B / (kms * 1e-3) / 1e12
             out["apg_vjp_roofline"] = {
                 "bound": "mfma", "achieved": tf, "peak": F32_PEAK_TFLOPS, "unit": "TFLOP/s",
-                "frac": tf / F32_PEAK_TFLOPS, "kernel": "vjp_kernel<..., true, 2> (mjl_env_step_vjp_replay, implicit)",
-                "kernel_ms": kms, "flops_per_env_step": fl["total"],
+                "frac": tf / F32_PEAK_TFLOPS, "kernel": "vjp_kernel<mjl::Dims<27, 17, 22, 20, 4, 4>, true, 2>",
+                "kernel_ms": kms, "launches_timed": H, "flops_per_env_step": fl["total"],
                 "flops_by_stage": {k: v for k, v in fl.items() if k != "total"},
                 "workload_mean_ncon_nefc_iter": [float(x) for x in s[:3]],
-                "workload_mean_active_rows_per_hessian": float(s[3])}
+                "traffic": pmc_traffic(B, "vjp_bytes_per_launch")}
         del tr, aenv, env
         free_gpu()
     out["apg_c4_config"] = (f"train_apg.py: {args.apg_envs} envs x {args.apg_horizon} horizon, CG 4/4, hidden 32x2, "

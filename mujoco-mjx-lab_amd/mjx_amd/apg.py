@@ -178,7 +178,7 @@ class APGTrainer:
             env.apg_obs_vjp(o_all[t], snap[t], self.rms, use_norm, og, gq, gv)
             gas[t] = ga
         torch.autograd.backward(self.policy(on_all.reshape(H * B, w)), grad_tensors=torch.cat(gas))
-        dropped = dropped_e.sum() + nonfinite[0]
+        dropped = torch.stack([dropped_e.sum(), nonfinite[0]])  # (forward guard, reverse guard)
         return loss.detach(), (rfin.mean(1).sum() / H).detach(), o_all, dropped
 
     def _loss_and_grad_torch(self, use_norm: bool, per_step_param_grad: bool = False, graph: bool = False):
@@ -200,6 +200,7 @@ class APGTrainer:
         disc = ret = rsum = None  # created from the first reward (dtype follows the env)
         alive = torch.ones(B, dtype=torch.bool, device=self.device)
         dropped = torch.zeros((), device=self.device)
+        rev_dropped = torch.zeros((), device=self.device)
         obs_traj = []
         for _ in range(H):
             tape.append(env.get_state())
@@ -253,7 +254,7 @@ class APGTrainer:
                 gq, gv, ga, gaux = env.step_vjp(acts[t].detach(), gq, gv, grew, gaux, nonfinite)
             if not guarded:
                 ok = torch.isfinite(gq).all(1) & torch.isfinite(gv).all(1) & torch.isfinite(ga).all(1)
-                dropped = dropped + (~ok).sum()
+                rev_dropped = rev_dropped + (~ok).sum()
                 gq = torch.where(ok[:, None], gq, torch.zeros_like(gq))
                 gv = torch.where(ok[:, None], gv, torch.zeros_like(gv))
                 ga = torch.where(ok[:, None], ga, torch.zeros_like(ga))
@@ -272,8 +273,7 @@ class APGTrainer:
         # policy inputs of the rollout (the same inputs; per step it was H small backward passes)
         if not per_step_param_grad:
             torch.autograd.backward(self.policy(torch.cat(pol_in)), grad_tensors=torch.cat(gas))
-        if guarded:
-            dropped = dropped + nonfinite[0]
+        dropped = torch.stack([dropped.to(torch.float32), (nonfinite[0] if guarded else rev_dropped).to(torch.float32)])
         return loss.detach(), (rsum / H).detach(), torch.stack(obs_traj), dropped
 
     def update(self, step: int) -> dict:
@@ -285,7 +285,7 @@ class APGTrainer:
         loss, mean_r, obs_traj, dropped = self.loss_and_grad(use_norm)
         params = list(self.policy.parameters())
         g = _flat_grads(params)
-        stats = torch.stack([loss, mean_r, dropped.to(loss.dtype)])
+        stats = torch.cat([torch.stack([loss, mean_r]), dropped.to(loss.dtype).reshape(2)])
         if self.dist is not None:
             self.dist.all_reduce(g)
             g /= self.world
@@ -304,7 +304,10 @@ class APGTrainer:
         steps = float(cfg.horizon * self.env.num_envs * self.world)
         self.total_env_steps += steps
         return {"loss": float(stats[0]), "return": float(-stats[0]), "mean_reward": float(stats[1]),
-                "grad_norm": float(gnorm), "env_steps_per_sec": steps / dt, "nonfinite_envs": int(stats[2])}
+                "grad_norm": float(gnorm), "env_steps_per_sec": steps / dt,
+                "nonfinite_envs": int(stats[2]) + int(stats[3]),  # dropped from the loss, either guard
+                "forward_dropped_envs": int(stats[2]),  # state / reward non-finite or |qvel| > diverge_qvel
+                "reverse_nonfinite_envs": int(stats[3])}  # cotangents overflowed in the VJP sweep
 
     def train(self, steps: Optional[int] = None, verbose: bool = True):
         n = self.cfg.total_steps if steps is None else steps

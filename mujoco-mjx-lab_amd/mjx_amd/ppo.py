@@ -78,9 +78,15 @@ class _SplitKLinear(torch.autograd.Function):
 SPLIT_ROWS = 2048  # rows per split of the split-K weight gradient (32 splits at a 65,536 minibatch)
 
 
+UPDATE_MIN_ROWS = 4096  # minibatches of at least this many rows take the native / split-K update path
+
+
 def _linear(lin: nn.Linear, x: torch.Tensor) -> torch.Tensor:
+    """Dense layer; in the update (grad enabled, >= UPDATE_MIN_ROWS rows) the split-K weight gradient,
+    whose fixed batched-GEMM + sum order is also deterministic: the library's single GEMM over K =
+    8,192 rows (the per-rank minibatch of C5 at 8 GPUs) was not bit-reproducible run to run."""
     n = x.shape[0] if x.dim() == 2 else 0
-    if x.is_cuda and torch.is_grad_enabled() and n >= 16384 and n % SPLIT_ROWS == 0:
+    if x.is_cuda and torch.is_grad_enabled() and n >= UPDATE_MIN_ROWS and n % SPLIT_ROWS == 0:
         return _SplitKLinear.apply(x, lin.weight, lin.bias, min(64, n // SPLIT_ROWS))
     return lin(x)
 
@@ -284,8 +290,8 @@ class _GaussianLogprob(torch.autograd.Function):
 
 def gaussian_logprob(mean, log_std, action, out=None):
     """train_ppo.py:121-126: diagonal Gaussian log-density summed over action dims."""
-    if (out is None and mean.is_cuda and torch.is_grad_enabled() and mean.dim() == 2 and mean.shape[0] >= 16384
-            and log_std.dim() == 1):
+    if (out is None and mean.is_cuda and torch.is_grad_enabled() and mean.dim() == 2
+            and mean.shape[0] >= UPDATE_MIN_ROWS and log_std.dim() == 1):
         return _GaussianLogprob.apply(mean, log_std, action)
     var = torch.exp(2.0 * log_std)
     s = torch.sum((action - mean) ** 2 / var + 2.0 * log_std + LOG2PI, dim=-1)
@@ -402,7 +408,7 @@ NATIVE_LOSSES = True  # tests switch the torch restatement back on
 
 
 def _native_loss_ok(x: torch.Tensor) -> bool:
-    return NATIVE_LOSSES and x.is_cuda and torch.is_grad_enabled() and x.shape[0] >= 16384
+    return NATIVE_LOSSES and x.is_cuda and torch.is_grad_enabled() and x.shape[0] >= UPDATE_MIN_ROWS
 
 
 def _global_adv_stats(adv, dist) -> torch.Tensor:

@@ -130,25 +130,35 @@ def test_ppo_c3_iterations_at_full_size(tmp_path):
                 np.testing.assert_allclose(obs_b[t + 1, i], oo[:obs_b.shape[2]], atol=5e-3 * (1 + np.abs(oo).max()))
 
 
-def _apg_trainer(B, H, seed=0):
+def _apg_trainer(B, H, seed=0, vjp="unrolled"):
     from mjx_amd import apg
     m = mjx_amd.load_model("humanoid_mjx")
     m.solver, m.iterations, m.ls_iterations = mjcf.SOLVER_CG, 4, 4  # train_apg.py:101-105
     cfg = APGConfig()
     cfg.batch_size, cfg.horizon, cfg.seed = B, H, seed
     env = HumanoidEnv(mjx.put_model(m), resolve_ids(m, EnvConfig()), B, seed=seed * 7919)
-    return cfg, env, apg.APGTrainer(cfg, apg.HumanoidAPGEnv(env, "unrolled"), device="cuda")
+    return cfg, env, apg.APGTrainer(cfg, apg.HumanoidAPGEnv(env, vjp), device="cuda")
 
 
-def test_apg_c4_update_at_full_size_is_finite():
-    cfg, env, tr = _apg_trainer(2048, 128)
-    met = tr.update(0)
-    assert np.isfinite(met["loss"]) and np.isfinite(met["grad_norm"]) and met["grad_norm"] > 0
-    assert met["nonfinite_envs"] < 2048 // 2
-    for p in tr.policy.parameters():
-        assert torch.isfinite(p).all()
-    met2 = tr.update(1)
-    assert np.isfinite(met2["loss"]) and np.isfinite(met2["grad_norm"])
+@pytest.mark.parametrize("vjp", ["implicit", "unrolled"])
+def test_apg_c4_update_at_full_size(vjp):
+    """C4 (2048 x 128, CG 4/4), two updates (the second a graph replay). Implicit VJP: no env's
+    cotangents overflow (reverse_nonfinite_envs == 0). Unrolled VJP (jax.grad through the truncated
+    solve): the chained per-step Jacobians grow x2.3 per reverse step and overflow fp32 for part of the
+    batch (measured ~700 of 2048), which the guard cuts; bounded here at 1,000. Either
+    way a few envs' forward states diverge under the truncated solve (forward_dropped_envs, the same
+    in both modes: the forward is identical)."""
+    cfg, env, tr = _apg_trainer(2048, 128, vjp=vjp)
+    for it in range(2):
+        met = tr.update(it)
+        assert np.isfinite(met["loss"]) and np.isfinite(met["grad_norm"]) and met["grad_norm"] > 0
+        for p in tr.policy.parameters():
+            assert torch.isfinite(p).all()
+        if vjp == "implicit":
+            assert met["reverse_nonfinite_envs"] == 0, met
+        else:
+            assert met["reverse_nonfinite_envs"] <= 1000, met
+        assert met["forward_dropped_envs"] <= 2048 // 20, met
 
 
 def test_apg_batched_param_grad_equals_per_step_accumulation():

@@ -1,4 +1,10 @@
-"""Minimal launch loop for rocprofv3 counter collection: speed-test (or env-step) kernel only."""
+"""Minimal launch loops for rocprofv3 (kernel trace / counter passes), one kernel family per mode:
+  speedtest     mjl_speedtest_step, B fresh speed-test states (the headline)
+  envstep       mjl_env_step with in-place auto-reset, random actions, after 50 warm steps
+  envstep_pool  the same with the trainer's reset pool (16 slots, refilled every 64 steps)
+  envstep_nr    the same steps without auto-reset (the physics + env post only)
+  vjp           mjl_env_step_vjp_replay over every slot of a 2048 x 128 CG 4/4 implicit APG tape
+python tools/prof_target.py MODE [B] [n]"""
 import os
 import sys
 
@@ -20,7 +26,7 @@ if mode == "speedtest":
     out = torch.empty_like(vel)
     for _ in range(n):
         mjx.speedtest_step(sys_, d, vel, out)
-else:
+elif mode.startswith("envstep"):
     from mjx_amd.config import reference_ppo_config
     from mjx_amd.envs import HumanoidEnv, resolve_ids
     cfg = resolve_ids(m, reference_ppo_config().env_config)
@@ -28,7 +34,35 @@ else:
     env.reset()
     g = torch.Generator(device="cuda").manual_seed(0)
     act = torch.rand((B, m.nu), generator=g, device="cuda") * 2 - 1
-    for _ in range(n):
+    pool = mode == "envstep_pool"
+    if pool:
+        env.enable_reset_pool(16)
+        npool = torch.tensor([16], dtype=torch.int32, device="cuda")
+    for _ in range(50):
         env.step(act)
+    for i in range(n):
+        if pool and i % 64 == 0:
+            env.fill_reset_pool(npool)
+        env.step(act, auto_reset=mode != "envstep_nr")
+elif mode == "vjp":
+    from mjx_amd.apg import APGTrainer, HumanoidAPGEnv
+    from mjx_amd.config import APGConfig, EnvConfig
+    from mjx_amd.envs import HumanoidEnv, resolve_ids
+    sys.path.insert(0, os.path.join(ROOT, "mujoco-mjx-lab_amd"))
+    from train_apg import apg_model
+    cfg = APGConfig()
+    cfg.batch_size, cfg.horizon = B, 128
+    ma = apg_model(cfg, solver="cg")
+    env = HumanoidEnv(mjx.put_model(ma), resolve_ids(ma, EnvConfig()), B, seed=cfg.seed)
+    aenv = HumanoidAPGEnv(env, "implicit")
+    tr = APGTrainer(cfg, aenv, device="cuda", use_graph=False)
+    tr.update(0)  # records the tape (eager)
+    act = torch.zeros((B, ma.nu), device="cuda")
+    gq, gv = torch.zeros((B, ma.nq), device="cuda"), torch.zeros((B, ma.nv), device="cuda")
+    grew = torch.full((B,), -1.0 / B, device="cuda")
+    nonf = torch.zeros(1, device="cuda")
+    for _ in range(max(1, n // cfg.horizon)):
+        for t in range(cfg.horizon - 1, -1, -1):
+            aenv.step_vjp_replay(t, act, gq, gv, None, grew, None, nonf)
 torch.cuda.synchronize()
 print("done", mode, B, n)
