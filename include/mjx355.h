@@ -405,6 +405,20 @@ int mjl_adam_dev(int nt, float* const* p, const float* const* g, float* const* m
                  const long long* numel, float lr, float beta1, float beta2, float eps, const float* step,
                  void* stream);
 
+/* PPO update dense layers (train_ppo.py:204-252: value_and_grad of ppo_loss_fn / value_loss_fn
+ * through the src/networks.py:22-61 MLPs), fp32 on the matrix cores, torch nn.Linear layouts
+ * (row-major x [M, K] with row stride ldx, w [N, K], b [N], y [M, N]); act: 0 none, 1 tanh.
+ * mjl_mlp_fwd: y = act(x w^T + b), bias and tanh in the GEMM's epilogue.
+ * mjl_mlp_bwd: dz = g (1 - y^2) (tanh; g for none) [M, N] written out, dx = dz w [M, K] (dx may be NULL:
+ *   the first layer), and colpart [mjl_mlp_colpart_rows(M), N] = dz's column sums per 128-row block
+ *   (the bias gradient is their column sum, mjl_colsum: fixed order). The weight gradient dz^T x is a
+ *   batched GEMM outside. Device pointers; w / dx 16-byte aligned and K % 4 == 0 when dx is given. */
+int mjl_mlp_fwd(const float* x, int ldx, const float* w, const float* b, int M, int N, int K, int act, float* y,
+                void* stream);
+long long mjl_mlp_colpart_rows(int M);
+int mjl_mlp_bwd(const float* g, const float* y, int M, int N, const float* w, int K, int act, float* dz, float* dx,
+                float* colpart, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

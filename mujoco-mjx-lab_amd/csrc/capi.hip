@@ -14,6 +14,7 @@
 #include "ppo_kernels.hip"
 #include "apg_kernels.hip"
 #include "ppo_loss_kernels.hip"
+#include "mlp_kernels.hip"
 
 using namespace mjl;
 
@@ -1148,4 +1149,52 @@ extern "C" int mjl_adam_dev(int nt, float* const* p, const float* const* g, floa
                             void* stream) {
   if (!step) return fail(MJL_ERR_ARG, "bad argument");
   return adam_launch(nt, p, g, m, v, numel, lr, beta1, beta2, eps, 0, step, stream);
+}
+
+// ---------------------------------------------------------------- PPO update dense layers
+static bool aligned16(const void* p) { return ((uintptr_t)p & 15) == 0; }
+
+extern "C" int mjl_mlp_fwd(const float* x, int ldx, const float* w, const float* b, int M, int N, int K, int act,
+                           float* y, void* stream) {
+  if (!x || !w || !b || !y || M < 0 || N <= 0 || K <= 0 || ldx < K || (act != MLP_ACT_NONE && act != MLP_ACT_TANH))
+    return fail(MJL_ERR_ARG, "bad argument");
+  if (M == 0) return MJL_OK;
+  hipStream_t s = (hipStream_t)stream;
+  const bool vec = K % 4 == 0 && ldx % 4 == 0 && aligned16(x) && aligned16(w);
+  if (N <= 32) {  // the heads (21 actions, 1 value): 256 x 32 tiles, 4 waves of 64 x 32
+    dim3 grid(1, (M + 255) / 256);
+    if (vec) hipLaunchKernelGGL((mlp_fwd_kernel<256, 32, 4, 1, true>), grid, dim3(256), 0, s, x, ldx, w, K, b, y, N, M, N, K, act);
+    else hipLaunchKernelGGL((mlp_fwd_kernel<256, 32, 4, 1, false>), grid, dim3(256), 0, s, x, ldx, w, K, b, y, N, M, N, K, act);
+  } else {  // 128 x 128 tiles, 4 waves of 64 x 64; a row block's column tiles are neighbours in launch order
+    dim3 grid((N + 127) / 128, (M + 127) / 128);
+    if (vec) hipLaunchKernelGGL((mlp_fwd_kernel<128, 128, 2, 2, true>), grid, dim3(256), 0, s, x, ldx, w, K, b, y, N, M, N, K, act);
+    else hipLaunchKernelGGL((mlp_fwd_kernel<128, 128, 2, 2, false>), grid, dim3(256), 0, s, x, ldx, w, K, b, y, N, M, N, K, act);
+  }
+  HIPCHK(hipGetLastError());
+  return MJL_OK;
+}
+
+extern "C" long long mjl_mlp_colpart_rows(int M) { return M > 0 ? (M + 127) / 128 : 0; }
+
+extern "C" int mjl_mlp_bwd(const float* g, const float* y, int M, int N, const float* w, int K, int act, float* dz,
+                           float* dx, float* colpart, void* stream) {
+  if (!g || !y || !dz || !colpart || M < 0 || N <= 0 || (dx && (!w || K <= 0 || K % 4 != 0)) ||
+      (act != MLP_ACT_NONE && act != MLP_ACT_TANH))
+    return fail(MJL_ERR_ARG, "bad argument");
+  if (M == 0) return MJL_OK;
+  hipStream_t s = (hipStream_t)stream;
+  const bool vec = N % 4 == 0 && aligned16(g) && aligned16(y) && aligned16(dz);
+  if (dx && !(aligned16(w) && aligned16(dx))) return fail(MJL_ERR_ARG, "mlp_bwd: 16-byte aligned w and dx expected");
+  const dim3 blk(256);
+  if (dx) {
+    dim3 grid((K + 127) / 128, (M + 127) / 128);
+    if (vec) hipLaunchKernelGGL((mlp_bwd_kernel<128, 128, 2, 2, true, true>), grid, blk, 0, s, g, y, N, w, K, dz, dx, K, colpart, M, N, K, act);
+    else hipLaunchKernelGGL((mlp_bwd_kernel<128, 128, 2, 2, true, false>), grid, blk, 0, s, g, y, N, w, K, dz, dx, K, colpart, M, N, K, act);
+  } else {
+    dim3 grid(1, (M + 127) / 128);
+    if (vec) hipLaunchKernelGGL((mlp_bwd_kernel<128, 128, 2, 2, false, true>), grid, blk, 0, s, g, y, N, w, 0, dz, nullptr, 0, colpart, M, N, 0, act);
+    else hipLaunchKernelGGL((mlp_bwd_kernel<128, 128, 2, 2, false, false>), grid, blk, 0, s, g, y, N, w, 0, dz, nullptr, 0, colpart, M, N, 0, act);
+  }
+  HIPCHK(hipGetLastError());
+  return MJL_OK;
 }

@@ -28,7 +28,7 @@ EXPORTS = [
     "mjl_step_vjp_full", "mjl_env_step_vjp_full", "mjl_env_fill_reset_pool",
     "mjl_apg_obs", "mjl_apg_post", "mjl_apg_obs_vjp", "mjl_env_step_record", "mjl_env_step_vjp_replay",
     "mjl_ppo_loss_scratch", "mjl_ppo_surrogate", "mjl_mse", "mjl_gather_rows", "mjl_adam",
-    "mjl_adam_dev",
+    "mjl_adam_dev", "mjl_mlp_fwd", "mjl_mlp_colpart_rows", "mjl_mlp_bwd",
 ]
 
 _lib = None
@@ -94,6 +94,10 @@ def lib() -> C.CDLL:
     L.mjl_gather_rows.argtypes = [vp, i32, C.c_longlong, i32, vp, vp, vp, vp]
     L.mjl_adam.argtypes = [i32, vp, vp, vp, vp, vp, C.c_float, C.c_float, C.c_float, C.c_float, i32, vp]
     L.mjl_adam_dev.argtypes = [i32, vp, vp, vp, vp, vp, C.c_float, C.c_float, C.c_float, C.c_float, vp, vp]
+    L.mjl_mlp_fwd.argtypes = [vp, i32, vp, vp, i32, i32, i32, i32, vp, vp]
+    L.mjl_mlp_colpart_rows.argtypes = [i32]
+    L.mjl_mlp_colpart_rows.restype = C.c_longlong
+    L.mjl_mlp_bwd.argtypes = [vp, vp, i32, i32, vp, i32, i32, vp, vp, vp, vp]
     L.mjl_env_step_record.argtypes = [vp, i32, vp, vp, vp, vp, vp, vp]
     L.mjl_env_step_vjp_replay.argtypes = [vp, i32] + [vp] * 12 + [vp]
     L.mjl_apg_obs.argtypes = [vp, vp, vp, vp, i32, vp, vp, vp, vp]

@@ -91,9 +91,89 @@ def _linear(lin: nn.Linear, x: torch.Tensor) -> torch.Tensor:
     return lin(x)
 
 
+# the dense layers on mjl_mlp_fwd / mjl_mlp_bwd (MJL_FUSED_MLP=1): off by default — measured against
+# hipBLASLt + torch's elementwise passes: equal at the 65,536-row minibatch (26.1 vs
+# 26.3 ms per C3 update), slower at the 8,192-row per-rank minibatch of C5 on 8 GPUs (64.5 vs 53.9 ms)
+FUSED_MLP = os.environ.get("MJL_FUSED_MLP", "0") == "1"
+_MLP_ACT = {"tanh": 1, "linear": 0, "none": 0}
+
+
+class _FusedMLP(torch.autograd.Function):
+    """A whole MLP (src/networks.py:55-61: Dense + activation per layer) on the native dense-layer
+    kernels: forward y_l = act_l(y_{l-1} W_l^T + b_l) with bias and tanh in the GEMM epilogue
+    (mjl_mlp_fwd); backward per layer, from the top, dz_l = g (1 - y_l^2) fused into the GEMM
+    dx = dz_l W_l with the bias gradient's per-block column sums on the way (mjl_mlp_bwd), the weight
+    gradient dz_l^T y_{l-1} as split-K batched GEMMs + a sum (as _SplitKLinear), the bias gradient a
+    fixed-order column sum. Where torch ran a GEMM, a tanh pass and, in the backward, a tanh-backward
+    pass and a column-sum pass per layer."""
+
+    @staticmethod
+    def forward(ctx, x, acts, *params):
+        from ._lib import check, lib
+        L = lib()
+        st = torch.cuda.current_stream(x.device).cuda_stream
+        h = x.contiguous()
+        M = h.shape[0]
+        ys = []
+        for l, act in enumerate(acts):
+            w, b = params[2 * l], params[2 * l + 1]
+            N, K = w.shape
+            y = torch.empty((M, N), dtype=torch.float32, device=x.device)
+            check(L.mjl_mlp_fwd(h.data_ptr(), K, w.data_ptr(), b.data_ptr(), M, N, K, act, y.data_ptr(), st))
+            ys.append(y)
+            h = y
+        ctx.acts = acts
+        ctx.save_for_backward(x.contiguous(), *params, *ys)
+        return h
+
+    @staticmethod
+    def backward(ctx, g):
+        from ._lib import check, lib
+        L = lib()
+        acts = ctx.acts
+        nl = len(acts)
+        saved = ctx.saved_tensors
+        x, params, ys = saved[0], saved[1:1 + 2 * nl], saved[1 + 2 * nl:]
+        st = torch.cuda.current_stream(x.device).cuda_stream
+        M = x.shape[0]
+        rows = int(L.mjl_mlp_colpart_rows(M))
+        grads = [None] * (2 * nl)
+        g = g.contiguous()
+        gx = None
+        for l in range(nl - 1, -1, -1):
+            w = params[2 * l]
+            N, K = w.shape
+            xin = x if l == 0 else ys[l - 1]
+            dz = torch.empty((M, N), dtype=torch.float32, device=x.device)
+            part = torch.empty((rows, N), dtype=torch.float32, device=x.device)
+            want_dx = l > 0 or ctx.needs_input_grad[0]
+            dx = torch.empty((M, K), dtype=torch.float32, device=x.device) if want_dx else None
+            check(L.mjl_mlp_bwd(g.data_ptr(), ys[l].data_ptr(), M, N, w.data_ptr() if want_dx else None, K, acts[l],
+                                dz.data_ptr(), dx.data_ptr() if want_dx else None, part.data_ptr(), st))
+            s = min(64, max(1, M // SPLIT_ROWS))
+            if M % s:
+                s = 1
+            grads[2 * l] = torch.bmm(dz.reshape(s, M // s, N).transpose(1, 2), xin.reshape(s, M // s, K)).sum(0)
+            grads[2 * l + 1] = colsum_native(part) if N > 1 else part.sum(0)
+            g = dx
+            if l == 0:
+                gx = dx
+        return (gx, None, *grads)
+
+
+def _fused_ok(mlp, x) -> bool:
+    return (FUSED_MLP and x.is_cuda and x.dim() == 2 and x.shape[0] >= UPDATE_MIN_ROWS and x.dtype == torch.float32
+            and all(a in _MLP_ACT for a in mlp.acts)
+            and all(p.dtype == torch.float32 and p.is_contiguous() for p in mlp.parameters())
+            and all(lin.out_features % 4 == 0 or lin is mlp.layers[-1] for lin in mlp.layers)
+            and (not x.requires_grad or mlp.layers[0].in_features % 4 == 0))
+
+
 class MLP(nn.Module):
     """src/networks.py:22-61: layers of (features, activation); Glorot-normal weights
-    N(0, 2/(in+out)), zero biases (networks.py:32-53). Unknown activations fall back to tanh."""
+    N(0, 2/(in+out)), zero biases (networks.py:32-53). Unknown activations fall back to tanh.
+    Batches of >= UPDATE_MIN_ROWS rows on the GPU (the PPO update's minibatches, the value pass over
+    the rollout) run on the native dense-layer kernels (_FusedMLP)."""
 
     def __init__(self, in_dim: int, layer_specs: Sequence[Tuple[int, str]], generator: Optional[torch.Generator] = None):
         super().__init__()
@@ -108,10 +188,19 @@ class MLP(nn.Module):
             d = int(feat)
         self.layers = nn.ModuleList(layers)
 
-    def forward(self, x):
+    def forward(self, x, out_tanh: bool = False):
+        """out_tanh: a tanh after the last layer (GaussianPolicy's mean, networks.py:103)."""
+        if _fused_ok(self, x):
+            acts = tuple(_MLP_ACT[a] for a in self.acts)
+            if out_tanh:
+                if acts[-1] != 0:
+                    raise ValueError("out_tanh after an activated last layer")
+                acts = acts[:-1] + (1,)
+            params = [t for lin in self.layers for t in (lin.weight, lin.bias)]
+            return _FusedMLP.apply(x, acts, *params)
         for lin, a in zip(self.layers, self.acts):
             x = ACTIVATIONS.get(a, torch.tanh)(_linear(lin, x))
-        return x
+        return torch.tanh(x) if out_tanh else x
 
 
 class GaussianPolicy(nn.Module):
@@ -123,7 +212,7 @@ class GaussianPolicy(nn.Module):
         self.log_std = nn.Parameter(torch.full((act_dim,), float(log_std_init)))
 
     def forward(self, x):
-        return torch.tanh(self.mlp(x)), torch.clamp(self.log_std, -20.0, 2.0)
+        return self.mlp(x, out_tanh=True), torch.clamp(self.log_std, -20.0, 2.0)
 
 
 class ValueNet(nn.Module):
@@ -146,7 +235,7 @@ class APGPolicy(nn.Module):
         self.mlp = MLP(obs_dim, specs + [(act_dim, "linear")], generator)
 
     def forward(self, x):
-        return torch.tanh(self.mlp(x))
+        return self.mlp(x, out_tanh=True)
 
 
 # ------------------------------------------------------------------------------------- statistics
@@ -665,7 +754,10 @@ class PPOUpdater:
         self.cuda = dev.type == "cuda"
         self.graph_ok = (bool(use_graph) and self.cuda and isinstance(opt_p, NativeAdam)
                          and isinstance(opt_v, NativeAdam))
-        self.side = _side_stream(dev) if (dist is None and self.cuda and TWO_STREAM_UPDATE) else None
+        # the value net's forward / backward (and, single-process, its Adam step) on a second stream beside
+        # the policy's: independent within a minibatch, and one net's GEMMs leave CUs idle — at the
+        # 8,192-row per-rank minibatch of C5 on 8 GPUs a 256-wide layer is 64 row tiles for 256 CUs
+        self.side = _side_stream(dev) if (self.cuda and TWO_STREAM_UPDATE) else None
         self.flat = None
         if dist is not None:
             n = sum(p.numel() for p in self.pp + self.vp)
@@ -685,6 +777,7 @@ class PPOUpdater:
         steps). Data-parallel: leaves both nets' gradients in self.flat."""
         cfg, opt_p, opt_v = self.cfg, self.opt_p, self.opt_v
         o, a, ol, r, ad = _gather_minibatch(idx, *src)
+        dp = self.dist is not None
         if self.side is not None:
             cur = torch.cuda.current_stream(o.device)
             self.side.wait_stream(cur)
@@ -693,20 +786,22 @@ class PPOUpdater:
             with torch.cuda.stream(self.side):
                 opt_v.zero_grad(set_to_none=True)
                 value_loss(self.value, o, r).backward()
-                opt_v.step()
+                if not dp:
+                    opt_v.step()
             opt_p.zero_grad(set_to_none=True)
-            ppo_policy_loss(self.policy, o, a, ol, ad, cfg.clip_eps, cfg.ent_coef).backward()
-            opt_p.step()
+            ppo_policy_loss(self.policy, o, a, ol, ad, cfg.clip_eps, cfg.ent_coef, adv_stats=st).backward()
+            if not dp:
+                opt_p.step()
             cur.wait_stream(self.side)
-            return
-        opt_p.zero_grad(set_to_none=True)
-        opt_v.zero_grad(set_to_none=True)
-        ppo_policy_loss(self.policy, o, a, ol, ad, cfg.clip_eps, cfg.ent_coef, adv_stats=st).backward()
-        value_loss(self.value, o, r).backward()
-        if self.dist is not None:
+        else:
+            opt_p.zero_grad(set_to_none=True)
+            opt_v.zero_grad(set_to_none=True)
+            ppo_policy_loss(self.policy, o, a, ol, ad, cfg.clip_eps, cfg.ent_coef, adv_stats=st).backward()
+            value_loss(self.value, o, r).backward()
+        if dp:
             torch.cat([(p.grad if p.grad is not None else torch.zeros_like(p)).reshape(-1) for p in self.pp + self.vp],
                       out=self.flat)
-        else:
+        elif self.side is None:
             opt_p.step()
             opt_v.step()
 

@@ -144,7 +144,32 @@ def shard(reps: int = 5, minibatch: int = 8192, envs: int = 1024):
                   f"{1e3 * w[-1]:.2f}); host enqueue median {1e3 * e[len(e) // 2]:.2f} ms", flush=True)
 
 
+def graph_update(envs: int = 2048, reps: int = 4):
+    """The single-process update as the trainer runs it (PPOUpdater, hipGraph replays) at `envs` x 256
+    steps, for a rocprofv3 kernel trace: per-kernel time of GEMMs vs elementwise vs losses / Adam."""
+    cfg = reference_ppo_config()
+    N = envs * 256
+    gd = torch.Generator(device="cuda").manual_seed(1)
+    obs, act = torch.randn((N, 54), generator=gd, device="cuda"), torch.randn((N, 21), generator=gd, device="cuda").clamp(-1, 1)
+    logp, ret, adv = (torch.randn(N, generator=gd, device="cuda") for _ in range(3))
+    g = torch.Generator().manual_seed(0)
+    pol = ppo.GaussianPolicy(54, 21, cfg.policy_hidden_layer_specs, cfg.log_std_init, g).cuda()
+    val = ppo.ValueNet(54, cfg.value_hidden_layer_specs, g).cuda()
+    op, ov = ppo._adam(pol.parameters(), 3e-4), ppo._adam(val.parameters(), 3e-4)
+    up = ppo.PPOUpdater(pol, val, op, ov, cfg, None, 1, use_graph=True)
+    for r in range(reps):
+        idx = ppo.make_index_batches(N, cfg.minibatch_size, cfg.epochs, torch.Generator(device="cuda").manual_seed(r), "cuda")
+        torch.cuda.synchronize()
+        t0 = time.time()
+        up.run(obs, act, logp, ret, adv, idx)
+        torch.cuda.synchronize()
+        print(f"update {r}: {1e3 * (time.time() - t0):.2f} ms ({'graph' if r else 'eager'})", flush=True)
+
+
 if __name__ == "__main__":
+    if len(sys.argv) > 1 and sys.argv[1] == "graph":
+        graph_update(int(sys.argv[2]) if len(sys.argv) > 2 else 2048)
+        sys.exit(0)
     if len(sys.argv) > 1 and sys.argv[1] == "shard":
         shard()
         sys.exit(0)
