@@ -1544,6 +1544,45 @@ template <class DM, class AT> INL void slot_a_io(GLBA float* sa, AT* A, LDSA flo
   mv((LDSA float*)A->Lc, sa + MJL_MAXQ + 3 * LD + 12, NV * LD);
 }
 
+// replay's load of a tape slot into LDS: every global load of the workspace (b128) and of the A part
+// issued before the first LDS store (as a loop of load -> store pairs each iteration waited for its
+// own load: ~28 dependent HBM round trips per replayed step)
+template <class DM, class AT> INL void slot_replay_load(GLBA const float* sw, GLBA const float* sa, LDSA WS<DM>* W,
+                                                      AT* A, LDSA float* aux, int lane) {
+  constexpr int LD = DM::LD, NV = DM::NV;
+  constexpr int NW = (int)(sizeof(WS<DM>) / 16), QW = (NW + 63) / 64;
+  constexpr int NA = slot_a_floats<DM>(), QA = (NA + 63) / 64;
+  constexpr int O1 = MJL_MAXQ, O2 = O1 + LD, O3 = O2 + 12, O4 = O3 + LD, O5 = O4 + LD;  // A-part segments
+  f32x4 w[QW];
+  float a[QA];
+#pragma unroll
+  for (int q = 0; q < QW; q++) {
+    const int i = lane + 64 * q;
+    if (i < NW) w[q] = ((GLBA const f32x4*)sw)[i];
+  }
+#pragma unroll
+  for (int q = 0; q < QA; q++) {
+    const int i = lane + 64 * q;
+    a[q] = i < NA ? sa[i] : 0.f;
+  }
+#pragma unroll
+  for (int q = 0; q < QW; q++) {
+    const int i = lane + 64 * q;
+    if (i < NW) ((LDSA f32x4*)W)[i] = w[q];
+  }
+#pragma unroll
+  for (int q = 0; q < QA; q++) {
+    const int i = lane + 64 * q;
+    if (i < O1) ((LDSA float*)A->qpos0)[i] = a[q];
+    else if (i < O2) ((LDSA float*)A->qvel0)[i - O1] = a[q];
+    else if (i < O3) { if (i - O2 < MJL_AUX_DIM) aux[i - O2] = a[q]; }
+    else if (i < O4) ((LDSA float*)A->ap)[i - O3] = a[q];
+    else if (i < O5) ((LDSA float*)A->invdc)[i - O4] = a[q];
+    else if (i < NA) ((LDSA float*)A->Lc)[i - O5] = a[q];
+  }
+  (void)NV;
+}
+
 // One wave per env: recompute the step from the batch state (not modified), then run the reverse
 // passes. ENV: the env step of envs.py (action flip / clip, reward, aux) without the reset merge.
 // TM (VJP tape): 0 recompute, as above; 1 record: the forward only — the env step itself (outputs
@@ -1565,14 +1604,14 @@ template <class D, bool ENV, int TM> __global__ __launch_bounds__(64, 1) void vj
   const StateBuf& S = P.s;
   if constexpr (TM != 1) {  // the VJP is linear in the cotangents: all-zero in -> all-zero out, without
      // the recompute (envs past termination in an APG rollout; also keeps 0 * non-finite out of their outputs)
-    bool nz = false;
-    if (lane < nq) nz |= V.g_qpos[(size_t)env * nq + lane] != 0.f;
-    if (lane < nv) nz |= V.g_qvel[(size_t)env * nv + lane] != 0.f;
-    if (V.g_ws && lane < nv) nz |= V.g_ws[(size_t)env * nv + lane] != 0.f;
-    if (ENV) {
-      if (lane == 0) nz |= V.g_rew[env] != 0.f;
-      if (lane < MJL_AUX_DIM) nz |= V.g_aux[(size_t)env * MJL_AUX_DIM + lane] != 0.f;
-    }
+    // clamped-index loads (no branch around each): all issue before the first compare
+    const int iq = lane < nq ? lane : nq - 1, iv = lane < nv ? lane : nv - 1;
+    const int ia = lane < MJL_AUX_DIM ? lane : MJL_AUX_DIM - 1;
+    const float cq = V.g_qpos[(size_t)env * nq + iq], cv = V.g_qvel[(size_t)env * nv + iv];
+    const float cw = V.g_ws ? V.g_ws[(size_t)env * nv + iv] : 0.f;
+    const float cr = ENV ? V.g_rew[env] : 0.f, ca = ENV ? V.g_aux[(size_t)env * MJL_AUX_DIM + ia] : 0.f;
+    bool nz = (lane < nq && cq != 0.f) || (lane < nv && (cv != 0.f || cw != 0.f));
+    if (ENV) nz = nz || (lane == 0 && cr != 0.f) || (lane < MJL_AUX_DIM && ca != 0.f);
     if (__ballot(nz) == 0ull) {
       if (lane < nq) V.o_qpos[(size_t)env * nq + lane] = 0.f;
       if (lane < nv) V.o_qvel[(size_t)env * nv + lane] = 0.f;
@@ -1604,10 +1643,7 @@ template <class D, bool ENV, int TM> __global__ __launch_bounds__(64, 1) void vj
   tp.nup = tp.nls = tp.nsets = tp.overflow = 0;
   Rows<true> R = global_rows<D>(TM ? (float*)(slot + V.s_r) : scr_env, P.gmax_efc, P.gmax_con);
   if constexpr (TM == 2) {  // replay: the forward's workspace, pre-step state and factors from the slot
-    const GLBA f32x4* src = (const GLBA f32x4*)(slot + V.s_w);
-    LDSA f32x4* dst = (LDSA f32x4*)W;
-    for (int i = lane; i < (int)(sizeof(WS<D>) / 16); i += 64) dst[i] = src[i];
-    slot_a_io<D>(slot + V.s_a, A, aux, lane, false);
+    slot_replay_load<D>(slot + V.s_w, slot + V.s_a, W, A, aux, lane);
     SYNC();
   } else {
   if (lane < nq) { W->qpos[lane] = S.qpos[(size_t)env * nq + lane]; A->qpos0[lane] = W->qpos[lane]; }
