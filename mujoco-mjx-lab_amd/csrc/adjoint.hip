@@ -1646,25 +1646,31 @@ template <class D, bool ENV, int TM> __global__ __launch_bounds__(64, 1) void vj
     slot_replay_load<D>(slot + V.s_w, slot + V.s_a, W, A, aux, lane);
     SYNC();
   } else {
-  if (lane < nq) { W->qpos[lane] = S.qpos[(size_t)env * nq + lane]; A->qpos0[lane] = W->qpos[lane]; }
-  if (lane < nv) {
-    W->qvel[lane] = S.qvel[(size_t)env * nv + lane]; A->qvel0[lane] = W->qvel[lane];
-    W->qacc_ws[lane] = S.qacc_warmstart[(size_t)env * nv + lane];
+  // every state load issues before the first wait (clamped lane indices, no branch per load)
+  const int iq = lane < nq ? lane : nq - 1, iv = lane < nv ? lane : nv - 1, iu = lane < nu ? lane : nu - 1;
+  const float q = S.qpos[(size_t)env * nq + iq];
+  const float v = S.qvel[(size_t)env * nv + iv], w = S.qacc_warmstart[(size_t)env * nv + iv];
+  float c = ENV ? V.act[(size_t)env * nu + iu] : S.ctrl[(size_t)env * nu + iu];
+  const float t = S.time[env];
+  float ax = 0.f, sgn = 1.f;
+  int perm = iu;
+  if (ENV) {
+    const int ia = lane < MJL_AUX_DIM ? lane : MJL_AUX_DIM - 1;
+    ax = S.aux[(size_t)env * MJL_AUX_DIM + ia];
+    perm = P.env->act_perm[iu];
+    sgn = P.env->act_sign[iu];
   }
-  if (lane == 0) W->sc[SC_TIME] = S.time[env];
-  if (ENV && lane < MJL_AUX_DIM) aux[lane] = S.aux[(size_t)env * MJL_AUX_DIM + lane];
-  SYNC();
-  if (ENV) {  // flip + clip the action (envs.py:335-344)
-    const mjlEnvConfig* c = P.env;
-    const bool flip = aux[0] > 0.5f;
-    if (lane < nu) {
-      const float a = flip ? V.act[(size_t)env * nu + c->act_perm[lane]] * c->act_sign[lane] : V.act[(size_t)env * nu + lane];
-      W->ctrl[lane] = fminf(fmaxf(a, -1.f), 1.f);
-    }
-    if (TM == 1 && lane == 0) W->sc[SC_FLIP] = aux[0];
-  } else if (lane < nu) {
-    W->ctrl[lane] = S.ctrl[(size_t)env * nu + lane];
+  if (lane < nq) { W->qpos[lane] = q; A->qpos0[lane] = q; }
+  if (lane < nv) { W->qvel[lane] = v; A->qvel0[lane] = v; W->qacc_ws[lane] = w; }
+  if (lane == 0) W->sc[SC_TIME] = t;
+  if (ENV) {  // flip + clip the action (envs.py:335-344): act[perm[j]] from lane perm[j]
+    if (lane < MJL_AUX_DIM) aux[lane] = ax;
+    const bool flip = rdlane(ax, 0) > 0.5f;
+    const float ap = __shfl(c, perm);
+    c = fminf(fmaxf(flip ? ap * sgn : c, -1.f), 1.f);
+    if (TM == 1 && lane == 0) W->sc[SC_FLIP] = ax;
   }
+  if (lane < nu) W->ctrl[lane] = c;
   SYNC();
   // ---- forward (forward() + integrate(), rows in the env's global slab)
   STAMP(0, lane);

@@ -2358,25 +2358,35 @@ template <class D, int MODE> __global__ __launch_bounds__(64, MJL_MINWAVES) void
       if (lane < nu) W->ctrl[lane] = 0.f;
       if (lane == 0) W->sc[SC_TIME] = 0.f;
     } else {
-      if (lane < nq) W->qpos[lane] = S.qpos[(size_t)env * nq + lane];
-      if (lane < nv) { W->qvel[lane] = S.qvel[(size_t)env * nv + lane]; W->qacc_ws[lane] = S.qacc_warmstart[(size_t)env * nv + lane]; }
-      if (lane < nu) W->ctrl[lane] = (MODE == MODE_STEP && P.in_ctrl) ? P.in_ctrl[(size_t)env * nu + lane]
-                                                                       : S.ctrl[(size_t)env * nu + lane];
-      if (lane == 0) W->sc[SC_TIME] = S.time[env];
-      if (MODE == MODE_ENV_STEP && lane < MJL_AUX_DIM) aux[lane] = S.aux[(size_t)env * MJL_AUX_DIM + lane];
+      // every state load issues before the first wait: clamped lane indices instead of a branch around
+      // each load (each branch waited for its own load: ~7 dependent HBM round trips per env step)
+      const int iq = lane < nq ? lane : nq - 1, iv = lane < nv ? lane : nv - 1, iu = lane < nu ? lane : nu - 1;
+      const float q = S.qpos[(size_t)env * nq + iq];
+      const float v = S.qvel[(size_t)env * nv + iv], w = S.qacc_warmstart[(size_t)env * nv + iv];
+      const float* csrc = (MODE == MODE_ENV_STEP || (MODE == MODE_STEP && P.in_ctrl)) ? P.in_ctrl : S.ctrl;
+      float c = csrc[(size_t)env * nu + iu];
+      const float t = S.time[env];
+      float ax = 0.f, sgn = 1.f;
+      int perm = iu;
+      if (MODE == MODE_ENV_STEP) {
+        const int ia = lane < MJL_AUX_DIM ? lane : MJL_AUX_DIM - 1;
+        ax = S.aux[(size_t)env * MJL_AUX_DIM + ia];
+        perm = P.env->act_perm[iu];
+        sgn = P.env->act_sign[iu];
+      }
+      if (lane < nq) W->qpos[lane] = q;
+      if (lane < nv) { W->qvel[lane] = v; W->qacc_ws[lane] = w; }
+      if (lane == 0) W->sc[SC_TIME] = t;
+      if (MODE == MODE_ENV_STEP) {  // flip + clip the action (envs.py:335-344): act[perm[j]] from lane perm[j]
+        if (lane < MJL_AUX_DIM) aux[lane] = ax;
+        const bool flip = rdlane(ax, 0) > 0.5f;
+        const float ap = __shfl(c, perm);
+        c = fminf(fmaxf(flip ? ap * sgn : c, -1.f), 1.f);
+        if (lane == 0) W->sc[SC_FLIP] = ax;
+      }
+      if (lane < nu) W->ctrl[lane] = c;
     }
     SYNC();
-    if (MODE == MODE_ENV_STEP) {  // flip + clip the action (envs.py:335-344)
-      const mjlEnvConfig* c = P.env;
-      bool flip = aux[0] > 0.5f;
-      if (lane < nu) {
-        float a = flip ? P.in_ctrl[(size_t)env * nu + c->act_perm[lane]] * c->act_sign[lane]
-                       : P.in_ctrl[(size_t)env * nu + lane];
-        W->ctrl[lane] = fminf(fmaxf(a, -1.f), 1.f);
-      }
-      if (lane == 0) W->sc[SC_FLIP] = aux[0];
-      SYNC();
-    }
     forward<D>(m, W, A.scratch_env, A.gmax_efc, A.gmax_con, A.force_global, lane, kp);
     if (MODE != MODE_FORWARD) integrate<D>(m, W, lane);
     STAMP(8, lane);
