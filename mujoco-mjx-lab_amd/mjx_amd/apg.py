@@ -179,11 +179,11 @@ class APGTrainer:
             gas[t] = ga
         torch.autograd.backward(self.policy(on_all.reshape(H * B, w)), grad_tensors=torch.cat(gas))
         dropped = torch.stack([dropped_e.sum(), nonfinite[0]])  # (forward guard, reverse guard)
-        return loss.detach(), (rfin.mean(1).sum() / H).detach(), o_all, dropped
+        return loss.detach(), (rfin.mean(1).sum() / H).detach(), (o_all, snap), dropped
 
     def _loss_and_grad_torch(self, use_norm: bool, per_step_param_grad: bool = False, graph: bool = False):
-        """One rollout + backward. Returns (loss, mean reward, obs trajectory, envs dropped as
-        non-finite); grads in .grad.
+        """One rollout + backward. Returns (loss, mean reward, (obs trajectory [H, B, nq + nv], in-loss
+        mask [H, B]: the env was alive at that step), envs dropped as non-finite); grads in .grad.
 
         An env whose state or reward turns non-finite, or whose max |qvel| passes cfg.diverge_qvel,
         is treated as terminated from that step on (its reward at that step is dropped); an env whose
@@ -201,7 +201,7 @@ class APGTrainer:
         alive = torch.ones(B, dtype=torch.bool, device=self.device)
         dropped = torch.zeros((), device=self.device)
         rev_dropped = torch.zeros((), device=self.device)
-        obs_traj = []
+        obs_traj, in_loss = [], []
         for _ in range(H):
             tape.append(env.get_state())
             o, on = self._obs(use_norm, alive)
@@ -210,6 +210,7 @@ class APGTrainer:
             obs_leaves.append(o)
             acts.append(a)
             obs_traj.append(o.detach())
+            in_loss.append(alive.clone())
             _, r, te, tr = env.step(a.detach(), auto_reset=False)
             if disc is None:
                 disc, ret, rsum = torch.ones_like(r), torch.zeros_like(r), torch.zeros_like(r[0])
@@ -274,7 +275,7 @@ class APGTrainer:
         if not per_step_param_grad:
             torch.autograd.backward(self.policy(torch.cat(pol_in)), grad_tensors=torch.cat(gas))
         dropped = torch.stack([dropped.to(torch.float32), (nonfinite[0] if guarded else rev_dropped).to(torch.float32)])
-        return loss.detach(), (rsum / H).detach(), torch.stack(obs_traj), dropped
+        return loss.detach(), (rsum / H).detach(), (torch.stack(obs_traj), torch.stack(in_loss)), dropped
 
     def update(self, step: int) -> dict:
         cfg = self.cfg
@@ -296,8 +297,12 @@ class APGTrainer:
         _set_grads(params, g)
         self.opt.step()
         if cfg.normalize_observations and step % cfg.rms_update_every == 0:
-            flat = obs_traj.reshape(-1, obs_traj.shape[-1])
-            self.rms.update(flat[torch.isfinite(flat).all(1)], self.dist)
+            obs, in_loss = obs_traj
+            flat = obs.reshape(-1, obs.shape[-1])
+            keep = torch.isfinite(flat).all(1)
+            if cfg.rms_in_loss_only:
+                keep = keep & in_loss.reshape(-1).bool()
+            self.rms.update(flat[keep], self.dist)
         if self.device.type == "cuda":
             torch.cuda.synchronize(self.device)
         dt = max(time.time() - t0, 1e-9)

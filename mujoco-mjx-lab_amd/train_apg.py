@@ -53,6 +53,9 @@ def main():
                     help="solver derivative: unrolled = jax.grad through the iterations (default with --solver cg), "
                          "implicit = at the converged active set (default with --solver model)")
     ap.add_argument("--results-dir", default=None)
+    ap.add_argument("--rms-all-obs", action="store_true",
+                    help="observation statistics from every rollout observation (train_apg.py:290-292), "
+                         "not only those of envs still in the loss (APGConfig.rms_in_loss_only)")
     a = ap.parse_args()
 
     cfg = APGConfig()
@@ -63,6 +66,8 @@ def main():
         cfg.total_steps = a.steps
     if a.results_dir:
         cfg.results_dir = a.results_dir
+    if a.rms_all_obs:
+        cfg.rms_in_loss_only = False
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank, local = int(os.environ.get("RANK", "0")), int(os.environ.get("LOCAL_RANK", "0"))

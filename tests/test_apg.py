@@ -109,6 +109,38 @@ def test_update_clips_global_norm():
     assert any(not torch.equal(a, b) for a, b in zip(before, tr.policy.parameters()))
 
 
+class _WideStartEnv(DiffPointEnv):
+    """DiffPointEnv whose resets start some envs past the termination bound (|q_z| > 1.5)."""
+
+    def reset(self):
+        super().reset()
+        self.q = self.q * 6.0
+
+
+@pytest.mark.parametrize("in_loss_only", [True, False])
+def test_obs_statistics_from_in_loss_observations(in_loss_only):
+    """cfg.rms_in_loss_only: the running observation statistics take only the observations of envs
+    still in the loss at that step; a terminated env's later (here: diverged) observations stay out."""
+    from mjx_amd.ppo import RunningMeanStd
+    cfg = _cfg(rms_in_loss_only=in_loss_only)
+    tr = apg.APGTrainer(cfg, _WideStartEnv(cfg.batch_size, 2), device="cpu")
+    tr.policy.double()
+    out = tr.loss_and_grad(use_norm=False)
+    obs, mask = out[2]
+    assert obs.shape == (cfg.horizon, cfg.batch_size, 6) and mask.shape == (cfg.horizon, cfg.batch_size)
+    assert bool(mask[0].all()) and 0 < int(mask.sum()) < mask.numel()
+    obs = obs.clone()
+    obs[~mask.bool()] = 1e12  # a fallen env diverging after it left the loss
+    tr.loss_and_grad = lambda use_norm, per_step_param_grad=False: (out[0], out[1], (obs, mask), out[3])
+    tr.update(0)
+    keep = mask.reshape(-1).bool() if in_loss_only else torch.ones(mask.numel(), dtype=torch.bool)
+    ref = RunningMeanStd(6, torch.device("cpu"))
+    ref.update(obs.reshape(-1, 6)[keep])
+    torch.testing.assert_close(tr.rms.mean, ref.mean)
+    torch.testing.assert_close(tr.rms.var, ref.var)
+    assert (float(tr.rms.var.max()) < 1e3) == in_loss_only
+
+
 def _port():
     s = socket.socket()
     s.bind(("127.0.0.1", 0))
