@@ -372,6 +372,12 @@ int mjl_apg_obs_vjp(int nenv, int nq, int nv, const float* o, const uint8_t* ali
  * scratch floats mjl_colsum needs (0: none, scratch may be NULL). */
 long long mjl_colsum_scratch(int n, int d);
 int mjl_colsum(const float* x, int n, int d, float* scratch, float* out, void* stream);
+/* Backward of y = tanh(z) for a row-major [n, d] layer output (the PPO update's hidden layers; replaces
+ * torch's tanh_backward + the bias gradient's column sum, src/networks.py:55-61 under jax.grad in
+ * train_ppo.py:204-231): dz = g (1 - y^2), colsum_out[d] = dz.sum(0) in a fixed order (scratch: as
+ * mjl_colsum). d % 4 == 0; g, y, dz, scratch and colsum_out 16-byte aligned. */
+int mjl_tanh_bwd_colsum(const float* g, const float* y, int n, int d, float* dz, float* scratch, float* colsum_out,
+                        void* stream);
 
 /* PPO update losses (train_ppo.py:204-220), forward and gradient in one pass, deterministic.
  * mjl_ppo_surrogate: loss = -mean_i min(r_i an_i, clip(r_i, 1 - clip_eps, 1 + clip_eps) an_i)

@@ -984,6 +984,28 @@ extern "C" int mjl_colsum(const float* x, int n, int d, float* scratch, float* o
   return MJL_OK;
 }
 
+extern "C" int mjl_tanh_bwd_colsum(const float* g, const float* y, int n, int d, float* dz, float* scratch,
+                                   float* colsum_out, void* stream) {
+  if (!g || !y || !dz || !colsum_out || n <= 0 || d <= 0) return fail(MJL_ERR_ARG, "bad argument");
+  if (d % 4 || ((uintptr_t)g | (uintptr_t)y | (uintptr_t)dz | (uintptr_t)colsum_out) % 16)
+    return fail(MJL_ERR_ARG, "tanh_bwd_colsum: d divisible by 4 and 16-byte aligned rows expected");
+  hipStream_t s = (hipStream_t)stream;
+  const ColsumPlan p(n, d);
+  if (p.R > 1 && (!scratch || (uintptr_t)scratch % 16))
+    return fail(MJL_ERR_ARG, "tanh_bwd_colsum needs mjl_colsum_scratch(n, d) floats of 16-byte aligned scratch");
+  const int dq = d / 4 < 64 ? d / 4 : 64;
+  const unsigned tiles1 = (unsigned)((d / 4 + dq - 1) / dq);
+  hipLaunchKernelGGL(tanh_bwd_colsum_kernel, dim3(tiles1, (unsigned)p.R), dim3(256), 0, s, g, y, n, d, dq, p.chunk, dz,
+                     p.R > 1 ? scratch : colsum_out);
+  HIPCHK(hipGetLastError());
+  if (p.R > 1) {
+    const unsigned tiles2 = (unsigned)((d + p.dc2 - 1) / p.dc2);
+    hipLaunchKernelGGL(colsum_kernel, dim3(tiles2, 1), dim3(256), 0, s, scratch, p.R, d, p.dc2, p.R, colsum_out);
+    HIPCHK(hipGetLastError());
+  }
+  return MJL_OK;
+}
+
 // jax.random.split over a batch of keys (train_ppo.py:132,150: random.split(rng); random.split(key, num_envs))
 __global__ void prng_split_kernel(const uint32_t* __restrict__ keys, int n, int num, int mode, uint32_t* __restrict__ out) {
   const int t = blockIdx.x * blockDim.x + threadIdx.x;

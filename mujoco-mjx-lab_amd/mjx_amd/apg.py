@@ -56,6 +56,9 @@ class APGTrainer:
         self.rank = dist.get_rank() if dist is not None else 0
         self.world = dist.get_world_size() if dist is not None else 1
         self.device = torch.device(device)
+        if self.device.type == "cuda":
+            from .tunable import use_tuned_gemms
+            use_tuned_gemms(self.device)
         self.obs_dim = env.nq + env.nv
         g = torch.Generator().manual_seed(int(cfg.seed))
         self.policy = APGPolicy(self.obs_dim, env.act_dim, cfg.hidden_size, cfg.hidden_depth, None, g).to(self.device)

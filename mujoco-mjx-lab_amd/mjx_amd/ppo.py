@@ -75,10 +75,66 @@ class _SplitKLinear(torch.autograd.Function):
         return gx, gw, gb, None
 
 
+def tanh_bwd_colsum_native(gy: torch.Tensor, y: torch.Tensor):
+    """(dz, db) = (gy (1 - y^2), dz.sum(0)) for y = tanh(z) [n, d] in one pass (mjl_tanh_bwd_colsum) plus
+    the column sum's small second stage: torch's tanh_backward and then a column sum re-reading dz."""
+    from ._lib import check, lib
+    n, d = y.shape
+    dz = torch.empty_like(y)
+    db = torch.empty(d, dtype=torch.float32, device=y.device)
+    st = torch.cuda.current_stream(y.device).cuda_stream
+    ns = int(lib().mjl_colsum_scratch(n, d))
+    scratch = None
+    if ns:
+        key = (y.device, ns, st)
+        scratch = _COLSUM_SCRATCH.get(key)
+        if scratch is None:
+            scratch = _COLSUM_SCRATCH[key] = torch.empty(ns, dtype=torch.float32, device=y.device)
+    check(lib().mjl_tanh_bwd_colsum(gy.data_ptr(), y.data_ptr(), n, d, dz.data_ptr(),
+                                    scratch.data_ptr() if scratch is not None else None, db.data_ptr(), st))
+    return dz, db
+
+
+class _TanhSplitKLinear(torch.autograd.Function):
+    """y = tanh(x Wᵀ + b) as _SplitKLinear + tanh, whose backward forms dz = dy (1 - y²) and the bias
+    gradient's column sums in one pass over dy and y (tanh_bwd_colsum_native) instead of torch's
+    tanh_backward followed by a column sum that reads dz again."""
+
+    @staticmethod
+    def forward(ctx, x, w, b, splits):
+        y = torch.addmm(b, x, w.t()).tanh_()
+        ctx.save_for_backward(x, w, y)
+        ctx.splits = splits
+        return y
+
+    @staticmethod
+    def backward(ctx, gy):
+        x, w, y = ctx.saved_tensors
+        s, n = ctx.splits, x.shape[0]
+        dz, gb = tanh_bwd_colsum_native(gy.contiguous(), y)
+        gx = dz @ w if ctx.needs_input_grad[0] else None
+        gw = torch.bmm(dz.reshape(s, n // s, -1).transpose(1, 2), x.reshape(s, n // s, -1)).sum(0)
+        return gx, gw, gb, None
+
+
 SPLIT_ROWS = 2048  # rows per split of the split-K weight gradient (32 splits at a 65,536 minibatch)
 
 
 UPDATE_MIN_ROWS = 4096  # minibatches of at least this many rows take the native / split-K update path
+
+
+# tanh layers of the update on _TanhSplitKLinear (MJL_TANH_FUSED=0: torch's tanh_backward + colsum)
+TANH_FUSED = os.environ.get("MJL_TANH_FUSED", "1") == "1"
+
+
+def _tanh_linear(lin: nn.Linear, x: torch.Tensor) -> torch.Tensor:
+    """tanh(Dense(x)); the update's layers (as _linear's split-K condition, width % 4 == 0) fuse the
+    tanh backward with the bias gradient's column sum (_TanhSplitKLinear)."""
+    n = x.shape[0] if x.dim() == 2 else 0
+    if (TANH_FUSED and x.is_cuda and torch.is_grad_enabled() and n >= UPDATE_MIN_ROWS and n % SPLIT_ROWS == 0
+            and lin.out_features % 4 == 0 and x.dtype == torch.float32):
+        return _TanhSplitKLinear.apply(x, lin.weight, lin.bias, min(64, n // SPLIT_ROWS))
+    return torch.tanh(_linear(lin, x))
 
 
 def _linear(lin: nn.Linear, x: torch.Tensor) -> torch.Tensor:
@@ -198,8 +254,15 @@ class MLP(nn.Module):
                 acts = acts[:-1] + (1,)
             params = [t for lin in self.layers for t in (lin.weight, lin.bias)]
             return _FusedMLP.apply(x, acts, *params)
-        for lin, a in zip(self.layers, self.acts):
-            x = ACTIVATIONS.get(a, torch.tanh)(_linear(lin, x))
+        last = len(self.layers) - 1
+        for l, (lin, a) in enumerate(zip(self.layers, self.acts)):
+            act = ACTIVATIONS.get(a, torch.tanh)
+            if act is torch.tanh:
+                x = _tanh_linear(lin, x)
+            elif l == last and out_tanh and a in ("linear", "none"):  # the mean's tanh on the last Dense
+                return _tanh_linear(lin, x)
+            else:
+                x = act(_linear(lin, x))
         return torch.tanh(x) if out_tanh else x
 
 
@@ -752,6 +815,9 @@ class PPOUpdater:
         self.pp, self.vp = list(policy.parameters()), list(value.parameters())
         dev = self.pp[0].device
         self.cuda = dev.type == "cuda"
+        if self.cuda:
+            from .tunable import use_tuned_gemms
+            use_tuned_gemms(dev)
         self.graph_ok = (bool(use_graph) and self.cuda and isinstance(opt_p, NativeAdam)
                          and isinstance(opt_v, NativeAdam))
         # the value net's forward / backward (and, single-process, its Adam step) on a second stream beside

@@ -83,9 +83,10 @@ def test_fused_mlp_matches_torch_autograd(net):
         m = ppo.ValueNet(54, cfg.value_hidden_layer_specs, gen).cuda()
     g = torch.Generator(device="cuda").manual_seed(4)
     x = torch.randn((65536, 54), generator=g, device="cuda")
-    res, prev = {}, ppo.FUSED_MLP
+    res, prev, prev_t = {}, ppo.FUSED_MLP, ppo.TANH_FUSED
     for fused in (True, False):
         ppo.FUSED_MLP = fused
+        ppo.TANH_FUSED = False  # the reference: nn.Linear + torch.tanh autograd
         try:
             for p in m.parameters():
                 p.grad = None
@@ -95,9 +96,56 @@ def test_fused_mlp_matches_torch_autograd(net):
             (y * w).sum().backward()
             res[fused] = (y.detach().clone(), [p.grad.clone() if p.grad is not None else None for p in m.parameters()])
         finally:
-            ppo.FUSED_MLP = prev
+            ppo.FUSED_MLP, ppo.TANH_FUSED = prev, prev_t
     torch.testing.assert_close(res[True][0], res[False][0], rtol=1e-5, atol=1e-5)
     for a, b in zip(res[True][1], res[False][1]):
         if b is None:
             continue
+        torch.testing.assert_close(a, b, rtol=1e-4, atol=1e-4 * float(b.abs().max()))
+
+
+@pytest.mark.parametrize("n,d", [(65536, 256), (8192, 256), (4133, 256), (300, 64), (129, 8)])
+def test_tanh_bwd_colsum_matches_float64(n, d):
+    """mjl_tanh_bwd_colsum: dz = g (1 - y^2) to an ulp (the kernel may contract 1 - y y into an fma),
+    its column sums (fixed order) within fp32 summation error, bit-identical run to run."""
+    g = torch.Generator(device="cuda").manual_seed(n + d)
+    gy = torch.randn((n, d), generator=g, device="cuda")
+    y = torch.tanh(torch.randn((n, d), generator=g, device="cuda"))
+    dz, db = ppo.tanh_bwd_colsum_native(gy, y)
+    torch.testing.assert_close(dz.double(), gy.double() * (1 - y.double() ** 2), rtol=1e-6, atol=1e-7)
+    zr = gy.double() * (1 - y.double() ** 2)
+    torch.testing.assert_close(db.double(), zr.sum(0), rtol=0, atol=1e-6 * float(zr.abs().sum(0).max()))
+    dz2, db2 = ppo.tanh_bwd_colsum_native(gy, y)
+    assert torch.equal(dz, dz2) and torch.equal(db, db2)
+
+
+@pytest.mark.parametrize("net", ["policy", "value"])
+def test_tanh_fused_layers_match_torch_autograd(net):
+    """The update's default path (_TanhSplitKLinear: tanh backward + bias-gradient column sum in one
+    pass, split-K weight gradient) against nn.Linear + torch.tanh autograd at a 65,536-row minibatch."""
+    cfg = reference_ppo_config()
+    gen = torch.Generator().manual_seed(3)
+    if net == "policy":
+        m = ppo.GaussianPolicy(54, 21, cfg.policy_hidden_layer_specs, 0.0, gen).cuda()
+    else:
+        m = ppo.ValueNet(54, cfg.value_hidden_layer_specs, gen).cuda()
+    x = torch.randn((65536, 54), generator=torch.Generator(device="cuda").manual_seed(4), device="cuda")
+    res, prev = {}, (ppo.FUSED_MLP, ppo.TANH_FUSED, ppo.UPDATE_MIN_ROWS)
+    for mode in ("tanh_fused", "torch"):
+        ppo.FUSED_MLP = False
+        ppo.TANH_FUSED = mode == "tanh_fused"
+        ppo.UPDATE_MIN_ROWS = 4096 if mode == "tanh_fused" else 1 << 30  # torch: plain nn.Linear
+        try:
+            for p in m.parameters():
+                p.grad = None
+            out = m(x)
+            y = out[0] if net == "policy" else out
+            w = torch.randn(y.shape, generator=torch.Generator(device="cuda").manual_seed(5), device="cuda")
+            (y * w).sum().backward()
+            res[mode] = (y.detach().clone(), [p.grad.clone() for p in m.parameters() if p.grad is not None])
+        finally:
+            ppo.FUSED_MLP, ppo.TANH_FUSED, ppo.UPDATE_MIN_ROWS = prev
+    torch.testing.assert_close(res["tanh_fused"][0], res["torch"][0], rtol=1e-5, atol=1e-5)
+    assert len(res["tanh_fused"][1]) == len(res["torch"][1])
+    for a, b in zip(res["tanh_fused"][1], res["torch"][1]):
         torch.testing.assert_close(a, b, rtol=1e-4, atol=1e-4 * float(b.abs().max()))
