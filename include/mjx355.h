@@ -378,6 +378,12 @@ int mjl_colsum(const float* x, int n, int d, float* scratch, float* out, void* s
  * mjl_colsum). d % 4 == 0; g, y, dz, scratch and colsum_out 16-byte aligned. */
 int mjl_tanh_bwd_colsum(const float* g, const float* y, int n, int d, float* dz, float* scratch, float* colsum_out,
                         void* stream);
+/* out[e] = sum over s < ns of x[s * m + e] (slices summed in order: the split-K weight gradient's sum
+ * over its batched GEMMs, in place of torch's sum(0)); m % 4 == 0, 16-byte aligned. */
+int mjl_slice_sum(const float* x, int ns, long long m, float* out, void* stream);
+/* x = tanh(x) elementwise in place (the update's hidden-layer activations, src/networks.py:55-61);
+ * n % 4 == 0, 16-byte aligned. */
+int mjl_tanh_inplace(float* x, long long n, void* stream);
 
 /* PPO update losses (train_ppo.py:204-220), forward and gradient in one pass, deterministic.
  * mjl_ppo_surrogate: loss = -mean_i min(r_i an_i, clip(r_i, 1 - clip_eps, 1 + clip_eps) an_i)
@@ -390,7 +396,7 @@ int mjl_tanh_bwd_colsum(const float* g, const float* y, int n, int d, float* dz,
  *   mjl_ppo_loss_scratch(n, A) floats (mjl_mse needs n / 256 + 1). A <= 32.
  * mjl_gather_rows: dst_k[r, :] = src_k[idx[r], :] for narr <= 5 row-major float arrays of nsrc rows
  *   and cols[k] columns (the minibatch gather of train_ppo.py:237-241), idx int64 [n]; one launch;
- *   an index outside [0, nsrc) gives a NaN row. */
+ *   an index outside [0, nsrc) gives a NaN row; n x (total columns) must be below 2^31. */
 long long mjl_ppo_loss_scratch(int n, int A);
 int mjl_ppo_surrogate(const float* mean, const float* log_std, const float* act, const float* old_logp,
                       const float* adv, const float* adv_stats, int n, int A, float clip_eps, float ent_coef,

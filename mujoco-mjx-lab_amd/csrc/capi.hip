@@ -1006,6 +1006,27 @@ extern "C" int mjl_tanh_bwd_colsum(const float* g, const float* y, int n, int d,
   return MJL_OK;
 }
 
+extern "C" int mjl_slice_sum(const float* x, int ns, long long m, float* out, void* stream) {
+  if (!x || !out || ns <= 0 || m <= 0) return fail(MJL_ERR_ARG, "bad argument");
+  if (m % 4 || ((uintptr_t)x | (uintptr_t)out) % 16)
+    return fail(MJL_ERR_ARG, "slice_sum: slice length divisible by 4 and 16-byte aligned buffers expected");
+  const long long q = m / 4;
+  hipLaunchKernelGGL(slice_sum_kernel, dim3((unsigned)((q + 255) / 256)), dim3(256), 0, (hipStream_t)stream, x, ns, m,
+                     out);
+  HIPCHK(hipGetLastError());
+  return MJL_OK;
+}
+
+extern "C" int mjl_tanh_inplace(float* x, long long n, void* stream) {
+  if (!x || n < 0) return fail(MJL_ERR_ARG, "bad argument");
+  if (n % 4 || (uintptr_t)x % 16) return fail(MJL_ERR_ARG, "tanh_inplace: length divisible by 4, 16-byte aligned");
+  if (n == 0) return MJL_OK;
+  const long long q = n / 4;
+  hipLaunchKernelGGL(tanh_inplace_kernel, dim3((unsigned)((q + 255) / 256)), dim3(256), 0, (hipStream_t)stream, x, q);
+  HIPCHK(hipGetLastError());
+  return MJL_OK;
+}
+
 // jax.random.split over a batch of keys (train_ppo.py:132,150: random.split(rng); random.split(key, num_envs))
 __global__ void prng_split_kernel(const uint32_t* __restrict__ keys, int n, int num, int mode, uint32_t* __restrict__ out) {
   const int t = blockIdx.x * blockDim.x + threadIdx.x;
@@ -1098,7 +1119,7 @@ extern "C" int mjl_ppo_surrogate(const float* mean, const float* log_std, const 
   if (!adv_stats) hipLaunchKernelGGL(adv_stats_kernel, dim3(nb), dim3(kLossT), 0, s, adv, n, adv_part);
   hipLaunchKernelGGL(ppo_surrogate_kernel, dim3(nb), dim3(kLossT), 0, s, mean, log_std, act, old_logp, adv, n, A,
                      clip_eps, adv_part, nb, adv_stats, g_mean, part);
-  hipLaunchKernelGGL(ppo_surrogate_final_kernel, dim3(1), dim3(64), 0, s, part, nb, n, A, log_std, ent_coef, loss,
+  hipLaunchKernelGGL(ppo_surrogate_final_kernel, dim3(A + 1), dim3(64), 0, s, part, nb, n, A, log_std, ent_coef, loss,
                      g_log_std);
   HIPCHK(hipGetLastError());
   return MJL_OK;
@@ -1128,6 +1149,7 @@ extern "C" int mjl_gather_rows(const long long* idx, int n, long long nsrc, int 
   }
   const long long work = (long long)n * tot;
   if (work == 0) return MJL_OK;
+  if (work + 255 >= (1ll << 31)) return fail(MJL_ERR_ARG, "gather_rows: rows x total columns must be below 2^31");
   hipLaunchKernelGGL(gather_rows_kernel, dim3((unsigned)((work + 255) / 256)), dim3(256), 0, (hipStream_t)stream, idx,
                      n, nsrc, g);
   HIPCHK(hipGetLastError());

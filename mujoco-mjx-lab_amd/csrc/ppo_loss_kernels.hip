@@ -38,16 +38,40 @@ __global__ __launch_bounds__(kLossT) void adv_stats_kernel(const float* __restri
   if (threadIdx.x == 0) { part[3 * blockIdx.x] = cnt; part[3 * blockIdx.x + 1] = mu; part[3 * blockIdx.x + 2] = m2; }
 }
 
-// the minibatch's advantage mean and population std from the block partials (Chan et al. pairwise
-// merge in block order; every caller reduces the same partials the same way)
-__device__ __forceinline__ void adv_merge(const float* __restrict__ part, int nb, float& mu, float& sd) {
+// sum over the 64 lanes of a wave (xor butterfly: every lane ends with the same, fixed-order sum)
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
+  return v;
+}
+
+// Chan et al. pairwise merge of (count, mean, M2) partials
+__device__ __forceinline__ void chan_merge(float& c, float& m, float& M2, float cb, float mb, float M2b) {
+  if (cb == 0.f) return;
+  const float tot = c + cb, d = mb - m;
+  m = m + d * (cb / tot);
+  M2 = M2 + M2b + d * d * (c * cb / tot);
+  c = tot;
+}
+
+// the minibatch's advantage mean and population std from the block partials, by one wave: lane l
+// merges partials l, l + 64, ... in order, then the lanes pairwise by a fixed butterfly (every caller
+// reduces the same partials the same way); valid in every lane
+__device__ __forceinline__ void adv_merge_wave(const float* __restrict__ part, int nb, int lane, float& mu, float& sd) {
   float c = 0.f, m = 0.f, M2 = 0.f;
-  for (int b = 0; b < nb; b++) {
-    const float cb = part[3 * b], mb = part[3 * b + 1], M2b = part[3 * b + 2];
-    const float tot = c + cb, d = mb - m;
-    m = m + d * (cb / tot);
-    M2 = M2 + M2b + d * d * (c * cb / tot);
-    c = tot;
+  for (int b = lane; b < nb; b += 64) chan_merge(c, m, M2, part[3 * b], part[3 * b + 1], part[3 * b + 2]);
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) {
+    const float cb = __shfl_xor(c, off), mb = __shfl_xor(m, off), M2b = __shfl_xor(M2, off);
+    // the lower lane of each pair merges (its, partner's); the upper adopts the lower's result so the
+    // pair holds one value: merge(a, b) is not symmetric in rounding
+    if (lane & off) {
+      float c2 = cb, m2 = mb, M22 = M2b;
+      chan_merge(c2, m2, M22, c, m, M2);
+      c = c2; m = m2; M2 = M22;
+    } else {
+      chan_merge(c, m, M2, cb, mb, M2b);
+    }
   }
   mu = m;
   sd = sqrtf(M2 / c);
@@ -55,35 +79,47 @@ __device__ __forceinline__ void adv_merge(const float* __restrict__ part, int nb
 
 // per row: logp = -1/2 (sum_j (a - m)^2 e^(-2 s_j) + sum_j (2 s_j + log 2 pi)), ratio = exp(logp -
 // old), surr = min(ratio an, clip(ratio, 1 - eps, 1 + eps) an) with an the normalised advantage;
-// d(-mean surr)/d mean written per row, block partials of sum surr and of d/d s_j
+// d(-mean surr)/d mean written per row, block partials of sum surr and of d/d s_j. The block's rows of
+// act and mean (contiguous: rows x A floats) come in through LDS with coalesced loads, and g_mean goes
+// out the same way (a thread per row striding A floats touched 64 lines per load); the partials are
+// per-wave butterfly sums, then the block's waves in order through LDS (one barrier for all A + 1).
 __global__ __launch_bounds__(kLossT) void ppo_surrogate_kernel(
     const float* __restrict__ mean, const float* __restrict__ log_std, const float* __restrict__ act,
     const float* __restrict__ old_logp, const float* __restrict__ adv, int n, int A, float clip_eps,
     const float* __restrict__ adv_part, int nb, const float* __restrict__ adv_stats, float* __restrict__ gmean,
     float* __restrict__ part) {
-  __shared__ float red[kLossT];
-  __shared__ float ivs[kLossMaxA], lss;
+  constexpr int NW = kLossT / 64;
+  __shared__ float sd[kLossT * kLossMaxA];  // a - m of the block's rows, row-major
+  __shared__ float sdl[kLossT];             // d logp per row
+  __shared__ float wred[NW][kLossMaxA + 1];
+  __shared__ float ivs[kLossMaxA], lsd[kLossMaxA], lss;
   __shared__ float mu_s, sd_s;
-  const int t = threadIdx.x, i = blockIdx.x * kLossT + t;
-  if (t < A) ivs[t] = expf(-2.f * log_std[t]);
-  if (t == 0) {
-    float s = 0.f;
-    for (int j = 0; j < A; j++) s += 2.f * log_std[j] + kLog2Pi;
-    lss = s;
-    float mu, sd;
-    if (adv_stats) { mu = adv_stats[0]; sd = adv_stats[1]; }  // global statistics (data-parallel)
-    else adv_merge(adv_part, nb, mu, sd);
-    mu_s = mu; sd_s = sd;
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6, r0 = blockIdx.x * kLossT, i = r0 + t;
+  const int rows = min(kLossT, n - r0), cnt = rows * A;
+  const size_t base = (size_t)r0 * A;
+  for (int e = t; e < cnt; e += kLossT) sd[e] = act[base + e] - mean[base + e];
+  if (t < A) {
+    const float ls = log_std[t];
+    lsd[t] = ls;
+    ivs[t] = expf(-2.f * ls);
+  }
+  if (w == 1) {  // the advantage statistics, beside the staging loads
+    float mu, sdv;
+    if (adv_stats) { mu = adv_stats[0]; sdv = adv_stats[1]; }  // global statistics (data-parallel)
+    else adv_merge_wave(adv_part, nb, lane, mu, sdv);
+    if (lane == 0) { mu_s = mu; sd_s = sdv; }
   }
   __syncthreads();
-  const bool in = i < n;
-  const float* ar = act + (size_t)(in ? i : 0) * A;
-  const float* mr = mean + (size_t)(in ? i : 0) * A;
-  float qs = 0.f;
-  for (int j = 0; j < A; j++) {
-    const float d = ar[j] - mr[j];
-    qs += d * d * ivs[j];
+  if (t == 0) {
+    float s = 0.f;
+    for (int j = 0; j < A; j++) s += 2.f * lsd[j] + kLog2Pi;
+    lss = s;
   }
+  __syncthreads();
+  const bool in = t < rows;
+  const float* dr = sd + (in ? t : 0) * A;
+  float qs = 0.f;
+  for (int j = 0; j < A; j++) qs += dr[j] * dr[j] * ivs[j];
   float surr = 0.f, dlogp = 0.f;
   if (in) {
     const float logp = -0.5f * (qs + lss);
@@ -99,33 +135,43 @@ __global__ __launch_bounds__(kLossT) void ppo_surrogate_kernel(
     const float w2 = t2 < t1 ? 1.f : (t1 == t2 ? 0.5f : 0.f);
     const float dratio = (-1.f / (float)n) * (w1 * an + ((ratio >= lo && ratio <= hi) ? w2 * an : 0.f));
     dlogp = dratio * ratio;
-    for (int j = 0; j < A; j++) gmean[(size_t)i * A + j] = dlogp * (ar[j] - mr[j]) * ivs[j];
   }
-  const float ssum = block_sum(surr, red);
-  if (t == 0) part[(size_t)blockIdx.x * (A + 1)] = ssum;
+  sdl[t] = dlogp;
+  const float ssum = wave_sum(surr);
+  if (lane == 0) wred[w][0] = ssum;
   for (int j = 0; j < A; j++) {  // d logp / d s_j = q_j - 1
-    const float d = ar[j] - mr[j];
-    const float c = block_sum(in ? dlogp * (d * d * ivs[j] - 1.f) : 0.f, red);
-    if (t == 0) part[(size_t)blockIdx.x * (A + 1) + 1 + j] = c;
+    const float d = dr[j];
+    const float c = wave_sum(in ? dlogp * (d * d * ivs[j] - 1.f) : 0.f);
+    if (lane == 0) wred[w][1 + j] = c;
+  }
+  __syncthreads();
+  for (int e = t; e < cnt; e += kLossT) {
+    const int r = e / A, j = e - r * A;
+    gmean[base + e] = sdl[r] * sd[e] * ivs[j];
+  }
+  if (t <= A) {
+    float acc = wred[0][t];
+#pragma unroll
+    for (int k = 1; k < NW; k++) acc += wred[k][t];
+    part[(size_t)blockIdx.x * (A + 1) + t] = acc;
   }
 }
 
 // loss = -sum surr / n - ent_coef * entropy; d loss / d s_j = sum of the partials - ent_coef / A
-// (entropy = 0.5 sum_j (1 + log 2 pi + 2 s_j) / A, train_ppo.py:215)
+// (entropy = 0.5 sum_j (1 + log 2 pi + 2 s_j) / A, train_ppo.py:215). One wave per column of the
+// [nb, A + 1] partials (blockIdx.x = column): lane l sums rows l, l + 64, ... in order, then wave_sum.
 __global__ __launch_bounds__(64) void ppo_surrogate_final_kernel(const float* __restrict__ part, int nb, int n, int A,
                                                                  const float* __restrict__ log_std, float ent_coef,
                                                                  float* __restrict__ loss, float* __restrict__ glog_std) {
-  const int t = threadIdx.x;
-  if (t <= A) {
-    float s = 0.f;
-    for (int b = 0; b < nb; b++) s += part[(size_t)b * (A + 1) + t];
-    if (t == 0) {
-      float e = 0.f;
-      for (int j = 0; j < A; j++) e += 1.f + kLog2Pi + 2.f * log_std[j];
-      loss[0] = -s / (float)n - ent_coef * (0.5f * e / (float)A);
-    } else {
-      glog_std[t - 1] = s - ent_coef / (float)A;
-    }
+  const int lane = threadIdx.x, col = blockIdx.x;
+  float s = 0.f;
+  for (int b = lane; b < nb; b += 64) s += part[(size_t)b * (A + 1) + col];
+  s = wave_sum(s);
+  if (col == 0) {
+    const float e = wave_sum(lane < A ? 1.f + kLog2Pi + 2.f * log_std[lane] : 0.f);
+    if (lane == 0) loss[0] = -s / (float)n - ent_coef * (0.5f * e / (float)A);
+  } else if (lane == 0) {
+    glog_std[col - 1] = s - ent_coef / (float)A;
   }
 }
 
@@ -144,11 +190,44 @@ __global__ __launch_bounds__(kLossT) void mse_kernel(const float* __restrict__ v
   if (threadIdx.x == 0) part[blockIdx.x] = s;
 }
 __global__ __launch_bounds__(64) void mse_final_kernel(const float* __restrict__ part, int nb, int n, float* __restrict__ loss) {
-  if (threadIdx.x == 0) {
-    float s = 0.f;
-    for (int b = 0; b < nb; b++) s += part[b];
-    loss[0] = s / (float)n;
+  float s = 0.f;
+  for (int b = threadIdx.x; b < nb; b += 64) s += part[b];
+  s = wave_sum(s);
+  if (threadIdx.x == 0) loss[0] = s / (float)n;
+}
+
+// out[e] = sum_s x[s][e] over `ns` slices of `m` floats, slices in order (the split-K weight
+// gradient's sum over its batched GEMMs); float4 per thread, m % 4 == 0
+__global__ __launch_bounds__(256) void slice_sum_kernel(const float* __restrict__ x, int ns, long long m,
+                                                        float* __restrict__ out) {
+  const long long q = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (q * 4 >= m) return;
+  const float4* src = reinterpret_cast<const float4*>(x) + q;
+  const long long stride = m / 4;
+  float4 acc = src[0];
+  int s = 1;
+  for (; s + 3 < ns; s += 4) {
+    const float4 a = src[s * stride], b = src[(s + 1) * stride], c = src[(s + 2) * stride], d = src[(s + 3) * stride];
+    acc.x += a.x; acc.y += a.y; acc.z += a.z; acc.w += a.w;
+    acc.x += b.x; acc.y += b.y; acc.z += b.z; acc.w += b.w;
+    acc.x += c.x; acc.y += c.y; acc.z += c.z; acc.w += c.w;
+    acc.x += d.x; acc.y += d.y; acc.z += d.z; acc.w += d.w;
   }
+  for (; s < ns; s++) {
+    const float4 a = src[s * stride];
+    acc.x += a.x; acc.y += a.y; acc.z += a.z; acc.w += a.w;
+  }
+  reinterpret_cast<float4*>(out)[q] = acc;
+}
+
+// elementwise tanh in place, float4 (the update's forward activations; torch's tanh kernel ran at
+// ~4 TB/s on the [65,536, 256] layer outputs)
+__global__ __launch_bounds__(256) void tanh_inplace_kernel(float* __restrict__ x, long long n4) {
+  const long long q = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (q >= n4) return;
+  float4 v = reinterpret_cast<float4*>(x)[q];
+  v.x = tanhf(v.x); v.y = tanhf(v.y); v.z = tanhf(v.z); v.w = tanhf(v.w);
+  reinterpret_cast<float4*>(x)[q] = v;
 }
 
 // minibatch gather: dst_k[r] = src_k[idx[r]] for up to 5 row-major arrays of `cols_k` columns
@@ -160,12 +239,14 @@ struct GatherArgs {
 };
 __global__ __launch_bounds__(256) void gather_rows_kernel(const long long* __restrict__ idx, int n, long long nsrc,
                                                           GatherArgs g) {
-  const long long tid = (long long)blockIdx.x * blockDim.x + threadIdx.x;
-  int tot = 0;
-  for (int k = 0; k < g.narr; k++) tot += g.cols[k];
-  if (tid >= (long long)n * tot) return;
+  // 32-bit index math (the launcher checks n * total columns < 2^31): a 64-bit divide per element
+  // was most of this kernel's time
+  const unsigned tid = blockIdx.x * blockDim.x + threadIdx.x;
+  unsigned tot = 0;
+  for (int k = 0; k < g.narr; k++) tot += (unsigned)g.cols[k];
+  if (tid >= (unsigned)n * tot) return;
   const int r = (int)(tid / tot);
-  int c = (int)(tid % tot), k = 0;
+  int c = (int)(tid - (unsigned)r * tot), k = 0;
   while (c >= g.cols[k]) { c -= g.cols[k]; k++; }
   const long long s = idx[r];  // an index outside [0, nsrc) yields NaN rows, not an out-of-bounds read
   g.dst[k][(size_t)r * g.cols[k] + c] = (s >= 0 && s < nsrc) ? g.src[k][(size_t)s * g.cols[k] + c] : __builtin_nanf("");

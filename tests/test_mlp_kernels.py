@@ -149,3 +149,23 @@ def test_tanh_fused_layers_match_torch_autograd(net):
     assert len(res["tanh_fused"][1]) == len(res["torch"][1])
     for a, b in zip(res["tanh_fused"][1], res["torch"][1]):
         torch.testing.assert_close(a, b, rtol=1e-4, atol=1e-4 * float(b.abs().max()))
+
+
+@pytest.mark.parametrize("ns,shape", [(32, (256, 256)), (4, (256, 54)), (64, (21, 32)), (3, (1, 4))])
+def test_slice_sum_matches_ordered_sum(ns, shape):
+    """mjl_slice_sum: the slices added in order 0, 1, ... (bit-equal to that loop) and within fp32
+    summation error of the float64 sum."""
+    x = torch.randn((ns,) + shape, generator=torch.Generator(device="cuda").manual_seed(ns), device="cuda")
+    out = ppo.slice_sum_native(x)
+    ref = x[0].clone()
+    for s in range(1, ns):
+        ref = ref + x[s]
+    assert torch.equal(out, ref)
+    torch.testing.assert_close(out.double(), x.double().sum(0), rtol=1e-5, atol=1e-5)
+
+
+def test_tanh_inplace_matches_torch():
+    x = torch.randn((4096, 256), generator=torch.Generator(device="cuda").manual_seed(1), device="cuda") * 3
+    ref = torch.tanh(x)
+    y = ppo.tanh_inplace_native(x.clone())
+    torch.testing.assert_close(y, ref, rtol=2e-7, atol=2e-7)

@@ -1,0 +1,11 @@
+# round 3: LDS-staged surrogate, slice-sum split-K reduction, float4 tanh, wider colsum stage 2
+# the update probe, and its kernel breakdown
+mkdir -p gpurun_out/r3l
+export TMPDIR=/tmp
+timeout -k 10 900 python -u -m pytest -x -v --timeout 300 --timeout-method thread tests/test_ppo.py tests/test_ppo_graph.py tests/test_dp_gpu.py tests/test_mlp_kernels.py -m gpu > gpurun_out/r3l/pytest.log 2>&1
+rc=$?
+echo "pytest rc=$rc"
+if [ $rc -ne 0 ]; then exit $rc; fi
+timeout -k 10 200 python -u tools/ppo_update_probe.py graph 2048 > gpurun_out/r3l/upd.txt 2>&1 || exit $?
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/r3l/prof -o upd -- python tools/ppo_update_probe.py graph 2048 > gpurun_out/r3l/prof.log 2>&1 || exit $?
+cat gpurun_out/r3l/upd.txt
