@@ -999,13 +999,22 @@ template <class D> INL void adj_collision(MP m, LDSA WS<D>* W, LDSA WSA<D>* A, R
 
 // geom frames (kinematics): gpos = xpos_b + xmat_b geom_pos, gaxis = xmat_b zaxis; lane = body
 template <class D> INL void adj_geom_frames(MP m, LDSA WSA<D>* A, int lane) {
+  static_assert(D::NG <= D::NV, "geom constants staged in A->ftmp");
+  // geom lanes stage their local pos / z axis (frame records) in A->ftmp, dead until adj_mass: the body
+  // lanes' geom loop then reads LDS instead of waiting on two global loads per geom
+  const bool isg = lane < m->ngeom;
+  const uint32_t gmask = m->body_geommask[lane < m->nbody ? lane : 0];
+  const FrameRec fr = ldrec(&m->frec[isg ? lane : 0]);
+  if (isg)
+    for (int j = 0; j < 3; j++) { A->ftmp[lane][j] = fr.pos[j]; A->ftmp[lane][3 + j] = fr.mat[j]; }
+  SYNC();
   if (lane > 0 && lane < m->nbody) {
-    for (uint32_t gm = m->body_geommask[lane]; gm; gm &= gm - 1) {
+    for (uint32_t gm = gmask; gm; gm &= gm - 1) {
       const int g = __ffs(gm) - 1;
       for (int i = 0; i < 3; i++) {
         const float pb = A->gposb[g][i], ab = A->gaxisb[g][i];
         A->xposb[lane][i] += pb;
-        for (int j = 0; j < 3; j++) A->xmatb[lane][3 * i + j] += pb * m->geom_pos[g][j] + ab * m->geom_zaxis[g][j];
+        for (int j = 0; j < 3; j++) A->xmatb[lane][3 * i + j] += pb * A->ftmp[g][j] + ab * A->ftmp[g][3 + j];
       }
     }
   }
@@ -1014,9 +1023,12 @@ template <class D> INL void adj_geom_frames(MP m, LDSA WSA<D>* A, int lane) {
 
 // qfrc_smooth = passive - bias + actuator: passive and actuation adjoints; bias-bar -> A->vtmp
 template <class D> INL void adj_forces(MP m, LDSA WS<D>* W, LDSA WSA<D>* A, int lane) {
-  const int nv = m->nv;
+  const int nv = m->nv, nu = m->nu;
+  const int ul = lane < nu ? lane : 0;  // actuator constants issued with the dof record
+  const int a_lim = m->actuator_ctrllimited[ul], a_dof = m->actuator_dof[ul];
+  const float a_lo = m->actuator_ctrlrange[ul][0], a_hi = m->actuator_ctrlrange[ul][1], a_gear = m->actuator_gear[ul];
+  const DofRec dr = ldrec(&m->drec[lane < nv ? lane : 0]);
   if (lane < nv) {
-    const DofRec dr = ldrec(&m->drec[lane]);
     const float fs = A->frcsb[lane];
     A->vtmp[lane] = -fs;
     A->frcactb[lane] += fs;
@@ -1024,11 +1036,10 @@ template <class D> INL void adj_forces(MP m, LDSA WS<D>* W, LDSA WSA<D>* A, int 
     if (dr.qadr_spring >= 0) A->qposb[dr.qadr_spring] += -dr.stiffness * fs;
   }
   SYNC();
-  if (lane < m->nu) {
+  if (lane < nu) {
     const float c = W->ctrl[lane];
-    const bool inside = !m->actuator_ctrllimited[lane] ||
-                        (c > m->actuator_ctrlrange[lane][0] && c < m->actuator_ctrlrange[lane][1]);
-    A->ctrlb[lane] += inside ? m->actuator_gear[lane] * A->frcactb[m->actuator_dof[lane]] : 0.f;
+    const bool inside = !a_lim || (c > a_lo && c < a_hi);
+    A->ctrlb[lane] += inside ? a_gear * A->frcactb[a_dof] : 0.f;
   }
   SYNC();
 }
@@ -1060,9 +1071,13 @@ template <class D> INL void body_vel_terms(LDSA WS<D>* W, const LDSA float* qvel
 template <class D> INL void adj_rne(MP m, LDSA WS<D>* W, LDSA WSA<D>* A, int lane) {
   const int nv = m->nv, nbody = m->nbody, maxlevel = m->maxlevel;
   const bool isb = lane > 0 && lane < nbody;
+  const int bl = lane < nbody ? lane : 0;  // the pass's model records, issued together
   const BodyRec br = ldrec(&m->brec[isb ? lane : 0]);
+  const int dbody = ldrec(&m->drec[lane < nv ? lane : 0]).bodyid;
+  const uint32_t ancm = m->body_ancmask[bl], chm = m->body_childmask[bl];
+  TSTART(tr);
   if (lane < nv) {  // bias_d = cdof_d . cfsub_body(d)
-    const int b = ldrec(&m->drec[lane]).bodyid;
+    const int b = dbody;
     for (int k = 0; k < 6; k++) A->cdofb[lane][k] += A->vtmp[lane] * W->cvel[b][k];
   }
   if (isb) {
@@ -1074,13 +1089,14 @@ template <class D> INL void adj_rne(MP m, LDSA WS<D>* W, LDSA WSA<D>* A, int lan
   SYNC();
   if (isb) {  // cfrc-bar_c = sum over ancestors-or-self b of cfsub-bar_b
     float s[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-    for (uint32_t mk = m->body_ancmask[lane]; mk;) {  // self, then up the chain
+    for (uint32_t mk = ancm; mk;) {  // self, then up the chain
       const int b = 31 - __clz(mk);
       mk &= ~(1u << b);
       for (int k = 0; k < 6; k++) s[k] += A->cfsubb[b][k];
     }
     for (int k = 0; k < 6; k++) A->cfrcb[lane][k] = s[k];
   }
+  TACC(25, tr, lane);
   // recompute cvel / cacc (tree pass of velocity_stage)
   float S[6], U[6], T[6];
   if (isb) body_vel_terms<D>(W, A->qvel0, br, S, U, T);
@@ -1099,6 +1115,7 @@ template <class D> INL void adj_rne(MP m, LDSA WS<D>* W, LDSA WSA<D>* A, int lan
     }
     SYNC();
   }
+  TACC(26, tr, lane);
   if (isb) {  // cfrc = I cacc + cvel x* (I cvel)
     float ci[10], cv[6], ca[6], fb[6], iv[6], ivb[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
     float cib[10] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f}, cvb[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
@@ -1113,6 +1130,7 @@ template <class D> INL void adj_rne(MP m, LDSA WS<D>* W, LDSA WSA<D>* A, int lan
     for (int i = 0; i < 6; i++) { A->cvelb[lane][i] += cvb[i]; A->caccb[lane][i] += cab[i]; }
   }
   SYNC();
+  TACC(27, tr, lane);
   // tree reverse: cvel_b = cvel_p + S, cacc_b = cacc_p + cvel_p x U + T; children -> parent gather
   float Sb[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f}, Ubr[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f}, Tbr[6];
   for (int L = maxlevel; L >= 1; L--) {
@@ -1124,13 +1142,14 @@ template <class D> INL void adj_rne(MP m, LDSA WS<D>* W, LDSA WSA<D>* A, int lan
     }
     SYNC();
     if (isb && br.level == L - 1) {
-      for (uint32_t mk = m->body_childmask[lane]; mk; mk &= mk - 1) {
+      for (uint32_t mk = chm; mk; mk &= mk - 1) {
         const int c = __ffs(mk) - 1;
         for (int i = 0; i < 6; i++) { A->cvelb[lane][i] += A->cfsubb[c][i]; A->caccb[lane][i] += A->cfrcb[c][i]; }
       }
     }
     SYNC();
   }
+  TACC(28, tr, lane);
   if (isb) {  // local terms -> cdof-bar, qvel-bar
     const int da = br.dofadr, dn = br.dofnum;
     if (br.isfree) {
@@ -1169,6 +1188,7 @@ template <class D> INL void adj_rne(MP m, LDSA WS<D>* W, LDSA WSA<D>* A, int lan
     }
   }
   SYNC();
+  TACC(29, tr, lane);
 }
 
 // mass matrix (crb / make_m): M[i][j] = cdof_j . I(crb_body(i)) cdof_i (+ armature), j in anc(i)
@@ -1177,6 +1197,9 @@ template <class D> INL void adj_mass(MP m, LDSA WS<D>* W, LDSA WSA<D>* A, int la
   const int nv = m->nv;
   const bool isd = lane < nv;
   const DofRec dr = ldrec(&m->drec[isd ? lane : 0]);
+  const uint32_t descm = m->dof_descmask[isd ? lane : 0];
+  const BodyRec brm = ldrec(&m->brec[lane > 0 && lane < m->nbody ? lane : 0]);  // the crb-bar pass below
+  TSTART(tm);
   if (isd) {
     float f6[6];
     inert_vec(f6, W->crb[dr.bodyid], W->cdof[lane]);
@@ -1193,15 +1216,22 @@ template <class D> INL void adj_mass(MP m, LDSA WS<D>* W, LDSA WSA<D>* A, int la
       for (int k = 0; k < 6; k++) fb[k] += vb * W->cdof[j][k];
     }
     const int j = lane;  // cdof-bar_j += sum over descendants i of vbar_ij f_i
+    // every dof in ascending order, the sum taking the descendants (the mask's bit loop, unrolled:
+    // a root dof has all nv as descendants, and the loop waited for each iteration's LDS reads)
     float cb[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-    for (uint32_t dm = m->dof_descmask[j]; dm; dm &= dm - 1) {
-      const int ii = __ffs(dm) - 1;
-      const float vb = (ii == j) ? A->Mb[j * LD + j] : A->Mb[ii * LD + j] + A->Mb[j * LD + ii];
-      for (int k = 0; k < 6; k++) cb[k] += vb * A->ftmp[ii][k];
+#pragma unroll
+    for (int ii = 0; ii < D::NV; ii++) {
+      const bool in = (descm >> ii) & 1u;
+      const float a = A->Mb[ii * LD + j], c = A->Mb[j * LD + ii];
+      const float vb = (ii == j) ? c : a + c;
+      float f[6];
+      for (int k = 0; k < 6; k++) f[k] = A->ftmp[ii][k];
+      for (int k = 0; k < 6; k++) cb[k] = in ? cb[k] + vb * f[k] : cb[k];
     }
     for (int k = 0; k < 6; k++) A->cdofb[j][k] += cb[k];
   }
   SYNC();
+  TACC(30, tm, lane);
   if (isd) {  // f_i = I(crb) cdof_i
     float t[6];
     inert_vec(t, W->crb[dr.bodyid], fb);
@@ -1209,7 +1239,7 @@ template <class D> INL void adj_mass(MP m, LDSA WS<D>* W, LDSA WSA<D>* A, int la
   }
   SYNC();
   if (lane > 0 && lane < m->nbody) {
-    const BodyRec br = ldrec(&m->brec[lane]);
+    const BodyRec& br = brm;
     float ib[10] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
     for (int d = br.dofadr; d < br.dofadr + br.dofnum; d++) {
       float f6[6], c6[6];
@@ -1219,6 +1249,7 @@ template <class D> INL void adj_mass(MP m, LDSA WS<D>* W, LDSA WSA<D>* A, int la
     for (int k = 0; k < 10; k++) A->crbb[lane][k] += ib[k];
   }
   SYNC();
+  TACC(31, tm, lane);
 }
 
 // crb_b = sum of cinert over the subtree of b: cinert-bar_c = sum of crb-bar over ancestors-or-self
@@ -1244,7 +1275,7 @@ template <class D> INL void adj_cinert(MP m, LDSA WS<D>* W, LDSA WSA<D>* A, int 
     const int b = lane, root = br.rootid;
     const float ms = br.mass;
     LDSA float* cb = A->cinertb[b];
-    const CSTA float* t = m->body_inertia[b];
+    const float* t = br.inertia;  // body_inertia[b], in the record
     const float Ib[9] = {t[0], t[3], t[4], t[3], t[1], t[5], t[4], t[5], t[2]};
     float X[9];
     for (int i = 0; i < 9; i++) X[i] = W->xmat[b][i];
@@ -1277,6 +1308,7 @@ template <class D> INL void adj_cdof(MP m, LDSA WS<D>* W, LDSA WSA<D>* A, int la
   const int nv = m->nv;
   const bool isd = lane < nv;
   const DofRec dr = ldrec(&m->drec[isd ? lane : 0]);
+  const JntRec jown = ldrec(&m->jrec[lane < m->njnt ? lane : 0]);  // the joint gather below
   float scb[3] = {0.f, 0.f, 0.f};
   if (isd) {
     const int d = lane, j = dr.jntid, b = dr.bodyid, root = dr.rootid, k = dr.kfree;
@@ -1297,7 +1329,7 @@ template <class D> INL void adj_cdof(MP m, LDSA WS<D>* W, LDSA WSA<D>* A, int la
   scom_reduce<D>(m, A, isd ? dr.rootid : -1, scb, lane);
   SYNC();
   if (lane < m->njnt) {  // gather the joint's dofs
-    const JntRec jr = ldrec(&m->jrec[lane]);
+    const JntRec& jr = jown;
     const int nd = jr.isfree ? 6 : 1;
     for (int q = 0; q < nd; q++) {
       const int d = jr.dofadr + q;
@@ -1314,17 +1346,34 @@ template <class D> INL void adj_cdof(MP m, LDSA WS<D>* W, LDSA WSA<D>* A, int la
 template <class D> INL void adj_kinematics(MP m, LDSA WS<D>* W, LDSA WSA<D>* A, int lane) {
   const int nbody = m->nbody, maxlevel = m->maxlevel, njnt = m->njnt;
   const bool isb = lane > 0 && lane < nbody;
+  // the pass's model records issued together up front (the loops below waited on one dependent
+  // record load per joint: ~10 global round trips per env): the lane's body and joint, its masks and
+  // root mass, then the body's first three hinges (one more round, through jntadr)
+  const int bl = lane < nbody ? lane : 0;
   const BodyRec br = ldrec(&m->brec[isb ? lane : 0]);
+  const JntRec jown = ldrec(&m->jrec[lane < njnt ? lane : 0]);
+  const uint32_t jgather = m->body_jgather[bl], cmask_nf = m->body_childmask_nf[bl];
+  const float rmass_own = m->body_rootmass[bl];
+  const int ja = isb && br.jntadr >= 0 ? br.jntadr : 0;
+  const JntRec bj0 = ldrec(&m->jrec[ja < njnt ? ja : 0]);
+  const JntRec bj1 = ldrec(&m->jrec[ja + 1 < njnt ? ja + 1 : 0]);
+  const JntRec bj2 = ldrec(&m->jrec[ja + 2 < njnt ? ja + 2 : 0]);
+  auto hinge = [&](int q) -> JntRec {
+    if (q < 3) return q == 0 ? bj0 : (q == 1 ? bj1 : bj2);
+    return ldrec(&m->jrec[br.jntadr + q]);
+  };
+  TSTART(tk);
+  const uint64_t freemask = __ballot(lane < njnt && jown.isfree);  // bit j: joint j is free
+  const float mr = __shfl(rmass_own, isb ? br.rootid : 0);         // body_rootmass[rootid]
   // scom_r = sum_c m_c xipos_c / sum_c m_c over the root's subtree
   if (isb) {
     const int r = br.rootid;
-    const float mr = m->body_rootmass[r];
     if (mr >= kMinVal) for (int i = 0; i < 3; i++) A->xiposb[lane][i] += br.mass / mr * A->scomb[r][i];
   }
   SYNC();
   // joint anchors / axes (world) -> parent frame cotangents; local anchor / axis cotangents in ftmp
   if (lane < njnt) {
-    const JntRec jr = ldrec(&m->jrec[lane]);
+    const JntRec& jr = jown;
     if (!jr.isfree) {
       const int p = jr.parent;
       float lab[3], lxb[3];
@@ -1334,12 +1383,12 @@ template <class D> INL void adj_kinematics(MP m, LDSA WS<D>* W, LDSA WSA<D>* A, 
     }
   }
   SYNC();
+  TACC(20, tk, lane);
   if (lane < nbody) {  // gather: free joint -> its body; hinge -> its parent frame (la, lx in local)
     float pb[3] = {0.f, 0.f, 0.f}, mb[9] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-    for (uint32_t mk = m->body_jgather[lane]; mk; mk &= mk - 1) {
+    for (uint32_t mk = jgather; mk; mk &= mk - 1) {
       const int j = __ffs(mk) - 1;
-      const JntRec jr = ldrec(&m->jrec[j]);
-      if (jr.isfree) {
+      if ((freemask >> j) & 1ull) {
         for (int i = 0; i < 3; i++) { pb[i] += A->xanchorb[j][i]; mb[3 * i + 2] += A->xaxisb[j][i]; }
       } else {
         // anc = xpos_p + xmat_p la, ax = xmat_p lx with la, lx the local values stored in xanchor/xaxis?
@@ -1358,6 +1407,7 @@ template <class D> INL void adj_kinematics(MP m, LDSA WS<D>* W, LDSA WSA<D>* A, 
     for (int i = 0; i < 9; i++) A->xmatb[lane][i] += mb[i];
   }
   SYNC();
+  TACC(21, tk, lane);
   if (isb) {  // xipos = xpos + xmat ipos
     for (int i = 0; i < 3; i++) {
       A->xposb[lane][i] += A->xiposb[lane][i];
@@ -1375,8 +1425,8 @@ template <class D> INL void adj_kinematics(MP m, LDSA WS<D>* W, LDSA WSA<D>* A, 
     } else {
       for (int i = 0; i < 3; i++) lp[i] = br.pos[i];
       for (int i = 0; i < 4; i++) lq[i] = br.quat[i];
-      for (int j = br.jntadr; j < br.jntadr + br.jntnum; j++) {
-        const JntRec jr = ldrec(&m->jrec[j]);
+      for (int q = 0; q < br.jntnum; q++) {
+        const JntRec jr = hinge(q);
         float mat[9], anc[3], off[3];
         q2m(mat, lq);
         mv3(anc, mat, jr.pos);
@@ -1394,6 +1444,7 @@ template <class D> INL void adj_kinematics(MP m, LDSA WS<D>* W, LDSA WSA<D>* A, 
     for (int i = 0; i < 4; i++) A->lq[lane][i] = lq[i];
   }
   SYNC();
+  TACC(22, tk, lane);
   // tree pass reverse; child contributions to the parent go through A->Sb (xquat 4, xpos 3) and
   // A->Tb (first 6 of xmat) + A->Ub (last 3 of xmat)
   float lpb[3] = {0.f, 0.f, 0.f}, lqb[4] = {0.f, 0.f, 0.f, 0.f};
@@ -1425,7 +1476,7 @@ template <class D> INL void adj_kinematics(MP m, LDSA WS<D>* W, LDSA WSA<D>* A, 
     }
     SYNC();
     if (isb && br.level == L - 1) {
-      for (uint32_t mk = m->body_childmask_nf[lane]; mk; mk &= mk - 1) {
+      for (uint32_t mk = cmask_nf; mk; mk &= mk - 1) {
         const int c = __ffs(mk) - 1;
         for (int i = 0; i < 4; i++) A->xquatb[lane][i] += A->Sb[c][i];
         A->xposb[lane][0] += A->Sb[c][4]; A->xposb[lane][1] += A->Sb[c][5]; A->xposb[lane][2] += A->Ub[c][0];
@@ -1435,6 +1486,7 @@ template <class D> INL void adj_kinematics(MP m, LDSA WS<D>* W, LDSA WSA<D>* A, 
     }
     SYNC();
   }
+  TACC(23, tk, lane);
   // local transforms reverse -> qpos-bar
   if (isb) {
     if (br.isfree) {
@@ -1452,7 +1504,7 @@ template <class D> INL void adj_kinematics(MP m, LDSA WS<D>* W, LDSA WSA<D>* A, 
       for (int i = 0; i < 4; i++) lq[i] = br.quat[i];
       const int jn = br.jntnum < KJ ? br.jntnum : KJ;
       for (int q = 0; q < jn; q++) {
-        const JntRec jr = ldrec(&m->jrec[br.jntadr + q]);
+        const JntRec jr = hinge(q);
         for (int i = 0; i < 4; i++) lqs[q][i] = lq[i];
         for (int i = 0; i < 3; i++) lps[q][i] = lp[i];
         float mat[9], anc[3], off[3];
@@ -1468,7 +1520,7 @@ template <class D> INL void adj_kinematics(MP m, LDSA WS<D>* W, LDSA WSA<D>* A, 
       }
       for (int q = jn - 1; q >= 0; q--) {
         const int j = br.jntadr + q;
-        const JntRec jr = ldrec(&m->jrec[j]);
+        const JntRec jr = hinge(q);
         const float ql[4] = {cs[q], jr.axis[0] * sn[q], jr.axis[1] * sn[q], jr.axis[2] * sn[q]};
         float lqa[4];
         qmul(lqa, lqs[q], ql);
@@ -1495,6 +1547,7 @@ template <class D> INL void adj_kinematics(MP m, LDSA WS<D>* W, LDSA WSA<D>* A, 
     }
   }
   SYNC();
+  TACC(24, tk, lane);
 }
 
 // ------------------------------------------------------------------- VJP kernel
@@ -1643,8 +1696,10 @@ template <class D, bool ENV, int TM> __global__ __launch_bounds__(64, 1) void vj
   tp.nup = tp.nls = tp.nsets = tp.overflow = 0;
   Rows<true> R = global_rows<D>(TM ? (float*)(slot + V.s_r) : scr_env, P.gmax_efc, P.gmax_con);
   if constexpr (TM == 2) {  // replay: the forward's workspace, pre-step state and factors from the slot
+    STAMP(0, lane);
     slot_replay_load<D>(slot + V.s_w, slot + V.s_a, W, A, aux, lane);
     SYNC();
+    STAMP(1, lane);
   } else {
   // every state load issues before the first wait (clamped lane indices, no branch per load)
   const int iq = lane < nq ? lane : nq - 1, iv = lane < nv ? lane : nv - 1, iu = lane < nu ? lane : nu - 1;
