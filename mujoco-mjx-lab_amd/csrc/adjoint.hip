@@ -118,27 +118,50 @@ INL float imp_dpos(const CSTA float* solimp, float pos) {
 }
 
 // ------------------------------------------------------------------- adjoint workspace (LDS)
+// WSA_P1..P3: the adjoint workspace around its dense arrays (Lc, invdc: the factor of Hc; Mb: the
+// cotangent of M; uv: unrolled-mode staging). WSAL<DM> (lean replay) drops them: it reads Lc / invdc
+// from the tape slot and forms M-bar from its rank-one terms (adj_mass), so the replay fits the
+// 20 KB / 8-waves-per-CU LDS budget with WSB.
+#define WSA_P1                                                                                       \
+  static constexpr int NV = DM::NV, LD = DM::LD, NB = DM::NB, NJ = DM::NJ, NG = DM::NG;             \
+  /* forward values kept for the reverse passes */                                                 \
+  float qpos0[MJL_MAXQ], qvel0[LD];    /* pre-step state */                                        \
+  float cvel[NB][6], cacc[NB][6];      /* recomputed in the RNE reverse */
+#define WSA_P2                                                                                       \
+  float ap[LD];                        /* integrator acceleration a' */                            \
+  float lp[NB][3], lq[NB][4];          /* body transform in the parent frame */                    \
+  float ftmp[NV][6];                   /* scratch: f_i = I(crb) cdof_i, then its cotangent */      \
+  /* cotangents */                                                                                 \
+  float qposb[MJL_MAXQ], qvelb[LD], ctrlb[MJL_MAXU], auxb[MJL_AUX_DIM + 3];                        \
+  float frcsb[LD], qaccb[LD], frcactb[LD], mu[LD], rb[LD], vtmp[LD];                               \
+  float xposb[NB][3], xquatb[NB][4], xmatb[NB][9], xiposb[NB][3], scomb[NB][3];                    \
+  float xanchorb[NJ][3], xaxisb[NJ][3], gposb[NG][3], gaxisb[NG][3];                               \
+  float cdofb[NV][6], cinertb[NB][10], crbb[NB][10], cvelb[NB][6], caccb[NB][6], cfrcb[NB][6], cfsubb[NB][6]; \
+  float Sb[NB][6], Ub[NB][6], Tb[NB][6];
+#define WSA_P3                                                                                       \
+  float qfcb[LD];                      /* unrolled mode: cotangent of the final qfrc_constraint */ \
+  float wsb[LD];                       /* unrolled mode: cotangent of the input qacc_warmstart */
 template <class DM> struct WSA {
-  static constexpr int NV = DM::NV, LD = DM::LD, NB = DM::NB, NJ = DM::NJ, NG = DM::NG;
-  // forward values kept for the reverse passes
-  float qpos0[MJL_MAXQ], qvel0[LD];    // pre-step state
-  float cvel[NB][6], cacc[NB][6];      // recomputed in the RNE reverse
+  WSA_P1
   alignas(16) float Lc[NV * LD];       // factor of Hc at the converged active set
   alignas(16) float invdc[LD];
-  float ap[LD];                        // integrator acceleration a'
-  float lp[NB][3], lq[NB][4];          // body transform in the parent frame
-  float ftmp[NV][6];                   // scratch: f_i = I(crb) cdof_i, then its cotangent
-  // cotangents
-  float qposb[MJL_MAXQ], qvelb[LD], ctrlb[MJL_MAXU], auxb[MJL_AUX_DIM + 3];
-  float frcsb[LD], qaccb[LD], frcactb[LD], mu[LD], rb[LD], vtmp[LD];
-  float xposb[NB][3], xquatb[NB][4], xmatb[NB][9], xiposb[NB][3], scomb[NB][3];
-  float xanchorb[NJ][3], xaxisb[NJ][3], gposb[NG][3], gaxisb[NG][3];
-  float cdofb[NV][6], cinertb[NB][10], crbb[NB][10], cvelb[NB][6], caccb[NB][6], cfrcb[NB][6], cfsubb[NB][6];
-  float Sb[NB][6], Ub[NB][6], Tb[NB][6];
+  WSA_P2
   alignas(16) float Mb[NV * LD];
-  float qfcb[LD];                      // unrolled mode: cotangent of the final qfrc_constraint
-  float wsb[LD];                       // unrolled mode: cotangent of the input qacc_warmstart
+  WSA_P3
   alignas(16) float uv[3][LD];         // unrolled mode: vectors staged for M v / J v products
+};
+template <class DM> struct WSAL {  // lean replay: WSA without Lc, invdc, Mb, uv
+  WSA_P1
+  WSA_P2
+  WSA_P3
+};
+template <class AT> struct is_lean { static constexpr bool value = false; };
+template <class DM> struct is_lean<WSAL<DM>> { static constexpr bool value = true; };
+
+// where the reverse passes find the dense arrays: M, H, invd (forward workspace) and Lc, invdc (factor
+// of Hc) in LDS (WS / WSA), or in the tape slot in global memory (lean replay)
+template <class P> struct AdjMats {
+  P M, H, invd, Lc, invdc;
 };
 
 // per-env global scratch of the adjoint (after the env's row slab): per row (alpha, gamma, posbar),
@@ -243,7 +266,7 @@ INL void wsum3_into(LDSA float* dst, const float* v, int lane) {
   if (lane == 0) { dst[0] += a; dst[1] += b; dst[2] += c; }
 }
 // per-root reduction of lane-held subtree-com cotangents (only roots' scom are read forward)
-template <class D> INL void scom_reduce(MP m, LDSA WSA<D>* A, int root_of_lane, const float* v, int lane) {
+template <class D, class AT> INL void scom_reduce(MP m, LDSA AT* A, int root_of_lane, const float* v, int lane) {
   for (int q = 0; q < m->nroot; q++) {
     const int r = m->root[q];
     float t[3] = {0.f, 0.f, 0.f};
@@ -255,7 +278,7 @@ template <class D> INL void scom_reduce(MP m, LDSA WSA<D>* A, int root_of_lane, 
 // ------------------------------------------------------------------- env step (envs.py:333-492)
 // Reward, aux' cotangents -> xpos / xquat of pelvis and head, qfrc_actuator, post-step qvel (in
 // A->vtmp), input aux. Mirrors env_post branch for branch.
-template <class D> INL void adj_env(MP m, LDSA WS<D>* W, LDSA WSA<D>* A, CP c, const float* aux, float rb,
+template <class D, class WT, class AT> INL void adj_env(MP m, LDSA WT* W, LDSA AT* A, CP c, const float* aux, float rb,
                                     const float* auxb_o, int lane) {
   const float dt = m->timestep;
   const float nj = (float)(m->nv - 6);
@@ -347,7 +370,8 @@ template <class D> INL void adj_env(MP m, LDSA WS<D>* W, LDSA WSA<D>* A, CP c, c
 // in: A->vtmp = cotangent of qvel', gq = cotangent of qpos' (global). out: A->qposb, A->qvelb,
 // A->qaccb, A->Mb (implicit / eulerdamp matrix path); unrolled mode: the matrix path's force is
 // qfrc_smooth + qfrc_constraint (A->frcsb, A->qfcb), not M qacc.
-template <class D> INL void adj_integrate(MP m, LDSA WS<D>* W, LDSA WSA<D>* A, const float* gq, bool unr, int lane) {
+template <class D, class WT, class AT, class MT> INL void adj_integrate(MP m, LDSA WT* W, LDSA AT* A, const MT& mt,
+                                                                      const float* gq, bool unr, int lane) {
   constexpr int LD = D::LD;
   const int nv = m->nv;
   const float dt = m->timestep;
@@ -390,19 +414,21 @@ template <class D> INL void adj_integrate(MP m, LDSA WS<D>* W, LDSA WSA<D>* A, c
   if (damp) {  // a' = Hd^-1 (M qacc), Hd = M + dt diag(damping), factor in W->H
     if (lane < LD) A->rb[lane] = (lane < nv) ? apb : 0.f;
     SYNC();
-    const float r = chol_solve<D>(W->H, W->invd, lane < nv ? A->rb[lane] : 0.f, lane);
+    const float r = chol_solve<D>(mt.H, mt.invd, lane < nv ? A->rb[lane] : 0.f, lane);
     SYNC();
     if (lane < LD) A->rb[lane] = (lane < nv) ? r : 0.f;
     SYNC();
     if (lane < nv) {
       const float rl = A->rb[lane];
-      if (unr) {  // a' = Hd^-1 (qfrc_smooth + qfrc_constraint)
+      if constexpr (is_lean<AT>::value) {  // M-bar's term rb (qacc - a')^T: formed in adj_mass
+        A->qaccb[lane] += rowdot<LD>(mt.M + lane * LD, A->rb);
+      } else if (unr) {  // a' = Hd^-1 (qfrc_smooth + qfrc_constraint)
         for (int k = 0; k < nv; k++) A->Mb[lane * LD + k] -= rl * A->ap[k];
         A->frcsb[lane] += rl;
         A->qfcb[lane] += rl;
       } else {
         for (int k = 0; k < nv; k++) A->Mb[lane * LD + k] += rl * (W->qacc[k] - A->ap[k]);
-        A->qaccb[lane] += mrow<D>(W, A->rb, lane);
+        A->qaccb[lane] += rowdot<LD>(mt.M + lane * LD, A->rb);  // (M rb)[lane] (mrow)
       }
     }
   } else if (lane < nv) {
@@ -437,7 +463,7 @@ template <class D> INL void adj_row_map(MP m, Rows<true> R, GLBA float* scr, int
   posb[r] = -k * imp * arefb + impb * imp_dpos(si, pos);
 }
 
-template <class D> INL void adj_rows_tail(MP m, LDSA WS<D>* W, LDSA WSA<D>* A, Rows<true> R, GLBA float* scr,
+template <class D, class WT, class AT> INL void adj_rows_tail(MP m, LDSA WT* W, LDSA AT* A, Rows<true> R, GLBA float* scr,
                                           int nefc_max, int lane) {
   constexpr int LD = D::LD;
   const int nv = m->nv, nefc = W->nefc;
@@ -468,17 +494,20 @@ template <class D> INL void adj_rows_tail(MP m, LDSA WS<D>* W, LDSA WSA<D>* A, R
 }
 
 // Implicit mode: derivative at the converged active set (mu = Hc^-1 qacc-bar).
-template <class D> INL void adj_solver_rows(MP m, LDSA WS<D>* W, LDSA WSA<D>* A, Rows<true> R, GLBA float* scr,
-                                            int nefc_max, int lane) {
+template <class D, class WT, class AT, class MT> INL void adj_solver_rows(MP m, LDSA WT* W, LDSA AT* A, const MT& mt,
+                                                                        Rows<true> R, GLBA float* scr, int nefc_max,
+                                                                        int lane) {
   constexpr int LD = D::LD;
   const int nv = m->nv, nefc = W->nefc;
-  const float mu = chol_solve<D>(A->Lc, A->invdc, lane < nv ? A->qaccb[lane] : 0.f, lane);
+  const float mu = chol_solve<D>(mt.Lc, mt.invdc, lane < nv ? A->qaccb[lane] : 0.f, lane);
   if (lane < LD) A->mu[lane] = (lane < nv) ? mu : 0.f;
   SYNC();
   if (lane < nv) {
     A->frcsb[lane] += A->mu[lane];
-    const float ml = A->mu[lane];
-    for (int k = 0; k < nv; k++) A->Mb[lane * LD + k] -= ml * W->qacc[k];
+    if constexpr (!is_lean<AT>::value) {  // lean: M-bar's term -mu qacc^T formed in adj_mass
+      const float ml = A->mu[lane];
+      for (int k = 0; k < nv; k++) A->Mb[lane * LD + k] -= ml * W->qacc[k];
+    }
   }
   for (int r = lane; r < nefc; r += 64) {
     const float jar = R.jar[r], Dr = R.D[r];
@@ -720,7 +749,7 @@ template <class D> INL void adj_solver_unrolled(MP m, LDSA WS<D>* W, LDSA WSA<D>
 // J rows of contact c from Jp_d = s_d (cdof_lin_d + cdof_ang_d x (pos - scom_root)); lanes 0..31 =
 // dof. Accumulates cdof-bar (lane-owned), scom-bar (per root), and the contact's pos / frame /
 // dist cotangents into the scratch record.
-template <class D> INL void adj_contact_jac(MP m, LDSA WS<D>* W, LDSA WSA<D>* A, Rows<true> R, GLBA float* scr,
+template <class D, class WT, class AT> INL void adj_contact_jac(MP m, LDSA WT* W, LDSA AT* A, Rows<true> R, GLBA float* scr,
                                             int nefc_max, GLBA const float* Jbar, int lane) {
   constexpr int LD = D::LD;
   const int nv = m->nv, ncon = W->ncon;
@@ -819,7 +848,7 @@ INL void seg_point_adj(const float* a, const float* b, const float* pt, const fl
   }
   for (int i = 0; i < 3; i++) { bb_[i] += abb[i]; ab_[i] -= abb[i]; }
 }
-template <class D> INL void collide_adj(const PairRec& pr, LDSA WS<D>* W, int k, float distb, const float* posb,
+template <class D, class WT> INL void collide_adj(const PairRec& pr, LDSA WT* W, int k, float distb, const float* posb,
                                         const float* frb, float* x1b, float* z1b, float* x2b, float* z2b) {
   const int kind = pr.kind, g1 = pr.g1, g2 = pr.g2;
   const float x1[3] = {W->gpos[g1][0], W->gpos[g1][1], W->gpos[g1][2]};
@@ -968,7 +997,7 @@ template <class D> INL void collide_adj(const PairRec& pr, LDSA WS<D>* W, int k,
 }
 
 // lane = contact: geometry cotangents into the scratch record; then lane = geom gathers them
-template <class D> INL void adj_collision(MP m, LDSA WS<D>* W, LDSA WSA<D>* A, Rows<true> R, GLBA float* scr,
+template <class D, class WT, class AT> INL void adj_collision(MP m, LDSA WT* W, LDSA AT* A, Rows<true> R, GLBA float* scr,
                                           int nefc_max, int lane) {
   const int ncon = W->ncon;
   GLBA float* conb = scr + 3 * nefc_max;
@@ -998,7 +1027,7 @@ template <class D> INL void adj_collision(MP m, LDSA WS<D>* W, LDSA WSA<D>* A, R
 }
 
 // geom frames (kinematics): gpos = xpos_b + xmat_b geom_pos, gaxis = xmat_b zaxis; lane = body
-template <class D> INL void adj_geom_frames(MP m, LDSA WSA<D>* A, int lane) {
+template <class D, class AT> INL void adj_geom_frames(MP m, LDSA AT* A, int lane) {
   static_assert(D::NG <= D::NV, "geom constants staged in A->ftmp");
   // geom lanes stage their local pos / z axis (frame records) in A->ftmp, dead until adj_mass: the body
   // lanes' geom loop then reads LDS instead of waiting on two global loads per geom
@@ -1022,7 +1051,7 @@ template <class D> INL void adj_geom_frames(MP m, LDSA WSA<D>* A, int lane) {
 }
 
 // qfrc_smooth = passive - bias + actuator: passive and actuation adjoints; bias-bar -> A->vtmp
-template <class D> INL void adj_forces(MP m, LDSA WS<D>* W, LDSA WSA<D>* A, int lane) {
+template <class D, class WT, class AT> INL void adj_forces(MP m, LDSA WT* W, LDSA AT* A, int lane) {
   const int nv = m->nv, nu = m->nu;
   const int ul = lane < nu ? lane : 0;  // actuator constants issued with the dof record
   const int a_lim = m->actuator_ctrllimited[ul], a_dof = m->actuator_dof[ul];
@@ -1045,7 +1074,7 @@ template <class D> INL void adj_forces(MP m, LDSA WS<D>* W, LDSA WSA<D>* A, int 
 }
 
 // per-body velocity terms (velocity_stage): S, U, T from cdof and qvel
-template <class D> INL void body_vel_terms(LDSA WS<D>* W, const LDSA float* qvel, const BodyRec& br, float* S,
+template <class D, class WT> INL void body_vel_terms(LDSA WT* W, const LDSA float* qvel, const BodyRec& br, float* S,
                                            float* U, float* T) {
   for (int i = 0; i < 6; i++) { S[i] = 0.f; U[i] = 0.f; T[i] = 0.f; }
   const int da = br.dofadr, dn = br.dofnum;
@@ -1068,7 +1097,7 @@ template <class D> INL void body_vel_terms(LDSA WS<D>* W, const LDSA float* qvel
 
 // recursive Newton-Euler (qfrc_bias) adjoint. In: bias-bar in A->vtmp. W->cvel holds the
 // subtree force sums, W->cacc the body forces (velocity_stage overwrote them).
-template <class D> INL void adj_rne(MP m, LDSA WS<D>* W, LDSA WSA<D>* A, int lane) {
+template <class D, class WT, class AT> INL void adj_rne(MP m, LDSA WT* W, LDSA AT* A, int lane) {
   const int nv = m->nv, nbody = m->nbody, maxlevel = m->maxlevel;
   const bool isb = lane > 0 && lane < nbody;
   const int bl = lane < nbody ? lane : 0;  // the pass's model records, issued together
@@ -1192,13 +1221,27 @@ template <class D> INL void adj_rne(MP m, LDSA WS<D>* W, LDSA WSA<D>* A, int lan
 }
 
 // mass matrix (crb / make_m): M[i][j] = cdof_j . I(crb_body(i)) cdof_i (+ armature), j in anc(i)
-template <class D> INL void adj_mass(MP m, LDSA WS<D>* W, LDSA WSA<D>* A, int lane) {
+template <class D, class WT, class AT> INL void adj_mass(MP m, LDSA WT* W, LDSA AT* A, int lane) {
   constexpr int LD = D::LD;
   const int nv = m->nv;
   const bool isd = lane < nv;
   const DofRec dr = ldrec(&m->drec[isd ? lane : 0]);
   const uint32_t descm = m->dof_descmask[isd ? lane : 0];
   const BodyRec brm = ldrec(&m->brec[lane > 0 && lane < m->nbody ? lane : 0]);  // the crb-bar pass below
+  // M-bar[i][j]: the accumulated array, or (lean replay) its rank-one terms in the order and form the
+  // array accumulated them: adj_integrate's rb (qacc - a')^T (damped implicit / eulerdamp), then
+  // adj_solver_rows' -mu qacc^T, each a fused multiply-add onto the running value from 0
+  const bool damp = (m->integrator == MJL_INT_IMPLICITFAST || m->eulerdamp) && m->any_damping;
+  auto mbar = [&](int i, int j) -> float {
+    if constexpr (is_lean<AT>::value) {
+      const float qa = W->qacc[j];
+      float t = 0.f;
+      if (damp) t = fmaf(A->rb[i], qa - A->ap[j], t);
+      return fmaf(-A->mu[i], qa, t);
+    } else {
+      return A->Mb[i * LD + j];
+    }
+  };
   TSTART(tm);
   if (isd) {
     float f6[6];
@@ -1212,17 +1255,17 @@ template <class D> INL void adj_mass(MP m, LDSA WS<D>* W, LDSA WSA<D>* A, int la
     for (uint32_t anc = dr.ancmask; anc;) {  // f-bar_i = sum_j vbar_ij cdof_j
       const int j = 31 - __builtin_clz(anc);
       anc &= ~(1u << j);
-      const float vb = (j == i) ? A->Mb[i * LD + i] : A->Mb[i * LD + j] + A->Mb[j * LD + i];
+      const float vb = (j == i) ? mbar(i, i) : mbar(i, j) + mbar(j, i);
       for (int k = 0; k < 6; k++) fb[k] += vb * W->cdof[j][k];
     }
     const int j = lane;  // cdof-bar_j += sum over descendants i of vbar_ij f_i
     // every dof in ascending order, the sum taking the descendants (the mask's bit loop, unrolled:
     // a root dof has all nv as descendants, and the loop waited for each iteration's LDS reads)
     float cb[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-#pragma unroll
+#pragma unroll 9
     for (int ii = 0; ii < D::NV; ii++) {
       const bool in = (descm >> ii) & 1u;
-      const float a = A->Mb[ii * LD + j], c = A->Mb[j * LD + ii];
+      const float a = mbar(ii, j), c = mbar(j, ii);
       const float vb = (ii == j) ? c : a + c;
       float f[6];
       for (int k = 0; k < 6; k++) f[k] = A->ftmp[ii][k];
@@ -1253,7 +1296,7 @@ template <class D> INL void adj_mass(MP m, LDSA WS<D>* W, LDSA WSA<D>* A, int la
 }
 
 // crb_b = sum of cinert over the subtree of b: cinert-bar_c = sum of crb-bar over ancestors-or-self
-template <class D> INL void adj_crb(MP m, LDSA WSA<D>* A, int lane) {
+template <class D, class AT> INL void adj_crb(MP m, LDSA AT* A, int lane) {
   if (lane > 0 && lane < m->nbody) {
     float s[10] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
     for (uint32_t mk = m->body_ancmask[lane]; mk;) {  // self, then up the chain
@@ -1267,7 +1310,7 @@ template <class D> INL void adj_crb(MP m, LDSA WSA<D>* A, int lane) {
 }
 
 // cinert (com_pos): rotated inertia about the root's subtree com -> xmat, xipos, scom
-template <class D> INL void adj_cinert(MP m, LDSA WS<D>* W, LDSA WSA<D>* A, int lane) {
+template <class D, class WT, class AT> INL void adj_cinert(MP m, LDSA WT* W, LDSA AT* A, int lane) {
   const bool isb = lane > 0 && lane < m->nbody;
   const BodyRec br = ldrec(&m->brec[isb ? lane : 0]);
   float scb[3] = {0.f, 0.f, 0.f};
@@ -1304,7 +1347,7 @@ template <class D> INL void adj_cinert(MP m, LDSA WS<D>* W, LDSA WSA<D>* A, int 
 }
 
 // cdof (com_pos): hinge (axis, axis x (scom_root - anchor)); free rotation uses xmat columns
-template <class D> INL void adj_cdof(MP m, LDSA WS<D>* W, LDSA WSA<D>* A, int lane) {
+template <class D, class WT, class AT> INL void adj_cdof(MP m, LDSA WT* W, LDSA AT* A, int lane) {
   const int nv = m->nv;
   const bool isd = lane < nv;
   const DofRec dr = ldrec(&m->drec[isd ? lane : 0]);
@@ -1343,7 +1386,7 @@ template <class D> INL void adj_cdof(MP m, LDSA WS<D>* W, LDSA WSA<D>* A, int la
 
 // kinematics: root subtree com, joint frames, xipos, the level-by-level tree pass, and the
 // per-body local transforms -> qpos-bar
-template <class D> INL void adj_kinematics(MP m, LDSA WS<D>* W, LDSA WSA<D>* A, int lane) {
+template <class D, class WT, class AT> INL void adj_kinematics(MP m, LDSA WT* W, LDSA AT* A, int lane) {
   const int nbody = m->nbody, maxlevel = m->maxlevel, njnt = m->njnt;
   const bool isb = lane > 0 && lane < nbody;
   // the pass's model records issued together up front (the loops below waited on one dependent
@@ -1636,17 +1679,66 @@ template <class DM, class AT> INL void slot_replay_load(GLBA const float* sw, GL
   (void)NV;
 }
 
+// the lean replay's slot load: the workspace image minus its matrix block (M, H, invd stay in the slot)
+// into WSB, and the A part's pre-step state, aux and a' (Lc, invdc stay in the slot); all global loads
+// issued before the first LDS store, as slot_replay_load
+template <class DM> INL void slot_replay_load_lean(GLBA const float* sw, GLBA const float* sa, LDSA WSB<DM>* W,
+                                                   LDSA WSAL<DM>* A, LDSA float* aux, int lane) {
+  constexpr int LD = DM::LD;
+  constexpr int MOFF = (int)(offsetof(WS<DM>, M) / 16), TOFF = (int)(offsetof(WS<DM>, frc_bias) / 16);
+  constexpr int NB16 = (int)(sizeof(WSB<DM>) / 16), QW = (NB16 + 63) / 64;
+  static_assert(offsetof(WSB<DM>, frc_bias) == offsetof(WS<DM>, M) && offsetof(WS<DM>, M) % 16 == 0 &&
+                    offsetof(WS<DM>, frc_bias) % 16 == 0 &&
+                    sizeof(WSB<DM>) + (offsetof(WS<DM>, frc_bias) - offsetof(WS<DM>, M)) == sizeof(WS<DM>),
+                "WSB is WS without its matrix block");
+  constexpr int O1 = MJL_MAXQ, O2 = O1 + LD, O3 = O2 + 12, O4 = O3 + LD;  // A-part segments up to a'
+  constexpr int QA = (O4 + 63) / 64;
+  f32x4 w[QW];
+  float a[QA];
+#pragma unroll
+  for (int q = 0; q < QW; q++) {
+    const int i = lane + 64 * q;  // WSB index; the slot's WS image has the matrix block at [MOFF, TOFF)
+    if (i < NB16) w[q] = ((GLBA const f32x4*)sw)[i < MOFF ? i : i + (TOFF - MOFF)];
+  }
+#pragma unroll
+  for (int q = 0; q < QA; q++) {
+    const int i = lane + 64 * q;
+    a[q] = i < O4 ? sa[i] : 0.f;
+  }
+#pragma unroll
+  for (int q = 0; q < QW; q++) {
+    const int i = lane + 64 * q;
+    if (i < NB16) ((LDSA f32x4*)W)[i] = w[q];
+  }
+#pragma unroll
+  for (int q = 0; q < QA; q++) {
+    const int i = lane + 64 * q;
+    if (i < O1) ((LDSA float*)A->qpos0)[i] = a[q];
+    else if (i < O2) ((LDSA float*)A->qvel0)[i - O1] = a[q];
+    else if (i < O3) { if (i - O2 < MJL_AUX_DIM) aux[i - O2] = a[q]; }
+    else if (i < O4) ((LDSA float*)A->ap)[i - O3] = a[q];
+  }
+}
+
 // One wave per env: recompute the step from the batch state (not modified), then run the reverse
 // passes. ENV: the env step of envs.py (action flip / clip, reward, aux) without the reset merge.
 // TM (VJP tape): 0 recompute, as above; 1 record: the forward only — the env step itself (outputs
 // and state write-back as mjl_env_step without auto-reset) — leaving in the step's tape slot what
 // the reverse passes read; 2 replay: the reverse passes from the slot, no recompute.
-template <class D, bool ENV, int TM> __global__ __launch_bounds__(64, 1) void vjp_kernel(KParams P, VjpArgs V) {
-  typedef typename std::conditional<TM == 1, WSAR<D>, WSA<D>>::type AT;
-  __shared__ WS<D> Ws;
+// LEAN (replay, implicit VJP): the forward workspace without its matrices (WSB) and the adjoint one
+// without its dense arrays (WSAL) in LDS -- M, H, invd, Lc, invdc read from the tape slot, M-bar formed
+// from its rank-one terms -- so the block fits 20 KB and 2048 envs run as one round of 8 per CU.
+template <class D, bool ENV, int TM, bool LEAN = false>
+__global__ __launch_bounds__(64, LEAN ? 2 : 1) void vjp_kernel(KParams P, VjpArgs V) {
+  static_assert(!LEAN || TM == 2, "the lean layout is the replay's");
+  typedef typename std::conditional<LEAN, WSAL<D>, typename std::conditional<TM == 1, WSAR<D>, WSA<D>>::type>::type AT;
+  typedef typename std::conditional<LEAN, WSB<D>, WS<D>>::type WT;
+  static_assert(!LEAN || sizeof(WT) + sizeof(AT) + 4 * (MJL_AUX_DIM + 3) <= kLdsBudget,
+                "lean replay workspace exceeds the 8-waves-per-CU LDS budget");
+  __shared__ WT Ws;
   __shared__ AT As;
   __shared__ float aux_s[MJL_AUX_DIM + 3];
-  LDSA WS<D>* W = (LDSA WS<D>*)&Ws;
+  LDSA WT* W = (LDSA WT*)&Ws;
   LDSA AT* A = (LDSA AT*)&As;
   LDSA float* aux = (LDSA float*)aux_s;
   constexpr int LD = D::LD;
@@ -1697,7 +1789,8 @@ template <class D, bool ENV, int TM> __global__ __launch_bounds__(64, 1) void vj
   Rows<true> R = global_rows<D>(TM ? (float*)(slot + V.s_r) : scr_env, P.gmax_efc, P.gmax_con);
   if constexpr (TM == 2) {  // replay: the forward's workspace, pre-step state and factors from the slot
     STAMP(0, lane);
-    slot_replay_load<D>(slot + V.s_w, slot + V.s_a, W, A, aux, lane);
+    if constexpr (LEAN) slot_replay_load_lean<D>(slot + V.s_w, slot + V.s_a, W, A, aux, lane);
+    else slot_replay_load<D>(slot + V.s_w, slot + V.s_a, W, A, aux, lane);
     SYNC();
     STAMP(1, lane);
   } else {
@@ -1784,12 +1877,27 @@ template <class D, bool ENV, int TM> __global__ __launch_bounds__(64, 1) void vj
   if (lane < nv) A->vtmp[lane] = V.g_qvel[(size_t)env * nv + lane];
   SYNC();
   if (ENV) adj_env<D>(m, W, A, (CP)P.env, (const float*)aux, V.g_rew[env], V.g_aux + (size_t)env * MJL_AUX_DIM, lane);
-  adj_integrate<D>(m, W, A, gq, unr, lane);
-  if (V.g_ws && lane < nv) A->qaccb[lane] += V.g_ws[(size_t)env * nv + lane];  // output warm start = qacc
-  SYNC();
-  STAMP(2, lane);
-  if (unr) adj_solver_unrolled<D>(m, W, A, R, scr_adj, P.gmax_efc, tp, lane);
-  else adj_solver_rows<D>(m, W, A, R, scr_adj, P.gmax_efc, lane);
+  // the dense arrays: in LDS, or (lean) in the slot's workspace image and A part in global memory
+  if constexpr (LEAN) {
+    GLBA const float* sw = slot + V.s_w;
+    GLBA const float* sa = slot + V.s_a;
+    constexpr int O4 = MJL_MAXQ + 2 * LD + 12, O5 = O4 + LD;  // invdc, Lc in the A part (slot_a_io)
+    const AdjMats<GLBA const float*> mt{sw + offsetof(WS<D>, M) / 4, sw + offsetof(WS<D>, H) / 4,
+                                        sw + offsetof(WS<D>, invd) / 4, sa + O5, sa + O4};
+    adj_integrate<D>(m, W, A, mt, gq, false, lane);
+    if (V.g_ws && lane < nv) A->qaccb[lane] += V.g_ws[(size_t)env * nv + lane];  // output warm start = qacc
+    SYNC();
+    STAMP(2, lane);
+    adj_solver_rows<D>(m, W, A, mt, R, scr_adj, P.gmax_efc, lane);
+  } else {
+    const AdjMats<const LDSA float*> mt{W->M, W->H, W->invd, A->Lc, A->invdc};
+    adj_integrate<D>(m, W, A, mt, gq, unr, lane);
+    if (V.g_ws && lane < nv) A->qaccb[lane] += V.g_ws[(size_t)env * nv + lane];  // output warm start = qacc
+    SYNC();
+    STAMP(2, lane);
+    if (unr) adj_solver_unrolled<D>(m, W, A, R, scr_adj, P.gmax_efc, tp, lane);
+    else adj_solver_rows<D>(m, W, A, mt, R, scr_adj, P.gmax_efc, lane);
+  }
   STAMP(3, lane);
   adj_contact_jac<D>(m, W, A, R, scr_adj, P.gmax_efc, unr ? (GLBA const float*)(tp.acc + 4 * P.gmax_efc) : nullptr,
                      lane);

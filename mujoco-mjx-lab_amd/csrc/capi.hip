@@ -5,6 +5,7 @@
 #include <cmath>
 #include <cstdarg>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <new>
 #include <string>
@@ -787,6 +788,16 @@ template <bool ENV, int TM = 0> static int launch_vjp(mjlBatch* B, const VjpArgs
   V.scratch_stride = B->adj_stride;
   V.row_floats = B->adj_row_floats;
   dim3 grid(B->nenv), block(64);
+  // the implicit replay on the humanoid dims takes the lean layout (20 KB of LDS: one round of 8 envs
+  // per CU; MJL_VJP_LEAN=0 keeps the full one, for A/B)
+  static const bool lean_ok = [] { const char* e = std::getenv("MJL_VJP_LEAN"); return !(e && e[0] == '0'); }();
+  if constexpr (TM == 2) {
+    if (B->model->nvc == 0 && !B->vjp_unrolled && lean_ok) {
+      hipLaunchKernelGGL((vjp_kernel<DHumV, ENV, TM, true>), grid, block, 0, (hipStream_t)stream, P, V);
+      HIPCHK(hipGetLastError());
+      return MJL_OK;
+    }
+  }
   if (B->model->nvc == 0)
     hipLaunchKernelGGL((vjp_kernel<DHumV, ENV, TM>), grid, block, 0, (hipStream_t)stream, P, V);
   else

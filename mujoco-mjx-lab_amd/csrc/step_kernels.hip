@@ -152,52 +152,63 @@ template <class T> INL T ldrec(const CSTA T* p) {
 // ---------------------------------------------------------------------------------------------
 // per-env LDS workspace
 // ---------------------------------------------------------------------------------------------
-template <class DM> struct WS {
-  static constexpr int NV = DM::NV, LD = DM::LD, NB = DM::NB, NJ = DM::NJ, NG = DM::NG;
-  alignas(16) float qpos[MJL_MAXQ];
-  alignas(16) float qvel[LD];
-  alignas(16) float qacc_ws[LD];
-  float ctrl[MJL_MAXU];
-  float xpos[NB][3], xquat[NB][4], xmat[NB][9], xipos[NB][3];
-  float xanchor[NJ][3], xaxis[NJ][3];
-  float gpos[NG][3], gaxis[NG][3];
-  float spos[MJL_MAXSITE][3], smat[MJL_MAXSITE][9];
-  float scom[NB][3];
-  float cdof[NV][6];
+// WS_HEAD / WS_TAIL: the workspace around its three dense-matrix arrays (M, H, invd). WSB<DM> is the
+// same layout without them (the lean replay VJP reads those from the tape slot in global memory):
+// every WSB field sits at its WS offset, shifted by the matrix block past the head.
+#define WS_HEAD                                                                                      \
+  static constexpr int NV = DM::NV, LD = DM::LD, NB = DM::NB, NJ = DM::NJ, NG = DM::NG;             \
+  alignas(16) float qpos[MJL_MAXQ];                                                                \
+  alignas(16) float qvel[LD];                                                                      \
+  alignas(16) float qacc_ws[LD];                                                                   \
+  float ctrl[MJL_MAXU];                                                                            \
+  float xpos[NB][3], xquat[NB][4], xmat[NB][9], xipos[NB][3];                                      \
+  float xanchor[NJ][3], xaxis[NJ][3];                                                              \
+  float gpos[NG][3], gaxis[NG][3];                                                                 \
+  float spos[MJL_MAXSITE][3], smat[MJL_MAXSITE][9];                                                \
+  float scom[NB][3];                                                                               \
+  float cdof[NV][6];                                                                               \
   float tenJ[MJL_MAXTENDON][LD], tenlen[MJL_MAXTENDON];
+#define WS_TAIL                                                                                      \
+  alignas(16) float frc_bias[LD];                                                                  \
+  alignas(16) float frc_passive[LD];                                                               \
+  alignas(16) float frc_act[LD];                                                                   \
+  alignas(16) float frc_smooth[LD];                                                                \
+  alignas(16) float qacc_smooth[LD];                                                               \
+  alignas(16) float qacc[LD];                                                                      \
+  alignas(16) float frc_con[LD];                                                                   \
+  alignas(16) float grad[LD];                                                                      \
+  alignas(16) float Mgrad[LD];                                                                     \
+  alignas(16) float search[LD];                                                                    \
+  alignas(16) float Ma[LD];                                                                        \
+  alignas(16) float Mv[LD];                                                                        \
+  alignas(16) float gradold[LD];                                                                   \
+  alignas(16) float Mgradold[LD];                                                                  \
+  float sens[MJL_MAXSENSOR];                                                                       \
+  float sc[16];                                                                                    \
+  int ncon, nefc, nlim, niter;                                                                     \
+  static constexpr int CAP = DM::CAP, CAPC = DM::CAPC;                                             \
+  union {                                                                                          \
+    /* smooth-dynamics scratch: dead once the constraint rows are built */                         \
+    struct { float cinert[NB][10], crb[NB][10], cvel[NB][6], cacc[NB][6]; };                       \
+    /* constraint rows that fit in LDS */                                                          \
+    struct {                                                                                       \
+      alignas(16) float J[CAP * LD];                                                               \
+      float D[CAP], aref[CAP], jar[CAP], force[CAP], Jv[CAP], epos[CAP], einvw[CAP];               \
+      int emeta[CAP];                                                                              \
+      float con[CAPC * CONW];                                                                      \
+      int con_pair[CAPC], con_efc[CAPC];                                                           \
+    };                                                                                             \
+  };
+template <class DM> struct WS {
+  WS_HEAD
   alignas(16) float M[NV * LD];
   alignas(16) float H[NV * LD];  // factor of M, Newton Hessian + factor, or implicit-integration factor
   alignas(16) float invd[LD];    // 1 / diag of the factor in H
-  alignas(16) float frc_bias[LD];
-  alignas(16) float frc_passive[LD];
-  alignas(16) float frc_act[LD];
-  alignas(16) float frc_smooth[LD];
-  alignas(16) float qacc_smooth[LD];
-  alignas(16) float qacc[LD];
-  alignas(16) float frc_con[LD];
-  alignas(16) float grad[LD];
-  alignas(16) float Mgrad[LD];
-  alignas(16) float search[LD];
-  alignas(16) float Ma[LD];
-  alignas(16) float Mv[LD];
-  alignas(16) float gradold[LD];
-  alignas(16) float Mgradold[LD];
-  float sens[MJL_MAXSENSOR];
-  float sc[16];
-  int ncon, nefc, nlim, niter;
-  static constexpr int CAP = DM::CAP, CAPC = DM::CAPC;
-  union {
-    // smooth-dynamics scratch: dead once the constraint rows are built
-    struct { float cinert[NB][10], crb[NB][10], cvel[NB][6], cacc[NB][6]; };
-    // constraint rows that fit in LDS
-    struct {
-      alignas(16) float J[CAP * LD];
-      float D[CAP], aref[CAP], jar[CAP], force[CAP], Jv[CAP], epos[CAP], einvw[CAP];
-      int emeta[CAP];
-      float con[CAPC * CONW];
-      int con_pair[CAPC], con_efc[CAPC];
-    };
-  };
+  WS_TAIL
+};
+template <class DM> struct WSB {  // WS without M, H, invd
+  WS_HEAD
+  WS_TAIL
 };
 static_assert(sizeof(WS<DHum>) <= kLdsBudget, "humanoid workspace exceeds the 8-waves-per-CU LDS budget");
 
@@ -562,7 +573,8 @@ template <class D> INL float chol_factor_solve(const LDSA float* src, LDSA float
 }
 
 // x distributed (lane i holds b_i, zero for i >= n) -> (L L^T)^-1 b, L from chol_factor
-template <class D> INL float chol_solve(const LDSA float* L, const LDSA float* invd_in, float x, int lane) {
+template <class D, class LP = const LDSA float*, class IP = const LDSA float*>
+INL float chol_solve(LP L, IP invd_in, float x, int lane) {  // L, invd in LDS, or in global memory (lean replay)
   constexpr int NV = D::NV, LD = D::LD;
   // unit-triangular forms, each lane scaling its own row / column by its own 1 / L[i][i]:
   // L y = b  <=>  (diag(L)^-1 L) y = diag(L)^-1 b;  L^T z = y  <=>  (L diag(L)^-1)^T z = diag(L)^-1 y,
