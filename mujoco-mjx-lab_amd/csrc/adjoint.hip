@@ -150,10 +150,11 @@ template <class DM> struct WSA {
   WSA_P3
   alignas(16) float uv[3][LD];         // unrolled mode: vectors staged for M v / J v products
 };
-template <class DM> struct WSAL {  // lean replay: WSA without Lc, invdc, Mb, uv
+template <class DM> struct WSAL {  // lean replay: WSA without Lc, invdc, Mb
   WSA_P1
   WSA_P2
   WSA_P3
+  alignas(16) float uv[3][LD];         // unrolled mode: vectors staged for M v / J v products
 };
 template <class AT> struct is_lean { static constexpr bool value = false; };
 template <class DM> struct is_lean<WSAL<DM>> { static constexpr bool value = true; };
@@ -162,6 +163,7 @@ template <class DM> struct is_lean<WSAL<DM>> { static constexpr bool value = tru
 // of Hc) in LDS (WS / WSA), or in the tape slot in global memory (lean replay)
 template <class P> struct AdjMats {
   P M, H, invd, Lc, invdc;
+  GLBA float* Mb;  // lean unrolled replay: M-bar rows in the env's global scratch (else unused)
 };
 
 // per-env global scratch of the adjoint (after the env's row slab): per row (alpha, gamma, posbar),
@@ -420,14 +422,19 @@ template <class D, class WT, class AT, class MT> INL void adj_integrate(MP m, LD
     SYNC();
     if (lane < nv) {
       const float rl = A->rb[lane];
-      if constexpr (is_lean<AT>::value) {  // M-bar's term rb (qacc - a')^T: formed in adj_mass
-        A->qaccb[lane] += rowdot<LD>(mt.M + lane * LD, A->rb);
-      } else if (unr) {  // a' = Hd^-1 (qfrc_smooth + qfrc_constraint)
-        for (int k = 0; k < nv; k++) A->Mb[lane * LD + k] -= rl * A->ap[k];
+      if (unr) {  // a' = Hd^-1 (qfrc_smooth + qfrc_constraint)
+        if constexpr (is_lean<AT>::value) {
+          GLBA float* row = mt.Mb + lane * LD;  // zeroed at kernel start
+          for (int k = 0; k < nv; k++) row[k] -= rl * A->ap[k];
+        } else {
+          for (int k = 0; k < nv; k++) A->Mb[lane * LD + k] -= rl * A->ap[k];
+        }
         A->frcsb[lane] += rl;
         A->qfcb[lane] += rl;
       } else {
-        for (int k = 0; k < nv; k++) A->Mb[lane * LD + k] += rl * (W->qacc[k] - A->ap[k]);
+        // lean: M-bar's term rb (qacc - a')^T is formed in adj_mass
+        if constexpr (!is_lean<AT>::value)
+          for (int k = 0; k < nv; k++) A->Mb[lane * LD + k] += rl * (W->qacc[k] - A->ap[k]);
         A->qaccb[lane] += rowdot<LD>(mt.M + lane * LD, A->rb);  // (M rb)[lane] (mrow)
       }
     }
@@ -524,9 +531,13 @@ template <class D, class WT, class AT, class MT> INL void adj_solver_rows(MP m, 
 // line). In: A->qaccb, A->qfcb (cotangents of the final qacc and qfrc_constraint). Out: A->Mb,
 // A->frcsb, the per-row aref / D cotangents (mapped by adj_row_map) and J-bar rows (u.rows Jbar,
 // read by adj_contact_jac). Vectors are lane-resident (lane = dof); uv[] stages M v / J v operands.
-template <class D> INL void adj_solver_unrolled(MP m, LDSA WS<D>* W, LDSA WSA<D>* A, Rows<true> R, GLBA float* scr,
-                                                int nefc_max, const SolveTape& tp, int lane) {
+// Lean replay (CG only): chol(M) comes from the tape slot (the record step's forward factor), and the
+// lane's M-bar row accumulates in registers between one load and one store of its global scratch row.
+template <class D, class WT, class AT, class MT>
+INL void adj_solver_unrolled(MP m, LDSA WT* W, LDSA AT* A, const MT& mt, Rows<true> R, GLBA float* scr, int nefc_max,
+                             const SolveTape& tp, int lane) {
   constexpr int LD = D::LD;
+  constexpr bool LEAN = is_lean<AT>::value;
   const int nv = m->nv, nefc = W->nefc;
   const bool cg = m->solver != MJL_SOLVER_NEWTON;
   const TapeDims& d = tp.d;
@@ -578,17 +589,36 @@ template <class D> INL void adj_solver_unrolled(MP m, LDSA WS<D>* W, LDSA WSA<D>
     }
     return x;
   };
+  float mbr[LEAN ? LD : 1];  // lean: this lane's M-bar row
+  if constexpr (LEAN) {
+    const GLBA f32x4* g = (const GLBA f32x4*)(mt.Mb + (isd ? lane : 0) * LD);
+#pragma unroll
+    for (int q = 0; q < LD / 4; q++) {
+      const f32x4 x = g[q];
+#pragma unroll
+      for (int e = 0; e < 4; e++) mbr[4 * q + e] = x[e];
+    }
+  }
   auto mb_outer = [&](float a, LDSA const float* v) {  // Mb[lane][:] += a v' (v zero beyond nv)
     if (isd) {
-      LDSA f32x4* row = (LDSA f32x4*)(A->Mb + lane * LD);
       const LDSA f32x4* vv = (const LDSA f32x4*)v;
+      if constexpr (LEAN) {
 #pragma unroll
-      for (int q = 0; q < LD / 4; q++) {
-        f32x4 x = row[q];
-        const f32x4 y = vv[q];
+        for (int q = 0; q < LD / 4; q++) {
+          const f32x4 y = vv[q];
 #pragma unroll
-        for (int e = 0; e < 4; e++) x[e] += a * y[e];
-        row[q] = x;
+          for (int e = 0; e < 4; e++) mbr[4 * q + e] += a * y[e];
+        }
+      } else {
+        LDSA f32x4* row = (LDSA f32x4*)(A->Mb + lane * LD);
+#pragma unroll
+        for (int q = 0; q < LD / 4; q++) {
+          f32x4 x = row[q];
+          const f32x4 y = vv[q];
+#pragma unroll
+          for (int e = 0; e < 4; e++) x[e] += a * y[e];
+          row[q] = x;
+        }
       }
     }
   };
@@ -597,11 +627,13 @@ template <class D> INL void adj_solver_unrolled(MP m, LDSA WS<D>* W, LDSA WSA<D>
     for (int r = 0; r < nefc; r++) Jbar[r * LD + lane] = 0.f;
   const int nup = (int)tp.t[0], nls = (int)tp.t[1], K = nup - 1;
   const int wsel = nup > 0 ? (int)tp.t[2] : 1;
-  // L(M) in A->Lc (CG preconditioner; the smooth warm start)
-  stage(V1, 0.f);
-  SYNC();
-  chol_factor_solve<D>(W->M, A->Lc, A->invdc, nv, V1, lane);
-  SYNC();
+  // L(M) in A->Lc (CG preconditioner; the smooth warm start); lean: mt.Lc, the slot's copy
+  if constexpr (!LEAN) {
+    stage(V1, 0.f);
+    SYNC();
+    chol_factor_solve<D>(W->M, A->Lc, A->invdc, nv, V1, lane);
+    SYNC();
+  }
   float qb = ld(A->qaccb), sb = 0.f, gb = 0.f, mgb = 0.f;
   for (int k = K; k >= 0; k--) {
     GLBA const float* u = tp.upd(k);
@@ -634,9 +666,9 @@ template <class D> INL void adj_solver_unrolled(MP m, LDSA WS<D>* W, LDSA WSA<D>
       stage(V1, mgb);
       stage(V2, mg_k);
       SYNC();
-      if (cg) {
-        lam = chol_solve<D>(A->Lc, A->invdc, mgb, lane);
-      } else {  // H_k = M + J' D_A J over update k's active rows (the tape's mask)
+      if (LEAN || cg) {
+        lam = chol_solve<D>(mt.Lc, mt.invdc, mgb, lane);
+      } else if constexpr (!LEAN) {  // H_k = M + J' D_A J over update k's active rows (the tape's mask)
         for (int r = lane; r < nefc; r += 64) R.jar[r] = bit(u + 3 * LD + 4, r) ? -1.f : 1.f;
         SYNC();
         if constexpr (D::NV < 32) {
@@ -670,7 +702,7 @@ template <class D> INL void adj_solver_unrolled(MP m, LDSA WS<D>* W, LDSA WSA<D>
     stage(V2, q_k);
     stage(V3, qfcb);
     SYNC();
-    qb += isd ? mrow<D>(W, V1, lane) : 0.f;
+    qb += isd ? rowdot<LD>(mt.M + lane * LD, V1) : 0.f;  // (M gb)[lane]
     mb_outer(gb, V2);
     for (int r = lane; r < nefc; r += 64) {
       const bool act = bit(u + 3 * LD + 4, r);
@@ -715,7 +747,7 @@ template <class D> INL void adj_solver_unrolled(MP m, LDSA WS<D>* W, LDSA WSA<D>
     }
     jbar_add(V1, V2);
     SYNC();
-    const float Ms = isd ? mrow<D>(W, V1, lane) : 0.f, Mq = isd ? mrow<D>(W, V2, lane) : 0.f;
+    const float Ms = isd ? rowdot<LD>(mt.M + lane * LD, V1) : 0.f, Mq = isd ? rowdot<LD>(mt.M + lane * LD, V2) : 0.f;
     const float f = ld(W->frc_smooth);
     sbp += c1b * (Mq - f) + 2.f * c2b * Ms + jt(ca);
     qb += c1b * Ms + jt(cb);
@@ -731,13 +763,26 @@ template <class D> INL void adj_solver_unrolled(MP m, LDSA WS<D>* W, LDSA WSA<D>
     stage(V1, qb);
     SYNC();
     float lam;
-    if (cg) lam = chol_solve<D>(A->Lc, A->invdc, qb, lane);
+    if constexpr (LEAN) lam = chol_solve<D>(mt.Lc, mt.invdc, qb, lane);
+    else if (cg) lam = chol_solve<D>(mt.Lc, mt.invdc, qb, lane);
     else lam = chol_factor_solve<D>(W->M, A->Lc, A->invdc, nv, V1, lane);
     if (!isd) lam = 0.f;
     if (isd) A->frcsb[lane] += lam;
     mb_outer(-lam, W->qacc_smooth);
   } else if (isd) {  // q_0 = qacc_warmstart: jax.grad carries this cotangent to the previous step
     A->wsb[lane] = qb;
+  }
+  if constexpr (LEAN) {  // the M-bar row back to its scratch row (adj_mass reads it)
+    if (isd) {
+      GLBA f32x4* g = (GLBA f32x4*)(mt.Mb + lane * LD);
+#pragma unroll
+      for (int q = 0; q < LD / 4; q++) {
+        f32x4 x;
+#pragma unroll
+        for (int e = 0; e < 4; e++) x[e] = mbr[4 * q + e];
+        g[q] = x;
+      }
+    }
   }
   SYNC();
   for (int r = lane; r < nefc; r += 64) adj_row_map<D>(m, R, scr, nefc_max, r, arefb[r], Dbar[r], 0.f);
@@ -1221,7 +1266,8 @@ template <class D, class WT, class AT> INL void adj_rne(MP m, LDSA WT* W, LDSA A
 }
 
 // mass matrix (crb / make_m): M[i][j] = cdof_j . I(crb_body(i)) cdof_i (+ armature), j in anc(i)
-template <class D, class WT, class AT> INL void adj_mass(MP m, LDSA WT* W, LDSA AT* A, int lane) {
+template <class D, class WT, class AT, class MT>
+INL void adj_mass(MP m, LDSA WT* W, LDSA AT* A, const MT& mt, bool unr, int lane) {
   constexpr int LD = D::LD;
   const int nv = m->nv;
   const bool isd = lane < nv;
@@ -1232,16 +1278,6 @@ template <class D, class WT, class AT> INL void adj_mass(MP m, LDSA WT* W, LDSA 
   // array accumulated them: adj_integrate's rb (qacc - a')^T (damped implicit / eulerdamp), then
   // adj_solver_rows' -mu qacc^T, each a fused multiply-add onto the running value from 0
   const bool damp = (m->integrator == MJL_INT_IMPLICITFAST || m->eulerdamp) && m->any_damping;
-  auto mbar = [&](int i, int j) -> float {
-    if constexpr (is_lean<AT>::value) {
-      const float qa = W->qacc[j];
-      float t = 0.f;
-      if (damp) t = fmaf(A->rb[i], qa - A->ap[j], t);
-      return fmaf(-A->mu[i], qa, t);
-    } else {
-      return A->Mb[i * LD + j];
-    }
-  };
   TSTART(tm);
   if (isd) {
     float f6[6];
@@ -1250,7 +1286,8 @@ template <class D, class WT, class AT> INL void adj_mass(MP m, LDSA WT* W, LDSA 
   }
   SYNC();
   float fb[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-  if (isd) {
+  // the loops, instantiated per M-bar source (the choice made once, outside them)
+  auto loops = [&](auto mbar) {
     const int i = lane;
     for (uint32_t anc = dr.ancmask; anc;) {  // f-bar_i = sum_j vbar_ij cdof_j
       const int j = 31 - __builtin_clz(anc);
@@ -1272,6 +1309,22 @@ template <class D, class WT, class AT> INL void adj_mass(MP m, LDSA WT* W, LDSA 
       for (int k = 0; k < 6; k++) cb[k] = in ? cb[k] + vb * f[k] : cb[k];
     }
     for (int k = 0; k < 6; k++) A->cdofb[j][k] += cb[k];
+  };
+  if (isd) {
+    if constexpr (is_lean<AT>::value) {
+      if (unr) {  // unrolled: the rows adj_solver_unrolled accumulated
+        loops([&](int i, int j) -> float { return mt.Mb[i * LD + j]; });
+      } else if (damp) {
+        loops([&](int i, int j) -> float {
+          const float qa = W->qacc[j];
+          return fmaf(-A->mu[i], qa, fmaf(A->rb[i], qa - A->ap[j], 0.f));
+        });
+      } else {
+        loops([&](int i, int j) -> float { return fmaf(-A->mu[i], W->qacc[j], 0.f); });
+      }
+    } else {
+      loops([&](int i, int j) -> float { return A->Mb[i * LD + j]; });
+    }
   }
   SYNC();
   TACC(30, tm, lane);
@@ -1833,6 +1886,13 @@ __global__ __launch_bounds__(64, LEAN ? 2 : 1) void vjp_kernel(KParams P, VjpArg
     if (lane < LD) W->qacc_smooth[lane] = (lane < nv) ? x : 0.f;
     SYNC();
   }
+  if constexpr (TM == 1) {  // unrolled CG: chol(M) -- the reverse sweep's preconditioner -- in the slot's Lc
+    if (unr && m->solver != MJL_SOLVER_NEWTON) {
+      for (int i = lane; i < D::NV * LD; i += 64) A->Lc[i] = W->H[i];
+      if (lane < LD) A->invdc[lane] = W->invd[lane];
+      SYNC();
+    }
+  }
   build_rows<D, true>(m, W, R, lane);
   if (unr) {
     solver_t<D, true>(m, W, R, lane, tp);  // the same solve, recording its tape
@@ -1873,31 +1933,36 @@ __global__ __launch_bounds__(64, LEAN ? 2 : 1) void vjp_kernel(KParams P, VjpArg
   }
   if constexpr (TM != 1) {
   // ---- reverse
+  const auto mats = [&] {
+    if constexpr (LEAN) {
+      GLBA const float* sw = slot + V.s_w;
+      GLBA const float* sa = slot + V.s_a;
+      constexpr int O4 = MJL_MAXQ + 2 * LD + 12, O5 = O4 + LD;  // invdc, Lc in the A part (slot_a_io)
+      return AdjMats<GLBA const float*>{sw + offsetof(WS<D>, M) / 4, sw + offsetof(WS<D>, H) / 4,
+                                        sw + offsetof(WS<D>, invd) / 4, sa + O5, sa + O4,
+                                        (GLBA float*)(scr_adj + adj_scratch_floats(P.gmax_efc, P.gmax_con))};
+    } else {
+      return AdjMats<const LDSA float*>{W->M, W->H, W->invd, A->Lc, A->invdc, nullptr};
+    }
+  }();
+  if constexpr (LEAN) {  // unrolled: zero this env's M-bar scratch rows
+    if (unr && lane < nv) {
+      GLBA f32x4* g = (GLBA f32x4*)(mats.Mb + lane * LD);
+#pragma unroll
+      for (int q = 0; q < LD / 4; q++) g[q] = f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+  }
   const float* gq = V.g_qpos + (size_t)env * nq;
   if (lane < nv) A->vtmp[lane] = V.g_qvel[(size_t)env * nv + lane];
   SYNC();
   if (ENV) adj_env<D>(m, W, A, (CP)P.env, (const float*)aux, V.g_rew[env], V.g_aux + (size_t)env * MJL_AUX_DIM, lane);
-  // the dense arrays: in LDS, or (lean) in the slot's workspace image and A part in global memory
-  if constexpr (LEAN) {
-    GLBA const float* sw = slot + V.s_w;
-    GLBA const float* sa = slot + V.s_a;
-    constexpr int O4 = MJL_MAXQ + 2 * LD + 12, O5 = O4 + LD;  // invdc, Lc in the A part (slot_a_io)
-    const AdjMats<GLBA const float*> mt{sw + offsetof(WS<D>, M) / 4, sw + offsetof(WS<D>, H) / 4,
-                                        sw + offsetof(WS<D>, invd) / 4, sa + O5, sa + O4};
-    adj_integrate<D>(m, W, A, mt, gq, false, lane);
-    if (V.g_ws && lane < nv) A->qaccb[lane] += V.g_ws[(size_t)env * nv + lane];  // output warm start = qacc
-    SYNC();
-    STAMP(2, lane);
-    adj_solver_rows<D>(m, W, A, mt, R, scr_adj, P.gmax_efc, lane);
-  } else {
-    const AdjMats<const LDSA float*> mt{W->M, W->H, W->invd, A->Lc, A->invdc};
-    adj_integrate<D>(m, W, A, mt, gq, unr, lane);
-    if (V.g_ws && lane < nv) A->qaccb[lane] += V.g_ws[(size_t)env * nv + lane];  // output warm start = qacc
-    SYNC();
-    STAMP(2, lane);
-    if (unr) adj_solver_unrolled<D>(m, W, A, R, scr_adj, P.gmax_efc, tp, lane);
-    else adj_solver_rows<D>(m, W, A, mt, R, scr_adj, P.gmax_efc, lane);
-  }
+  // the dense arrays (mats): in LDS, or (lean) in the slot's workspace image and A part in global memory
+  adj_integrate<D>(m, W, A, mats, gq, unr, lane);
+  if (V.g_ws && lane < nv) A->qaccb[lane] += V.g_ws[(size_t)env * nv + lane];  // output warm start = qacc
+  SYNC();
+  STAMP(2, lane);
+  if (unr) adj_solver_unrolled<D>(m, W, A, mats, R, scr_adj, P.gmax_efc, tp, lane);
+  else adj_solver_rows<D>(m, W, A, mats, R, scr_adj, P.gmax_efc, lane);
   STAMP(3, lane);
   adj_contact_jac<D>(m, W, A, R, scr_adj, P.gmax_efc, unr ? (GLBA const float*)(tp.acc + 4 * P.gmax_efc) : nullptr,
                      lane);
@@ -1910,7 +1975,7 @@ __global__ __launch_bounds__(64, LEAN ? 2 : 1) void vjp_kernel(KParams P, VjpArg
   STAMP(7, lane);
   adj_rne<D>(m, W, A, lane);
   STAMP(8, lane);
-  adj_mass<D>(m, W, A, lane);
+  adj_mass<D>(m, W, A, mats, unr, lane);
   STAMP(9, lane);
   adj_crb<D>(m, A, lane);
   STAMP(10, lane);

@@ -769,6 +769,7 @@ template <bool ENV, int TM = 0> static int launch_vjp(mjlBatch* B, const VjpArgs
     B->adj_row_floats = B->gmax_efc * (LD + 8) + B->gmax_con * (CONW + 2);
     B->adj_row_floats = (B->adj_row_floats + 3) & ~3;
     B->adj_stride = B->adj_row_floats + adj_scratch_floats(B->gmax_efc, B->gmax_con);
+    if (B->model->nvc == 0) B->adj_stride += DHumV::NV * DHumV::LD;  // lean unrolled replay: M-bar rows
     B->adj_stride = (B->adj_stride + 3) & ~3;
     hipError_t e = hipMalloc(&B->d_adj_scratch, (size_t)B->adj_stride * B->nenv * sizeof(float));
     if (e != hipSuccess) { B->d_adj_scratch = nullptr; return fail(MJL_ERR_HIP, "adjoint scratch: %s", hipGetErrorString(e)); }
@@ -788,11 +789,13 @@ template <bool ENV, int TM = 0> static int launch_vjp(mjlBatch* B, const VjpArgs
   V.scratch_stride = B->adj_stride;
   V.row_floats = B->adj_row_floats;
   dim3 grid(B->nenv), block(64);
-  // the implicit replay on the humanoid dims takes the lean layout (20 KB of LDS: one round of 8 envs
-  // per CU; MJL_VJP_LEAN=0 keeps the full one, for A/B)
+  // the replay on the humanoid dims takes the lean layout (20 KB of LDS: one round of 8 envs per CU;
+  // MJL_VJP_LEAN=0 keeps the full one, for A/B)
   static const bool lean_ok = [] { const char* e = std::getenv("MJL_VJP_LEAN"); return !(e && e[0] == '0'); }();
   if constexpr (TM == 2) {
-    if (B->model->nvc == 0 && !B->vjp_unrolled && lean_ok) {
+    // (unrolled: CG only -- its reverse sweep refactors nothing; Newton's per-iteration Hessian factors
+    // need the full layout's LDS)
+    if (B->model->nvc == 0 && (!B->vjp_unrolled || B->model->desc.solver == MJL_SOLVER_CG) && lean_ok) {
       hipLaunchKernelGGL((vjp_kernel<DHumV, ENV, TM, true>), grid, block, 0, (hipStream_t)stream, P, V);
       HIPCHK(hipGetLastError());
       return MJL_OK;
