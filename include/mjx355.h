@@ -338,7 +338,9 @@ int mjl_policy_fwd(const float* obs, const float* mean, const float* var, float 
  * the pre-step qpos / qvel / aux, the factor of the converged Hessian, the unrolled solve's tape);
  * mjl_env_step_vjp_replay is mjl_env_step_vjp_full of that step from the slot, without the
  * recompute and without restoring the pre-step state first. Requires MJL_OPT_VJP_TAPE; the VJP mode
- * (MJL_OPT_VJP_UNROLLED) must be the same at record and replay. */
+ * (MJL_OPT_VJP_UNROLLED) must be the same at record and replay. On the humanoid dims the replay
+ * (implicit, or unrolled with the CG solver) runs the lean layout: 19.5 KB of LDS per env, the dense
+ * matrices read from the slot (environment MJL_VJP_LEAN=0 selects the full layout; same results). */
 int mjl_env_step_record(mjlBatch* batch, int slot, const float* act, float* obs, float* rew, float* term,
                         float* trunc, void* stream);
 int mjl_env_step_vjp_replay(mjlBatch* batch, int slot, const float* act, const float* g_qpos, const float* g_qvel,
@@ -364,6 +366,16 @@ int mjl_apg_post(mjlBatch* batch, const float* rew, const float* term, const flo
                  void* stream);
 int mjl_apg_obs_vjp(int nenv, int nq, int nv, const float* o, const uint8_t* alive_snap, const float* mean,
                     const float* var, int use_norm, const float* go, float* g_qpos, float* g_qvel, void* stream);
+/* The APG policy's per-step passes (src/networks.py:63-80 APGPolicy: Dense + tanh per layer, the
+ * output tanh-squashed; train_apg.py:177 and its jax.grad): nl <= 4 layers, widths and k0 <= 64,
+ * float32 row-major, w[l] = [widths[l], k_l] (torch Linear.weight), b[l] = [widths[l]], k_l = l ?
+ * widths[l-1] : k0. mjl_small_mlp_fwd: ys[l] = tanh(ys[l-1] w[l]^T + b[l]) ([B, widths[l]], ys[-1] =
+ * x), every sum in k order from the bias. mjl_small_mlp_bwd_input: g_x = d/dx of <g_out, ys[nl-1]>
+ * from the forward's ys (the observation cotangent of the reverse sweep; no parameter gradients). */
+int mjl_small_mlp_fwd(const float* x, int B, int k0, int nl, const int* widths, const float* const* w,
+                      const float* const* b, float* const* ys, void* stream);
+int mjl_small_mlp_bwd_input(const float* g_out, int B, int k0, int nl, const int* widths, const float* const* w,
+                            const float* const* ys, float* g_x, void* stream);
 
 /* PPO update (train_ppo.py:233-252, the bias-gradient column sums of every dense layer's backward
  * in value_and_grad of ppo_loss_fn / value_loss_fn, and the split-K weight-gradient sum):

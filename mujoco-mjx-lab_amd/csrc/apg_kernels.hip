@@ -103,4 +103,84 @@ __global__ void apg_obs_vjp_kernel(int B, int nq, int nv, const float* __restric
   else g_qvel[(size_t)e * nv + (j - nq)] = g_qvel[(size_t)e * nv + (j - nq)] + g;
 }
 
+// The APG policy's per-step passes (networks.py:63-80: a tanh MLP with a tanh-squashed output;
+// mjx_amd APGPolicy) as one launch each, where torch ran three GEMMs and three tanh launches forward
+// and three GEMMs and three tanh-backward launches for the observation cotangent (~4.5 us each at
+// 2048 rows: 12 launches per rollout step). A block takes kSmlThreads / U rows, thread (row, unit
+// < U) one output unit; each layer's weights are staged through LDS (transposed for the forward so
+// the units read consecutive words), activations through LDS, sums in k order from the bias.
+constexpr int kSmlMaxW = 64, kSmlMaxL = 4, kSmlThreads = 256;
+struct SmallMlp {
+  int nl, k0, u;            // layers, input width, units per row slot (32 or 64: >= every width)
+  int n[kSmlMaxL];          // layer widths; layer l reads k = l ? n[l - 1] : k0
+  const float* w[kSmlMaxL];  // [n_l, k_l] row-major (torch Linear.weight)
+  const float* b[kSmlMaxL];
+  float* y[kSmlMaxL];       // [B, n_l] tanh outputs: written by the forward, read by the backward
+};
+
+__global__ __launch_bounds__(kSmlThreads) void small_mlp_fwd_kernel(const float* __restrict__ x, int B, SmallMlp P) {
+  __shared__ float wt[kSmlMaxW * kSmlMaxW];
+  __shared__ float h[2][kSmlThreads / 32][kSmlMaxW];
+  const int U = P.u, R = kSmlThreads / U, t = threadIdx.x, r = t / U, j = t - r * U;
+  const int row0 = blockIdx.x * R, row = row0 + r;
+  for (int e = t; e < R * P.k0; e += kSmlThreads) {
+    const int rr = e / P.k0, k = e - rr * P.k0;
+    h[0][rr][k] = row0 + rr < B ? x[(size_t)(row0 + rr) * P.k0 + k] : 0.f;
+  }
+  int K = P.k0, cur = 0;
+  for (int l = 0; l < P.nl; l++) {
+    const int N = P.n[l];
+    const float* __restrict__ W = P.w[l];
+    __syncthreads();  // the previous layer's activations written, its weights no longer read
+    for (int e = t; e < N * K; e += kSmlThreads) {
+      const int jj = e / K, k = e - jj * K;
+      wt[k * N + jj] = W[e];
+    }
+    __syncthreads();
+    if (j < N) {
+      float s = P.b[l][j];
+      for (int k = 0; k < K; k++) s = fmaf(wt[k * N + j], h[cur][r][k], s);
+      const float y = tanhf(s);
+      h[cur ^ 1][r][j] = y;
+      if (row < B) P.y[l][(size_t)row * N + j] = y;
+    }
+    cur ^= 1;
+    K = N;
+  }
+}
+
+// d loss / d x from d loss / d y_L (ga): g = ga (1 - y_L^2), then per layer from the top
+// g_in = W_l^T g, times (1 - y_{l-1}^2) below the first layer; gx = W_0^T g
+__global__ __launch_bounds__(kSmlThreads) void small_mlp_bwd_input_kernel(const float* __restrict__ ga, int B,
+                                                                          SmallMlp P, float* __restrict__ gx) {
+  __shared__ float wl[kSmlMaxW * kSmlMaxW];
+  __shared__ float g[2][kSmlThreads / 32][kSmlMaxW];
+  const int U = P.u, R = kSmlThreads / U, t = threadIdx.x, r = t / U, u = t - r * U;
+  const int row = blockIdx.x * R + r;
+  const int L = P.nl, NL = P.n[L - 1];
+  if (u < NL) {
+    const float y = row < B ? P.y[L - 1][(size_t)row * NL + u] : 0.f;
+    g[0][r][u] = row < B ? ga[(size_t)row * NL + u] * (1.f - y * y) : 0.f;
+  }
+  int cur = 0;
+  for (int l = L - 1; l >= 0; l--) {
+    const int N = P.n[l], K = l ? P.n[l - 1] : P.k0;
+    const float* __restrict__ W = P.w[l];
+    __syncthreads();
+    for (int e = t; e < N * K; e += kSmlThreads) wl[e] = W[e];
+    __syncthreads();
+    if (u < K) {
+      float s = 0.f;
+      for (int jj = 0; jj < N; jj++) s = fmaf(wl[jj * K + u], g[cur][r][jj], s);
+      if (l) {
+        const float y = row < B ? P.y[l - 1][(size_t)row * K + u] : 0.f;
+        g[cur ^ 1][r][u] = s * (1.f - y * y);
+      } else if (row < B) {
+        gx[(size_t)row * K + u] = s;
+      }
+    }
+    cur ^= 1;
+  }
+}
+
 }  // namespace mjl

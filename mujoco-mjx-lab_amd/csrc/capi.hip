@@ -1074,6 +1074,53 @@ extern "C" int mjl_prng_split(const uint32_t* keys, int n, int num, int mode, ui
 }
 
 // ---------------------------------------------------------------- APG rollout bookkeeping
+static int small_mlp_setup(int B, int k0, int nl, const int* widths, const float* const* w, const float* const* b,
+                           float* const* ys, SmallMlp& P) {
+  if (B < 0 || nl < 1 || nl > kSmlMaxL || k0 < 1 || k0 > kSmlMaxW || !widths || !w || !b || !ys)
+    return fail(MJL_ERR_ARG, "small MLP: 1..%d layers of width 1..%d expected", kSmlMaxL, kSmlMaxW);
+  std::memset(&P, 0, sizeof(P));
+  P.nl = nl; P.k0 = k0;
+  int wmax = k0;
+  for (int l = 0; l < nl; l++) {
+    if (widths[l] < 1 || widths[l] > kSmlMaxW || !w[l] || !b[l] || !ys[l])
+      return fail(MJL_ERR_ARG, "small MLP: layer %d: width 1..%d and non-null pointers expected", l, kSmlMaxW);
+    P.n[l] = widths[l]; P.w[l] = w[l]; P.b[l] = b[l]; P.y[l] = ys[l];
+    wmax = widths[l] > wmax ? widths[l] : wmax;
+  }
+  P.u = wmax <= 32 ? 32 : 64;
+  return MJL_OK;
+}
+
+extern "C" int mjl_small_mlp_fwd(const float* x, int B, int k0, int nl, const int* widths, const float* const* w,
+                                 const float* const* b, float* const* ys, void* stream) {
+  SmallMlp P;
+  int rc = small_mlp_setup(B, k0, nl, widths, w, b, ys, P);
+  if (rc != MJL_OK) return rc;
+  if (!x && B > 0) return fail(MJL_ERR_ARG, "bad argument");
+  if (B == 0) return MJL_OK;
+  const int R = kSmlThreads / P.u;
+  hipLaunchKernelGGL(small_mlp_fwd_kernel, dim3((unsigned)((B + R - 1) / R)), dim3(kSmlThreads), 0, (hipStream_t)stream,
+                     x, B, P);
+  HIPCHK(hipGetLastError());
+  return MJL_OK;
+}
+
+extern "C" int mjl_small_mlp_bwd_input(const float* g_out, int B, int k0, int nl, const int* widths,
+                                       const float* const* w, const float* const* ys, float* g_x, void* stream) {
+  SmallMlp P;
+  if (!w || !w[0]) return fail(MJL_ERR_ARG, "bad argument");
+  const float* nob[kSmlMaxL] = {w[0], w[0], w[0], w[0]};  // biases unused by the backward
+  int rc = small_mlp_setup(B, k0, nl, widths, w, nob, (float* const*)ys, P);
+  if (rc != MJL_OK) return rc;
+  if ((!g_out || !g_x) && B > 0) return fail(MJL_ERR_ARG, "bad argument");
+  if (B == 0) return MJL_OK;
+  const int R = kSmlThreads / P.u;
+  hipLaunchKernelGGL(small_mlp_bwd_input_kernel, dim3((unsigned)((B + R - 1) / R)), dim3(kSmlThreads), 0,
+                     (hipStream_t)stream, g_out, B, P, g_x);
+  HIPCHK(hipGetLastError());
+  return MJL_OK;
+}
+
 extern "C" int mjl_apg_obs(mjlBatch* B, const uint8_t* alive, const float* mean, const float* var, int use_norm,
                            float* o, float* on, uint8_t* alive_snap, void* stream) {
   if (!B || !alive || !o || !on || !alive_snap || (use_norm && (!mean || !var))) return fail(MJL_ERR_ARG, "bad argument");

@@ -23,7 +23,8 @@ EXPORTS = [
     "mjl_forward", "mjl_step", "mjl_speedtest_step", "mjl_env_config", "mjl_env_step", "mjl_env_reset",
     "mjl_step_vjp", "mjl_env_step_vjp", "mjl_gae", "mjl_batch_set_counter_base",
     "mjl_env_set_reset_keys", "mjl_prng_split", "mjl_env_step_vjp_guarded", "mjl_state_size", "mjl_get_state",
-    "mjl_set_state", "mjl_obs_normalize", "mjl_policy_head", "mjl_colsum_scratch", "mjl_colsum", "mjl_tanh_bwd_colsum", "mjl_slice_sum", "mjl_tanh_inplace",
+    "mjl_set_state", "mjl_obs_normalize", "mjl_policy_head", "mjl_colsum_scratch", "mjl_colsum", "mjl_tanh_bwd_colsum", "mjl_slice_sum", "mjl_tanh_inplace", "mjl_small_mlp_fwd",
+    "mjl_small_mlp_bwd_input",
     "mjl_policy_param_floats", "mjl_policy_fwd",
     "mjl_step_vjp_full", "mjl_env_step_vjp_full", "mjl_env_fill_reset_pool",
     "mjl_apg_obs", "mjl_apg_post", "mjl_apg_obs_vjp", "mjl_env_step_record", "mjl_env_step_vjp_replay",
@@ -122,6 +123,8 @@ def lib() -> C.CDLL:
     L.mjl_tanh_bwd_colsum.argtypes = [f32p, f32p, i32, i32, f32p, f32p, f32p, vp]
     L.mjl_slice_sum.argtypes = [f32p, i32, C.c_longlong, f32p, vp]
     L.mjl_tanh_inplace.argtypes = [f32p, C.c_longlong, vp]
+    L.mjl_small_mlp_fwd.argtypes = [vp, i32, i32, i32, vp, vp, vp, vp, vp]
+    L.mjl_small_mlp_bwd_input.argtypes = [vp, i32, i32, i32, vp, vp, vp, vp, vp]
     L.mjl_step_vjp.argtypes = [vp, f32p, f32p, f32p, f32p, f32p, vp]
     L.mjl_env_step_vjp.argtypes = [vp, f32p, f32p, f32p, f32p, f32p, f32p, f32p, f32p, f32p, vp]
     L.mjl_step_vjp_full.argtypes = [vp] + [f32p] * 7 + [vp]

@@ -34,6 +34,62 @@ def _u8(t: torch.Tensor):
     return ctypes.c_void_p(t.data_ptr())
 
 
+class NativeAPGPolicy:
+    """APGPolicy's per-step passes on the native small-MLP kernels (mjl_small_mlp_fwd /
+    mjl_small_mlp_bwd_input, include/mjx355.h): the forward keeps every layer's tanh output, the
+    backward returns the input cotangent only (the parameter gradient is one torch pass over all
+    H x B policy inputs at the end of the sweep). One launch each per rollout step where torch ran
+    six. Reads the parameters in place (Adam updates them in place). MJL_APG_NATIVE_POLICY=0
+    keeps torch."""
+
+    def __init__(self, policy):
+        layers = list(policy.mlp.layers)
+        self.k0 = layers[0].in_features
+        self.widths = [lin.out_features for lin in layers]
+        self.params = [(lin.weight, lin.bias) for lin in layers]
+        nl = len(layers)
+        self._widths = (ctypes.c_int * nl)(*self.widths)
+
+    @staticmethod
+    def eligible(policy, device) -> bool:
+        mlp = getattr(policy, "mlp", None)
+        if (torch.device(device).type != "cuda" or not isinstance(policy, APGPolicy) or mlp is None
+                or os.environ.get("MJL_APG_NATIVE_POLICY", "1") == "0"):
+            return False
+        from .ppo import ACTIVATIONS
+        layers = list(mlp.layers)
+        acts = list(mlp.acts)
+        if not 1 <= len(layers) <= 4 or acts[-1] not in ("linear", "none"):
+            return False
+        if any(ACTIVATIONS.get(a, torch.tanh) is not torch.tanh for a in acts[:-1]):
+            return False
+        dims = [layers[0].in_features] + [lin.out_features for lin in layers]
+        return all(1 <= d <= 64 for d in dims) and all(
+            lin.weight.dtype == torch.float32 and lin.weight.is_contiguous() and lin.bias is not None
+            for lin in layers)
+
+    def _ptrs(self, ts):
+        return (ctypes.c_void_p * len(ts))(*[t.data_ptr() for t in ts])
+
+    def forward(self, x: torch.Tensor, ys) -> torch.Tensor:
+        """ys[l]: [B, widths[l]] outputs (written); returns ys[-1], the action mean (tanh-squashed)."""
+        from ._lib import check, lib
+        x = x.contiguous()
+        check(lib().mjl_small_mlp_fwd(x.data_ptr(), x.shape[0], self.k0, len(self.widths), self._widths,
+                                      self._ptrs([w for w, _ in self.params]), self._ptrs([b for _, b in self.params]),
+                                      self._ptrs(ys), torch.cuda.current_stream(x.device).cuda_stream))
+        return ys[-1]
+
+    def backward_input(self, g_out: torch.Tensor, ys) -> torch.Tensor:
+        from ._lib import check, lib
+        g_out = g_out.contiguous()
+        gx = torch.empty((g_out.shape[0], self.k0), device=g_out.device)
+        check(lib().mjl_small_mlp_bwd_input(g_out.data_ptr(), g_out.shape[0], self.k0, len(self.widths), self._widths,
+                                            self._ptrs([w for w, _ in self.params]), self._ptrs(ys), gx.data_ptr(),
+                                            torch.cuda.current_stream(g_out.device).cuda_stream))
+        return gx
+
+
 def apg_normalize(rms: RunningMeanStd, x: torch.Tensor) -> torch.Tensor:
     """train_apg.py:171-176 (note sqrt(var) + 1e-8, unlike PPO's sqrt(var + 1e-8))."""
     return torch.clamp((x - rms.mean) / (torch.sqrt(rms.var) + 1e-8), -10.0, 10.0)
@@ -66,6 +122,7 @@ class APGTrainer:
             for p in self.policy.parameters():
                 dist.broadcast(p.data, 0)
         self.opt = torch.optim.Adam(self.policy.parameters(), lr=cfg.lr, betas=(0.9, 0.999), eps=1e-8)
+        self.native_policy = NativeAPGPolicy(self.policy) if NativeAPGPolicy.eligible(self.policy, self.device) else None
         self.rms = RunningMeanStd(self.obs_dim, self.device)
         self.total_env_steps = 0.0
         self.start = time.time()
@@ -144,14 +201,19 @@ class APGTrainer:
         if taped and getattr(env, "tape_slots", 0) < H:
             env.enable_vjp_tape(H)
         tape, acts, leaves = [], [], []
+        nat = self.native_policy
+        ys_all = [torch.empty((H, B, n), device=dev) for n in nat.widths] if nat is not None else None
         for t in range(H):
             if not taped:
                 tape.append(env.get_state())
             env.apg_obs(alive, self.rms, use_norm, o_all[t], on_all[t], snap[t])
-            on = on_all[t].detach().requires_grad_(True)
-            a = self.policy(on)
+            if nat is not None:  # one launch; the layers' outputs kept for the reverse
+                a = nat.forward(on_all[t], [y[t] for y in ys_all])
+            else:
+                on = on_all[t].detach().requires_grad_(True)
+                a = self.policy(on)
+                leaves.append(on)
             acts.append(a)
-            leaves.append(on)
             if taped:  # the step, leaving its forward workspace in tape slot t
                 _, r, te, tr = env.step_record(t, a.detach())
             else:
@@ -177,7 +239,10 @@ class APGTrainer:
                                                               nonfinite)
                 else:
                     gq, gv, ga, gaux = env.step_vjp(acts[t].detach(), gq, gv, grew_all[t], gaux, nonfinite)
-            og, = torch.autograd.grad(acts[t], leaves[t], grad_outputs=ga)
+            if nat is not None:
+                og = nat.backward_input(ga, [y[t] for y in ys_all])
+            else:
+                og, = torch.autograd.grad(acts[t], leaves[t], grad_outputs=ga)
             env.apg_obs_vjp(o_all[t], snap[t], self.rms, use_norm, og, gq, gv)
             gas[t] = ga
         torch.autograd.backward(self.policy(on_all.reshape(H * B, w)), grad_tensors=torch.cat(gas))
@@ -200,6 +265,8 @@ class APGTrainer:
         else:
             env.reset()
         tape, obs_leaves, acts, discs, pol_in = [], [], [], [], []
+        nat = self.native_policy  # the same policy numerics as the native sweep (rollouts amplify ulps)
+        ons, ys_steps = [], []
         disc = ret = rsum = None  # created from the first reward (dtype follows the env)
         alive = torch.ones(B, dtype=torch.bool, device=self.device)
         dropped = torch.zeros((), device=self.device)
@@ -208,7 +275,13 @@ class APGTrainer:
         for _ in range(H):
             tape.append(env.get_state())
             o, on = self._obs(use_norm, alive)
-            a = self.policy(on)
+            if nat is not None:
+                ys = [torch.empty((B, n), device=self.device) for n in nat.widths]
+                a = nat.forward(on.detach(), ys)
+                ys_steps.append(ys)
+                ons.append(on)
+            else:
+                a = self.policy(on)
             pol_in.append(on.detach())
             obs_leaves.append(o)
             acts.append(a)
@@ -264,7 +337,14 @@ class APGTrainer:
                 ga = torch.where(ok[:, None], ga, torch.zeros_like(ga))
             # the chain needs only the observation cotangent here; the parameter gradient (a sum over
             # steps) is taken once below from all steps' action cotangents
-            if per_step_param_grad:  # the unbatched form (tests): parameter gradient accumulated per step
+            if nat is not None:  # native policy backward to its input, torch for the normalisation
+                g_on = nat.backward_input(ga, ys_steps[t])
+                og, = torch.autograd.grad(ons[t], obs_leaves[t], grad_outputs=g_on.to(ons[t].dtype))
+                if per_step_param_grad:
+                    pg = torch.autograd.grad(self.policy(pol_in[t]), list(self.policy.parameters()), grad_outputs=ga)
+                    for p_, g_ in zip(self.policy.parameters(), pg):
+                        p_.grad = g_ if p_.grad is None else p_.grad + g_
+            elif per_step_param_grad:  # the unbatched form (tests): parameter gradient accumulated per step
                 og, *pg = torch.autograd.grad(acts[t], [obs_leaves[t]] + list(self.policy.parameters()), grad_outputs=ga)
                 for p_, g_ in zip(self.policy.parameters(), pg):
                     p_.grad = g_ if p_.grad is None else p_.grad + g_

@@ -368,3 +368,29 @@ def test_apg_native_bookkeeping_matches_torch_ops(solver, vjp):
             assert ms[0][k] == pytest.approx(ms[1][k], rel=1e-5, abs=1e-6), f"update {step}: {k}"
         for p, q in zip(trs[0].policy.parameters(), trs[1].policy.parameters()):
             torch.testing.assert_close(p, q, rtol=1e-5, atol=1e-6)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("k0,hidden,depth,act_dim,B", [(55, 32, 2, 21, 2048), (55, 64, 3, 21, 1000), (7, 16, 1, 3, 5)])
+def test_native_apg_policy_matches_torch(k0, hidden, depth, act_dim, B):
+    """mjl_small_mlp_fwd / mjl_small_mlp_bwd_input against the APGPolicy's torch forward and the
+    autograd input cotangent (float64 reference): outputs to 2e-6, input cotangent to 1e-5 of its scale."""
+    from mjx_amd.ppo import APGPolicy
+    pol = APGPolicy(k0, act_dim, hidden, depth, None, torch.Generator().manual_seed(k0 + B)).cuda()
+    assert apg.NativeAPGPolicy.eligible(pol, "cuda")
+    nat = apg.NativeAPGPolicy(pol)
+    g = torch.Generator(device="cuda").manual_seed(1)
+    x = torch.randn((B, k0), generator=g, device="cuda") * 2
+    ga = torch.randn((B, act_dim), generator=g, device="cuda")
+    ys = [torch.empty((B, n), device="cuda") for n in nat.widths]
+    a = nat.forward(x, ys)
+    gx = nat.backward_input(ga, ys)
+    pol64 = APGPolicy(k0, act_dim, hidden, depth).cuda().double()
+    pol64.load_state_dict({k: v.double() for k, v in pol.state_dict().items()})
+    x64 = x.double().requires_grad_(True)
+    a64 = pol64(x64)
+    gx64, = torch.autograd.grad(a64, x64, grad_outputs=ga.double())
+    torch.testing.assert_close(a.double(), a64, rtol=0, atol=2e-6)
+    torch.testing.assert_close(gx.double(), gx64, rtol=0, atol=1e-5 * float(gx64.abs().max()))
+    ys2 = [torch.empty_like(y) for y in ys]
+    assert torch.equal(nat.forward(x, ys2), a) and torch.equal(nat.backward_input(ga, ys2), gx)  # deterministic
