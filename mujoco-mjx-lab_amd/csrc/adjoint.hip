@@ -1542,27 +1542,54 @@ template <class D, class WT, class AT> INL void adj_kinematics(MP m, LDSA WT* W,
   SYNC();
   TACC(22, tk, lane);
   // tree pass reverse; child contributions to the parent go through A->Sb (xquat 4, xpos 3) and
-  // A->Tb (first 6 of xmat) + A->Ub (last 3 of xmat)
+  // A->Tb (first 6 of xmat) + A->Ub (last 3 of xmat). The body's cotangent accumulators (xquat, xpos,
+  // xmat) live in its lane's registers through the level loop (its children's contributions are added
+  // there), and the forward-only operands (its and its parent's frames, the local transform, the
+  // pre-normalisation quaternion and its norm) are loaded / formed once before the loop: each level's
+  // chain is then the cotangent arithmetic and one LDS exchange with one barrier (each body writes
+  // only its own Sb / Tb / Ub row, once, so no second barrier protects them).
   float lpb[3] = {0.f, 0.f, 0.f}, lqb[4] = {0.f, 0.f, 0.f, 0.f};
+  float qacc[4] = {0.f, 0.f, 0.f, 0.f}, pacc[3] = {0.f, 0.f, 0.f};
+  float macc[9] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  float xqb[4] = {1.f, 0.f, 0.f, 0.f}, xqp[4] = {1.f, 0.f, 0.f, 0.f}, lqv[4] = {1.f, 0.f, 0.f, 0.f};
+  float xmp[9] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f}, lpv[3] = {0.f, 0.f, 0.f};
+  float qn[4] = {0.f, 0.f, 0.f, 0.f}, qinv = 0.f;
+  bool qok = false;
+  if (isb) {
+    for (int i = 0; i < 4; i++) { qacc[i] = A->xquatb[lane][i]; xqb[i] = W->xquat[lane][i]; }
+    for (int i = 0; i < 3; i++) pacc[i] = A->xposb[lane][i];
+    for (int i = 0; i < 9; i++) macc[i] = A->xmatb[lane][i];
+    if (!br.isfree) {
+      const int p = br.parent;
+      for (int i = 0; i < 4; i++) { xqp[i] = W->xquat[p][i]; lqv[i] = A->lq[lane][i]; }
+      for (int i = 0; i < 9; i++) xmp[i] = W->xmat[p][i];
+      for (int i = 0; i < 3; i++) lpv[i] = A->lp[lane][i];
+      float pre[4];
+      qmul(pre, xqp, lqv);
+      const float n = sqrtf(pre[0] * pre[0] + pre[1] * pre[1] + pre[2] * pre[2] + pre[3] * pre[3]);  // qnorm_adj
+      qok = !(n < kMinVal);
+      qinv = 1.f / n;
+      for (int i = 0; i < 4; i++) qn[i] = pre[i] * qinv;
+    }
+  }
   for (int L = maxlevel; L >= 1; L--) {
     if (isb && br.level == L) {
       const int b = lane;
-      float qb[4] = {A->xquatb[b][0], A->xquatb[b][1], A->xquatb[b][2], A->xquatb[b][3]};
-      q2m_adj(W->xquat[b], A->xmatb[b], qb);
+      float qb[4] = {qacc[0], qacc[1], qacc[2], qacc[3]};
+      q2m_adj(xqb, macc, qb);
       float cq[4] = {0.f, 0.f, 0.f, 0.f}, cp[3] = {0.f, 0.f, 0.f}, cm[9] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
       if (br.isfree) {
-        for (int i = 0; i < 3; i++) lpb[i] = A->xposb[b][i];
+        for (int i = 0; i < 3; i++) lpb[i] = pacc[i];
         for (int i = 0; i < 4; i++) lqb[i] = qb[i];
       } else {
-        const int p = br.parent;
-        float pre[4];
-        qmul(pre, W->xquat[p], A->lq[b]);
         float preb[4] = {0.f, 0.f, 0.f, 0.f};
-        qnorm_adj(pre, qb, preb);
-        qmul_adj(W->xquat[p], A->lq[b], preb, cq, lqb);
-        for (int i = 0; i < 3; i++) cp[i] = A->xposb[b][i];
-        const float xpb[3] = {A->xposb[b][0], A->xposb[b][1], A->xposb[b][2]};
-        mv3_adj(W->xmat[p], A->lp[b], xpb, cm, lpb);
+        if (qok) {  // qnorm_adj(pre, qb, preb) with the forward's part formed above
+          const float d = qn[0] * qb[0] + qn[1] * qb[1] + qn[2] * qb[2] + qn[3] * qb[3];
+          for (int i = 0; i < 4; i++) preb[i] += (qb[i] - qn[i] * d) * qinv;
+        }
+        qmul_adj(xqp, lqv, preb, cq, lqb);
+        for (int i = 0; i < 3; i++) cp[i] = pacc[i];
+        mv3_adj(xmp, lpv, pacc, cm, lpb);
       }
       for (int i = 0; i < 4; i++) A->Sb[b][i] = cq[i];
       for (int i = 0; i < 2; i++) A->Sb[b][4 + i] = cp[i];
@@ -1574,14 +1601,14 @@ template <class D, class WT, class AT> INL void adj_kinematics(MP m, LDSA WT* W,
     if (isb && br.level == L - 1) {
       for (uint32_t mk = cmask_nf; mk; mk &= mk - 1) {
         const int c = __ffs(mk) - 1;
-        for (int i = 0; i < 4; i++) A->xquatb[lane][i] += A->Sb[c][i];
-        A->xposb[lane][0] += A->Sb[c][4]; A->xposb[lane][1] += A->Sb[c][5]; A->xposb[lane][2] += A->Ub[c][0];
-        for (int i = 0; i < 6; i++) A->xmatb[lane][i] += A->Tb[c][i];
-        for (int i = 0; i < 3; i++) A->xmatb[lane][6 + i] += A->Ub[c][1 + i];
+        for (int i = 0; i < 4; i++) qacc[i] += A->Sb[c][i];
+        pacc[0] += A->Sb[c][4]; pacc[1] += A->Sb[c][5]; pacc[2] += A->Ub[c][0];
+        for (int i = 0; i < 6; i++) macc[i] += A->Tb[c][i];
+        for (int i = 0; i < 3; i++) macc[6 + i] += A->Ub[c][1 + i];
       }
     }
-    SYNC();
   }
+  SYNC();
   TACC(23, tk, lane);
   // local transforms reverse -> qpos-bar
   if (isb) {
