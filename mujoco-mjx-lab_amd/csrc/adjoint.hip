@@ -1171,58 +1171,61 @@ template <class D, class WT, class AT> INL void adj_rne(MP m, LDSA WT* W, LDSA A
     for (int k = 0; k < 6; k++) A->cfrcb[lane][k] = s[k];
   }
   TACC(25, tr, lane);
-  // recompute cvel / cacc (tree pass of velocity_stage)
+  // recompute cvel / cacc (tree pass of velocity_stage) level by level in registers: each body lane
+  // pulls its parent's values by lane shuffle (every lane takes part), no LDS round trip or barrier
   float S[6], U[6], T[6];
   if (isb) body_vel_terms<D>(W, A->qvel0, br, S, U, T);
-  if (lane == 0) {
-    for (int i = 0; i < 6; i++) A->cvel[0][i] = 0.f;
-    A->cacc[0][0] = A->cacc[0][1] = A->cacc[0][2] = 0.f;
-    A->cacc[0][3] = -m->gravity[0]; A->cacc[0][4] = -m->gravity[1]; A->cacc[0][5] = -m->gravity[2];
-  }
-  SYNC();
+  float cv[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  float ca[6] = {0.f, 0.f, 0.f, -m->gravity[0], -m->gravity[1], -m->gravity[2]};  // the world's (lane 0)
+  const int par = isb ? br.parent : 0;
   for (int L = 1; L <= maxlevel; L++) {
+    float pv[6], pa[6];
+    for (int i = 0; i < 6; i++) { pv[i] = __shfl(cv[i], par); pa[i] = __shfl(ca[i], par); }
     if (isb && br.level == L) {
-      const int p = br.parent;
       float x[6];
-      cross_motion(x, A->cvel[p], U);
-      for (int i = 0; i < 6; i++) { A->cvel[lane][i] = A->cvel[p][i] + S[i]; A->cacc[lane][i] = A->cacc[p][i] + x[i] + T[i]; }
+      cross_motion(x, pv, U);
+      for (int i = 0; i < 6; i++) { cv[i] = pv[i] + S[i]; ca[i] = pa[i] + x[i] + T[i]; }
     }
-    SYNC();
   }
+  float pcv[6];  // the parent's cvel, for the tree reverse
+  for (int i = 0; i < 6; i++) pcv[i] = __shfl(cv[i], par);
   TACC(26, tr, lane);
-  if (isb) {  // cfrc = I cacc + cvel x* (I cvel)
-    float ci[10], cv[6], ca[6], fb[6], iv[6], ivb[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  // cfrc = I cacc + cvel x* (I cvel); the cvel / cacc cotangent accumulators stay in registers
+  float cvacc[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f}, caacc[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  if (isb) {
+    float ci[10], fb[6], iv[6], ivb[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
     float cib[10] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f}, cvb[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
     float cab[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
     for (int i = 0; i < 10; i++) ci[i] = W->cinert[lane][i];
-    for (int i = 0; i < 6; i++) { cv[i] = A->cvel[lane][i]; ca[i] = A->cacc[lane][i]; fb[i] = A->cfrcb[lane][i]; }
+    for (int i = 0; i < 6; i++) fb[i] = A->cfrcb[lane][i];
     inert_vec(iv, ci, cv);
     inert_vec_adj(ci, ca, fb, cib, cab);
     cross_force_adj(cv, iv, fb, cvb, ivb);
     inert_vec_adj(ci, cv, ivb, cib, cvb);
     for (int i = 0; i < 10; i++) A->cinertb[lane][i] += cib[i];
-    for (int i = 0; i < 6; i++) { A->cvelb[lane][i] += cvb[i]; A->caccb[lane][i] += cab[i]; }
+    for (int i = 0; i < 6; i++) { cvacc[i] = 0.f + cvb[i]; caacc[i] = 0.f + cab[i]; }
   }
   SYNC();
   TACC(27, tr, lane);
   // tree reverse: cvel_b = cvel_p + S, cacc_b = cacc_p + cvel_p x U + T; children -> parent gather
+  // through each body's own cfsubb / cfrcb row (written once, at its level: one barrier per level)
   float Sb[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f}, Ubr[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f}, Tbr[6];
   for (int L = maxlevel; L >= 1; L--) {
     if (isb && br.level == L) {
       float pvb[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-      for (int i = 0; i < 6; i++) { Sb[i] = A->cvelb[lane][i]; Tbr[i] = A->caccb[lane][i]; }
-      cross_motion_adj(A->cvel[br.parent], U, Tbr, pvb, Ubr);
+      for (int i = 0; i < 6; i++) { Sb[i] = cvacc[i]; Tbr[i] = caacc[i]; }
+      cross_motion_adj(pcv, U, Tbr, pvb, Ubr);
       for (int i = 0; i < 6; i++) { A->cfsubb[lane][i] = Sb[i] + pvb[i]; A->cfrcb[lane][i] = Tbr[i]; }
     }
     SYNC();
     if (isb && br.level == L - 1) {
       for (uint32_t mk = chm; mk; mk &= mk - 1) {
         const int c = __ffs(mk) - 1;
-        for (int i = 0; i < 6; i++) { A->cvelb[lane][i] += A->cfsubb[c][i]; A->caccb[lane][i] += A->cfrcb[c][i]; }
+        for (int i = 0; i < 6; i++) { cvacc[i] += A->cfsubb[c][i]; caacc[i] += A->cfrcb[c][i]; }
       }
     }
-    SYNC();
   }
+  SYNC();
   TACC(28, tr, lane);
   if (isb) {  // local terms -> cdof-bar, qvel-bar
     const int da = br.dofadr, dn = br.dofnum;
@@ -1510,7 +1513,10 @@ template <class D, class WT, class AT> INL void adj_kinematics(MP m, LDSA WT* W,
       for (int k = 0; k < 3; k++) A->xmatb[lane][3 * i + k] += A->xiposb[lane][i] * br.ipos[k];
     }
   }
-  // local transforms (as the forward computes them), kept in A->lp / A->lq
+  // local transforms (as the forward computes them), kept in A->lp / A->lq; the first three hinges'
+  // intermediates (quaternion before the joint, sin / cos of its half angle) stay in registers for
+  // the reverse below, which recomputed the chain
+  float kq[3][4], ks[3], kc[3];
   if (isb) {
     float lp[3], lq[4];
     if (br.isfree) {
@@ -1521,19 +1527,30 @@ template <class D, class WT, class AT> INL void adj_kinematics(MP m, LDSA WT* W,
     } else {
       for (int i = 0; i < 3; i++) lp[i] = br.pos[i];
       for (int i = 0; i < 4; i++) lq[i] = br.quat[i];
-      for (int q = 0; q < br.jntnum; q++) {
+      auto joint = [&](int q, float& s, float& c) {
         const JntRec jr = hinge(q);
         float mat[9], anc[3], off[3];
         q2m(mat, lq);
         mv3(anc, mat, jr.pos);
         for (int i = 0; i < 3; i++) anc[i] += lp[i];
-        float s, c;
         sincosf(0.5f * (A->qpos0[jr.qadr] - jr.qpos0), &s, &c);
         const float ql[4] = {c, jr.axis[0] * s, jr.axis[1] * s, jr.axis[2] * s};
         qmul(lq, lq, ql);
         q2m(mat, lq);
         mv3(off, mat, jr.pos);
         for (int i = 0; i < 3; i++) lp[i] = anc[i] - off[i];
+      };
+      const int jn = br.jntnum;
+#pragma unroll
+      for (int q = 0; q < 3; q++) {
+        if (q < jn) {
+          for (int i = 0; i < 4; i++) kq[q][i] = lq[i];
+          joint(q, ks[q], kc[q]);
+        }
+      }
+      for (int q = 3; q < jn; q++) {
+        float s, c;
+        joint(q, s, c);
       }
     }
     for (int i = 0; i < 3; i++) A->lp[lane][i] = lp[i];
@@ -1619,6 +1636,33 @@ template <class D, class WT, class AT> INL void adj_kinematics(MP m, LDSA WT* W,
       float qb[4] = {0.f, 0.f, 0.f, 0.f};
       qnorm_adj(q, lqb, qb);
       for (int i = 0; i < 4; i++) A->qposb[qa + 3 + i] += qb[i];
+    } else if (br.jntnum <= 3) {  // the intermediates cached above
+#pragma unroll
+      for (int q = 2; q >= 0; q--) {
+        if (q < br.jntnum) {
+          const int j = br.jntadr + q;
+          const JntRec jr = hinge(q);
+          const float ql[4] = {kc[q], jr.axis[0] * ks[q], jr.axis[1] * ks[q], jr.axis[2] * ks[q]};
+          float lqa[4];
+          qmul(lqa, kq[q], ql);
+          float ancb[3] = {lpb[0], lpb[1], lpb[2]};
+          float m2b[9];
+          for (int i = 0; i < 3; i++)
+            for (int k = 0; k < 3; k++) m2b[3 * i + k] = -lpb[i] * jr.pos[k];
+          q2m_adj(lqa, m2b, lqb);
+          float lqbb[4] = {0.f, 0.f, 0.f, 0.f}, qlb[4] = {0.f, 0.f, 0.f, 0.f};
+          qmul_adj(kq[q], ql, lqb, lqbb, qlb);
+          const float thb = -ks[q] * qlb[0] + kc[q] * (jr.axis[0] * qlb[1] + jr.axis[1] * qlb[2] + jr.axis[2] * qlb[3]);
+          A->qposb[jr.qadr] += 0.5f * thb;
+          for (int i = 0; i < 3; i++) ancb[i] += A->ftmp[j][i];
+          float mb[9];
+          for (int i = 0; i < 3; i++)
+            for (int k = 0; k < 3; k++) mb[3 * i + k] = ancb[i] * jr.pos[k] + A->ftmp[j][3 + i] * jr.axis[k];
+          q2m_adj(kq[q], mb, lqbb);
+          for (int i = 0; i < 3; i++) lpb[i] = ancb[i];
+          for (int i = 0; i < 4; i++) lqb[i] = lqbb[i];
+        }
+      }
     } else {
       constexpr int KJ = 8;  // joints per body kept for the reverse sweep
       float lqs[KJ][4], lps[KJ][3], sn[KJ], cs[KJ];
