@@ -126,7 +126,7 @@ INL float imp_dpos(const CSTA float* solimp, float pos) {
   static constexpr int NV = DM::NV, LD = DM::LD, NB = DM::NB, NJ = DM::NJ, NG = DM::NG;             \
   /* forward values kept for the reverse passes */                                                 \
   float qpos0[MJL_MAXQ], qvel0[LD];    /* pre-step state */                                        \
-  float cvel[NB][6], cacc[NB][6];      /* recomputed in the RNE reverse */
+  alignas(16) float mq[LD][4];         /* lean mass reverse: (mu, rb, qacc, a') per dof */
 #define WSA_P2                                                                                       \
   float ap[LD];                        /* integrator acceleration a' */                            \
   float lp[NB][3], lq[NB][4];          /* body transform in the parent frame */                    \
@@ -377,6 +377,10 @@ template <class D, class WT, class AT, class MT> INL void adj_integrate(MP m, LD
   constexpr int LD = D::LD;
   const int nv = m->nv;
   const float dt = m->timestep;
+  // lean replay: the implicit-integration factor's row and column come from the slot in global
+  // memory; their loads go out before the joint pass, whose work hides their latency
+  [[maybe_unused]] CholOps<D::NV> hops;
+  if constexpr (is_lean<AT>::value) hops = chol_load<D>(mt.H, mt.invd, lane);
   if (lane < m->njnt) {
     const JntRec jr = ldrec(&m->jrec[lane]);
     const int q = jr.qadr, d = jr.dofadr;
@@ -416,7 +420,10 @@ template <class D, class WT, class AT, class MT> INL void adj_integrate(MP m, LD
   if (damp) {  // a' = Hd^-1 (M qacc), Hd = M + dt diag(damping), factor in W->H
     if (lane < LD) A->rb[lane] = (lane < nv) ? apb : 0.f;
     SYNC();
-    const float r = chol_solve<D>(mt.H, mt.invd, lane < nv ? A->rb[lane] : 0.f, lane);
+    const float rx = lane < nv ? A->rb[lane] : 0.f;
+    float r;
+    if constexpr (is_lean<AT>::value) r = chol_apply(hops, rx);
+    else r = chol_solve<D>(mt.H, mt.invd, rx, lane);
     SYNC();
     if (lane < LD) A->rb[lane] = (lane < nv) ? r : 0.f;
     SYNC();
@@ -1287,6 +1294,13 @@ INL void adj_mass(MP m, LDSA WT* W, LDSA AT* A, const MT& mt, bool unr, int lane
     inert_vec(f6, W->crb[dr.bodyid], W->cdof[lane]);
     for (int k = 0; k < 6; k++) A->ftmp[lane][k] = f6[k];
   }
+  if constexpr (is_lean<AT>::value) {  // M-bar's rank-one operands packed per dof: one b128 read per (i, j)
+    if (lane < LD) {
+      f32x4 v;
+      v[0] = A->mu[lane]; v[1] = A->rb[lane]; v[2] = W->qacc[lane]; v[3] = A->ap[lane];
+      ((LDSA f32x4*)A->mq)[lane] = v;
+    }
+  }
   SYNC();
   float fb[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
   // the loops, instantiated per M-bar source (the choice made once, outside them)
@@ -1319,11 +1333,14 @@ INL void adj_mass(MP m, LDSA WT* W, LDSA AT* A, const MT& mt, bool unr, int lane
         loops([&](int i, int j) -> float { return mt.Mb[i * LD + j]; });
       } else if (damp) {
         loops([&](int i, int j) -> float {
-          const float qa = W->qacc[j];
-          return fmaf(-A->mu[i], qa, fmaf(A->rb[i], qa - A->ap[j], 0.f));
+          const f32x4 a = ((const LDSA f32x4*)A->mq)[i], b = ((const LDSA f32x4*)A->mq)[j];
+          return fmaf(-a[0], b[2], fmaf(a[1], b[2] - b[3], 0.f));
         });
       } else {
-        loops([&](int i, int j) -> float { return fmaf(-A->mu[i], W->qacc[j], 0.f); });
+        loops([&](int i, int j) -> float {
+          const f32x4 a = ((const LDSA f32x4*)A->mq)[i], b = ((const LDSA f32x4*)A->mq)[j];
+          return fmaf(-a[0], b[2], 0.f);
+        });
       }
     } else {
       loops([&](int i, int j) -> float { return A->Mb[i * LD + j]; });
@@ -2027,6 +2044,7 @@ __global__ __launch_bounds__(64, LEAN ? 2 : 1) void vjp_kernel(KParams P, VjpArg
   if (lane < nv) A->vtmp[lane] = V.g_qvel[(size_t)env * nv + lane];
   SYNC();
   if (ENV) adj_env<D>(m, W, A, (CP)P.env, (const float*)aux, V.g_rew[env], V.g_aux + (size_t)env * MJL_AUX_DIM, lane);
+  STAMP(14, lane);
   // the dense arrays (mats): in LDS, or (lean) in the slot's workspace image and A part in global memory
   adj_integrate<D>(m, W, A, mats, gq, unr, lane);
   if (V.g_ws && lane < nv) A->qaccb[lane] += V.g_ws[(size_t)env * nv + lane];  // output warm start = qacc

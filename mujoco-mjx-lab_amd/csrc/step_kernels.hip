@@ -573,29 +573,41 @@ template <class D> INL float chol_factor_solve(const LDSA float* src, LDSA float
 }
 
 // x distributed (lane i holds b_i, zero for i >= n) -> (L L^T)^-1 b, L from chol_factor
+// unit-triangular forms, each lane scaling its own row / column by its own 1 / L[i][i]:
+// L y = b  <=>  (diag(L)^-1 L) y = diag(L)^-1 b;  L^T z = y  <=>  (L diag(L)^-1)^T z = diag(L)^-1 y,
+// so every serial step is one readlane and one fma. chol_load issues the lane's row and column of L
+// (clamped addresses, loads unconditional; masks against an opaque lane index, see opaque_int) --
+// callers with L in global memory issue it early, ahead of other work -- and chol_apply runs the two
+// substitutions.
+template <int NV> struct CholOps {
+  float wr[NV], wc[NV], invd;
+};
 template <class D, class LP = const LDSA float*, class IP = const LDSA float*>
-INL float chol_solve(LP L, IP invd_in, float x, int lane) {  // L, invd in LDS, or in global memory (lean replay)
+INL CholOps<D::NV> chol_load(LP L, IP invd_in, int lane) {
   constexpr int NV = D::NV, LD = D::LD;
-  // unit-triangular forms, each lane scaling its own row / column by its own 1 / L[i][i]:
-  // L y = b  <=>  (diag(L)^-1 L) y = diag(L)^-1 b;  L^T z = y  <=>  (L diag(L)^-1)^T z = diag(L)^-1 y,
-  // so every serial step is one readlane and one fma
-  // (clamped addresses, loads unconditional; masks against an opaque lane index, see opaque_int)
   const int li = lane < NV ? lane : 0, lo = opaque_int(lane);
-  const float invd = (lane < NV) ? invd_in[li] : 1.f;
-  float wr[NV], wc[NV];
+  CholOps<NV> c;
+  c.invd = (lane < NV) ? invd_in[li] : 1.f;
 #pragma unroll
   for (int k = 0; k < NV; k++) {
-    const float r = L[li * LD + k], c = L[k * LD + li];
-    wr[k] = (lo < NV && lo > k) ? r * invd : 0.f;  // L[i][k] / L[i][i]
-    wc[k] = (lo < k) ? c * invd : 0.f;             // L[k][i] / L[i][i]
+    const float r = L[li * LD + k], cl = L[k * LD + li];
+    c.wr[k] = (lo < NV && lo > k) ? r * c.invd : 0.f;  // L[i][k] / L[i][i]
+    c.wc[k] = (lo < k) ? cl * c.invd : 0.f;             // L[k][i] / L[i][i]
   }
-  x *= invd;
+  return c;
+}
+template <int NV> INL float chol_apply(const CholOps<NV>& c, float x) {
+  x *= c.invd;
 #pragma unroll
-  for (int k = 0; k < NV; k++) x = fmaf(-wr[k], rdlane(x, k), x);
-  x *= invd;
+  for (int k = 0; k < NV; k++) x = fmaf(-c.wr[k], rdlane(x, k), x);
+  x *= c.invd;
 #pragma unroll
-  for (int k = NV - 1; k >= 0; k--) x = fmaf(-wc[k], rdlane(x, k), x);
+  for (int k = NV - 1; k >= 0; k--) x = fmaf(-c.wc[k], rdlane(x, k), x);
   return x;
+}
+template <class D, class LP = const LDSA float*, class IP = const LDSA float*>
+INL float chol_solve(LP L, IP invd_in, float x, int lane) {  // L, invd in LDS, or in global memory (lean replay)
+  return chol_apply(chol_load<D>(L, invd_in, lane), x);
 }
 
 // ---------------------------------------------------------------------------------------------

@@ -82,3 +82,5 @@ subs = {20: "kin: scom + joint frames", 21: "kin: joint gather", 22: "kin: xipos
         30: "mass: f + M-bar loops", 31: "mass: crb-bar"}
 for i, n in subs.items():
     print(f"      {n:30s} {s[ok][:, i].mean():9.0f}")
+if (s[ok][:, 14] > 0).all():
+    print(f"      {'env: reward / obs adjoint':30s} {(s[ok][:, 14] - s[ok][:, 1]).mean():9.0f}")
