@@ -510,7 +510,8 @@ def ppo_c3(args, local) -> dict:
 def apg_c4(args, local) -> dict:
     """C4: train_apg.py at 2048 envs x 128 horizon, CG 4/4, under the reference's solve derivative
     (unrolled: jax.grad through the iterations) and the implicit one; plus the replay VJP kernel's
-    roofline from standalone launches of the last update's first tape slot."""
+    roofline from a reverse sweep over the last update's tape (HIP events around each launch)."""
+    from mjx_amd import abi
     from mjx_amd import flops as flops_mod
     from mjx_amd import mjx
     from mjx_amd.apg import APGTrainer, HumanoidAPGEnv
@@ -544,12 +545,24 @@ def apg_c4(args, local) -> dict:
             gq, gv = torch.zeros((B, m.nq), device=dev), torch.zeros((B, m.nv), device=dev)
             grew = torch.full((B,), -1.0 / B, device=dev)  # the reward's cotangent: every env runs the reverse
             nonf = torch.zeros(1, device=dev)
+            gaux = torch.zeros((B, abi.AUX_DIM), device=dev)  # no per-call zero fill beside the kernel
 
-            def sweep():
+            def sweep(events=None):
                 for t in range(H - 1, -1, -1):
-                    aenv.step_vjp_replay(t, act, gq, gv, None, grew, None, nonf)
-            _, kms = timed_launches(sweep, 1, 1, None)
-            kms /= H
+                    if events is not None:
+                        events.append((torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)))
+                        events[-1][0].record()
+                    aenv.step_vjp_replay(t, act, gq, gv, None, grew, gaux, nonf)
+                    if events is not None:
+                        events[-1][1].record()
+            sweep()  # warm-up
+            sync(dev)
+            # one HIP event pair around each replay launch on its stream (the eager sweep's host gaps
+            # between launches stay out of the kernel time)
+            evs = []
+            sweep(evs)
+            sync(dev)
+            kms = sum(e0.elapsed_time(e1) for e0, e1 in evs) / H
             # the rollout's solver statistics (the same policy from fresh resets; CG reports no active-row
             # count, so the implicit Hessian is counted over all rows)
             env.data.set_option(0, 1)
@@ -564,7 +577,7 @@ def apg_c4(args, local) -> dict:
             tf = fl["total"] * B / (kms * 1e-3) / 1e12
             out["apg_vjp_roofline"] = {
                 "bound": "mfma", "achieved": tf, "peak": F32_PEAK_TFLOPS, "unit": "TFLOP/s",
-                "frac": tf / F32_PEAK_TFLOPS, "kernel": "vjp_kernel<mjl::Dims<27, 17, 22, 20, 4, 4>, true, 2>",
+                "frac": tf / F32_PEAK_TFLOPS, "kernel": "vjp_kernel<mjl::Dims<27, 17, 22, 20, 4, 4>, true, 2, true>",
                 "kernel_ms": kms, "launches_timed": H, "flops_per_env_step": fl["total"],
                 "flops_by_stage": {k: v for k, v in fl.items() if k != "total"},
                 "workload_mean_ncon_nefc_iter": [float(x) for x in s[:3]],

@@ -24,7 +24,7 @@ KERNELS = {
     "envstep": "step_kernel<mjl::Dims<27, 17, 22, 20, 48, 16>, 3>",
     "envstep_pool": "step_kernel<mjl::Dims<27, 17, 22, 20, 48, 16>, 3>",
     "envstep_nr": "step_kernel<mjl::Dims<27, 17, 22, 20, 48, 16>, 3>",
-    "vjp": "vjp_kernel<mjl::Dims<27, 17, 22, 20, 4, 4>, true, 2>",
+    "vjp": "vjp_kernel<mjl::Dims<27, 17, 22, 20, 4, 4>, true, 2, true>",
 }
 TRAFFIC_KEY = {"speedtest": "bytes_per_launch", "envstep": "env_step_bytes_per_launch",
                "vjp": "vjp_bytes_per_launch"}
