@@ -2351,6 +2351,7 @@ template <class D, int MODE> __global__ __launch_bounds__(64, MJL_MINWAVES) void
     if (P.pool_slot == 0 && lane == 0) { P.pool_ctl[2 * env] = 0; P.pool_ctl[2 * env + 1] = n; }
     if (P.pool_slot >= n) return;
   }
+  STAMP(36, lane);
   const int nq = m->nq, nv = m->nv, nu = m->nu;
   const StateBuf& S = P.s;
   EnvArgs A;
@@ -2417,6 +2418,7 @@ template <class D, int MODE> __global__ __launch_bounds__(64, MJL_MINWAVES) void
     if (MODE == MODE_ENV_STEP) {
       float* obs = P.obs + (size_t)env * P.env->obs_dim;
       env_post<D>(m, W, P.env, aux, obs, lane, P.auto_reset != 0);
+      STAMP(37, lane);
       if (lane == 0) { P.rew[env] = W->sc[SC_REW]; P.term[env] = W->sc[SC_TERM]; P.trunc[env] = W->sc[SC_TRUNC]; }
       bool bad = (lane < nq && !isfinite(W->qpos[lane])) || (lane < nv && !isfinite(W->qvel[lane]));
       bool anybad = __ballot(bad) != 0ull;
@@ -2435,6 +2437,7 @@ template <class D, int MODE> __global__ __launch_bounds__(64, MJL_MINWAVES) void
           env_reset<D>(m, W, &A, env, lane, aux, obs);
         }
       }
+      STAMP(38, lane);
     }
   }
   SYNC();
@@ -2474,6 +2477,7 @@ template <class D, int MODE> __global__ __launch_bounds__(64, MJL_MINWAVES) void
     }
   }
   if (MODE == MODE_ENV_RESET && P.pool_slot >= 0 && lane == 0) S.stats[(size_t)env * 4 + 3] = W->sc[SC_HEIGHT];
+  STAMP(39, lane);
 }
 
 }  // namespace mjl
