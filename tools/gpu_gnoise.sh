@@ -1,7 +1,10 @@
 #!/bin/bash
 # A/B of the gradient-noise Newton exit (MJL_GNOISE_EXIT builds in tools/_ab): env-step stage stamps
 # (iterations of each launch's slowest env), then the speed test + env-step launch times per build,
-# interleaved twice.
+# interleaved twice. The A/B builds are made beforehand on the CPU (the exit itself was dropped
+# after this measurement; it was a `gsq <= (k eps)^2 * sum(|Ma|+|f|+|J'f|)^2` break after
+# the MJX tolerance test in solver_t, under -DMJL_GNOISE_EXIT=k), e.g.
+#   hipcc $HIPFLAGS -DMJL_TIMING [-DMJL_GNOISE_EXIT=16] -o tools/_ab/libtiming[_gn16].so capi.hip
 set -o pipefail
 O=gpurun_out/gnoise; mkdir -p $O
 for v in timing timing_gn16; do
