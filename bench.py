@@ -485,7 +485,8 @@ def ppo_trainer(args, envs, dist, rank, local, eval_envs=0):
 
 
 def grad_numel(tr) -> int:
-    return sum(p.numel() for p in list(tr.policy.parameters()) + list(tr.value.parameters()))
+    """Floats in one per-minibatch all-reduce (the updater's gradient buffer)."""
+    return tr.updater.allreduce_numel()
 
 
 def ppo_c3(args, local) -> dict:

@@ -396,6 +396,22 @@ int mjl_slice_sum(const float* x, int ns, long long m, float* out, void* stream)
 /* x = tanh(x) elementwise in place (the update's hidden-layer activations, src/networks.py:55-61);
  * n % 4 == 0, 16-byte aligned. */
 int mjl_tanh_inplace(float* x, long long n, void* stream);
+/* The same reductions over nb stacked matrices (the twin update: the policy and value nets' layers
+ * as one batched GEMM per layer, train_ppo.py:233-252 taking both nets' steps per minibatch):
+ * x [nb][n][d] -> out [nb][d], each matrix summed in mjl_colsum's order; for nb > 1, n must be a
+ * multiple of the 128-row chunk (n > 256). scratch: mjl_colsum_batched_scratch(nb, n, d) floats.
+ * mjl_slice_sum_batched: out[b][e] = sum over s < ns of x[(b * ns + s) * m + e]. */
+long long mjl_colsum_batched_scratch(int nb, int n, int d);
+int mjl_colsum_batched(const float* x, int nb, int n, int d, float* scratch, float* out, void* stream);
+int mjl_tanh_bwd_colsum_batched(const float* g, const float* y, int nb, int n, int d, float* dz, float* scratch,
+                                float* colsum_out, void* stream);
+int mjl_slice_sum_batched(const float* x, int nb, int ns, long long m, float* out, void* stream);
+/* The twin update's output-layer backward: mean [M, A] = tanh of the policy's last Dense (networks.py:
+ * 103), g_mean [M, A] = d loss / d mean (mjl_ppo_surrogate), g_v [M] = d loss / d value (mjl_mse);
+ * dz4 [2][M][A]: dz4[0] = g_mean (1 - mean^2), dz4[1][:, 0] = g_v, dz4[1][:, 1:] = 0 (the value net's
+ * output layer is padded to A rows). */
+int mjl_twin_head_bwd(const float* g_mean, const float* mean, const float* g_v, int M, int A, float* dz4,
+                      void* stream);
 
 /* PPO update losses (train_ppo.py:204-220), forward and gradient in one pass, deterministic.
  * mjl_ppo_surrogate: loss = -mean_i min(r_i an_i, clip(r_i, 1 - clip_eps, 1 + clip_eps) an_i)
@@ -414,6 +430,9 @@ int mjl_ppo_surrogate(const float* mean, const float* log_std, const float* act,
                       const float* adv, const float* adv_stats, int n, int A, float clip_eps, float ent_coef,
                       float* scratch, float* loss, float* g_mean, float* g_log_std, void* stream);
 int mjl_mse(const float* v, const float* r, int n, float* scratch, float* loss, float* g_v, void* stream);
+/* mjl_mse with v[i] read at v + i * vstride (the value column of the twin update's padded output). */
+int mjl_mse_strided(const float* v, int vstride, const float* r, int n, float* scratch, float* loss, float* g_v,
+                    void* stream);
 int mjl_gather_rows(const long long* idx, int n, long long nsrc, int narr, const float* const* src, float* const* dst,
                     const int* cols, void* stream);
 /* Adam (optax.adam defaults as train_ppo.py:84-85 build them; torch.optim.Adam's fused update) over

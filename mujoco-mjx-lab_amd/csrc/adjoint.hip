@@ -1891,10 +1891,10 @@ __global__ __launch_bounds__(64, LEAN ? 2 : 1) void vjp_kernel(KParams P, VjpArg
   if constexpr (TM != 1) {  // the VJP is linear in the cotangents: all-zero in -> all-zero out, without
      // the recompute (envs past termination in an APG rollout; also keeps 0 * non-finite out of their outputs)
     // clamped-index loads (no branch around each): all issue before the first compare
-    const int iq = lane < nq ? lane : nq - 1, iv = lane < nv ? lane : nv - 1;
+    const int iq = lane < nq ? lane : max(nq - 1, 0), iv = lane < nv ? lane : max(nv - 1, 0);
     const int ia = lane < MJL_AUX_DIM ? lane : MJL_AUX_DIM - 1;
-    const float cq = V.g_qpos[(size_t)env * nq + iq], cv = V.g_qvel[(size_t)env * nv + iv];
-    const float cw = V.g_ws ? V.g_ws[(size_t)env * nv + iv] : 0.f;
+    const float cq = nq > 0 ? V.g_qpos[(size_t)env * nq + iq] : 0.f, cv = nv > 0 ? V.g_qvel[(size_t)env * nv + iv] : 0.f;
+    const float cw = (V.g_ws && nv > 0) ? V.g_ws[(size_t)env * nv + iv] : 0.f;
     const float cr = ENV ? V.g_rew[env] : 0.f, ca = ENV ? V.g_aux[(size_t)env * MJL_AUX_DIM + ia] : 0.f;
     bool nz = (lane < nq && cq != 0.f) || (lane < nv && (cv != 0.f || cw != 0.f));
     if (ENV) nz = nz || (lane == 0 && cr != 0.f) || (lane < MJL_AUX_DIM && ca != 0.f);
@@ -1936,18 +1936,21 @@ __global__ __launch_bounds__(64, LEAN ? 2 : 1) void vjp_kernel(KParams P, VjpArg
     STAMP(1, lane);
   } else {
   // every state load issues before the first wait (clamped lane indices, no branch per load)
-  const int iq = lane < nq ? lane : nq - 1, iv = lane < nv ? lane : nv - 1, iu = lane < nu ? lane : nu - 1;
-  const float q = S.qpos[(size_t)env * nq + iq];
-  const float v = S.qvel[(size_t)env * nv + iv], w = S.qacc_warmstart[(size_t)env * nv + iv];
-  float c = ENV ? V.act[(size_t)env * nu + iu] : S.ctrl[(size_t)env * nu + iu];
+  // (a zero-size field clamps to index 0 and is not read)
+  const int iq = lane < nq ? lane : max(nq - 1, 0), iv = lane < nv ? lane : max(nv - 1, 0);
+  const int iu = lane < nu ? lane : max(nu - 1, 0);
+  const float q = nq > 0 ? S.qpos[(size_t)env * nq + iq] : 0.f;
+  const float v = nv > 0 ? S.qvel[(size_t)env * nv + iv] : 0.f;
+  const float w = nv > 0 ? S.qacc_warmstart[(size_t)env * nv + iv] : 0.f;
+  float c = nu > 0 ? (ENV ? V.act[(size_t)env * nu + iu] : S.ctrl[(size_t)env * nu + iu]) : 0.f;
   const float t = S.time[env];
   float ax = 0.f, sgn = 1.f;
   int perm = iu;
   if (ENV) {
     const int ia = lane < MJL_AUX_DIM ? lane : MJL_AUX_DIM - 1;
     ax = S.aux[(size_t)env * MJL_AUX_DIM + ia];
-    perm = P.env->act_perm[iu];
-    sgn = P.env->act_sign[iu];
+    perm = nu > 0 ? P.env->act_perm[iu] : 0;
+    sgn = nu > 0 ? P.env->act_sign[iu] : 1.f;
   }
   if (lane < nq) { W->qpos[lane] = q; A->qpos0[lane] = q; }
   if (lane < nv) { W->qvel[lane] = v; A->qvel0[lane] = v; W->qacc_ws[lane] = w; }

@@ -51,6 +51,7 @@ struct mjlModel {
 struct mjlBatch {
   const mjlModel* model;
   int device, nenv, store_derived, force_global_rows;
+  int simds;  // SIMDs of the device (4 per CU): the largest launch that is one wave per SIMD
   ModelF* d_model;
   mjlEnvConfig* d_env;
   int has_env, obs_dim;
@@ -371,6 +372,11 @@ int mjl_batch_create(const mjlModel* model, int nenv, int device, mjlBatch** out
   if (!B) return fail(MJL_ERR_ARG, "out of host memory");
   std::memset(B, 0, sizeof(*B));
   B->model = model; B->device = device; B->nenv = nenv; B->store_derived = 1;
+  {
+    int ncu = 0;
+    if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess) ncu = 0;
+    B->simds = 4 * ncu;
+  }
   const mjlModelDesc& d = model->desc;
   int* dim = B->dim;
   dim[MJL_FIELD_QPOS] = d.nq; dim[MJL_FIELD_QVEL] = d.nv; dim[MJL_FIELD_QACC_WARMSTART] = d.nv;
@@ -615,10 +621,22 @@ static KParams make_params(mjlBatch* B) {
   return P;
 }
 
+// env-step launches of at most one wave per SIMD (nenv <= 4 x CUs: C3's 1024-env rollout) take the
+// one-wave instantiation (MJL_ONE_WAVE=0 disables it, for A/B runs). Measured (profiles/r4_onewave_ab.jsonl,
+// interleaved): pooled env step at 1024 envs 81.4 -> 77.0 us, in-place 109.5 -> 106.4 us; the speed test
+// at 1024 envs ran 2 % slower one-wave (55.6 -> 56.7 us), so it keeps the two-wave kernel.
+static bool one_wave_launch(const mjlBatch* B) {
+  static const bool on = [] { const char* e = std::getenv("MJL_ONE_WAVE"); return !(e && e[0] == '0'); }();
+  return on && B->nenv <= B->simds;
+}
+
 template <int MODE> static int launch(mjlBatch* B, const KParams& P, void* stream) {
   HIPCHK(hipSetDevice(B->device));
   dim3 grid(B->nenv), block(64);
-  if (B->model->nvc == 0)
+  constexpr bool kOneWave = MODE == MODE_ENV_STEP;
+  if (B->model->nvc == 0 && kOneWave && one_wave_launch(B))
+    hipLaunchKernelGGL((step_kernel<DHum, MODE, kOneWave ? 1 : MJL_MINWAVES>), grid, block, 0, (hipStream_t)stream, P);
+  else if (B->model->nvc == 0)
     hipLaunchKernelGGL((step_kernel<DHum, MODE>), grid, block, 0, (hipStream_t)stream, P);
   else
     hipLaunchKernelGGL((step_kernel<DGen, MODE>), grid, block, 0, (hipStream_t)stream, P);
@@ -977,22 +995,62 @@ extern "C" long long mjl_colsum_scratch(int n, int d) {
   return p.R > 1 ? (long long)p.R * d : 0;
 }
 
-extern "C" int mjl_colsum(const float* x, int n, int d, float* scratch, float* out, void* stream) {
-  if ((!x && n > 0) || !out || n < 0 || d <= 0) return fail(MJL_ERR_ARG, "bad argument");
+// batched plans (nb > 1): the stage-1 chunks must not straddle two matrices, so n % chunk == 0; the
+// stage-2 "chunk" is then one matrix's R / nb chunk rows, and stage 2 writes out[b][d] directly
+static int batched_plan_ok(int nb, int n, const ColsumPlan& p) { return nb == 1 || (p.R > 1 && n % p.chunk == 0); }
+
+extern "C" long long mjl_colsum_batched_scratch(int nb, int n, int d) {
+  if (nb <= 0 || n <= 0 || d <= 0) return 0;
+  const ColsumPlan p(n, d);
+  return p.R > 1 ? (long long)nb * p.R * d : 0;
+}
+
+extern "C" int mjl_colsum_batched(const float* x, int nb, int n, int d, float* scratch, float* out, void* stream) {
+  if ((!x && n > 0) || !out || nb <= 0 || n < 0 || d <= 0) return fail(MJL_ERR_ARG, "bad argument");
   hipStream_t s = (hipStream_t)stream;
   if (n == 0) {
-    HIPCHK(hipMemsetAsync(out, 0, sizeof(float) * (size_t)d, s));
+    HIPCHK(hipMemsetAsync(out, 0, sizeof(float) * (size_t)d * nb, s));
     return MJL_OK;
   }
   const ColsumPlan p(n, d);
-  if (p.R > 1 && !scratch) return fail(MJL_ERR_ARG, "colsum needs mjl_colsum_scratch(n, d) floats of scratch");
+  if (!batched_plan_ok(nb, n, p)) return fail(MJL_ERR_ARG, "colsum_batched: n must be a multiple of %d", p.chunk);
+  if (p.R > 1 && !scratch) return fail(MJL_ERR_ARG, "colsum needs mjl_colsum_batched_scratch(nb, n, d) floats of scratch");
   const unsigned tiles1 = (unsigned)((d + p.dc1 - 1) / p.dc1);
-  hipLaunchKernelGGL(colsum_kernel, dim3(tiles1, (unsigned)p.R), dim3(256), 0, s, x, n, d, p.dc1, p.chunk,
+  hipLaunchKernelGGL(colsum_kernel, dim3(tiles1, (unsigned)(p.R * nb)), dim3(256), 0, s, x, n * nb, d, p.dc1, p.chunk,
                      p.R > 1 ? scratch : out);
   HIPCHK(hipGetLastError());
   if (p.R > 1) {
     const unsigned tiles2 = (unsigned)((d + p.dc2 - 1) / p.dc2);
-    hipLaunchKernelGGL(colsum_kernel, dim3(tiles2, 1), dim3(256), 0, s, scratch, p.R, d, p.dc2, p.R, out);
+    hipLaunchKernelGGL(colsum_kernel, dim3(tiles2, (unsigned)nb), dim3(256), 0, s, scratch, p.R * nb, d, p.dc2, p.R,
+                       out);
+    HIPCHK(hipGetLastError());
+  }
+  return MJL_OK;
+}
+
+extern "C" int mjl_colsum(const float* x, int n, int d, float* scratch, float* out, void* stream) {
+  return mjl_colsum_batched(x, 1, n, d, scratch, out, stream);
+}
+
+extern "C" int mjl_tanh_bwd_colsum_batched(const float* g, const float* y, int nb, int n, int d, float* dz,
+                                           float* scratch, float* colsum_out, void* stream) {
+  if (!g || !y || !dz || !colsum_out || nb <= 0 || n <= 0 || d <= 0) return fail(MJL_ERR_ARG, "bad argument");
+  if (d % 4 || ((uintptr_t)g | (uintptr_t)y | (uintptr_t)dz | (uintptr_t)colsum_out) % 16)
+    return fail(MJL_ERR_ARG, "tanh_bwd_colsum: d divisible by 4 and 16-byte aligned rows expected");
+  hipStream_t s = (hipStream_t)stream;
+  const ColsumPlan p(n, d);
+  if (!batched_plan_ok(nb, n, p)) return fail(MJL_ERR_ARG, "tanh_bwd_colsum_batched: n must be a multiple of %d", p.chunk);
+  if (p.R > 1 && (!scratch || (uintptr_t)scratch % 16))
+    return fail(MJL_ERR_ARG, "tanh_bwd_colsum needs mjl_colsum_batched_scratch(nb, n, d) floats of 16-byte aligned scratch");
+  const int dq = d / 4 < 64 ? d / 4 : 64;
+  const unsigned tiles1 = (unsigned)((d / 4 + dq - 1) / dq);
+  hipLaunchKernelGGL(tanh_bwd_colsum_kernel, dim3(tiles1, (unsigned)(p.R * nb)), dim3(256), 0, s, g, y, n * nb, d, dq,
+                     p.chunk, dz, p.R > 1 ? scratch : colsum_out);
+  HIPCHK(hipGetLastError());
+  if (p.R > 1) {
+    const unsigned tiles2 = (unsigned)((d + p.dc2 - 1) / p.dc2);
+    hipLaunchKernelGGL(colsum_kernel, dim3(tiles2, (unsigned)nb), dim3(256), 0, s, scratch, p.R * nb, d, p.dc2, p.R,
+                       colsum_out);
     HIPCHK(hipGetLastError());
   }
   return MJL_OK;
@@ -1000,33 +1058,30 @@ extern "C" int mjl_colsum(const float* x, int n, int d, float* scratch, float* o
 
 extern "C" int mjl_tanh_bwd_colsum(const float* g, const float* y, int n, int d, float* dz, float* scratch,
                                    float* colsum_out, void* stream) {
-  if (!g || !y || !dz || !colsum_out || n <= 0 || d <= 0) return fail(MJL_ERR_ARG, "bad argument");
-  if (d % 4 || ((uintptr_t)g | (uintptr_t)y | (uintptr_t)dz | (uintptr_t)colsum_out) % 16)
-    return fail(MJL_ERR_ARG, "tanh_bwd_colsum: d divisible by 4 and 16-byte aligned rows expected");
-  hipStream_t s = (hipStream_t)stream;
-  const ColsumPlan p(n, d);
-  if (p.R > 1 && (!scratch || (uintptr_t)scratch % 16))
-    return fail(MJL_ERR_ARG, "tanh_bwd_colsum needs mjl_colsum_scratch(n, d) floats of 16-byte aligned scratch");
-  const int dq = d / 4 < 64 ? d / 4 : 64;
-  const unsigned tiles1 = (unsigned)((d / 4 + dq - 1) / dq);
-  hipLaunchKernelGGL(tanh_bwd_colsum_kernel, dim3(tiles1, (unsigned)p.R), dim3(256), 0, s, g, y, n, d, dq, p.chunk, dz,
-                     p.R > 1 ? scratch : colsum_out);
+  return mjl_tanh_bwd_colsum_batched(g, y, 1, n, d, dz, scratch, colsum_out, stream);
+}
+
+extern "C" int mjl_slice_sum_batched(const float* x, int nb, int ns, long long m, float* out, void* stream) {
+  if (!x || !out || nb <= 0 || ns <= 0 || m <= 0) return fail(MJL_ERR_ARG, "bad argument");
+  if (m % 4 || ((uintptr_t)x | (uintptr_t)out) % 16)
+    return fail(MJL_ERR_ARG, "slice_sum: slice length divisible by 4 and 16-byte aligned buffers expected");
+  const long long q = m / 4;
+  hipLaunchKernelGGL(slice_sum_kernel, dim3((unsigned)((q + 255) / 256), (unsigned)nb), dim3(256), 0,
+                     (hipStream_t)stream, x, ns, m, out);
   HIPCHK(hipGetLastError());
-  if (p.R > 1) {
-    const unsigned tiles2 = (unsigned)((d + p.dc2 - 1) / p.dc2);
-    hipLaunchKernelGGL(colsum_kernel, dim3(tiles2, 1), dim3(256), 0, s, scratch, p.R, d, p.dc2, p.R, colsum_out);
-    HIPCHK(hipGetLastError());
-  }
   return MJL_OK;
 }
 
 extern "C" int mjl_slice_sum(const float* x, int ns, long long m, float* out, void* stream) {
-  if (!x || !out || ns <= 0 || m <= 0) return fail(MJL_ERR_ARG, "bad argument");
-  if (m % 4 || ((uintptr_t)x | (uintptr_t)out) % 16)
-    return fail(MJL_ERR_ARG, "slice_sum: slice length divisible by 4 and 16-byte aligned buffers expected");
-  const long long q = m / 4;
-  hipLaunchKernelGGL(slice_sum_kernel, dim3((unsigned)((q + 255) / 256)), dim3(256), 0, (hipStream_t)stream, x, ns, m,
-                     out);
+  return mjl_slice_sum_batched(x, 1, ns, m, out, stream);
+}
+
+extern "C" int mjl_twin_head_bwd(const float* g_mean, const float* mean, const float* g_v, int M, int A, float* dz4,
+                                 void* stream) {
+  if (!g_mean || !mean || !g_v || !dz4 || M <= 0 || A <= 0) return fail(MJL_ERR_ARG, "bad argument");
+  const long long n = 2LL * M * A;
+  hipLaunchKernelGGL(twin_head_bwd_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, (hipStream_t)stream,
+                     g_mean, mean, g_v, M, A, dz4);
   HIPCHK(hipGetLastError());
   return MJL_OK;
 }
@@ -1186,14 +1241,19 @@ extern "C" int mjl_ppo_surrogate(const float* mean, const float* log_std, const 
   return MJL_OK;
 }
 
-extern "C" int mjl_mse(const float* v, const float* r, int n, float* scratch, float* loss, float* g_v, void* stream) {
-  if (!v || !r || !scratch || !loss || !g_v || n <= 0) return fail(MJL_ERR_ARG, "bad argument");
+extern "C" int mjl_mse_strided(const float* v, int vstride, const float* r, int n, float* scratch, float* loss,
+                               float* g_v, void* stream) {
+  if (!v || !r || !scratch || !loss || !g_v || n <= 0 || vstride <= 0) return fail(MJL_ERR_ARG, "bad argument");
   hipStream_t s = (hipStream_t)stream;
   const int nb = (n + kLossT - 1) / kLossT;
-  hipLaunchKernelGGL(mse_kernel, dim3(nb), dim3(kLossT), 0, s, v, r, n, g_v, scratch);
+  hipLaunchKernelGGL(mse_kernel, dim3(nb), dim3(kLossT), 0, s, v, vstride, r, n, g_v, scratch);
   hipLaunchKernelGGL(mse_final_kernel, dim3(1), dim3(64), 0, s, scratch, nb, n, loss);
   HIPCHK(hipGetLastError());
   return MJL_OK;
+}
+
+extern "C" int mjl_mse(const float* v, const float* r, int n, float* scratch, float* loss, float* g_v, void* stream) {
+  return mjl_mse_strided(v, 1, r, n, scratch, loss, g_v, stream);
 }
 
 extern "C" int mjl_gather_rows(const long long* idx, int n, long long nsrc, int narr, const float* const* src,

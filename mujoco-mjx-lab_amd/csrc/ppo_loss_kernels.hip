@@ -175,14 +175,15 @@ __global__ __launch_bounds__(64) void ppo_surrogate_final_kernel(const float* __
   }
 }
 
-// value MSE: per block sum of (v - r)^2 and d/dv = 2 (v - r) / n
-__global__ __launch_bounds__(kLossT) void mse_kernel(const float* __restrict__ v, const float* __restrict__ r, int n,
-                                                     float* __restrict__ gv, float* __restrict__ part) {
+// value MSE: per block sum of (v - r)^2 and d/dv = 2 (v - r) / n (v[i] at v + i * vstride: the value
+// column of the twin update's padded output layer)
+__global__ __launch_bounds__(kLossT) void mse_kernel(const float* __restrict__ v, int vstride, const float* __restrict__ r,
+                                                     int n, float* __restrict__ gv, float* __restrict__ part) {
   __shared__ float red[kLossT];
   const int i = blockIdx.x * kLossT + threadIdx.x;
   float e = 0.f;
   if (i < n) {
-    const float d = v[i] - r[i];
+    const float d = v[(size_t)i * vstride] - r[i];
     e = d * d;
     gv[i] = 2.f * d / (float)n;
   }
@@ -196,12 +197,15 @@ __global__ __launch_bounds__(64) void mse_final_kernel(const float* __restrict__
   if (threadIdx.x == 0) loss[0] = s / (float)n;
 }
 
-// out[e] = sum_s x[s][e] over `ns` slices of `m` floats, slices in order (the split-K weight
-// gradient's sum over its batched GEMMs); float4 per thread, m % 4 == 0
+// out[b][e] = sum_s x[b][s][e] over `ns` slices of `m` floats, slices in order (the split-K weight
+// gradient's sum over its batched GEMMs; b = blockIdx.y, the net of the twin update); float4 per
+// thread, m % 4 == 0
 __global__ __launch_bounds__(256) void slice_sum_kernel(const float* __restrict__ x, int ns, long long m,
                                                         float* __restrict__ out) {
   const long long q = (long long)blockIdx.x * blockDim.x + threadIdx.x;
   if (q * 4 >= m) return;
+  x += (size_t)blockIdx.y * ns * m;
+  out += (size_t)blockIdx.y * m;
   const float4* src = reinterpret_cast<const float4*>(x) + q;
   const long long stride = m / 4;
   float4 acc = src[0];
@@ -218,6 +222,26 @@ __global__ __launch_bounds__(256) void slice_sum_kernel(const float* __restrict_
     acc.x += a.x; acc.y += a.y; acc.z += a.z; acc.w += a.w;
   }
   reinterpret_cast<float4*>(out)[q] = acc;
+}
+
+// The twin update's output-layer backward (ppo.py TwinUpdate): the policy's mean = tanh(z) sits in
+// out4[0] ([M, A], after the in-place tanh), the value in column 0 of out4[1]; g_mean = d loss / d mean
+// (mjl_ppo_surrogate), g_v = d loss / d value (mjl_mse). dz4[0] = g_mean (1 - mean^2), dz4[1][:, 0] =
+// g_v, dz4[1][:, 1:] = 0 (the value's padded output rows get no gradient).
+__global__ __launch_bounds__(256) void twin_head_bwd_kernel(const float* __restrict__ g_mean,
+                                                            const float* __restrict__ mean,
+                                                            const float* __restrict__ g_v, int M, int A,
+                                                            float* __restrict__ dz4) {
+  const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  const long long n = (long long)M * A;
+  if (i >= 2 * n) return;
+  if (i < n) {
+    const float y = mean[i];
+    dz4[i] = g_mean[i] * (1.f - y * y);
+  } else {
+    const long long j = i - n, r = j / A;
+    dz4[i] = (j - r * A == 0) ? g_v[r] : 0.f;
+  }
 }
 
 // elementwise tanh in place, float4 (the update's forward activations; torch's tanh kernel ran at

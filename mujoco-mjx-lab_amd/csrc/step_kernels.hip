@@ -1951,7 +1951,9 @@ template <class D, bool G> PHASE void sensors(MP m_, LDSA WS<D>* W, Rows<G> R, i
 }
 
 // rows that do not fit in LDS: the cold path, kept out of line
-template <class D> NOINL void global_rows_path(MP m, LDSA WS<D>* W, float* scratch_env, int gmax_efc, int gmax_con,
+// MW: the calling kernel's waves-per-SIMD bound. A callee shared by kernels of different bounds is
+// compiled for the loosest, and its register use then caps the tighter kernel's occupancy.
+template <class D, int MW = MJL_MINWAVES> NOINL void global_rows_path(MP m, LDSA WS<D>* W, float* scratch_env, int gmax_efc, int gmax_con,
                                                int lane) {
   Rows<true> R = global_rows<D>(scratch_env, gmax_efc, gmax_con);
   build_rows<D, true>(m, W, R, lane);
@@ -1960,7 +1962,7 @@ template <class D> NOINL void global_rows_path(MP m, LDSA WS<D>* W, float* scrat
 }
 
 // full forward pass (mjx.forward)
-template <class D> PHASE void forward(MP m_, LDSA WS<D>* W, float* scratch_env, int gmax_efc, int gmax_con,
+template <class D, int MW = MJL_MINWAVES> PHASE void forward(MP m_, LDSA WS<D>* W, float* scratch_env, int gmax_efc, int gmax_con,
                                       int force_global, int lane, const KinPre& kp) {
   MP m = uniform_ptr(m_);
   constexpr int LD = D::LD;
@@ -1985,7 +1987,7 @@ template <class D> PHASE void forward(MP m_, LDSA WS<D>* W, float* scratch_env, 
     sensors<D, false>(m, W, R, lane);
     STAMP(7, lane);
   } else {  // more rows than fit in LDS (or forced): this env's slab of global scratch
-    global_rows_path<D>(m, W, scratch_env, gmax_efc, gmax_con, lane);
+    global_rows_path<D, MW>(m, W, scratch_env, gmax_efc, gmax_con, lane);
   }
 }
 
@@ -2152,7 +2154,8 @@ INL float jax_uniform(int mode, uint32_t k0, uint32_t k1, int i, int n) {
   return jax_bits_to_unit(i < h ? x0 : x1);
 }
 
-struct EnvArgs {  // per-launch env arguments
+struct EnvArgs {  // per-launch env arguments (built inside env_reset: a caller-side struct passed by
+                  // pointer lived in the private segment, stored by every wave in the kernel prologue)
   const mjlEnvConfig* cfg;
   const float* noise;
   float* scratch_env;
@@ -2163,10 +2166,17 @@ struct EnvArgs {  // per-launch env arguments
 };
 
 // single_reset (envs.py:115-202): random pose / velocity, forward, target, aux, obs
-template <class D> NOINL void env_reset(MP m_, LDSA WS<D>* W, const EnvArgs* Ap, int env, int lane,
-                                        LDSA float* aux_out, float* obs_out) {
+// (the launch's arguments come as the KParams fields the reset reads, passed by value: the call's
+// argument registers, no private-segment copy)
+template <class D, int MW = MJL_MINWAVES> NOINL void env_reset(MP m_, LDSA WS<D>* W, const mjlEnvConfig* cfg, const float* noise,
+                                        float* scratch_env, int gmax_efc, int gmax_con, int force_global,
+                                        uint32_t s0, uint32_t s1, uint32_t c0, uint32_t c1, const uint32_t* keys,
+                                        int key_mode, int env, int lane, LDSA float* aux_out, float* obs_out) {
   MP m = uniform_ptr(m_);
-  EnvArgs A = *Ap;
+  EnvArgs A;
+  A.cfg = cfg; A.noise = noise; A.scratch_env = scratch_env;
+  A.gmax_efc = gmax_efc; A.gmax_con = gmax_con; A.force_global = force_global;
+  A.s0 = s0; A.s1 = s1; A.c0 = c0; A.c1 = c1; A.keys = keys; A.key_mode = key_mode;
   CP c = (CP)A.cfg;
   const int nj = m->nq - 7, nv = m->nv, nd = nj + nv + 2;
   float u = 0.f;
@@ -2210,7 +2220,7 @@ template <class D> NOINL void env_reset(MP m_, LDSA WS<D>* W, const EnvArgs* Ap,
     if (lane == 0) { W->qvel[0] = vx; W->qvel[1] = vy; }
     SYNC();
   }
-  forward<D>(m, W, A.scratch_env, A.gmax_efc, A.gmax_con, A.force_global, lane, kp);
+  forward<D, MW>(m, W, A.scratch_env, A.gmax_efc, A.gmax_con, A.force_global, lane, kp);
   if (lane == 0) {
     LDSA float* bp = W->xpos[c->pelvis_body_id];
     float tx = bp[0] + c->target_dist, ty = bp[1], tz = bp[2];
@@ -2335,7 +2345,10 @@ template <class D> INL void rs_load(MP m, const KParams& P, LDSA WS<D>* W, LDSA 
 // ---------------------------------------------------------------------------------------------
 // the kernel: one workgroup (= one wavefront) per env
 // ---------------------------------------------------------------------------------------------
-template <class D, int MODE> __global__ __launch_bounds__(64, MJL_MINWAVES) void step_kernel(KParams P) {
+// MW = the waves per SIMD the register budget is sized for: 2 (248 VGPRs, the full-occupancy launches:
+// 2048 envs resident on 256 CUs) or 1 (the whole 512-entry register file: launches of at most one wave
+// per SIMD, e.g. C3's 1024-env rollout, where a second wave's share of the file would sit unused)
+template <class D, int MODE, int MW = MJL_MINWAVES> __global__ __launch_bounds__(64, MW) void step_kernel(KParams P) {
   __shared__ WS<D> Ws;
   __shared__ float aux_s[MJL_AUX_DIM + 3];
   LDSA WS<D>* W = (LDSA WS<D>*)&Ws;
@@ -2354,15 +2367,14 @@ template <class D, int MODE> __global__ __launch_bounds__(64, MJL_MINWAVES) void
   STAMP(36, lane);
   const int nq = m->nq, nv = m->nv, nu = m->nu;
   const StateBuf& S = P.s;
-  EnvArgs A;
-  A.cfg = P.env; A.noise = P.noise; A.scratch_env = P.scratch + (size_t)env * (size_t)P.scratch_stride;
-  A.gmax_efc = P.gmax_efc; A.gmax_con = P.gmax_con; A.force_global = P.force_global_rows;
-  A.s0 = P.seed_lo; A.s1 = P.seed_hi;
-  A.keys = P.keys; A.key_mode = P.key_mode;
-  {  // RNG counter = launch counter + the batch's device counter base (hipGraph replays)
-    unsigned long long c = ((unsigned long long)P.ctr_hi << 32 | P.ctr_lo) + (P.ctr_base ? *P.ctr_base : 0ull);
-    A.c0 = (uint32_t)c; A.c1 = (uint32_t)(c >> 32);
-  }
+  float* const scratch_env = P.scratch + (size_t)env * (size_t)P.scratch_stride;
+  // an in-place reset's arguments (the RNG counter = launch counter + the batch's device counter base,
+  // for hipGraph replays), formed only on the reset path
+  auto do_reset = [&](float* obs_out) {
+    const unsigned long long c = ((unsigned long long)P.ctr_hi << 32 | P.ctr_lo) + (P.ctr_base ? *P.ctr_base : 0ull);
+    env_reset<D, MW>(m, W, P.env, P.noise, scratch_env, P.gmax_efc, P.gmax_con, P.force_global_rows, P.seed_lo,
+                 P.seed_hi, (uint32_t)c, (uint32_t)(c >> 32), P.keys, P.key_mode, env, lane, aux, obs_out);
+  };
 
   // vectors beyond nv must read as zero in the LD-wide row kernels
   for (int i = lane; i < LD; i += 64) {
@@ -2374,7 +2386,7 @@ template <class D, int MODE> __global__ __launch_bounds__(64, MJL_MINWAVES) void
   SYNC();
 
   if (MODE == MODE_ENV_RESET) {
-    env_reset<D>(m, W, &A, env, lane, aux, P.obs ? P.obs + (size_t)env * P.env->obs_dim : nullptr);
+    do_reset(P.obs ? P.obs + (size_t)env * P.env->obs_dim : nullptr);
   } else {
     const KinPre kp = kin_prefetch(m, lane);  // issued before the state loads: the latencies overlap
     if (MODE == MODE_SPEEDTEST) {  // fresh make_data, qvel[0] = vel (mjx_humanoid_speed_test.py:50-55)
@@ -2385,19 +2397,22 @@ template <class D, int MODE> __global__ __launch_bounds__(64, MJL_MINWAVES) void
     } else {
       // every state load issues before the first wait: clamped lane indices instead of a branch around
       // each load (each branch waited for its own load: ~7 dependent HBM round trips per env step)
-      const int iq = lane < nq ? lane : nq - 1, iv = lane < nv ? lane : nv - 1, iu = lane < nu ? lane : nu - 1;
-      const float q = S.qpos[(size_t)env * nq + iq];
-      const float v = S.qvel[(size_t)env * nv + iv], w = S.qacc_warmstart[(size_t)env * nv + iv];
+      // (a zero-size field clamps to index 0 and is not read: no load before a user buffer's start)
+      const int iq = lane < nq ? lane : max(nq - 1, 0), iv = lane < nv ? lane : max(nv - 1, 0);
+      const int iu = lane < nu ? lane : max(nu - 1, 0);
+      const float q = nq > 0 ? S.qpos[(size_t)env * nq + iq] : 0.f;
+      const float v = nv > 0 ? S.qvel[(size_t)env * nv + iv] : 0.f;
+      const float w = nv > 0 ? S.qacc_warmstart[(size_t)env * nv + iv] : 0.f;
       const float* csrc = (MODE == MODE_ENV_STEP || (MODE == MODE_STEP && P.in_ctrl)) ? P.in_ctrl : S.ctrl;
-      float c = csrc[(size_t)env * nu + iu];
+      float c = nu > 0 ? csrc[(size_t)env * nu + iu] : 0.f;
       const float t = S.time[env];
       float ax = 0.f, sgn = 1.f;
       int perm = iu;
       if (MODE == MODE_ENV_STEP) {
         const int ia = lane < MJL_AUX_DIM ? lane : MJL_AUX_DIM - 1;
         ax = S.aux[(size_t)env * MJL_AUX_DIM + ia];
-        perm = P.env->act_perm[iu];
-        sgn = P.env->act_sign[iu];
+        perm = nu > 0 ? P.env->act_perm[iu] : 0;
+        sgn = nu > 0 ? P.env->act_sign[iu] : 1.f;
       }
       if (lane < nq) W->qpos[lane] = q;
       if (lane < nv) { W->qvel[lane] = v; W->qacc_ws[lane] = w; }
@@ -2412,7 +2427,7 @@ template <class D, int MODE> __global__ __launch_bounds__(64, MJL_MINWAVES) void
       if (lane < nu) W->ctrl[lane] = c;
     }
     SYNC();
-    forward<D>(m, W, A.scratch_env, A.gmax_efc, A.gmax_con, A.force_global, lane, kp);
+    forward<D, MW>(m, W, scratch_env, P.gmax_efc, P.gmax_con, P.force_global_rows, lane, kp);
     if (MODE != MODE_FORWARD) integrate<D>(m, W, lane);
     STAMP(8, lane);
     if (MODE == MODE_ENV_STEP) {
@@ -2434,7 +2449,7 @@ template <class D, int MODE> __global__ __launch_bounds__(64, MJL_MINWAVES) void
           rs_load<D>(m, P, W, aux, obs, (size_t)slot * P.nenv + env, lane);
           if (lane == 0) P.pool_ctl[2 * env] = slot + 1;
         } else {
-          env_reset<D>(m, W, &A, env, lane, aux, obs);
+          do_reset(obs);
         }
       }
       STAMP(38, lane);

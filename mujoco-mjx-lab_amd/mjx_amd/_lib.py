@@ -30,6 +30,8 @@ EXPORTS = [
     "mjl_apg_obs", "mjl_apg_post", "mjl_apg_obs_vjp", "mjl_env_step_record", "mjl_env_step_vjp_replay",
     "mjl_ppo_loss_scratch", "mjl_ppo_surrogate", "mjl_mse", "mjl_gather_rows", "mjl_adam",
     "mjl_adam_dev", "mjl_mlp_fwd", "mjl_mlp_colpart_rows", "mjl_mlp_bwd",
+    "mjl_colsum_batched_scratch", "mjl_colsum_batched", "mjl_tanh_bwd_colsum_batched", "mjl_slice_sum_batched",
+    "mjl_twin_head_bwd", "mjl_mse_strided",
 ]
 
 _lib = None
@@ -123,6 +125,13 @@ def lib() -> C.CDLL:
     L.mjl_tanh_bwd_colsum.argtypes = [f32p, f32p, i32, i32, f32p, f32p, f32p, vp]
     L.mjl_slice_sum.argtypes = [f32p, i32, C.c_longlong, f32p, vp]
     L.mjl_tanh_inplace.argtypes = [f32p, C.c_longlong, vp]
+    L.mjl_colsum_batched_scratch.argtypes = [i32, i32, i32]
+    L.mjl_colsum_batched_scratch.restype = C.c_longlong
+    L.mjl_colsum_batched.argtypes = [f32p, i32, i32, i32, f32p, f32p, vp]
+    L.mjl_tanh_bwd_colsum_batched.argtypes = [f32p, f32p, i32, i32, i32, f32p, f32p, f32p, vp]
+    L.mjl_slice_sum_batched.argtypes = [f32p, i32, i32, C.c_longlong, f32p, vp]
+    L.mjl_twin_head_bwd.argtypes = [f32p, f32p, f32p, i32, i32, f32p, vp]
+    L.mjl_mse_strided.argtypes = [vp, i32, vp, i32, vp, vp, vp, vp]
     L.mjl_small_mlp_fwd.argtypes = [vp, i32, i32, i32, vp, vp, vp, vp, vp]
     L.mjl_small_mlp_bwd_input.argtypes = [vp, i32, i32, i32, vp, vp, vp, vp, vp]
     L.mjl_step_vjp.argtypes = [vp, f32p, f32p, f32p, f32p, f32p, vp]

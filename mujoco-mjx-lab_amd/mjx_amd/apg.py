@@ -112,9 +112,6 @@ class APGTrainer:
         self.rank = dist.get_rank() if dist is not None else 0
         self.world = dist.get_world_size() if dist is not None else 1
         self.device = torch.device(device)
-        if self.device.type == "cuda":
-            from .tunable import use_tuned_gemms
-            use_tuned_gemms(self.device)
         self.obs_dim = env.nq + env.nv
         g = torch.Generator().manual_seed(int(cfg.seed))
         self.policy = APGPolicy(self.obs_dim, env.act_dim, cfg.hidden_size, cfg.hidden_depth, None, g).to(self.device)
@@ -122,7 +119,11 @@ class APGTrainer:
             for p in self.policy.parameters():
                 dist.broadcast(p.data, 0)
         self.opt = torch.optim.Adam(self.policy.parameters(), lr=cfg.lr, betas=(0.9, 0.999), eps=1e-8)
-        self.native_policy = NativeAPGPolicy(self.policy) if NativeAPGPolicy.eligible(self.policy, self.device) else None
+        # MJL_APG_NATIVE_POLICY=0 (or native_policy = None): the policy's per-step passes through torch,
+        # so the torch restatement (_loss_and_grad_torch) checks the native kernels independently
+        use_nat = os.environ.get("MJL_APG_NATIVE_POLICY", "1") != "0"
+        self.native_policy = (NativeAPGPolicy(self.policy)
+                              if use_nat and NativeAPGPolicy.eligible(self.policy, self.device) else None)
         self.rms = RunningMeanStd(self.obs_dim, self.device)
         self.total_env_steps = 0.0
         self.start = time.time()
@@ -141,6 +142,12 @@ class APGTrainer:
         return o, (apg_normalize(self.rms, x) if use_norm else x)
 
     def loss_and_grad(self, use_norm: bool, per_step_param_grad: bool = False):
+        """_loss_and_grad_graphed under the tuned GEMM table (mjx_amd/tunable.py: on only here)."""
+        from .tunable import tuned_gemms
+        with tuned_gemms(self.device):
+            return self._loss_and_grad_graphed(use_norm, per_step_param_grad)
+
+    def _loss_and_grad_graphed(self, use_norm: bool, per_step_param_grad: bool = False):
         """One rollout + backward (see _loss_and_grad). On the GPU the second and later calls per
         `use_norm` replay one hipGraph of the whole thing: ~60 launches per rollout step (env step,
         VJP, the policy's forward and backward, the guard's elementwise ops) with no host in between;

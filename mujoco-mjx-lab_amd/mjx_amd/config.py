@@ -85,12 +85,13 @@ class APGConfig(BaseConfig):
     # (dropped from the loss from that step on). Truncated solves (CG 4/4) diverge for some envs under
     # MJX's integrator rules (DESIGN.md "Truncated solves"); the reference's loss turns NaN/huge there.
     diverge_qvel: float = 1e3
-    # not in the reference (train_apg.py:290-292 feeds every rollout observation to the statistics): only
+    # off = the reference (train_apg.py:290-292 feeds every rollout observation to the statistics). On
+    # (opt-in, train_apg.py --rms-in-loss-only; not the reference's normalisation, parity unpinned): only
     # the observations that enter the loss -- of envs not yet terminated, diverged or non-finite -- update
     # them. A fallen env keeps stepping to the horizon; under CG 4/4 some of those diverge (|qvel| ~1e13)
     # and, included, their variance swamps the statistics: when normalisation starts at update 100 every
     # policy input collapses to ~const and the return drops from ~-130 to ~-416 (DESIGN.md "APG C4").
-    rms_in_loss_only: bool = True
+    rms_in_loss_only: bool = False
 
 
 @dataclass

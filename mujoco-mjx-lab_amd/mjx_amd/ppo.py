@@ -163,7 +163,8 @@ def _linear(lin: nn.Linear, x: torch.Tensor) -> torch.Tensor:
     whose fixed batched-GEMM + sum order is also deterministic: the library's single GEMM over K =
     8,192 rows (the per-rank minibatch of C5 at 8 GPUs) was not bit-reproducible run to run."""
     n = x.shape[0] if x.dim() == 2 else 0
-    if x.is_cuda and torch.is_grad_enabled() and n >= UPDATE_MIN_ROWS and n % SPLIT_ROWS == 0:
+    if (x.is_cuda and torch.is_grad_enabled() and n >= UPDATE_MIN_ROWS and n % SPLIT_ROWS == 0
+            and x.dtype == torch.float32):
         return _SplitKLinear.apply(x, lin.weight, lin.bias, min(64, n // SPLIT_ROWS))
     return lin(x)
 
@@ -828,7 +829,12 @@ class PPOUpdater:
 
     The graphs need NativeAdam (its step count is device state). The first run is eager (library
     handles, allocator pools, GEMM choices); the second captures. Replays equal the eager bodies bit
-    for bit (tests/test_ppo_graph.py)."""
+    for bit (tests/test_ppo_graph.py).
+
+    With NativeAdam on the GPU and the reference's network pair (same tanh hidden layers), the two
+    nets run as one batched pass per layer (twin.TwinNets, MJL_TWIN_UPDATE=0 disables): their
+    parameters become views of stacked storage, the gradients land in one flat buffer that is also
+    the data-parallel all-reduce buffer, and no second stream is needed."""
 
     def __init__(self, policy, value, opt_p, opt_v, cfg, dist=None, world=1, use_graph=True):
         self.policy, self.value, self.opt_p, self.opt_v, self.cfg = policy, value, opt_p, opt_v, cfg
@@ -836,9 +842,6 @@ class PPOUpdater:
         self.pp, self.vp = list(policy.parameters()), list(value.parameters())
         dev = self.pp[0].device
         self.cuda = dev.type == "cuda"
-        if self.cuda:
-            from .tunable import use_tuned_gemms
-            use_tuned_gemms(dev)
         self.graph_ok = (bool(use_graph) and self.cuda and isinstance(opt_p, NativeAdam)
                          and isinstance(opt_v, NativeAdam))
         # the value net's forward / backward (and, single-process, its Adam step) on a second stream beside
@@ -854,17 +857,43 @@ class PPOUpdater:
                 views.append(self.flat[o:o + p.numel()].view_as(p))
                 o += p.numel()
             self.views_p, self.views_v = views[:len(self.pp)], views[len(self.pp):]
+        self.twin = None
+        if self.cuda and isinstance(opt_p, NativeAdam) and isinstance(opt_v, NativeAdam):
+            from .twin import twin_for
+            self.twin = twin_for(policy, value)
+        self._tw = False  # this run takes the twin path (minibatch shape permitting)
         self.runs = 0
         self._src = self._idx = self._st = None
         self._ga = self._gb = None
 
+    def _twin_ok(self, rows: int, act_dim: int) -> bool:
+        return (self.twin is not None and rows >= UPDATE_MIN_ROWS and rows % SPLIT_ROWS == 0 and rows % 128 == 0
+                and act_dim == self.twin.A and self.twin.owns_storage())
+
+    def _grad_buffer(self):
+        """The data-parallel all-reduce buffer of this run: the twin's flat gradients or self.flat."""
+        return self.twin.grad if self._tw else self.flat
+
+    def allreduce_numel(self) -> int:
+        """Floats per all-reduce (the twin layout pads the value's output layer to the policy's width)."""
+        if self.twin is not None:
+            return int(self.twin.grad.numel())
+        return sum(p.numel() for p in self.pp + self.vp)
+
     # ------------------------------------------------------------------ bodies
     def _body_a(self, idx, src, st):
         """Gather the minibatch; forward + backward of both nets (and, single-process, both Adam
-        steps). Data-parallel: leaves both nets' gradients in self.flat."""
+        steps). Data-parallel: leaves both nets' gradients in the all-reduce buffer."""
         cfg, opt_p, opt_v = self.cfg, self.opt_p, self.opt_v
         o, a, ol, r, ad = _gather_minibatch(idx, *src)
         dp = self.dist is not None
+        if self._tw:
+            tw = self.twin
+            tw.forward_backward(o, a, ol, r, ad, st, cfg.clip_eps, cfg.ent_coef, min(64, o.shape[0] // SPLIT_ROWS))
+            if not dp:
+                opt_p.step(grads=tw.grads_p)
+                opt_v.step(grads=tw.grads_v)
+            return
         if self.side is not None:
             cur = torch.cuda.current_stream(o.device)
             self.side.wait_stream(cur)
@@ -894,6 +923,11 @@ class PPOUpdater:
 
     def _body_b(self):
         """Data-parallel: the all-reduced gradient sum -> mean, then both Adam steps."""
+        if self._tw:
+            self.twin.grad.div_(self.world)
+            self.opt_p.step(grads=self.twin.grads_p)
+            self.opt_v.step(grads=self.twin.grads_v)
+            return
         self.flat.div_(self.world)
         if isinstance(self.opt_p, NativeAdam):
             self.opt_p.step(grads=self.views_p)
@@ -912,7 +946,7 @@ class PPOUpdater:
             else:
                 ev = _HostTimer()
                 ev.record(0)
-        self.dist.all_reduce(self.flat)
+        self.dist.all_reduce(self._grad_buffer())
         if ev is not None:
             if self.cuda:
                 ev[1].record()
@@ -923,9 +957,19 @@ class PPOUpdater:
     # ------------------------------------------------------------------ driver
     def run(self, obs, acts, logp, ret, adv, index_batches, events: Optional[list] = None):
         """One update over `index_batches` [n_minibatches, rows] of the flattened rollout arrays.
-        `events` (a list) collects one timing pair per all-reduce (event_ms)."""
+        `events` (a list) collects one timing pair per all-reduce (event_ms). The update's GEMMs run
+        under the tuned GEMM table (mjx_amd/tunable.py: on only inside this call)."""
+        from .tunable import tuned_gemms
+        with tuned_gemms(self.pp[0].device if self.cuda else None):
+            self._run(obs, acts, logp, ret, adv, index_batches, events)
+
+    def _run(self, obs, acts, logp, ret, adv, index_batches, events):
         src = (obs, acts, logp, ret, adv)
         stats = minibatch_adv_stats(adv, index_batches, self.dist) if self.dist is not None else None
+        tw = self._twin_ok(int(index_batches.shape[1]), int(acts.shape[1]) if acts.dim() == 2 else -1)
+        if tw != self._tw:
+            self._ga = self._gb = None  # the captured bodies belong to the other path
+        self._tw = tw
         use_graph = self.graph_ok and self.runs > 0
         self.runs += 1
         if not use_graph:

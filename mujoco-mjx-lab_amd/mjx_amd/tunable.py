@@ -8,9 +8,15 @@ TunableOp's own numerical check against the default solution). Loading it switch
 lookup-only mode: shapes in the file run their tuned solution, others the default, nothing is tuned
 at run time. Measured: PPO update at 2048 envs 51.6 -> 47.5 ms (tools/ppo_update_probe.py graph).
 
+Scope: the table is loaded once per process, but TunableOp is switched on only inside `tuned_gemms()`
+(the PPO update's minibatch steps, the APG policy's parameter-gradient pass) and restored to its
+previous state on exit, so GEMMs elsewhere in the user's process (evaluation, user code) keep the
+library's default choices. A hipGraph captured inside the scope keeps the tuned kernels it captured.
+
 The file's validators (torch, HIP, hipBLASLt, rocBLAS versions and the gfx arch) must match the
 running stack or TunableOp ignores it (then: the default solutions, as without this module).
 MJL_TUNED_GEMMS=0 disables; a user's own PYTORCH_TUNABLEOP_* configuration takes precedence."""
+import contextlib
 import os
 import tempfile
 
@@ -21,7 +27,8 @@ _state = {"done": False, "loaded": False}
 
 
 def use_tuned_gemms(device) -> bool:
-    """Enable the tuned GEMM table for `device` (once per process). Returns whether it is active."""
+    """Load the tuned GEMM table for `device` (once per process; TunableOp stays off outside
+    tuned_gemms()). Returns whether the table is loaded."""
     if _state["done"]:
         return _state["loaded"]
     dev = torch.device(device)
@@ -38,6 +45,28 @@ def use_tuned_gemms(device) -> bool:
     # results are written back only when tuning is on; point the file name away from the cwd anyway
     tn.set_filename(os.path.join(tempfile.gettempdir(), f"mjl_tunableop_{os.getpid()}_%d.csv"))
     _state["loaded"] = bool(tn.read_file(TUNED_CSV))
-    if not _state["loaded"]:
-        tn.enable(False)
+    tn.enable(False)  # on only inside tuned_gemms()
     return _state["loaded"]
+
+
+def table_loaded() -> bool:
+    """Whether the tuned table is loaded in this process (recorded in the bench line)."""
+    return bool(_state["loaded"])
+
+
+@contextlib.contextmanager
+def tuned_gemms(device=None):
+    """TunableOp on (lookup only, the loaded table) for the GEMMs issued inside; its previous state
+    restored on exit. A no-op when the table is not loaded or `device` is not a GPU."""
+    if device is not None and torch.device(device).type == "cuda":
+        use_tuned_gemms(device)
+    if not _state["loaded"]:
+        yield False
+        return
+    import torch.cuda.tunable as tn
+    prev = tn.is_enabled()
+    tn.enable(True)
+    try:
+        yield True
+    finally:
+        tn.enable(prev)

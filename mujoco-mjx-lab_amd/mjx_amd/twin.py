@@ -1,0 +1,182 @@
+"""The PPO update's two networks as one batched pass per layer (train_ppo.py:233-252).
+
+Per minibatch the reference takes a policy step (value_and_grad of ppo_loss_fn through the policy MLP)
+and a value step (value_loss_fn through the value MLP), src/networks.py:22-131. With the reference's
+src/config.json both MLPs have the same hidden layers (3 x 256 tanh) and read the same normalised
+observations, so every hidden layer of the two nets is one strided-batched GEMM of batch 2 — twice the
+tiles of one net's GEMM per launch — and every elementwise / reduction pass runs over both nets at
+once. At the 8,192-row per-rank minibatch of C5 (8 GPUs) one net's 256-wide layer is 64 row tiles
+for 256 CUs; the pair is 128, and the number of launches per minibatch step halves.
+
+Layout (`TwinNets`): each layer's weights live in one stacked tensor W[l] [2, N, K] and b[l] [2, N]
+(net 0 = policy, net 1 = value); the nn.Linear parameters of both modules become views of it, so
+the rollout's packed policy, evaluation, checkpoints and the optimisers see the same storage. The
+value's output layer (1 unit) is padded to the policy's A units with zero rows that receive zero
+gradient (Adam leaves them at zero). The gradients land in one flat buffer laid out the same way,
+which is also the data-parallel all-reduce buffer (no concatenation).
+
+Forward: H_l = tanh(H_{l-1} W_lᵀ + b_l) as torch.baddbmm + the native in-place tanh; Z = H W_outᵀ +
+b_out; mean = tanh(Z[0]); v = Z[1][:, 0]. Losses: mjl_ppo_surrogate on (mean, clamp(log_std)),
+mjl_mse_strided on v. Backward, by hand in the order autograd takes: mjl_twin_head_bwd forms
+dZ; each layer's weight gradient is the split-K batched GEMM dZᵀ X over both nets (2 x splits
+slices, summed in order by mjl_slice_sum_batched), its bias gradient the fixed-order column sums
+(mjl_colsum_batched / mjl_tanh_bwd_colsum_batched, which also forms dZ_l = dH (1 - H²)), dH =
+dZ W as one batched GEMM. Same formulas as the per-net path (ppo.py _SplitKLinear /
+_TanhSplitKLinear + the native losses); the GEMMs are the library's batched kernels instead of its
+single ones, so results agree to rounding, not bit for bit (tests/test_twin.py)."""
+from __future__ import annotations
+
+import os
+from typing import List, Optional
+
+import torch
+
+from ._lib import check, lib
+
+TWIN_UPDATE = os.environ.get("MJL_TWIN_UPDATE", "1") != "0"
+
+
+def _align4(n: int) -> int:
+    return (n + 3) // 4 * 4
+
+
+class TwinNets:
+    """Stacked storage for a GaussianPolicy and a ValueNet with identical tanh hidden layers; builds
+    the views and runs one minibatch's forward + backward into the flat gradient buffer."""
+
+    @staticmethod
+    def eligible(policy, value) -> bool:
+        pm, vm = policy.mlp, value.mlp
+        if len(pm.layers) != len(vm.layers) or len(pm.layers) < 2:
+            return False
+        if not all(a == "tanh" for a in pm.acts[:-1]) or not all(a == "tanh" for a in vm.acts[:-1]):
+            return False
+        if pm.acts[-1] not in ("linear", "none") or vm.acts[-1] not in ("linear", "none"):
+            return False
+        for lp, lv in zip(pm.layers[:-1], vm.layers[:-1]):
+            if lp.weight.shape != lv.weight.shape or lp.out_features % 4:
+                return False
+        A = pm.layers[-1].out_features
+        ps = list(policy.parameters()) + list(value.parameters())
+        return (vm.layers[-1].out_features == 1 and 1 <= A <= 32 and pm.layers[-1].in_features == vm.layers[-1].in_features
+                and all(p.is_cuda and p.dtype == torch.float32 for p in ps) and policy.log_std.numel() == A)
+
+    def __init__(self, policy, value):
+        self.policy, self.value = policy, value
+        pm, vm = policy.mlp, value.mlp
+        dev = pm.layers[0].weight.device
+        self.nl = len(pm.layers)
+        self.A = pm.layers[-1].out_features
+        self.K0 = pm.layers[0].in_features
+        shapes = [tuple(l.weight.shape) for l in pm.layers]  # [N, K]; the output layer's N = A
+        # one flat buffer for the stacked parameters and one for their gradients (+ log_std's)
+        offs, o = [], 0
+        for N, K in shapes:
+            offs.append((o, _align4(o + 2 * N * K)))
+            o = _align4(o + 2 * N * K) + _align4(2 * N)
+        self.numel = o
+        self.glog_off = o
+        self.grad = torch.zeros(o + _align4(self.A), device=dev)
+        self.store = torch.zeros(o, device=dev)
+        self.W, self.b, self.gW, self.gb = [], [], [], []
+        for (N, K), (ow, ob) in zip(shapes, offs):
+            self.W.append(self.store[ow:ow + 2 * N * K].view(2, N, K))
+            self.b.append(self.store[ob:ob + 2 * N].view(2, N))
+            self.gW.append(self.grad[ow:ow + 2 * N * K].view(2, N, K))
+            self.gb.append(self.grad[ob:ob + 2 * N].view(2, N))
+        self.g_log_std = self.grad[self.glog_off:self.glog_off + self.A]
+        with torch.no_grad():
+            for l, (lp, lv) in enumerate(zip(pm.layers, vm.layers)):
+                n_v = lv.out_features
+                self.W[l][0].copy_(lp.weight)
+                self.b[l][0].copy_(lp.bias)
+                self.W[l][1, :n_v].copy_(lv.weight)
+                self.b[l][1, :n_v].copy_(lv.bias)
+                lp.weight.data = self.W[l][0]
+                lp.bias.data = self.b[l][0]
+                lv.weight.data = self.W[l][1, :n_v]
+                lv.bias.data = self.b[l][1, :n_v]
+        # gradient views in each module's parameters() order (the optimisers' order)
+        self.grads_p: List[torch.Tensor] = [t for l in range(self.nl) for t in (self.gW[l][0], self.gb[l][0])]
+        self.grads_p.append(self.g_log_std)
+        self.grads_v: List[torch.Tensor] = [t for l in range(self.nl) for t in (
+            self.gW[l][1, :vm.layers[l].out_features], self.gb[l][1, :vm.layers[l].out_features])]
+        self._scr = {}
+
+    def owns_storage(self) -> bool:
+        """Whether the modules' parameters still are views of the stacked storage (a load_state_dict
+        copies into them and keeps it; re-assigning .data would not)."""
+        pm = self.policy.mlp
+        return all(l.weight.data_ptr() == self.W[i][0].data_ptr() for i, l in enumerate(pm.layers))
+
+    def _scratch(self, key, floats: int) -> torch.Tensor:
+        st = torch.cuda.current_stream(self.grad.device).cuda_stream
+        k = (key, floats, st)
+        t = self._scr.get(k)
+        if t is None:
+            t = self._scr[k] = torch.empty(max(floats, 4), device=self.grad.device)
+        return t
+
+    def forward_backward(self, o, acts, old_logp, ret, adv, adv_stats, clip_eps: float, ent_coef: float, splits: int):
+        """Both nets' losses and gradients for one minibatch (o [M, K0], acts [M, A], old_logp / ret /
+        adv [M]); the gradients into self.grad. Returns (policy loss, value loss) device scalars."""
+        L = lib()
+        dev = o.device
+        st = torch.cuda.current_stream(dev).cuda_stream
+        M, A, nl = o.shape[0], self.A, self.nl
+        s = splits
+        # ---- forward
+        x = o.unsqueeze(0).expand(2, M, self.K0).contiguous()  # both nets read the same observations
+        hs = [x]
+        for l in range(nl - 1):
+            h = torch.baddbmm(self.b[l].unsqueeze(1), hs[-1], self.W[l].transpose(1, 2))
+            check(L.mjl_tanh_inplace(h.data_ptr(), h.numel(), st))
+            hs.append(h)
+        z = torch.baddbmm(self.b[nl - 1].unsqueeze(1), hs[-1], self.W[nl - 1].transpose(1, 2))  # [2, M, A]
+        mean = z[0]
+        check(L.mjl_tanh_inplace(mean.data_ptr(), mean.numel(), st)) if (M * A) % 4 == 0 else mean.tanh_()
+        # ---- losses (networks.py:103 clamps log_std to [-20, 2]; its gradient passes inside the bounds)
+        log_std = self.policy.log_std
+        ls = torch.clamp(log_std.detach(), -20.0, 2.0).contiguous()
+        loss_p = torch.empty((), device=dev)
+        loss_v = torch.empty((), device=dev)
+        gm = torch.empty((M, A), device=dev)
+        gs = torch.empty(A, device=dev)
+        scr = self._scratch("loss", int(L.mjl_ppo_loss_scratch(M, A)))
+        check(L.mjl_ppo_surrogate(mean.data_ptr(), ls.data_ptr(), acts.data_ptr(), old_logp.data_ptr(), adv.data_ptr(),
+                                  None if adv_stats is None else adv_stats.data_ptr(), M, A, float(clip_eps),
+                                  float(ent_coef), scr.data_ptr(), loss_p.data_ptr(), gm.data_ptr(), gs.data_ptr(), st))
+        gv = torch.empty(M, device=dev)
+        scr_v = self._scratch("mse", M // 256 + 1)
+        check(L.mjl_mse_strided(z[1].data_ptr(), A, ret.data_ptr(), M, scr_v.data_ptr(), loss_v.data_ptr(),
+                                gv.data_ptr(), st))
+        inside = (log_std.detach() >= -20.0) & (log_std.detach() <= 2.0)
+        torch.where(inside, gs, torch.zeros_like(gs), out=self.g_log_std)
+        # ---- backward
+        dz = torch.empty((2, M, A), device=dev)
+        check(L.mjl_twin_head_bwd(gm.data_ptr(), mean.data_ptr(), gv.data_ptr(), M, A, dz.data_ptr(), st))
+        ncs = int(L.mjl_colsum_batched_scratch(2, M, max(A, self.W[0].shape[1])))
+        cs = self._scratch("colsum", ncs)
+        check(L.mjl_colsum_batched(dz.data_ptr(), 2, M, A, cs.data_ptr(), self.gb[nl - 1].data_ptr(), st))
+        g = dz
+        for l in range(nl - 1, -1, -1):
+            N, K = self.W[l].shape[1], self.W[l].shape[2]
+            xin = hs[l]  # the layer's input: H_{l-1}, or the observations for l = 0
+            if l < nl - 1:  # tanh layer: dZ = dH (1 - H^2) and the bias gradient in one pass
+                dzl = torch.empty_like(g)
+                check(L.mjl_tanh_bwd_colsum_batched(g.data_ptr(), hs[l + 1].data_ptr(), 2, M, N, dzl.data_ptr(),
+                                                    cs.data_ptr(), self.gb[l].data_ptr(), st))
+            else:
+                dzl = g
+            part = torch.bmm(dzl.view(2 * s, M // s, N).transpose(1, 2), xin.view(2 * s, M // s, K))  # [2s, N, K]
+            check(L.mjl_slice_sum_batched(part.data_ptr(), 2, s, N * K, self.gW[l].data_ptr(), st))
+            if l > 0:
+                g = torch.bmm(dzl, self.W[l])  # [2, M, K]
+        return loss_p, loss_v
+
+
+def twin_for(policy, value) -> Optional[TwinNets]:
+    """A TwinNets over (policy, value) when MJL_TWIN_UPDATE is on and the pair is eligible."""
+    if TWIN_UPDATE and TwinNets.eligible(policy, value):
+        return TwinNets(policy, value)
+    return None

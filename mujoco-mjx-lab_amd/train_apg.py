@@ -53,9 +53,11 @@ def main():
                     help="solver derivative: unrolled = jax.grad through the iterations (default with --solver cg), "
                          "implicit = at the converged active set (default with --solver model)")
     ap.add_argument("--results-dir", default=None)
-    ap.add_argument("--rms-all-obs", action="store_true",
-                    help="observation statistics from every rollout observation (train_apg.py:290-292), "
-                         "not only those of envs still in the loss (APGConfig.rms_in_loss_only)")
+    ap.add_argument("--rms-in-loss-only", action="store_true",
+                    help="observation statistics only from the observations of envs still in the loss "
+                         "(APGConfig.rms_in_loss_only; not the reference's rule, which takes every rollout "
+                         "observation, train_apg.py:290-292 -- the default)")
+    ap.add_argument("--rms-all-obs", action="store_true", help="the default (kept for old command lines)")
     a = ap.parse_args()
 
     cfg = APGConfig()
@@ -66,8 +68,7 @@ def main():
         cfg.total_steps = a.steps
     if a.results_dir:
         cfg.results_dir = a.results_dir
-    if a.rms_all_obs:
-        cfg.rms_in_loss_only = False
+    cfg.rms_in_loss_only = bool(a.rms_in_loss_only) and not a.rms_all_obs
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank, local = int(os.environ.get("RANK", "0")), int(os.environ.get("LOCAL_RANK", "0"))

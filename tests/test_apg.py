@@ -371,6 +371,35 @@ def test_apg_native_bookkeeping_matches_torch_ops(solver, vjp):
 
 
 @pytest.mark.gpu
+def test_apg_native_sweep_matches_pure_torch_restatement():
+    """The native sweep (native bookkeeping + the native policy's per-step passes, mjl_small_mlp_fwd /
+    mjl_small_mlp_bwd_input) against the torch restatement with the policy in torch too (native_policy =
+    None: torch GEMMs, autograd for the input cotangent), so the native policy is checked independently.
+    Newton 10/20 (converged solves, implicit VJP), 64 envs x 8 steps, 3 updates: the two policies round
+    their GEMMs differently, so loss / gradient norm / parameters agree to 1e-4, not bit for bit."""
+    import mjx_amd
+    from mjx_amd import mjx
+    from mjx_amd.config import reference_ppo_config
+    from mjx_amd.envs import HumanoidEnv, resolve_ids
+    m = mjx_amd.load_model("humanoid_mjx")
+    ecfg = resolve_ids(m, reference_ppo_config().env_config)
+    cfg = _cfg(batch_size=64, horizon=8, hidden_size=32)
+    envs = [apg.HumanoidAPGEnv(HumanoidEnv(mjx.put_model(m), ecfg, cfg.batch_size, seed=3), "implicit")
+            for _ in range(2)]
+    envs[1].native_apg = False
+    trs = [apg.APGTrainer(cfg, e, device="cuda", use_graph=False, vjp_tape=False) for e in envs]
+    assert trs[0].native_policy is not None
+    trs[1].native_policy = None
+    for step in range(3):
+        ms = [tr.update(step) for tr in trs]
+        assert ms[0]["nonfinite_envs"] == ms[1]["nonfinite_envs"]
+        for k in ("loss", "grad_norm", "mean_reward"):
+            assert ms[0][k] == pytest.approx(ms[1][k], rel=1e-4, abs=1e-5), f"update {step}: {k}"
+        for p, q in zip(trs[0].policy.parameters(), trs[1].policy.parameters()):
+            torch.testing.assert_close(p, q, rtol=1e-4, atol=1e-5)
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("k0,hidden,depth,act_dim,B", [(55, 32, 2, 21, 2048), (55, 64, 3, 21, 1000), (7, 16, 1, 3, 5)])
 def test_native_apg_policy_matches_torch(k0, hidden, depth, act_dim, B):
     """mjl_small_mlp_fwd / mjl_small_mlp_bwd_input against the APGPolicy's torch forward and the

@@ -145,7 +145,8 @@ def test_apg_c4_update_at_full_size(vjp):
     """C4 (2048 x 128, CG 4/4), two updates (the second a graph replay). Implicit VJP: no env's
     cotangents overflow (reverse_nonfinite_envs == 0). Unrolled VJP (jax.grad through the truncated
     solve): the chained per-step Jacobians grow x2.3 per reverse step and overflow fp32 for part of the
-    batch (measured ~700 of 2048), which the guard cuts; bounded here at 1,000. Either
+    batch (measured 700-770 of 2048 in updates 0-1), which the guard cuts; bounded here at
+    800 (a regression that raised the overflow rate would show). Either
     way a few envs' forward states diverge under the truncated solve (forward_dropped_envs, the same
     in both modes: the forward is identical)."""
     cfg, env, tr = _apg_trainer(2048, 128, vjp=vjp)
@@ -157,7 +158,7 @@ def test_apg_c4_update_at_full_size(vjp):
         if vjp == "implicit":
             assert met["reverse_nonfinite_envs"] == 0, met
         else:
-            assert met["reverse_nonfinite_envs"] <= 1000, met
+            assert met["reverse_nonfinite_envs"] <= 800, met
         assert met["forward_dropped_envs"] <= 2048 // 20, met
 
 

@@ -1,0 +1,96 @@
+"""The twin PPO update (mjx_amd/twin.py: the policy and value nets' layers as one batched GEMM per layer,
+train_ppo.py:233-252) against autograd of the reference's loss formulas in float64
+(train_ppo.py:204-220 restated as torch ops, ppo.NATIVE_LOSSES = False): every gradient of both nets to
+1e-4 of its scale, at the 8,192-row per-rank minibatch of C5 (8 GPUs) and the 65,536-row one of C3;
+and the twin updater against the per-net updater (MJL_TWIN_UPDATE path off) over a whole update."""
+import pytest
+import torch
+
+from mjx_amd import ppo, twin
+from mjx_amd.config import reference_ppo_config
+
+pytestmark = pytest.mark.gpu
+
+
+def _nets(cfg, seed=0):
+    g = torch.Generator().manual_seed(seed)
+    pol = ppo.GaussianPolicy(54, 21, cfg.policy_hidden_layer_specs, cfg.log_std_init, g).cuda()
+    val = ppo.ValueNet(54, cfg.value_hidden_layer_specs, g).cuda()
+    with torch.no_grad():  # non-trivial biases and log_std (the init zeroes them)
+        for p in list(pol.parameters()) + list(val.parameters()):
+            if p.dim() == 1:
+                p.add_(torch.randn(p.shape, generator=g).cuda() * 0.1)
+    return pol, val
+
+
+def _data(n, seed=1):
+    gd = torch.Generator(device="cuda").manual_seed(seed)
+    return (torch.randn((n, 54), generator=gd, device="cuda"),
+            torch.rand((n, 21), generator=gd, device="cuda") * 1.8 - 0.9,
+            torch.randn(n, generator=gd, device="cuda") - 20.0,
+            torch.randn(n, generator=gd, device="cuda"), torch.randn(n, generator=gd, device="cuda"))
+
+
+@pytest.mark.parametrize("n", [8192, 65536])
+def test_twin_gradients_match_float64_autograd(n):
+    cfg = reference_ppo_config()
+    pol, val = _nets(cfg)
+    ref_p = ppo.GaussianPolicy(54, 21, cfg.policy_hidden_layer_specs).cuda().double()
+    ref_v = ppo.ValueNet(54, cfg.value_hidden_layer_specs).cuda().double()
+    ref_p.load_state_dict({k: v.double() for k, v in pol.state_dict().items()})
+    ref_v.load_state_dict({k: v.double() for k, v in val.state_dict().items()})
+    assert twin.TwinNets.eligible(pol, val)
+    tw = twin.TwinNets(pol, val)
+    o, a, ol, r, ad = _data(n)
+    lp, lv = tw.forward_backward(o, a, ol, r, ad, None, cfg.clip_eps, cfg.ent_coef, min(64, n // ppo.SPLIT_ROWS))
+    torch.cuda.synchronize()
+    old = ppo.NATIVE_LOSSES
+    ppo.NATIVE_LOSSES = False
+    try:
+        loss_p = ppo.ppo_policy_loss(ref_p, o.double(), a.double(), ol.double(), ad.double(), cfg.clip_eps,
+                                     cfg.ent_coef)
+        loss_v = ppo.value_loss(ref_v, o.double(), r.double())
+        (loss_p + loss_v).backward()
+    finally:
+        ppo.NATIVE_LOSSES = old
+    assert float(lp) == pytest.approx(float(loss_p), rel=1e-5, abs=1e-6)
+    assert float(lv) == pytest.approx(float(loss_v), rel=1e-5)
+    for got, p in zip(tw.grads_p + tw.grads_v, list(ref_p.parameters()) + list(ref_v.parameters())):
+        want = p.grad.float()
+        scale = float(want.abs().max()) + 1e-12
+        err = float((got - want).abs().max())
+        assert err <= 1e-4 * scale, f"{tuple(want.shape)}: max error {err:.3e} of scale {scale:.3e}"
+    # the modules' parameters are views of the stacked storage, the value's padded output rows stay 0
+    assert tw.owns_storage()
+    assert float(tw.W[-1][1, 1:].abs().max()) == 0.0 and float(tw.gW[-1][1, 1:].abs().max()) == 0.0
+
+
+def test_twin_update_matches_per_net_update():
+    """One update (2 minibatches of 8,192 rows x 2 epochs) through PPOUpdater with and without the
+    twin path: parameters and Adam moments agree to rounding (the batched GEMMs round like the single
+    ones up to the library's kernel choice)."""
+    cfg = reference_ppo_config()
+    cfg.minibatch_size, cfg.epochs = 8192, 2
+    runs = []
+    for use_twin in (True, False):
+        pol, val = _nets(cfg)
+        op, ov = ppo._adam(pol.parameters(), cfg.lr_policy), ppo._adam(val.parameters(), cfg.lr_value)
+        saved = twin.TWIN_UPDATE
+        twin.TWIN_UPDATE = use_twin
+        try:
+            up = ppo.PPOUpdater(pol, val, op, ov, cfg, use_graph=False)
+        finally:
+            twin.TWIN_UPDATE = saved
+        assert (up.twin is not None) == use_twin
+        idx = ppo.make_index_batches(2 * 8192, 8192, 2, torch.Generator(device="cuda").manual_seed(5), "cuda")
+        up.run(*_data(2 * 8192), idx)
+        torch.cuda.synchronize()
+        runs.append([t.detach().clone() for t in list(pol.parameters()) + list(val.parameters())])
+    for a, b in zip(*runs):
+        # 4 Adam steps of lr 3e-4: all but 1e-3 of the entries to 2e-6 + 2e-5 relative; an entry whose
+        # gradient is at rounding-noise level may take a different O(lr) step, so every entry within
+        # 2 lr per step
+        err = (a - b).abs()
+        off = err > 2e-6 + 2e-5 * b.abs()
+        assert off.float().mean().item() <= 1e-3, f"{int(off.sum())} of {off.numel()} entries off"
+        assert err.max().item() <= 2 * 3e-4 * 4

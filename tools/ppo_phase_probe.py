@@ -1,7 +1,12 @@
 """Where one C3 PPO iteration goes (1024 envs x 256 x 4 epochs, minibatch 65,536): rollout (one
 hipGraph replay), the between-phase work (observation statistics, value net over (T + 1) B
 observations, GAE, minibatch permutations) and the update (16 minibatch graph replays), timed with
-events on the trainer's stream after 2 warm-up iterations (graph capture). One JSON line."""
+events on the trainer's stream after 2 warm-up iterations (graph capture). One JSON line.
+
+PROBE_B=envs (default 1024); PROBE_MB=rows: the minibatch rows of one rank. With PROBE_DP=1 the
+trainer runs its data-parallel path on a one-rank gloo group (graph A, the all-reduce of both nets'
+gradients, graph B per minibatch), so PROBE_MB=8192 is one C5 rank's update at 8 GPUs (128
+minibatch steps) without the other ranks' link time."""
 import json
 import os
 import statistics
@@ -17,11 +22,21 @@ from mjx_amd.ppo import compute_gae, make_index_batches  # noqa: E402
 
 def main():
     args = bench.parse()
-    tr = bench.ppo_trainer(args, int(os.environ.get("PROBE_B", "1024")), None, 0, 0)
+    dist = None
+    if os.environ.get("PROBE_DP") == "1":
+        import torch.distributed as dist
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        os.environ.setdefault("MASTER_PORT", str(bench.free_port()))
+        torch.cuda.set_device(0)
+        dist.init_process_group("gloo", rank=0, world_size=1)
+    tr = bench.ppo_trainer(args, int(os.environ.get("PROBE_B", "1024")), dist, 0, 0)
+    if os.environ.get("PROBE_MB"):
+        tr.cfg.minibatch_size = int(os.environ["PROBE_MB"])
     for it in range(2):
         tr.iteration(it)
     cfg, dev = tr.cfg, tr.device
     ms = {"rollout": [], "between": [], "update": [], "total": []}
+    ar_ms, n_ar = [], []
     for _ in range(5):
         ev = [torch.cuda.Event(enable_timing=True) for _ in range(4)]
         torch.cuda.synchronize()
@@ -37,15 +52,26 @@ def main():
             adv, ret = compute_gae(r_t, v, te_t, tr_t, cfg.gamma, cfg.lam)
         idx = make_index_batches(T * B, cfg.minibatch_size, cfg.epochs, tr.idx_gen, dev)
         ev[2].record()
+        evs = [] if dist is not None else None
         tr.updater.run(obs_n.reshape(T * B, -1), act_t.reshape(T * B, -1), logp_t.reshape(-1), ret.reshape(-1),
-                       adv.reshape(-1), idx, None)
+                       adv.reshape(-1), idx, evs)
         ev[3].record()
         torch.cuda.synchronize()
         ms["rollout"].append(ev[0].elapsed_time(ev[1]))
         ms["between"].append(ev[1].elapsed_time(ev[2]))
         ms["update"].append(ev[2].elapsed_time(ev[3]))
         ms["total"].append(ev[0].elapsed_time(ev[3]))
-    print(json.dumps({k: round(statistics.median(v), 3) for k, v in ms.items()}), flush=True)
+        if evs is not None:
+            from mjx_amd.ppo import event_ms
+            ar_ms.append(sum(event_ms(e) for e in evs))
+            n_ar.append(len(evs))
+    line = {k: round(statistics.median(v), 3) for k, v in ms.items()}
+    line.update(envs=tr.env.num_envs, minibatch_rows=int(idx.shape[1]), minibatches=int(idx.shape[0]),
+                data_parallel=dist is not None)
+    if ar_ms:
+        line.update(allreduce_total_ms=round(statistics.median(ar_ms), 3), allreduces=n_ar[0],
+                    allreduce_backend="gloo, one rank (copy + host round trip; no link time)")
+    print(json.dumps(line), flush=True)
 
 
 if __name__ == "__main__":
