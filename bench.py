@@ -36,6 +36,7 @@ import numpy as np  # noqa: E402
 import torch  # noqa: E402
 
 REF_DEVICE_STEPS_PER_S = 72618.0  # HUMANOID_MJX device steps/s (README.md:77), batch 4096
+REF_HUMANOID_XML_STEPS_PER_S = 6176.0  # README.md:76 HUMANOID row (humanoid.xml)
 HBM_PEAK_GBS = 8000.0             # MI355X_MICROARCH.md: HBM3E peak 8.0 TB/s (spec)
 F32_PEAK_TFLOPS = 157.3           # MI355X_MICROARCH.md: peak FP32 matrix (dense) = FP32 vector
 SPEEDTEST_KERNEL = "step_kernel<mjl::Dims<27, 17, 22, 20, 48, 16>, 2>"  # rocprofv3 kernel name
@@ -328,7 +329,7 @@ def speedtest(args, dist, world, local):
         "config": {"workload": f"{args.model}.xml speed-test step (fresh state per step), {B} envs per GPU",
                    "envs_per_gpu": B, "parallelism": f"env-sharded x{world}, no collective in the speed test",
                    "baseline_note": "vs_baseline divides by the README HUMANOID_MJX row (72,618 steps/s, batch 4096)"},
-        "roofline": {"bound": "mfma", "achieved": achieved_tflops, "peak": F32_PEAK_TFLOPS, "unit": "TFLOP/s",
+        "roofline": {"bound": "valu", "achieved": achieved_tflops, "peak": F32_PEAK_TFLOPS, "unit": "TFLOP/s",
                      "frac": achieved_tflops / F32_PEAK_TFLOPS, "traffic": pmc_traffic(B),
                      "kernel": SPEEDTEST_KERNEL, "kernel_ms": kern_ms,
                      "flops_per_env_step": fl["total"],
@@ -336,9 +337,10 @@ def speedtest(args, dist, world, local):
                      "workload_mean_active_rows_per_hessian": float(wst[3]),
                      "hbm_algorithmic_bytes_per_launch": bytes_per_env * B,
                      "hbm_achieved_gbs": achieved_gbs, "hbm_frac": achieved_gbs / HBM_PEAK_GBS,
-                     "note": "FP32 roof (dense MFMA = vector peak); achieved = algorithmic FP32 FLOPs "
-                             "(mjx_amd/flops.py) / kernel time; traffic = HBM bytes per launch from the "
-                             "committed FETCH_SIZE/WRITE_SIZE passes (profiles/, DESIGN.md)"},
+                     "note": "bound: VALU issue / dependency latency of one env per wave (SQ counters, "
+                             "DESIGN.md 3), priced against the FP32 roof (vector peak = dense MFMA peak); "
+                             "achieved = algorithmic FP32 FLOPs (mjx_amd/flops.py) / kernel time; traffic = "
+                             "HBM bytes per launch from the committed FETCH_SIZE/WRITE_SIZE passes (profiles/)"},
     }
     return line, (model, sys_)
 
@@ -399,7 +401,7 @@ def speedtest_extras(args, model, sys_, local):
                                                          args.warmup, None)
     tf = fl["total"] * B / (ek * 1e-3) / 1e12
     ex["env_step_roofline"] = {
-        "bound": "mfma", "achieved": tf, "peak": F32_PEAK_TFLOPS, "unit": "TFLOP/s", "frac": tf / F32_PEAK_TFLOPS,
+        "bound": "valu", "achieved": tf, "peak": F32_PEAK_TFLOPS, "unit": "TFLOP/s", "frac": tf / F32_PEAK_TFLOPS,
         "kernel": "step_kernel<mjl::Dims<27, 17, 22, 20, 48, 16>, 3>", "kernel_ms": ek,
         "flops_per_env_step": fl["total"], "flops_by_stage": {k: v for k, v in fl.items() if k != "total"},
         "workload_mean_ncon_nefc_iter": [float(x) for x in est[:3]],
@@ -408,6 +410,20 @@ def speedtest_extras(args, model, sys_, local):
         "hbm_algorithmic_bytes_per_launch": ENV_STEP_BYTES * B,
         "hbm_frac": ENV_STEP_BYTES * B / (ek * 1e-3) / 1e9 / HBM_PEAK_GBS}
     del env, dd
+    # the README's HUMANOID row (humanoid.xml, 159 candidate pairs, Newton 100/50, Euler + eulerdamp;
+    # mjx_humanoid_speed_test.py:140, README.md:76: 6,176 steps/s) on the same speed test at B envs
+    import mjx_amd
+    mh = mjx_amd.load_model("humanoid")
+    sh = mjx.put_model(mh)
+    dh = mjx.make_data(sh, B, device=local)
+    dh.set_option(0, 0)
+    vh = torch.linspace(0.0, 1.0, B, device=dev)
+    oh = torch.empty_like(vh)
+    hw, hk = timed_launches(lambda: mjx.speedtest_step(sh, dh, vh, oh), args.steps, args.warmup, None)
+    ex["speedtest_humanoid_xml_steps_per_s"] = B * args.steps / hw
+    ex["speedtest_humanoid_xml_kernel_ms"] = hk
+    ex["speedtest_humanoid_xml_vs_readme"] = ex["speedtest_humanoid_xml_steps_per_s"] / REF_HUMANOID_XML_STEPS_PER_S
+    del dh
     # the reference's own batch size for the README row
     d4 = mjx.make_data(sys_, 4096, device=local)
     v4 = torch.linspace(0.0, 1.0, 4096, device=dev)
@@ -435,6 +451,7 @@ def ppo_leg(tr, iters: int, warmup: int, dist, device, curve=()) -> dict:
     for _ in range(warmup):
         one()
     tr.allreduce_events = []
+    tr.phase_events = []
     sync(device)
     barrier(dist)
     sync(device)
@@ -447,6 +464,14 @@ def ppo_leg(tr, iters: int, warmup: int, dist, device, curve=()) -> dict:
     ar = [event_ms(e) for e in tr.allreduce_events]
     tr.allreduce_events = None
     ar_ms = max_over_ranks(sum(ar) / len(ar) if ar else 0.0, dist, device)
+    # phase split of the timed iterations (events on the trainer's stream), median, max over ranks
+    phases = {}
+    if tr.phase_events:
+        import statistics
+        for name, (a, b) in (("rollout", (0, 1)), ("between", (1, 2)), ("update", (2, 3))):
+            phases[name] = max_over_ranks(statistics.median(e[a].elapsed_time(e[b]) for e in tr.phase_events), dist,
+                                          device)
+    tr.phase_events = None
     while curve and it[0] <= max(curve):
         one()
     world = 1 if dist is None else dist.get_world_size()
@@ -455,7 +480,7 @@ def ppo_leg(tr, iters: int, warmup: int, dist, device, curve=()) -> dict:
             "warmup": warmup, "envs_per_rank": tr.env.num_envs, "ranks": world,
             "allreduce_ms": ar_ms, "allreduces_per_iter": len(ar) // max(1, iters),
             "train_return_avg": [r["train_return_avg"] for r in res], "return_at_iter": returns,
-            "next_iteration": it[0]}
+            "next_iteration": it[0], "phase_ms": phases, "update_rows": getattr(tr, "last_update_rows", 0)}
 
 
 def c5_fields(res: dict, world: int, backend: str, grad_numel: int) -> dict:
@@ -465,7 +490,7 @@ def c5_fields(res: dict, world: int, backend: str, grad_numel: int) -> dict:
             "allreduce_ms_per_minibatch": res["allreduce_ms"], "allreduces_per_iteration": res["allreduces_per_iter"],
             "allreduce_bytes": 4 * grad_numel, "collective_backend": backend, "collective_ranks": world,
             "rccl_ranks": world if backend == "nccl" else 0,
-            "ppo_c5_train_return_avg": res["train_return_avg"]}
+            "ppo_c5_train_return_avg": res["train_return_avg"], "ppo_c5_phase_ms_per_rank": res["phase_ms"]}
 
 
 def ppo_trainer(args, envs, dist, rank, local, eval_envs=0):
@@ -489,12 +514,74 @@ def grad_numel(tr) -> int:
     return tr.updater.allreduce_numel()
 
 
+def update_roofline(tr, res) -> dict:
+    """The PPO update phase against the FP32 matrix roof: algorithmic FLOPs of both nets' forward +
+    backward over every minibatch row of one update (mjx_amd/flops.py ppo_update_flops) / the update
+    phase's event time on the trainer's stream."""
+    from mjx_amd import flops as flops_mod
+    cfg = tr.cfg
+    fl = flops_mod.ppo_update_flops(tr.env.obs_dim, tr.env.act_dim, cfg.policy_hidden_layer_specs,
+                                    cfg.value_hidden_layer_specs)
+    ms = res["phase_ms"].get("update")
+    if not ms:
+        return {}
+    rows = res["update_rows"]
+    tf = fl["total"] * rows / (ms * 1e-3) / 1e12
+    return {"bound": "mfma", "achieved": tf, "peak": F32_PEAK_TFLOPS, "unit": "TFLOP/s", "frac": tf / F32_PEAK_TFLOPS,
+            "update_ms": ms, "rows_per_update": rows, "flops_per_row": fl["total"],
+            "flops_per_row_by_net": {k: v for k, v in fl.items() if k != "total"},
+            "twin_update": tr.updater.twin is not None,
+            "note": "both nets' fwd + bwd GEMMs (fp32 on the matrix cores through hipBLASLt) + elementwise; "
+                    "achieved = algorithmic FLOPs / update-phase time (HIP events on the trainer's stream)"}
+
+
+def policy_roofline(tr, local) -> dict:
+    """The rollout's fused policy launch (mjl_policy_fwd: normalisation + MLP + Gaussian head, one
+    launch per rollout step) over the trainer's envs: 100 launches captured in one hipGraph, HIP events
+    around its replay."""
+    from mjx_amd import flops as flops_mod
+    from mjx_amd import ppo
+    bf, B = tr._buf, tr.env.num_envs
+    if bf is None or tr._pol_dims is None:
+        return {}
+
+    def launch():
+        ppo.policy_fwd_native(bf["obs"][0], tr.rms.mean, tr.rms.var, 10.0, tr._pol_params, tr._pol_dims,
+                              tr.policy.log_std, bf["eps"][0], bf["act"][0], bf["logp"][0])
+
+    dev = f"cuda:{local}"
+    launch()
+    sync(dev)
+    n = 100
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        for _ in range(n):
+            launch()
+    g.replay()
+    sync(dev)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    g.replay()
+    e1.record()
+    sync(dev)
+    kms = e0.elapsed_time(e1) / n
+    del g
+    cfg = tr.cfg
+    fl = flops_mod.policy_rollout_flops(tr.env.obs_dim, tr.env.act_dim, cfg.policy_hidden_layer_specs)
+    tf = fl["total"] * B / (kms * 1e-3) / 1e12
+    return {"bound": "mfma", "achieved": tf, "peak": F32_PEAK_TFLOPS, "unit": "TFLOP/s", "frac": tf / F32_PEAK_TFLOPS,
+            "kernel": "policy_rollout_kernel", "kernel_ms": kms, "envs": B, "flops_per_env": fl["total"],
+            "note": "fused rollout policy (v_mfma_f32_16x16x4_f32 tiles, 16 envs per workgroup); kernel_ms from "
+                    "HIP events around a replayed hipGraph of 100 launches"}
+
+
 def ppo_c3(args, local) -> dict:
     """C3: src/config.json PPO at 1024 envs on one GPU, throughput and return@iter (seed 42)."""
     tr = ppo_trainer(args, args.ppo_envs, None, 0, local, eval_envs=32)
     curve = tuple(i for i in PPO_CURVE_ITERS if i <= args.ppo_curve) if args.ppo_curve > 0 else ()
     t0 = time.perf_counter()
     res = ppo_leg(tr, args.ppo_iters, 2, None, f"cuda:{local}", curve)
+    upd = update_roofline(tr, res)
     ev_it = res["next_iteration"] - 1
     eval_ret = tr.evaluate(ev_it) if curve else None
     out = {"ppo_c3_env_steps_per_s": res["env_steps_per_s"], "ppo_c3_ms_per_iter": res["ms_per_iter"],
@@ -502,7 +589,12 @@ def ppo_c3(args, local) -> dict:
                             f"seed 42; {res['iters']} timed iterations after 2 (graph capture)",
            "ppo_return_at_iter": {str(k): v for k, v in sorted(res["return_at_iter"].items())},
            "ppo_eval_return_at_iter": {str(ev_it): eval_ret} if eval_ret is not None else {},
-           "ppo_curve_wall_s": time.perf_counter() - t0}
+           "ppo_curve_wall_s": time.perf_counter() - t0,
+           "ppo_c3_phase_ms": res["phase_ms"], "ppo_update_roofline": upd,
+           "ppo_update_tflops": upd.get("achieved"), "ppo_update_frac": upd.get("frac"),
+           "ppo_policy_roofline": policy_roofline(tr, local)}
+    from mjx_amd import tunable
+    out["tuned_gemm_table"] = tunable.table_loaded()
     del tr
     free_gpu()
     return out
@@ -540,6 +632,9 @@ def apg_c4(args, local) -> dict:
         out[f"{key}_ms_per_update"] = wall / len(res) * 1e3
         out[f"{key}_returns"] = [r["return"] for r in res]
         out[f"{key}_nonfinite_envs"] = [r["nonfinite_envs"] for r in res]
+        # the share of the batch whose cotangents overflowed and were cut from the gradient (unrolled
+        # VJP under CG 4/4: DESIGN.md 3b), per timed update
+        out[f"{key}_reverse_cut_frac"] = [r["reverse_nonfinite_envs"] / cfg.batch_size for r in res]
         if vjp == "implicit":  # the replay VJP kernel alone: one reverse sweep over the last update's tape
             B, H = cfg.batch_size, cfg.horizon
             act = torch.zeros((B, m.nu), device=dev)
@@ -558,12 +653,21 @@ def apg_c4(args, local) -> dict:
                         events[-1][1].record()
             sweep()  # warm-up
             sync(dev)
-            # one HIP event pair around each replay launch on its stream (the eager sweep's host gaps
-            # between launches stay out of the kernel time)
-            evs = []
-            sweep(evs)
+            # the H replay launches captured in one hipGraph, HIP events around its replay: the
+            # launches run back to back as in the trainer's graph (per-launch event pairs around eager
+            # launches also timed the gaps between them: 127 against rocprofv3's 101 us in round 3)
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g):
+                sweep()
+            g.replay()
             sync(dev)
-            kms = sum(e0.elapsed_time(e1) for e0, e1 in evs) / H
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            g.replay()
+            e1.record()
+            sync(dev)
+            kms = e0.elapsed_time(e1) / H
+            del g
             # the rollout's solver statistics (the same policy from fresh resets; CG reports no active-row
             # count, so the implicit Hessian is counted over all rows)
             env.data.set_option(0, 1)
@@ -577,9 +681,10 @@ def apg_c4(args, local) -> dict:
             fl = flops_mod.vjp_replay_flops(m, float(s[0]), float(s[1]), float(s[2]))
             tf = fl["total"] * B / (kms * 1e-3) / 1e12
             out["apg_vjp_roofline"] = {
-                "bound": "mfma", "achieved": tf, "peak": F32_PEAK_TFLOPS, "unit": "TFLOP/s",
+                "bound": "valu", "achieved": tf, "peak": F32_PEAK_TFLOPS, "unit": "TFLOP/s",
                 "frac": tf / F32_PEAK_TFLOPS, "kernel": "vjp_kernel<mjl::Dims<27, 17, 22, 20, 4, 4>, true, 2, true>",
-                "kernel_ms": kms, "launches_timed": H, "flops_per_env_step": fl["total"],
+                "kernel_ms": kms, "launches_timed": H, "timing": "one captured sweep of H replay launches",
+                "flops_per_env_step": fl["total"],
                 "flops_by_stage": {k: v for k, v in fl.items() if k != "total"},
                 "workload_mean_ncon_nefc_iter": [float(x) for x in s[:3]],
                 "traffic": pmc_traffic(B, "vjp_bytes_per_launch")}
@@ -587,7 +692,8 @@ def apg_c4(args, local) -> dict:
         free_gpu()
     out["apg_c4_config"] = (f"train_apg.py: {args.apg_envs} envs x {args.apg_horizon} horizon, CG 4/4, hidden 32x2, "
                             f"lr 5e-5, clip 0.3; {args.apg_updates} timed updates after 2 (graph capture); "
-                            f"apg_c4 = unrolled VJP (jax.grad semantics), apg_c4_implicit = implicit VJP")
+                            f"apg_c4 = unrolled VJP (jax.grad semantics), apg_c4_implicit = implicit VJP; observation "
+                            f"statistics: {'in-loss observations only (not the reference rule)' if APGConfig().rms_in_loss_only else 'every rollout observation (train_apg.py:290-292)'}")
     return out
 
 

@@ -430,6 +430,13 @@ int mjl_ppo_surrogate(const float* mean, const float* log_std, const float* act,
                       const float* adv, const float* adv_stats, int n, int A, float clip_eps, float ent_coef,
                       float* scratch, float* loss, float* g_mean, float* g_log_std, void* stream);
 int mjl_mse(const float* v, const float* r, int n, float* scratch, float* loss, float* g_v, void* stream);
+/* mjl_ppo_surrogate with log_std clipped to [log_std_lo, log_std_hi] on read (networks.py:103 clips it
+ * to [-20, 2]) and g_log_std zero where the raw value lies outside (torch.clamp's backward, bounds
+ * inclusive); +-INFINITY bounds = mjl_ppo_surrogate. */
+int mjl_ppo_surrogate_clipped(const float* mean, const float* log_std, const float* act, const float* old_logp,
+                              const float* adv, const float* adv_stats, int n, int A, float clip_eps, float ent_coef,
+                              float log_std_lo, float log_std_hi, float* scratch, float* loss, float* g_mean,
+                              float* g_log_std, void* stream);
 /* mjl_mse with v[i] read at v + i * vstride (the value column of the twin update's padded output). */
 int mjl_mse_strided(const float* v, int vstride, const float* r, int n, float* scratch, float* loss, float* g_v,
                     void* stream);

@@ -1221,10 +1221,10 @@ extern "C" long long mjl_ppo_loss_scratch(int n, int A) {
   return 3 * nb + nb * (A + 1);
 }
 
-extern "C" int mjl_ppo_surrogate(const float* mean, const float* log_std, const float* act, const float* old_logp,
-                                 const float* adv, const float* adv_stats, int n, int A, float clip_eps,
-                                 float ent_coef, float* scratch, float* loss, float* g_mean, float* g_log_std,
-                                 void* stream) {
+extern "C" int mjl_ppo_surrogate_clipped(const float* mean, const float* log_std, const float* act,
+                                         const float* old_logp, const float* adv, const float* adv_stats, int n, int A,
+                                         float clip_eps, float ent_coef, float log_std_lo, float log_std_hi,
+                                         float* scratch, float* loss, float* g_mean, float* g_log_std, void* stream) {
   if (!mean || !log_std || !act || !old_logp || !adv || !scratch || !loss || !g_mean || !g_log_std || n <= 0 || A <= 0)
     return fail(MJL_ERR_ARG, "bad argument");
   if (A > kLossMaxA) return fail(MJL_ERR_UNSUPPORTED, "ppo surrogate: at most %d action columns", kLossMaxA);
@@ -1234,11 +1234,19 @@ extern "C" int mjl_ppo_surrogate(const float* mean, const float* log_std, const 
   float* part = scratch + 3 * (size_t)nb;
   if (!adv_stats) hipLaunchKernelGGL(adv_stats_kernel, dim3(nb), dim3(kLossT), 0, s, adv, n, adv_part);
   hipLaunchKernelGGL(ppo_surrogate_kernel, dim3(nb), dim3(kLossT), 0, s, mean, log_std, act, old_logp, adv, n, A,
-                     clip_eps, adv_part, nb, adv_stats, g_mean, part);
+                     clip_eps, adv_part, nb, adv_stats, g_mean, part, log_std_lo, log_std_hi);
   hipLaunchKernelGGL(ppo_surrogate_final_kernel, dim3(A + 1), dim3(64), 0, s, part, nb, n, A, log_std, ent_coef, loss,
-                     g_log_std);
+                     g_log_std, log_std_lo, log_std_hi);
   HIPCHK(hipGetLastError());
   return MJL_OK;
+}
+
+extern "C" int mjl_ppo_surrogate(const float* mean, const float* log_std, const float* act, const float* old_logp,
+                                 const float* adv, const float* adv_stats, int n, int A, float clip_eps,
+                                 float ent_coef, float* scratch, float* loss, float* g_mean, float* g_log_std,
+                                 void* stream) {
+  return mjl_ppo_surrogate_clipped(mean, log_std, act, old_logp, adv, adv_stats, n, A, clip_eps, ent_coef, -INFINITY,
+                                   INFINITY, scratch, loss, g_mean, g_log_std, stream);
 }
 
 extern "C" int mjl_mse_strided(const float* v, int vstride, const float* r, int n, float* scratch, float* loss,

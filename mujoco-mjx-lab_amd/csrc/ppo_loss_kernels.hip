@@ -87,7 +87,7 @@ __global__ __launch_bounds__(kLossT) void ppo_surrogate_kernel(
     const float* __restrict__ mean, const float* __restrict__ log_std, const float* __restrict__ act,
     const float* __restrict__ old_logp, const float* __restrict__ adv, int n, int A, float clip_eps,
     const float* __restrict__ adv_part, int nb, const float* __restrict__ adv_stats, float* __restrict__ gmean,
-    float* __restrict__ part) {
+    float* __restrict__ part, float ls_lo, float ls_hi) {
   constexpr int NW = kLossT / 64;
   __shared__ float sd[kLossT * kLossMaxA];  // a - m of the block's rows, row-major
   __shared__ float sdl[kLossT];             // d logp per row
@@ -99,7 +99,7 @@ __global__ __launch_bounds__(kLossT) void ppo_surrogate_kernel(
   const size_t base = (size_t)r0 * A;
   for (int e = t; e < cnt; e += kLossT) sd[e] = act[base + e] - mean[base + e];
   if (t < A) {
-    const float ls = log_std[t];
+    const float ls = fminf(fmaxf(log_std[t], ls_lo), ls_hi);  // networks.py:103's clip (bounds +-inf: none)
     lsd[t] = ls;
     ivs[t] = expf(-2.f * ls);
   }
@@ -160,18 +160,22 @@ __global__ __launch_bounds__(kLossT) void ppo_surrogate_kernel(
 // loss = -sum surr / n - ent_coef * entropy; d loss / d s_j = sum of the partials - ent_coef / A
 // (entropy = 0.5 sum_j (1 + log 2 pi + 2 s_j) / A, train_ppo.py:215). One wave per column of the
 // [nb, A + 1] partials (blockIdx.x = column): lane l sums rows l, l + 64, ... in order, then wave_sum.
+// s_j = clip(log_std_j, ls_lo, ls_hi); the gradient passes to log_std inside the bounds (inclusive:
+// torch.clamp's backward), 0 outside.
 __global__ __launch_bounds__(64) void ppo_surrogate_final_kernel(const float* __restrict__ part, int nb, int n, int A,
                                                                  const float* __restrict__ log_std, float ent_coef,
-                                                                 float* __restrict__ loss, float* __restrict__ glog_std) {
+                                                                 float* __restrict__ loss, float* __restrict__ glog_std,
+                                                                 float ls_lo, float ls_hi) {
   const int lane = threadIdx.x, col = blockIdx.x;
   float s = 0.f;
   for (int b = lane; b < nb; b += 64) s += part[(size_t)b * (A + 1) + col];
   s = wave_sum(s);
   if (col == 0) {
-    const float e = wave_sum(lane < A ? 1.f + kLog2Pi + 2.f * log_std[lane] : 0.f);
+    const float e = wave_sum(lane < A ? 1.f + kLog2Pi + 2.f * fminf(fmaxf(log_std[lane], ls_lo), ls_hi) : 0.f);
     if (lane == 0) loss[0] = -s / (float)n - ent_coef * (0.5f * e / (float)A);
   } else if (lane == 0) {
-    glog_std[col - 1] = s - ent_coef / (float)A;
+    const float ls = log_std[col - 1];
+    glog_std[col - 1] = (ls >= ls_lo && ls <= ls_hi) ? s - ent_coef / (float)A : 0.f;
   }
 }
 

@@ -125,6 +125,7 @@ class APGTrainer:
         self.native_policy = (NativeAPGPolicy(self.policy)
                               if use_nat and NativeAPGPolicy.eligible(self.policy, self.device) else None)
         self.rms = RunningMeanStd(self.obs_dim, self.device)
+        self.diag = None  # a dict: the eager native sweep adds per-env action-cotangent energy (probes)
         self.total_env_steps = 0.0
         self.start = time.time()
         self.out_dir = out_dir if self.rank == 0 else None
@@ -252,6 +253,9 @@ class APGTrainer:
                 og, = torch.autograd.grad(acts[t], leaves[t], grad_outputs=ga)
             env.apg_obs_vjp(o_all[t], snap[t], self.rms, use_norm, og, gq, gv)
             gas[t] = ga
+            if self.diag is not None and not graph:  # sum over steps of |d loss / d a_t|^2 per env
+                e = (ga.double() ** 2).sum(1)
+                self.diag["ga_sq"] = e if t == H - 1 else self.diag["ga_sq"] + e
         torch.autograd.backward(self.policy(on_all.reshape(H * B, w)), grad_tensors=torch.cat(gas))
         dropped = torch.stack([dropped_e.sum(), nonfinite[0]])  # (forward guard, reverse guard)
         return loss.detach(), (rfin.mean(1).sum() / H).detach(), (o_all, snap), dropped

@@ -90,3 +90,55 @@ def vjp_replay_flops(m, ncon: float, nefc: float, iters: float, nact=None, unrol
     f["env_post"] = 2.0 * env_post_flops(m)
     f["total"] = sum(f.values())
     return f
+
+
+def mlp_dims(in_dim: int, layer_specs, out_dim: int):
+    """[(K, N, activated)] of an MLP (src/networks.py:22-61): hidden (features, act) layers + a linear
+    output layer of out_dim units."""
+    dims, k = [], in_dim
+    for feat, act in layer_specs:
+        dims.append((k, int(feat), str(act).lower() not in ("linear", "none")))
+        k = int(feat)
+    dims.append((k, out_dim, False))
+    return dims
+
+
+def mlp_forward_flops(dims, out_tanh: bool = False) -> float:
+    """FLOPs per row of one forward pass: 2 K N per Dense + bias N + tanh (counted as 1 FLOP per
+    element: the algorithmic count, not the transcendental's instruction sequence)."""
+    f = 0.0
+    for i, (k, n, act) in enumerate(dims):
+        f += 2.0 * k * n + n + (n if act or (out_tanh and i == len(dims) - 1) else 0)
+    return f
+
+
+def mlp_train_flops(dims, out_tanh: bool = False) -> float:
+    """FLOPs per row of forward + backward (train_ppo.py value_and_grad through the MLP): the forward,
+    then per layer dZ = dH (1 - H^2) (3 per element when activated), the weight gradient dZᵀ X (2 K N),
+    the bias gradient (N) and dX = dZ W (2 K N, not for the first layer: the observations need none)."""
+    f = mlp_forward_flops(dims, out_tanh)
+    for i, (k, n, act) in enumerate(dims):
+        tanh_here = act or (out_tanh and i == len(dims) - 1)
+        f += (3.0 * n if tanh_here else 0.0) + 2.0 * k * n + n + (2.0 * k * n if i > 0 else 0.0)
+    return f
+
+
+def ppo_update_flops(obs_dim: int, act_dim: int, policy_specs, value_specs) -> dict:
+    """Per minibatch row: both nets' forward + backward (train_ppo.py:204-252), the losses (log-prob,
+    ratio, clip, entropy: ~12 FLOPs per action dimension; MSE 3) and Adam is per parameter, not per row
+    (left out: 151K parameters x 2 nets x ~12 FLOPs per minibatch is < 0.1 % at 8,192 rows)."""
+    pd = mlp_dims(obs_dim, policy_specs, act_dim)
+    vd = mlp_dims(obs_dim, value_specs, 1)
+    f = {"policy": mlp_train_flops(pd, out_tanh=True), "value": mlp_train_flops(vd), "losses": 12.0 * act_dim + 3.0}
+    f["total"] = sum(f.values())
+    return f
+
+
+def policy_rollout_flops(obs_dim: int, act_dim: int, policy_specs) -> dict:
+    """Per env per rollout step (the fused policy launch, mjl_policy_fwd): observation normalisation
+    (3 per input), the MLP forward with the mean's tanh, and the Gaussian head (sample, log-prob: ~8
+    per action dimension)."""
+    d = mlp_dims(obs_dim, policy_specs, act_dim)
+    f = {"normalise": 3.0 * obs_dim, "mlp": mlp_forward_flops(d, out_tanh=True), "head": 8.0 * act_dim}
+    f["total"] = sum(f.values())
+    return f

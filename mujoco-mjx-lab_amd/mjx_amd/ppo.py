@@ -464,7 +464,7 @@ class _GaussianLogprob(torch.autograd.Function):
 
 def gaussian_logprob(mean, log_std, action, out=None):
     """train_ppo.py:121-126: diagonal Gaussian log-density summed over action dims."""
-    if (out is None and mean.is_cuda and torch.is_grad_enabled() and mean.dim() == 2
+    if (out is None and mean.is_cuda and torch.is_grad_enabled() and mean.dim() == 2 and mean.dtype == torch.float32
             and mean.shape[0] >= UPDATE_MIN_ROWS and log_std.dim() == 1):
         return _GaussianLogprob.apply(mean, log_std, action)
     var = torch.exp(2.0 * log_std)
@@ -1070,6 +1070,7 @@ class PPOTrainer:
             env.enable_reset_pool(int(reset_pool))
             self._pool_n = torch.full((1,), min(4, int(reset_pool)), dtype=torch.int32, device=self.device)
         self.allreduce_events = None  # a list to time the per-minibatch all-reduce (bench.py, event_ms)
+        self.phase_events = None  # a list: per iteration 4 CUDA events (rollout | between | update), bench.py
         self.total_env_steps = 0.0
         self.start = time.time()
         self.out_dir = out_dir if self.rank == 0 else None
@@ -1194,12 +1195,22 @@ class PPOTrainer:
         self.obs = bf["obs"][T]
         return bf["obs"][:T], bf["act"], bf["logp"], bf["rew"], bf["term"], bf["trunc"]
 
+    def _mark(self, evs, i):
+        if evs is not None:
+            evs[i].record()
+
     def iteration(self, it: int) -> dict:
         cfg, dev = self.cfg, self.device
         if dev.type == "cuda":
             torch.cuda.synchronize(dev)
+        evs = None
+        if self.phase_events is not None and dev.type == "cuda":
+            evs = [torch.cuda.Event(enable_timing=True) for _ in range(4)]
+            self.phase_events.append(evs)
         t0 = time.time()
+        self._mark(evs, 0)
         obs_t, act_t, logp_t, r_t, te_t, tr_t = self.collect_rollout()
+        self._mark(evs, 1)
         T, B = r_t.shape
         if self.jax_keys:
             self._jax_split_main()  # train_ppo.py:359 rng_idx (the minibatch permutation is torch's)
@@ -1211,8 +1222,11 @@ class PPOTrainer:
             adv, ret = compute_gae(r_t, v, te_t, tr_t, cfg.gamma, cfg.lam)
         mb = cfg.minibatch_size // self.world
         idx = make_index_batches(T * B, mb, cfg.epochs, self.idx_gen, dev)
+        self._mark(evs, 2)
         self.updater.run(obs_n.reshape(T * B, -1), act_t.reshape(T * B, -1), logp_t.reshape(-1), ret.reshape(-1),
                          adv.reshape(-1), idx, self.allreduce_events)
+        self._mark(evs, 3)
+        self.last_update_rows = int(idx.numel())
         if dev.type == "cuda":
             torch.cuda.synchronize(dev)
         dt = max(time.time() - t0, 1e-9)

@@ -16,7 +16,7 @@ gradient (Adam leaves them at zero). The gradients land in one flat buffer laid 
 which is also the data-parallel all-reduce buffer (no concatenation).
 
 Forward: H_l = tanh(H_{l-1} W_lᵀ + b_l) as torch.baddbmm + the native in-place tanh; Z = H W_outᵀ +
-b_out; mean = tanh(Z[0]); v = Z[1][:, 0]. Losses: mjl_ppo_surrogate on (mean, clamp(log_std)),
+b_out; mean = tanh(Z[0]); v = Z[1][:, 0]. Losses: mjl_ppo_surrogate_clipped (log_std clipped in the kernel),
 mjl_mse_strided on v. Backward, by hand in the order autograd takes: mjl_twin_head_bwd forms
 dZ; each layer's weight gradient is the split-K batched GEMM dZᵀ X over both nets (2 x splits
 slices, summed in order by mjl_slice_sum_batched), its bias gradient the fixed-order column sums
@@ -135,23 +135,20 @@ class TwinNets:
         z = torch.baddbmm(self.b[nl - 1].unsqueeze(1), hs[-1], self.W[nl - 1].transpose(1, 2))  # [2, M, A]
         mean = z[0]
         check(L.mjl_tanh_inplace(mean.data_ptr(), mean.numel(), st)) if (M * A) % 4 == 0 else mean.tanh_()
-        # ---- losses (networks.py:103 clamps log_std to [-20, 2]; its gradient passes inside the bounds)
+        # ---- losses (networks.py:103 clips log_std to [-20, 2]: in the kernel, with its gradient mask)
         log_std = self.policy.log_std
-        ls = torch.clamp(log_std.detach(), -20.0, 2.0).contiguous()
         loss_p = torch.empty((), device=dev)
         loss_v = torch.empty((), device=dev)
         gm = torch.empty((M, A), device=dev)
-        gs = torch.empty(A, device=dev)
         scr = self._scratch("loss", int(L.mjl_ppo_loss_scratch(M, A)))
-        check(L.mjl_ppo_surrogate(mean.data_ptr(), ls.data_ptr(), acts.data_ptr(), old_logp.data_ptr(), adv.data_ptr(),
-                                  None if adv_stats is None else adv_stats.data_ptr(), M, A, float(clip_eps),
-                                  float(ent_coef), scr.data_ptr(), loss_p.data_ptr(), gm.data_ptr(), gs.data_ptr(), st))
+        check(L.mjl_ppo_surrogate_clipped(mean.data_ptr(), log_std.data_ptr(), acts.data_ptr(), old_logp.data_ptr(),
+                                          adv.data_ptr(), None if adv_stats is None else adv_stats.data_ptr(), M, A,
+                                          float(clip_eps), float(ent_coef), -20.0, 2.0, scr.data_ptr(),
+                                          loss_p.data_ptr(), gm.data_ptr(), self.g_log_std.data_ptr(), st))
         gv = torch.empty(M, device=dev)
         scr_v = self._scratch("mse", M // 256 + 1)
         check(L.mjl_mse_strided(z[1].data_ptr(), A, ret.data_ptr(), M, scr_v.data_ptr(), loss_v.data_ptr(),
                                 gv.data_ptr(), st))
-        inside = (log_std.detach() >= -20.0) & (log_std.detach() <= 2.0)
-        torch.where(inside, gs, torch.zeros_like(gs), out=self.g_log_std)
         # ---- backward
         dz = torch.empty((2, M, A), device=dev)
         check(L.mjl_twin_head_bwd(gm.data_ptr(), mean.data_ptr(), gv.data_ptr(), M, A, dz.data_ptr(), st))

@@ -30,6 +30,7 @@ def main():
     ap.add_argument("--num-envs", type=int, default=None, help="total envs over all ranks")
     ap.add_argument("--model", default=None, help="humanoid_mjx | humanoid | path to .xml")
     ap.add_argument("--results-dir", default=None)
+    ap.add_argument("--seed", type=int, default=None, help="override the config's seed")
     ap.add_argument("--jax-keys", action="store_true",
                     help="draw env resets from train_ppo.py's jax.random key chain (same reset stream as the reference)")
     a = ap.parse_args()
@@ -44,6 +45,8 @@ def main():
         cfg.total_iterations = a.iterations
     if a.results_dir:
         cfg.results_dir = a.results_dir
+    if a.seed is not None:
+        cfg.seed = a.seed
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank, local = int(os.environ.get("RANK", "0")), int(os.environ.get("LOCAL_RANK", "0"))

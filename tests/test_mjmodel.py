@@ -19,7 +19,7 @@ from mjx_amd.mjmodel import compile_mjmodel
 # MuJoCo's enum values (mjmodel.h, 3.3) — the filler reads them from the module it is given
 _E = {
     "mjtObj": {"mjOBJ_BODY": 1, "mjOBJ_JOINT": 3, "mjOBJ_GEOM": 5, "mjOBJ_SITE": 6, "mjOBJ_ACTUATOR": 19,
-               "mjOBJ_TENDON": 18, "mjOBJ_SENSOR": 20, "mjOBJ_KEY": 23},
+               "mjOBJ_TENDON": 18, "mjOBJ_SENSOR": 20, "mjOBJ_TUPLE": 23, "mjOBJ_KEY": 24},
     "mjtCone": {"mjCONE_PYRAMIDAL": 0, "mjCONE_ELLIPTIC": 1},
     "mjtSolver": {"mjSOL_PGS": 0, "mjSOL_CG": 1, "mjSOL_NEWTON": 2},
     "mjtIntegrator": {"mjINT_EULER": 0, "mjINT_RK4": 1, "mjINT_IMPLICIT": 2, "mjINT_IMPLICITFAST": 3},
@@ -29,7 +29,7 @@ _E = {
     "mjtTrn": {"mjTRN_JOINT": 0}, "mjtDyn": {"mjDYN_NONE": 0}, "mjtGain": {"mjGAIN_FIXED": 0},
     "mjtBias": {"mjBIAS_NONE": 0}, "mjtWrap": {"mjWRAP_JOINT": 1}, "mjtSensor": {"mjSENS_TOUCH": 0},
 }
-_OBJ_KIND = {1: "body", 3: "joint", 5: "geom", 6: "site", 19: "actuator", 18: "tendon", 20: "sensor", 23: "key"}
+_OBJ_KIND = {1: "body", 3: "joint", 5: "geom", 6: "site", 19: "actuator", 18: "tendon", 20: "sensor", 24: "key"}
 
 
 def _mat2quat(R):
