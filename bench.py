@@ -39,7 +39,7 @@ REF_DEVICE_STEPS_PER_S = 72618.0  # HUMANOID_MJX device steps/s (RE
 REF_HUMANOID_XML_STEPS_PER_S = 6176.0  # README.md:76 HUMANOID row (humanoid.xml)
 HBM_PEAK_GBS = 8000.0             # MI355X_MICROARCH.md: HBM3E peak 8.0 TB/s (spec)
 F32_PEAK_TFLOPS = 157.3           # MI355X_MICROARCH.md: peak FP32 matrix (dense) = FP32 vector
-SPEEDTEST_KERNEL = "step_kernel<mjl::Dims<27, 17, 22, 20, 48, 16>, 2>"  # rocprofv3 kernel name
+SPEEDTEST_KERNEL = "step_kernel<mjl::Dims<27, 17, 22, 20, 48, 16>, 2, 2>"  # rocprofv3 kernel name
 ENV_STEP_BYTES = 1048             # 113 floats in + 149 out per fused env step
 PPO_CURVE_ITERS = (0, 25, 50, 100)
 
@@ -402,7 +402,7 @@ def speedtest_extras(args, model, sys_, local):
     tf = fl["total"] * B / (ek * 1e-3) / 1e12
     ex["env_step_roofline"] = {
         "bound": "valu", "achieved": tf, "peak": F32_PEAK_TFLOPS, "unit": "TFLOP/s", "frac": tf / F32_PEAK_TFLOPS,
-        "kernel": "step_kernel<mjl::Dims<27, 17, 22, 20, 48, 16>, 3>", "kernel_ms": ek,
+        "kernel": "step_kernel<mjl::Dims<27, 17, 22, 20, 48, 16>, 3, 2>", "kernel_ms": ek,
         "flops_per_env_step": fl["total"], "flops_by_stage": {k: v for k, v in fl.items() if k != "total"},
         "workload_mean_ncon_nefc_iter": [float(x) for x in est[:3]],
         "workload_mean_active_rows_per_hessian": float(est[3]), "reset_frac_per_step": reset_frac,

@@ -412,6 +412,10 @@ int mjl_slice_sum_batched(const float* x, int nb, int ns, long long m, float* ou
  * output layer is padded to A rows). */
 int mjl_twin_head_bwd(const float* g_mean, const float* mean, const float* g_v, int M, int A, float* dz4,
                       void* stream);
+/* x[b][r][j] = act_b(x[b][r][j] + bias[b][j]) in place over nb stacked row-major [rows, n] matrices,
+ * act_b = tanh when bit b of act_mask is set, else the identity (the twin update's dense-layer
+ * epilogue, src/networks.py:55-61, after a bias-less batched GEMM). */
+int mjl_bias_act(float* x, const float* bias, int nb, long long rows, int n, unsigned act_mask, void* stream);
 
 /* PPO update losses (train_ppo.py:204-220), forward and gradient in one pass, deterministic.
  * mjl_ppo_surrogate: loss = -mean_i min(r_i an_i, clip(r_i, 1 - clip_eps, 1 + clip_eps) an_i)

@@ -1076,6 +1076,22 @@ extern "C" int mjl_slice_sum(const float* x, int ns, long long m, float* out, vo
   return mjl_slice_sum_batched(x, 1, ns, m, out, stream);
 }
 
+extern "C" int mjl_bias_act(float* x, const float* bias, int nb, long long rows, int n, unsigned act_mask,
+                            void* stream) {
+  if (!x || !bias || nb <= 0 || rows < 0 || n <= 0) return fail(MJL_ERR_ARG, "bad argument");
+  if (rows == 0) return MJL_OK;
+  if ((long long)nb * rows * n >= (1LL << 31)) return fail(MJL_ERR_ARG, "bias_act: at most 2^31 elements");
+  const bool v4 = n % 4 == 0 && (uintptr_t)x % 16 == 0;
+  const long long groups = (long long)nb * rows * n / (v4 ? 4 : 1);
+  const dim3 grid((unsigned)((groups + 255) / 256));
+  if (v4)
+    hipLaunchKernelGGL(bias_act_kernel<4>, grid, dim3(256), 0, (hipStream_t)stream, x, bias, nb, rows, n, act_mask);
+  else
+    hipLaunchKernelGGL(bias_act_kernel<1>, grid, dim3(256), 0, (hipStream_t)stream, x, bias, nb, rows, n, act_mask);
+  HIPCHK(hipGetLastError());
+  return MJL_OK;
+}
+
 extern "C" int mjl_twin_head_bwd(const float* g_mean, const float* mean, const float* g_v, int M, int A, float* dz4,
                                  void* stream) {
   if (!g_mean || !mean || !g_v || !dz4 || M <= 0 || A <= 0) return fail(MJL_ERR_ARG, "bad argument");

@@ -248,6 +248,33 @@ __global__ __launch_bounds__(256) void twin_head_bwd_kernel(const float* __restr
   }
 }
 
+// x[b][r][j] = act_b(x[b][r][j] + bias[b][j]) in place over nb stacked [rows, n] matrices (the twin
+// update's layer epilogue after a bias-less batched GEMM: torch.baddbmm materialises the broadcast
+// bias into its output with a copy kernel first); act_b = tanh when bit b of act_mask is set, else
+// the identity. V = 4: n % 4 == 0, float4 per thread; V = 1: one element per thread.
+template <int V>
+__global__ __launch_bounds__(256) void bias_act_kernel(float* __restrict__ x, const float* __restrict__ bias, int nb,
+                                                       long long rows, int n, unsigned act_mask) {
+  // 32-bit index math (the launcher checks nb * rows * n < 2^31): 64-bit divides dominated such kernels
+  const unsigned q = blockIdx.x * blockDim.x + threadIdx.x;
+  const unsigned per = (unsigned)(rows * n / V);  // V-groups per matrix
+  if (q >= per * (unsigned)nb) return;
+  const unsigned b = q / per;
+  const unsigned e = (q - b * per) * V;  // element index within the matrix
+  const int j = (int)(e % (unsigned)n);
+  const bool th = (act_mask >> b) & 1u;
+  const float* bb = bias + (size_t)b * n + j;
+  if constexpr (V == 4) {
+    float4 v = reinterpret_cast<float4*>(x)[q];
+    v.x += bb[0]; v.y += bb[1]; v.z += bb[2]; v.w += bb[3];
+    if (th) { v.x = tanhf(v.x); v.y = tanhf(v.y); v.z = tanhf(v.z); v.w = tanhf(v.w); }
+    reinterpret_cast<float4*>(x)[q] = v;
+  } else {
+    float v = x[q] + bb[0];
+    x[q] = th ? tanhf(v) : v;
+  }
+}
+
 // elementwise tanh in place, float4 (the update's forward activations; torch's tanh kernel ran at
 // ~4 TB/s on the [65,536, 256] layer outputs)
 __global__ __launch_bounds__(256) void tanh_inplace_kernel(float* __restrict__ x, long long n4) {

@@ -1508,6 +1508,9 @@ template <class D, bool G> INL f32x16 solver_hessian_acc(MP m_, LDSA WS<D>* W, R
   f32x16 acc;
 #pragma unroll
   for (int v = 0; v < 16; v++) acc[v] = 0.f;
+#ifdef MJL_HESS_2ACC
+  f32x16 acc2 = acc;
+#endif
 #ifndef MJL_HESS_DENSE
   // only active rows (jar < 0) contribute: take them in order from each 64-row ballot, 8 rows per
   // trip (uniform row indices from s_ff1), loads of the trip first, then one MFMA per row pair
@@ -1531,11 +1534,23 @@ template <class D, bool G> INL f32x16 solver_hessian_acc(MP m_, LDSA WS<D>* W, R
         b[u] = ok ? j : 0.f;
         a[u] = ok ? dr * j : 0.f;
       }
+#ifdef MJL_HESS_2ACC  // diagnostic variant: even / odd row pairs on two accumulator chains
+#pragma unroll
+      for (int u = 0; u < 4; u += 2) {
+        if (rr[2 * u] >= 0) acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a[u], b[u], acc, 0, 0, 0);
+        if (rr[2 * u + 2] >= 0) acc2 = __builtin_amdgcn_mfma_f32_32x32x2f32(a[u + 1], b[u + 1], acc2, 0, 0, 0);
+      }
+#else
 #pragma unroll
       for (int u = 0; u < 4; u++)
         if (rr[2 * u] >= 0) acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a[u], b[u], acc, 0, 0, 0);
+#endif
     }
   }
+#ifdef MJL_HESS_2ACC
+#pragma unroll
+  for (int v = 0; v < 16; v++) acc[v] += acc2[v];
+#endif
   return acc;
 #endif
   for (int r0 = 0; r0 < nefc; r0 += 8) {

@@ -31,7 +31,7 @@ EXPORTS = [
     "mjl_ppo_loss_scratch", "mjl_ppo_surrogate", "mjl_mse", "mjl_gather_rows", "mjl_adam",
     "mjl_adam_dev", "mjl_mlp_fwd", "mjl_mlp_colpart_rows", "mjl_mlp_bwd",
     "mjl_colsum_batched_scratch", "mjl_colsum_batched", "mjl_tanh_bwd_colsum_batched", "mjl_slice_sum_batched",
-    "mjl_twin_head_bwd", "mjl_mse_strided", "mjl_ppo_surrogate_clipped",
+    "mjl_twin_head_bwd", "mjl_mse_strided", "mjl_ppo_surrogate_clipped", "mjl_bias_act",
 ]
 
 _lib = None
@@ -132,6 +132,7 @@ def lib() -> C.CDLL:
     L.mjl_slice_sum_batched.argtypes = [f32p, i32, i32, C.c_longlong, f32p, vp]
     L.mjl_twin_head_bwd.argtypes = [f32p, f32p, f32p, i32, i32, f32p, vp]
     L.mjl_mse_strided.argtypes = [vp, i32, vp, i32, vp, vp, vp, vp]
+    L.mjl_bias_act.argtypes = [vp, vp, i32, C.c_longlong, i32, C.c_uint, vp]
     L.mjl_ppo_surrogate_clipped.argtypes = [vp, vp, vp, vp, vp, vp, i32, i32, C.c_float, C.c_float, C.c_float,
                                             C.c_float, vp, vp, vp, vp, vp]
     L.mjl_small_mlp_fwd.argtypes = [vp, i32, i32, i32, vp, vp, vp, vp, vp]

@@ -15,8 +15,9 @@ value's output layer (1 unit) is padded to the policy's A units with zero rows t
 gradient (Adam leaves them at zero). The gradients land in one flat buffer laid out the same way,
 which is also the data-parallel all-reduce buffer (no concatenation).
 
-Forward: H_l = tanh(H_{l-1} W_lᵀ + b_l) as torch.baddbmm + the native in-place tanh; Z = H W_outᵀ +
-b_out; mean = tanh(Z[0]); v = Z[1][:, 0]. Losses: mjl_ppo_surrogate_clipped (log_std clipped in the kernel),
+Forward: H_l = tanh(H_{l-1} W_lᵀ + b_l) as a bias-less torch.bmm + one native bias-and-tanh pass
+(mjl_bias_act; baddbmm would first copy the broadcast bias into its output); Z = H W_outᵀ + b_out;
+mean = tanh(Z[0]); v = Z[1][:, 0]. Losses: mjl_ppo_surrogate_clipped (log_std clipped in the kernel),
 mjl_mse_strided on v. Backward, by hand in the order autograd takes: mjl_twin_head_bwd forms
 dZ; each layer's weight gradient is the split-K batched GEMM dZᵀ X over both nets (2 x splits
 slices, summed in order by mjl_slice_sum_batched), its bias gradient the fixed-order column sums
@@ -96,11 +97,15 @@ class TwinNets:
                 lp.bias.data = self.b[l][0]
                 lv.weight.data = self.W[l][1, :n_v]
                 lv.bias.data = self.b[l][1, :n_v]
-        # gradient views in each module's parameters() order (the optimisers' order)
-        self.grads_p: List[torch.Tensor] = [t for l in range(self.nl) for t in (self.gW[l][0], self.gb[l][0])]
-        self.grads_p.append(self.g_log_std)
-        self.grads_v: List[torch.Tensor] = [t for l in range(self.nl) for t in (
-            self.gW[l][1, :vm.layers[l].out_features], self.gb[l][1, :vm.layers[l].out_features])]
+        # gradient views in each module's parameters() order (the optimisers' order: a module's own
+        # parameters come before its submodules', so GaussianPolicy yields log_std first)
+        gview = {id(policy.log_std): self.g_log_std}
+        for l in range(self.nl):
+            n_v = vm.layers[l].out_features
+            gview[id(pm.layers[l].weight)], gview[id(pm.layers[l].bias)] = self.gW[l][0], self.gb[l][0]
+            gview[id(vm.layers[l].weight)], gview[id(vm.layers[l].bias)] = self.gW[l][1, :n_v], self.gb[l][1, :n_v]
+        self.grads_p: List[torch.Tensor] = [gview[id(p)] for p in policy.parameters()]
+        self.grads_v: List[torch.Tensor] = [gview[id(p)] for p in value.parameters()]
         self._scr = {}
 
     def owns_storage(self) -> bool:
@@ -125,16 +130,16 @@ class TwinNets:
         st = torch.cuda.current_stream(dev).cuda_stream
         M, A, nl = o.shape[0], self.A, self.nl
         s = splits
-        # ---- forward
-        x = o.unsqueeze(0).expand(2, M, self.K0).contiguous()  # both nets read the same observations
+        # ---- forward: bias-less batched GEMMs, the bias and tanh in one native pass (mjl_bias_act)
+        x = o.unsqueeze(0).expand(2, M, self.K0)  # both nets read the same observations (batch stride 0)
         hs = [x]
         for l in range(nl - 1):
-            h = torch.baddbmm(self.b[l].unsqueeze(1), hs[-1], self.W[l].transpose(1, 2))
-            check(L.mjl_tanh_inplace(h.data_ptr(), h.numel(), st))
+            h = torch.bmm(hs[-1], self.W[l].transpose(1, 2))
+            check(L.mjl_bias_act(h.data_ptr(), self.b[l].data_ptr(), 2, M, h.shape[2], 3, st))
             hs.append(h)
-        z = torch.baddbmm(self.b[nl - 1].unsqueeze(1), hs[-1], self.W[nl - 1].transpose(1, 2))  # [2, M, A]
+        z = torch.bmm(hs[-1], self.W[nl - 1].transpose(1, 2))  # [2, M, A]
+        check(L.mjl_bias_act(z.data_ptr(), self.b[nl - 1].data_ptr(), 2, M, A, 1, st))  # tanh: the policy's mean
         mean = z[0]
-        check(L.mjl_tanh_inplace(mean.data_ptr(), mean.numel(), st)) if (M * A) % 4 == 0 else mean.tanh_()
         # ---- losses (networks.py:103 clips log_std to [-20, 2]: in the kernel, with its gradient mask)
         log_std = self.policy.log_std
         loss_p = torch.empty((), device=dev)
@@ -165,7 +170,11 @@ class TwinNets:
                                                     cs.data_ptr(), self.gb[l].data_ptr(), st))
             else:
                 dzl = g
-            part = torch.bmm(dzl.view(2 * s, M // s, N).transpose(1, 2), xin.view(2 * s, M // s, K))  # [2s, N, K]
+            if l == 0:  # the shared observations: [2, M, K0] with batch stride 0 -> per split, both nets
+                xs = o.view(1, s, M // s, K).expand(2, s, M // s, K).reshape(2 * s, M // s, K)
+            else:
+                xs = xin.view(2 * s, M // s, K)
+            part = torch.bmm(dzl.view(2 * s, M // s, N).transpose(1, 2), xs)  # [2s, N, K]
             check(L.mjl_slice_sum_batched(part.data_ptr(), 2, s, N * K, self.gW[l].data_ptr(), st))
             if l > 0:
                 g = torch.bmm(dzl, self.W[l])  # [2, M, K]

@@ -21,6 +21,10 @@ from mjx_amd.envs import HumanoidEnv, resolve_ids  # noqa: E402
 STAGES = [("state loads", 36, 0), ("kinematics", 0, 1), ("com_pos+crb+M", 1, 2), ("velocity", 2, 3),
           ("factor M", 3, 4), ("collision+rows", 4, 5), ("solver", 5, 6), ("sensors", 6, 7),
           ("integrate", 7, 8), ("env post", 8, 37), ("reset merge", 37, 38), ("write-back", 38, 39)]
+# the solver's accumulated sub-phase stamps (TACC slots) and counters (TCOUNT)
+SOLVER_SUBS = {9: "warm start", 10: "line search (+step)", 11: "update + convergence", 12: "hessian J'DJ",
+               13: "cholesky factor+solve", 28: "ls: M s, J s", 29: "ls: |s|, c1, c2, p0", 30: "ls: segment test + q",
+               31: "ls: 3-point loop", 14: "count: 3-point iterations", 15: "count: line searches"}
 
 
 def main():
@@ -43,6 +47,7 @@ def main():
             env.step(torch.rand((B, env.act_dim), generator=g, device="cuda") * 2 - 1)
     env.fill_reset_pool(pool_n)
     rows, slow, it_all, it_slow, ev_us = [], [], [], [], []
+    subs_all, subs_slow = [], []
     for _ in range(20):
         act = torch.rand((B, env.act_dim), generator=g, device="cuda") * 2 - 1
         torch.cuda.synchronize()
@@ -60,6 +65,9 @@ def main():
         k = int(np.argmax(tot))
         rows.append(d)
         slow.append(d[k])
+        sv = np.stack([s[:, i] for i in SOLVER_SUBS], 1)
+        subs_all.append(sv)
+        subs_slow.append(sv[k])
         it_all.append(st[:, 2].mean())
         it_slow.append(st[k, 2])
     d = np.concatenate(rows)
@@ -69,6 +77,9 @@ def main():
            "mean_newton_iters": float(np.mean(it_all)), "slowest_env_newton_iters": float(np.mean(it_slow)),
            "stages_mean": {n: round(float(d[:, i].mean())) for i, (n, _, _) in enumerate(STAGES)},
            "stages_slowest": {n: round(float(sl[:, i].mean())) for i, (n, _, _) in enumerate(STAGES)}}
+    sa, ss = np.concatenate(subs_all), np.stack(subs_slow)
+    out["solver_subs_mean"] = {n: round(float(sa[:, j].mean()), 2) for j, n in enumerate(SOLVER_SUBS.values())}
+    out["solver_subs_slowest"] = {n: round(float(ss[:, j].mean()), 2) for j, n in enumerate(SOLVER_SUBS.values())}
     print(json.dumps(out), flush=True)
 
 

@@ -23,12 +23,16 @@ from mjx_amd.ppo import compute_gae, make_index_batches  # noqa: E402
 def main():
     args = bench.parse()
     dist = None
-    if os.environ.get("PROBE_DP") == "1":
+    backend = {"1": "gloo", "gloo": "gloo", "nccl": "nccl"}.get(os.environ.get("PROBE_DP", ""))
+    if backend:  # PROBE_DP=nccl: RCCL on one rank (the all-reduce stays on the stream, as at 8 GPUs)
         import torch.distributed as dist
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         os.environ.setdefault("MASTER_PORT", str(bench.free_port()))
         torch.cuda.set_device(0)
-        dist.init_process_group("gloo", rank=0, world_size=1)
+        if backend == "nccl":
+            dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda", 0))
+        else:
+            dist.init_process_group("gloo", rank=0, world_size=1)
     tr = bench.ppo_trainer(args, int(os.environ.get("PROBE_B", "1024")), dist, 0, 0)
     if os.environ.get("PROBE_MB"):
         tr.cfg.minibatch_size = int(os.environ["PROBE_MB"])
@@ -70,7 +74,7 @@ def main():
                 data_parallel=dist is not None)
     if ar_ms:
         line.update(allreduce_total_ms=round(statistics.median(ar_ms), 3), allreduces=n_ar[0],
-                    allreduce_backend="gloo, one rank (copy + host round trip; no link time)")
+                    allreduce_backend=f"{backend}, one rank (no link time)")
     print(json.dumps(line), flush=True)
 
 

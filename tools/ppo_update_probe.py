@@ -106,6 +106,43 @@ class _NoComm:
         return 1
 
 
+def shard_twin(reps: int = 5, envs: int = 1024):
+    """Graph-replayed updates, twin path (mjx_amd/twin.py) vs per-net two-stream path, interleaved:
+    C5's per-rank shard (8,192-row minibatches through the data-parallel bodies, identity
+    collective, 128 steps) and C3's single-process update (65,536-row minibatches, 16 steps)."""
+    from mjx_amd import twin
+    cfg = reference_ppo_config()
+    N = envs * 256
+    gd = torch.Generator(device="cuda").manual_seed(1)
+    obs, act = torch.randn((N, 54), generator=gd, device="cuda"), torch.randn((N, 21), generator=gd, device="cuda").clamp(-1, 1)
+    logp, ret, adv = (torch.randn(N, generator=gd, device="cuda") for _ in range(3))
+    for mb, dist in ((8192, _NoComm()), (65536, None)):
+        cfg.minibatch_size = mb
+        ups = {}
+        for tw in (True, False):
+            g = torch.Generator().manual_seed(0)
+            pol = ppo.GaussianPolicy(54, 21, cfg.policy_hidden_layer_specs, cfg.log_std_init, g).cuda()
+            val = ppo.ValueNet(54, cfg.value_hidden_layer_specs, g).cuda()
+            op, ov = ppo._adam(pol.parameters(), 3e-4), ppo._adam(val.parameters(), 3e-4)
+            twin.TWIN_UPDATE = tw
+            ups[tw] = ppo.PPOUpdater(pol, val, op, ov, cfg, dist, 1, use_graph=True)
+            assert (ups[tw].twin is not None) == tw
+        ts = {True: [], False: []}
+        for r in range(reps + 2):
+            idx = ppo.make_index_batches(N, mb, cfg.epochs, torch.Generator(device="cuda").manual_seed(r), "cuda")
+            for tw in (True, False):
+                torch.cuda.synchronize()
+                t0 = time.time()
+                ups[tw].run(obs, act, logp, ret, adv, idx)
+                torch.cuda.synchronize()
+                if r >= 2:
+                    ts[tw].append(time.time() - t0)
+        for tw in (True, False):
+            w = sorted(ts[tw])
+            print(f"{'dp-shard' if dist is not None else 'single'} minibatch={mb} steps={idx.shape[0]} twin={tw}: "
+                  f"wall median {1e3 * w[len(w) // 2]:.2f} ms (min {1e3 * w[0]:.2f}, max {1e3 * w[-1]:.2f})", flush=True)
+
+
 def shard(reps: int = 5, minibatch: int = 8192, envs: int = 1024):
     """One rank's update in the C5 configuration on 8 GPUs (1024 envs x 256 steps, 4 epochs of
     8,192-row minibatches: 128 minibatch steps) through PPOUpdater's data-parallel bodies with the
@@ -172,6 +209,9 @@ if __name__ == "__main__":
         sys.exit(0)
     if len(sys.argv) > 1 and sys.argv[1] == "shard":
         shard()
+        sys.exit(0)
+    if len(sys.argv) > 1 and sys.argv[1] == "twin":
+        shard_twin()
         sys.exit(0)
     if len(sys.argv) > 1 and sys.argv[1] == "two":
         two_stream(2048)

@@ -1,4 +1,6 @@
-"""Round-3 measurement record from gpurun_out/prof3/ (tools/profile_r3.sh) into profiles/.
+"""Round measurement record from gpurun_out/prof<N>/ (tools/profile_r3.sh, tools/r4/profile.sh) into
+profiles/. Usage: python tools/summarize_r3.py [round] [dir] (default r3 gpurun_out/prof3; round 4:
+r4 gpurun_out/prof4, files under profiles/r4/).
 
 Per kernel family (speed test, env step with in-place resets / with the reset pool / without resets,
 APG replay VJP): the rocprofv3 --stats average duration, HBM bytes per launch (2 x FETCH_SIZE +
@@ -18,12 +20,15 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "mujoco-mjx-lab_amd"))
 from mjx_amd import _lib  # noqa: E402
 
-P = os.path.join(ROOT, "gpurun_out", "prof3")
+ROUND = sys.argv[1] if len(sys.argv) > 1 else "r3"
+P = os.path.join(ROOT, sys.argv[2]) if len(sys.argv) > 2 else os.path.join(ROOT, "gpurun_out", "prof3")
+# round 4 added the waves-per-SIMD template argument (2 at the 2048-env launches profiled here)
+_MW = ", 2>" if ROUND != "r3" else ">"
 KERNELS = {
-    "speedtest": "step_kernel<mjl::Dims<27, 17, 22, 20, 48, 16>, 2>",
-    "envstep": "step_kernel<mjl::Dims<27, 17, 22, 20, 48, 16>, 3>",
-    "envstep_pool": "step_kernel<mjl::Dims<27, 17, 22, 20, 48, 16>, 3>",
-    "envstep_nr": "step_kernel<mjl::Dims<27, 17, 22, 20, 48, 16>, 3>",
+    "speedtest": "step_kernel<mjl::Dims<27, 17, 22, 20, 48, 16>, 2" + _MW,
+    "envstep": "step_kernel<mjl::Dims<27, 17, 22, 20, 48, 16>, 3" + _MW,
+    "envstep_pool": "step_kernel<mjl::Dims<27, 17, 22, 20, 48, 16>, 3" + _MW,
+    "envstep_nr": "step_kernel<mjl::Dims<27, 17, 22, 20, 48, 16>, 3" + _MW,
     "vjp": "vjp_kernel<mjl::Dims<27, 17, 22, 20, 4, 4>, true, 2, true>",
 }
 TRAFFIC_KEY = {"speedtest": "bytes_per_launch", "envstep": "env_step_bytes_per_launch",
@@ -64,7 +69,9 @@ def mean(v):
 
 def main():
     out = os.path.join(ROOT, "profiles")
-    rec = {"round": "r3", "src_hash": _lib.source_hash(), "envs": 2048,
+    pre = os.path.join(out, "r4", "") if ROUND == "r4" else os.path.join(out, ROUND + "_")
+    os.makedirs(os.path.dirname(pre), exist_ok=True)
+    rec = {"round": ROUND, "src_hash": _lib.source_hash(), "envs": 2048,
            "units": {"kernel_us": "rocprofv3 --stats AverageNs / 1e3",
                      "hbm_bytes_per_launch": "2 * FETCH_SIZE + WRITE_SIZE (KB counters x 1024)",
                      "sq_per_wave": "counter / SQ_WAVES per dispatch (SQ_*CYCLES and WAIT/ACTIVE in units of 4 cycles)"},
@@ -75,7 +82,7 @@ def main():
         if st:
             ns, calls = stats_avg_ns(st, kern)
             r["kernel_us"], r["calls"] = (ns / 1e3 if ns else None), calls
-            shutil.copy(st, os.path.join(out, f"r3_{mode}_kernel_stats.csv"))
+            shutil.copy(st, f"{pre}{mode}_kernel_stats.csv")
         f = one(f"{mode}/fetch/**/fetch_counter_collection.csv")
         w = one(f"{mode}/write/**/write_counter_collection.csv")
         if f and w:
@@ -97,11 +104,11 @@ def main():
         rec["kernels"][mode] = r
     b = one("bench_trace/**/trace_kernel_stats.csv")
     if b:
-        shutil.copy(b, os.path.join(out, "r3_bench_kernel_stats.csv"))
+        shutil.copy(b, f"{pre}bench_kernel_stats.csv")
         rec["bench_command_stats"] = {m: (stats_avg_ns(b, k)[0] or 0) / 1e3 for m, k in KERNELS.items()
                                       if m in ("speedtest", "envstep", "vjp")}
-    json.dump(rec, open(os.path.join(out, "r3_kernels.json"), "w"), indent=1)
-    traffic = {"round": "r3", "src_hash": rec["src_hash"], "envs": 2048,
+    json.dump(rec, open(f"{pre}kernels.json", "w"), indent=1)
+    traffic = {"round": ROUND, "src_hash": rec["src_hash"], "envs": 2048,
                "formula": "2*FETCH_SIZE + WRITE_SIZE (gfx950 FETCH_SIZE counts 128-B requests at 64 B)"}
     for mode, key in TRAFFIC_KEY.items():
         k = rec["kernels"].get(mode, {})
