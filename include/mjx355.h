@@ -400,18 +400,21 @@ int mjl_tanh_inplace(float* x, long long n, void* stream);
  * as one batched GEMM per layer, train_ppo.py:233-252 taking both nets' steps per minibatch):
  * x [nb][n][d] -> out [nb][d], each matrix summed in mjl_colsum's order; for nb > 1, n must be a
  * multiple of the 128-row chunk (n > 256). scratch: mjl_colsum_batched_scratch(nb, n, d) floats.
+ * done (device int, zero before the first call, left zero; or NULL): one launch instead of two, the
+ * last block of the first stage summing the chunk rows.
  * mjl_slice_sum_batched: out[b][e] = sum over s < ns of x[(b * ns + s) * m + e]. */
 long long mjl_colsum_batched_scratch(int nb, int n, int d);
-int mjl_colsum_batched(const float* x, int nb, int n, int d, float* scratch, float* out, void* stream);
+int mjl_colsum_batched(const float* x, int nb, int n, int d, float* scratch, float* out, int* done, void* stream);
 int mjl_tanh_bwd_colsum_batched(const float* g, const float* y, int nb, int n, int d, float* dz, float* scratch,
-                                float* colsum_out, void* stream);
+                                float* colsum_out, int* done, void* stream);
 int mjl_slice_sum_batched(const float* x, int nb, int ns, long long m, float* out, void* stream);
 /* The twin update's output-layer backward: mean [M, A] = tanh of the policy's last Dense (networks.py:
- * 103), g_mean [M, A] = d loss / d mean (mjl_ppo_surrogate), g_v [M] = d loss / d value (mjl_mse);
- * dz4 [2][M][A]: dz4[0] = g_mean (1 - mean^2), dz4[1][:, 0] = g_v, dz4[1][:, 1:] = 0 (the value net's
- * output layer is padded to A rows). */
-int mjl_twin_head_bwd(const float* g_mean, const float* mean, const float* g_v, int M, int A, float* dz4,
-                      void* stream);
+ * 103), g_mean [M, A] = d loss / d mean (mjl_ppo_surrogate), v[r] = v[r * vstride] the value net's
+ * output and ret [M] its targets (train_ppo.py:218-220, value loss mean (v - ret)^2);
+ * dz4 [2][M][A]: dz4[0] = g_mean (1 - mean^2), dz4[1][:, 0] = 2 (v - ret) / M, dz4[1][:, 1:] = 0 (the
+ * value net's output layer is padded to A rows). */
+int mjl_twin_head_bwd(const float* g_mean, const float* mean, const float* v, int vstride, const float* ret, int M,
+                      int A, float* dz4, void* stream);
 /* x[b][r][j] = act_b(x[b][r][j] + bias[b][j]) in place over nb stacked row-major [rows, n] matrices,
  * act_b = tanh when bit b of act_mask is set, else the identity (the twin update's dense-layer
  * epilogue, src/networks.py:55-61, after a bias-less batched GEMM). */
@@ -436,16 +439,20 @@ int mjl_ppo_surrogate(const float* mean, const float* log_std, const float* act,
 int mjl_mse(const float* v, const float* r, int n, float* scratch, float* loss, float* g_v, void* stream);
 /* mjl_ppo_surrogate with log_std clipped to [log_std_lo, log_std_hi] on read (networks.py:103 clips it
  * to [-20, 2]) and g_log_std zero where the raw value lies outside (torch.clamp's backward, bounds
- * inclusive); +-INFINITY bounds = mjl_ppo_surrogate. */
+ * inclusive); +-INFINITY bounds = mjl_ppo_surrogate. stats_row (device int, or NULL): adv_stats is an
+ * [n_minibatches, 2] table read at that row (a captured minibatch step reads its row at run time). */
 int mjl_ppo_surrogate_clipped(const float* mean, const float* log_std, const float* act, const float* old_logp,
-                              const float* adv, const float* adv_stats, int n, int A, float clip_eps, float ent_coef,
-                              float log_std_lo, float log_std_hi, float* scratch, float* loss, float* g_mean,
-                              float* g_log_std, void* stream);
+                              const float* adv, const float* adv_stats, const int* stats_row, int n, int A,
+                              float clip_eps, float ent_coef, float log_std_lo, float log_std_hi, float* scratch,
+                              float* loss, float* g_mean, float* g_log_std, void* stream);
 /* mjl_mse with v[i] read at v + i * vstride (the value column of the twin update's padded output). */
 int mjl_mse_strided(const float* v, int vstride, const float* r, int n, float* scratch, float* loss, float* g_v,
                     void* stream);
 int mjl_gather_rows(const long long* idx, int n, long long nsrc, int narr, const float* const* src, float* const* dst,
                     const int* cols, void* stream);
+/* mjl_gather_rows from row *idx_row (device int) of an [n_minibatches, n] index table (NULL: idx). */
+int mjl_gather_rows_indexed(const long long* idx, const int* idx_row, int n, long long nsrc, int narr,
+                            const float* const* src, float* const* dst, const int* cols, void* stream);
 /* Adam (optax.adam defaults as train_ppo.py:84-85 build them; torch.optim.Adam's fused update) over
  * nt <= 16 float32 tensors in one launch: m = b1 m + (1 - b1) g, v = b2 v + (1 - b2) g^2,
  * p -= lr / (1 - b1^step) m / (sqrt(v) / sqrt(1 - b2^step) + eps); g[k] NULL skips tensor k. */
@@ -458,6 +465,16 @@ int mjl_adam(int nt, float* const* p, const float* const* g, float* const* m, fl
 int mjl_adam_dev(int nt, float* const* p, const float* const* g, float* const* m, float* const* v,
                  const long long* numel, float lr, float beta1, float beta2, float eps, const float* step,
                  void* stream);
+
+/* Adam over nt <= 24 tensors of up to 2 optimisers in one launch (the PPO update's policy and value
+ * steps, train_ppo.py:246-251): tensor k uses group[k]'s lr and device step counter step[group[k]]
+ * (float, the count before this step: the launch takes step + 1 and advances every group's counter
+ * by one when it completes); g is scaled by gscale (the data-parallel mean: 1 / world size); ctr
+ * (device int, or NULL) is advanced with the counters; done is a device int that must be zero before
+ * the first launch (the kernel leaves it zero). Same arithmetic as mjl_adam_dev. */
+int mjl_adam_multi(int nt, float* const* p, const float* const* g, float* const* m, float* const* v,
+                   const long long* numel, const int* group, int ngroups, const float* lr, float beta1, float beta2,
+                   float eps, float gscale, float* const* step, int* done, int* ctr, void* stream);
 
 /* PPO update dense layers (train_ppo.py:204-252: value_and_grad of ppo_loss_fn / value_loss_fn
  * through the src/networks.py:22-61 MLPs), fp32 on the matrix cores, torch nn.Linear layouts

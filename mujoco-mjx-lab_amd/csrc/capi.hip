@@ -1005,7 +1005,8 @@ extern "C" long long mjl_colsum_batched_scratch(int nb, int n, int d) {
   return p.R > 1 ? (long long)nb * p.R * d : 0;
 }
 
-extern "C" int mjl_colsum_batched(const float* x, int nb, int n, int d, float* scratch, float* out, void* stream) {
+extern "C" int mjl_colsum_batched(const float* x, int nb, int n, int d, float* scratch, float* out, int* done,
+                                  void* stream) {
   if ((!x && n > 0) || !out || nb <= 0 || n < 0 || d <= 0) return fail(MJL_ERR_ARG, "bad argument");
   hipStream_t s = (hipStream_t)stream;
   if (n == 0) {
@@ -1016,24 +1017,25 @@ extern "C" int mjl_colsum_batched(const float* x, int nb, int n, int d, float* s
   if (!batched_plan_ok(nb, n, p)) return fail(MJL_ERR_ARG, "colsum_batched: n must be a multiple of %d", p.chunk);
   if (p.R > 1 && !scratch) return fail(MJL_ERR_ARG, "colsum needs mjl_colsum_batched_scratch(nb, n, d) floats of scratch");
   const unsigned tiles1 = (unsigned)((d + p.dc1 - 1) / p.dc1);
+  int* one = p.R > 1 ? done : nullptr;  // single launch: the last block sums the chunk rows
   hipLaunchKernelGGL(colsum_kernel, dim3(tiles1, (unsigned)(p.R * nb)), dim3(256), 0, s, x, n * nb, d, p.dc1, p.chunk,
-                     p.R > 1 ? scratch : out);
+                     p.R > 1 ? scratch : out, nb, p.R, out, one);
   HIPCHK(hipGetLastError());
-  if (p.R > 1) {
+  if (p.R > 1 && !one) {
     const unsigned tiles2 = (unsigned)((d + p.dc2 - 1) / p.dc2);
     hipLaunchKernelGGL(colsum_kernel, dim3(tiles2, (unsigned)nb), dim3(256), 0, s, scratch, p.R * nb, d, p.dc2, p.R,
-                       out);
+                       out, 0, 0, (float*)nullptr, (int*)nullptr);
     HIPCHK(hipGetLastError());
   }
   return MJL_OK;
 }
 
 extern "C" int mjl_colsum(const float* x, int n, int d, float* scratch, float* out, void* stream) {
-  return mjl_colsum_batched(x, 1, n, d, scratch, out, stream);
+  return mjl_colsum_batched(x, 1, n, d, scratch, out, nullptr, stream);
 }
 
 extern "C" int mjl_tanh_bwd_colsum_batched(const float* g, const float* y, int nb, int n, int d, float* dz,
-                                           float* scratch, float* colsum_out, void* stream) {
+                                           float* scratch, float* colsum_out, int* done, void* stream) {
   if (!g || !y || !dz || !colsum_out || nb <= 0 || n <= 0 || d <= 0) return fail(MJL_ERR_ARG, "bad argument");
   if (d % 4 || ((uintptr_t)g | (uintptr_t)y | (uintptr_t)dz | (uintptr_t)colsum_out) % 16)
     return fail(MJL_ERR_ARG, "tanh_bwd_colsum: d divisible by 4 and 16-byte aligned rows expected");
@@ -1044,13 +1046,14 @@ extern "C" int mjl_tanh_bwd_colsum_batched(const float* g, const float* y, int n
     return fail(MJL_ERR_ARG, "tanh_bwd_colsum needs mjl_colsum_batched_scratch(nb, n, d) floats of 16-byte aligned scratch");
   const int dq = d / 4 < 64 ? d / 4 : 64;
   const unsigned tiles1 = (unsigned)((d / 4 + dq - 1) / dq);
+  int* one = p.R > 1 ? done : nullptr;
   hipLaunchKernelGGL(tanh_bwd_colsum_kernel, dim3(tiles1, (unsigned)(p.R * nb)), dim3(256), 0, s, g, y, n * nb, d, dq,
-                     p.chunk, dz, p.R > 1 ? scratch : colsum_out);
+                     p.chunk, dz, p.R > 1 ? scratch : colsum_out, nb, p.R, colsum_out, one);
   HIPCHK(hipGetLastError());
-  if (p.R > 1) {
+  if (p.R > 1 && !one) {
     const unsigned tiles2 = (unsigned)((d + p.dc2 - 1) / p.dc2);
     hipLaunchKernelGGL(colsum_kernel, dim3(tiles2, (unsigned)nb), dim3(256), 0, s, scratch, p.R * nb, d, p.dc2, p.R,
-                       colsum_out);
+                       colsum_out, 0, 0, (float*)nullptr, (int*)nullptr);
     HIPCHK(hipGetLastError());
   }
   return MJL_OK;
@@ -1058,7 +1061,7 @@ extern "C" int mjl_tanh_bwd_colsum_batched(const float* g, const float* y, int n
 
 extern "C" int mjl_tanh_bwd_colsum(const float* g, const float* y, int n, int d, float* dz, float* scratch,
                                    float* colsum_out, void* stream) {
-  return mjl_tanh_bwd_colsum_batched(g, y, 1, n, d, dz, scratch, colsum_out, stream);
+  return mjl_tanh_bwd_colsum_batched(g, y, 1, n, d, dz, scratch, colsum_out, nullptr, stream);
 }
 
 extern "C" int mjl_slice_sum_batched(const float* x, int nb, int ns, long long m, float* out, void* stream) {
@@ -1092,12 +1095,13 @@ extern "C" int mjl_bias_act(float* x, const float* bias, int nb, long long rows,
   return MJL_OK;
 }
 
-extern "C" int mjl_twin_head_bwd(const float* g_mean, const float* mean, const float* g_v, int M, int A, float* dz4,
-                                 void* stream) {
-  if (!g_mean || !mean || !g_v || !dz4 || M <= 0 || A <= 0) return fail(MJL_ERR_ARG, "bad argument");
+extern "C" int mjl_twin_head_bwd(const float* g_mean, const float* mean, const float* v, int vstride, const float* ret,
+                                 int M, int A, float* dz4, void* stream) {
+  if (!g_mean || !mean || !v || !ret || !dz4 || M <= 0 || A <= 0 || vstride <= 0) return fail(MJL_ERR_ARG, "bad argument");
   const long long n = 2LL * M * A;
+  if (n >= (1LL << 31)) return fail(MJL_ERR_ARG, "twin_head_bwd: 2 M A must be below 2^31");
   hipLaunchKernelGGL(twin_head_bwd_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, (hipStream_t)stream,
-                     g_mean, mean, g_v, M, A, dz4);
+                     g_mean, mean, v, vstride, ret, M, A, dz4);
   HIPCHK(hipGetLastError());
   return MJL_OK;
 }
@@ -1238,9 +1242,10 @@ extern "C" long long mjl_ppo_loss_scratch(int n, int A) {
 }
 
 extern "C" int mjl_ppo_surrogate_clipped(const float* mean, const float* log_std, const float* act,
-                                         const float* old_logp, const float* adv, const float* adv_stats, int n, int A,
-                                         float clip_eps, float ent_coef, float log_std_lo, float log_std_hi,
-                                         float* scratch, float* loss, float* g_mean, float* g_log_std, void* stream) {
+                                         const float* old_logp, const float* adv, const float* adv_stats,
+                                         const int* stats_row, int n, int A, float clip_eps, float ent_coef,
+                                         float log_std_lo, float log_std_hi, float* scratch, float* loss,
+                                         float* g_mean, float* g_log_std, void* stream) {
   if (!mean || !log_std || !act || !old_logp || !adv || !scratch || !loss || !g_mean || !g_log_std || n <= 0 || A <= 0)
     return fail(MJL_ERR_ARG, "bad argument");
   if (A > kLossMaxA) return fail(MJL_ERR_UNSUPPORTED, "ppo surrogate: at most %d action columns", kLossMaxA);
@@ -1250,7 +1255,7 @@ extern "C" int mjl_ppo_surrogate_clipped(const float* mean, const float* log_std
   float* part = scratch + 3 * (size_t)nb;
   if (!adv_stats) hipLaunchKernelGGL(adv_stats_kernel, dim3(nb), dim3(kLossT), 0, s, adv, n, adv_part);
   hipLaunchKernelGGL(ppo_surrogate_kernel, dim3(nb), dim3(kLossT), 0, s, mean, log_std, act, old_logp, adv, n, A,
-                     clip_eps, adv_part, nb, adv_stats, g_mean, part, log_std_lo, log_std_hi);
+                     clip_eps, adv_part, nb, adv_stats, g_mean, part, log_std_lo, log_std_hi, stats_row);
   hipLaunchKernelGGL(ppo_surrogate_final_kernel, dim3(A + 1), dim3(64), 0, s, part, nb, n, A, log_std, ent_coef, loss,
                      g_log_std, log_std_lo, log_std_hi);
   HIPCHK(hipGetLastError());
@@ -1261,8 +1266,8 @@ extern "C" int mjl_ppo_surrogate(const float* mean, const float* log_std, const 
                                  const float* adv, const float* adv_stats, int n, int A, float clip_eps,
                                  float ent_coef, float* scratch, float* loss, float* g_mean, float* g_log_std,
                                  void* stream) {
-  return mjl_ppo_surrogate_clipped(mean, log_std, act, old_logp, adv, adv_stats, n, A, clip_eps, ent_coef, -INFINITY,
-                                   INFINITY, scratch, loss, g_mean, g_log_std, stream);
+  return mjl_ppo_surrogate_clipped(mean, log_std, act, old_logp, adv, adv_stats, nullptr, n, A, clip_eps, ent_coef,
+                                   -INFINITY, INFINITY, scratch, loss, g_mean, g_log_std, stream);
 }
 
 extern "C" int mjl_mse_strided(const float* v, int vstride, const float* r, int n, float* scratch, float* loss,
@@ -1280,8 +1285,8 @@ extern "C" int mjl_mse(const float* v, const float* r, int n, float* scratch, fl
   return mjl_mse_strided(v, 1, r, n, scratch, loss, g_v, stream);
 }
 
-extern "C" int mjl_gather_rows(const long long* idx, int n, long long nsrc, int narr, const float* const* src,
-                               float* const* dst, const int* cols, void* stream) {
+extern "C" int mjl_gather_rows_indexed(const long long* idx, const int* idx_row, int n, long long nsrc, int narr,
+                                       const float* const* src, float* const* dst, const int* cols, void* stream) {
   if (!idx || n < 0 || nsrc < 0 || narr < 1 || narr > 5 || !src || !dst || !cols) return fail(MJL_ERR_ARG, "bad argument");
   GatherArgs g;
   std::memset(&g, 0, sizeof(g));
@@ -1296,9 +1301,14 @@ extern "C" int mjl_gather_rows(const long long* idx, int n, long long nsrc, int 
   if (work == 0) return MJL_OK;
   if (work + 255 >= (1ll << 31)) return fail(MJL_ERR_ARG, "gather_rows: rows x total columns must be below 2^31");
   hipLaunchKernelGGL(gather_rows_kernel, dim3((unsigned)((work + 255) / 256)), dim3(256), 0, (hipStream_t)stream, idx,
-                     n, nsrc, g);
+                     n, nsrc, g, idx_row);
   HIPCHK(hipGetLastError());
   return MJL_OK;
+}
+
+extern "C" int mjl_gather_rows(const long long* idx, int n, long long nsrc, int narr, const float* const* src,
+                               float* const* dst, const int* cols, void* stream) {
+  return mjl_gather_rows_indexed(idx, nullptr, n, nsrc, narr, src, dst, cols, stream);
 }
 
 static int adam_launch(int nt, float* const* p, const float* const* g, float* const* m, float* const* v,
@@ -1338,6 +1348,38 @@ extern "C" int mjl_adam_dev(int nt, float* const* p, const float* const* g, floa
                             void* stream) {
   if (!step) return fail(MJL_ERR_ARG, "bad argument");
   return adam_launch(nt, p, g, m, v, numel, lr, beta1, beta2, eps, 0, step, stream);
+}
+
+extern "C" int mjl_adam_multi(int nt, float* const* p, const float* const* g, float* const* m, float* const* v,
+                              const long long* numel, const int* group, int ngroups, const float* lr, float beta1,
+                              float beta2, float eps, float gscale, float* const* step, int* done, int* ctr,
+                              void* stream) {
+  if (nt < 1 || nt > kAdamMultiMaxT || ngroups < 1 || ngroups > kAdamMaxGroups || !p || !g || !m || !v || !numel ||
+      !group || !lr || !step || !done)
+    return fail(MJL_ERR_ARG, "bad argument");
+  AdamMultiArgs a;
+  std::memset(&a, 0, sizeof(a));
+  a.nt = nt; a.ngroups = ngroups;
+  for (int k = 0; k < nt; k++) {
+    if (!p[k] || !m[k] || !v[k] || numel[k] < 0 || group[k] < 0 || group[k] >= ngroups)
+      return fail(MJL_ERR_ARG, "bad argument");
+    a.p[k] = p[k]; a.g[k] = g[k]; a.m[k] = m[k]; a.v[k] = v[k]; a.grp[k] = group[k]; a.numel[k] = numel[k];
+    const long long nb = (numel[k] + 255) / 256;
+    if ((long long)a.blk[k] + nb >= (1LL << 30)) return fail(MJL_ERR_ARG, "adam_multi: too many elements");
+    a.blk[k + 1] = a.blk[k] + (int)nb;
+  }
+  for (int gi = 0; gi < ngroups; gi++) {
+    if (!step[gi]) return fail(MJL_ERR_ARG, "bad argument");
+    for (int gj = 0; gj < gi; gj++)
+      if (step[gj] == step[gi]) return fail(MJL_ERR_ARG, "adam_multi: groups need distinct step counters");
+    a.lr[gi] = lr[gi]; a.step[gi] = step[gi];
+  }
+  a.b1 = beta1; a.b2 = beta2; a.eps = eps; a.gscale = gscale;
+  a.done = done; a.ctr = ctr;
+  const unsigned blocks = (unsigned)(a.blk[nt] > 0 ? a.blk[nt] : 1);  // >= 1: the counters advance
+  hipLaunchKernelGGL(adam_multi_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, a);
+  HIPCHK(hipGetLastError());
+  return MJL_OK;
 }
 
 // ---------------------------------------------------------------- PPO update dense layers

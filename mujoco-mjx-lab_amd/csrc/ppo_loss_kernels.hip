@@ -87,7 +87,7 @@ __global__ __launch_bounds__(kLossT) void ppo_surrogate_kernel(
     const float* __restrict__ mean, const float* __restrict__ log_std, const float* __restrict__ act,
     const float* __restrict__ old_logp, const float* __restrict__ adv, int n, int A, float clip_eps,
     const float* __restrict__ adv_part, int nb, const float* __restrict__ adv_stats, float* __restrict__ gmean,
-    float* __restrict__ part, float ls_lo, float ls_hi) {
+    float* __restrict__ part, float ls_lo, float ls_hi, const int* __restrict__ stats_row) {
   constexpr int NW = kLossT / 64;
   __shared__ float sd[kLossT * kLossMaxA];  // a - m of the block's rows, row-major
   __shared__ float sdl[kLossT];             // d logp per row
@@ -105,7 +105,10 @@ __global__ __launch_bounds__(kLossT) void ppo_surrogate_kernel(
   }
   if (w == 1) {  // the advantage statistics, beside the staging loads
     float mu, sdv;
-    if (adv_stats) { mu = adv_stats[0]; sdv = adv_stats[1]; }  // global statistics (data-parallel)
+    if (adv_stats) {  // global statistics (data-parallel); row *stats_row of a [n_minibatches, 2] table
+      const float* st = adv_stats + (stats_row ? 2 * (size_t)*stats_row : 0);
+      mu = st[0]; sdv = st[1];
+    }
     else adv_merge_wave(adv_part, nb, lane, mu, sdv);
     if (lane == 0) { mu_s = mu; sd_s = sdv; }
   }
@@ -228,23 +231,27 @@ __global__ __launch_bounds__(256) void slice_sum_kernel(const float* __restrict_
   reinterpret_cast<float4*>(out)[q] = acc;
 }
 
-// The twin update's output-layer backward (ppo.py TwinUpdate): the policy's mean = tanh(z) sits in
-// out4[0] ([M, A], after the in-place tanh), the value in column 0 of out4[1]; g_mean = d loss / d mean
-// (mjl_ppo_surrogate), g_v = d loss / d value (mjl_mse). dz4[0] = g_mean (1 - mean^2), dz4[1][:, 0] =
-// g_v, dz4[1][:, 1:] = 0 (the value's padded output rows get no gradient).
+// The twin update's output-layer backward (twin.py): the policy's mean = tanh(z) sits in out[0]
+// ([M, A]), the value in column 0 of out[1] (v[r] = v[r * vstride]); g_mean = d loss / d mean
+// (mjl_ppo_surrogate). dz[0] = g_mean (1 - mean^2); dz[1][:, 0] = d mean((v - ret)^2) / d v =
+// 2 (v - ret) / M (mse_kernel's gradient: the value loss itself is not needed by the update);
+// dz[1][:, 1:] = 0 (the value's padded output rows get no gradient). 32-bit indices (M A < 2^30).
 __global__ __launch_bounds__(256) void twin_head_bwd_kernel(const float* __restrict__ g_mean,
                                                             const float* __restrict__ mean,
-                                                            const float* __restrict__ g_v, int M, int A,
+                                                            const float* __restrict__ v, int vstride,
+                                                            const float* __restrict__ ret, int M, int A,
                                                             float* __restrict__ dz4) {
-  const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
-  const long long n = (long long)M * A;
+  const unsigned i = blockIdx.x * blockDim.x + threadIdx.x;
+  const unsigned n = (unsigned)M * (unsigned)A;
   if (i >= 2 * n) return;
   if (i < n) {
     const float y = mean[i];
     dz4[i] = g_mean[i] * (1.f - y * y);
   } else {
-    const long long j = i - n, r = j / A;
-    dz4[i] = (j - r * A == 0) ? g_v[r] : 0.f;
+    const unsigned j = i - n, r = j / (unsigned)A;
+    float g = 0.f;
+    if (j - r * (unsigned)A == 0) g = 2.f * (v[(size_t)r * vstride] - ret[r]) / (float)M;
+    dz4[i] = g;
   }
 }
 
@@ -293,7 +300,8 @@ struct GatherArgs {
   int narr;
 };
 __global__ __launch_bounds__(256) void gather_rows_kernel(const long long* __restrict__ idx, int n, long long nsrc,
-                                                          GatherArgs g) {
+                                                          GatherArgs g, const int* __restrict__ idx_row) {
+  if (idx_row) idx += (size_t)*idx_row * n;  // row *idx_row of an [n_minibatches, n] index table
   // 32-bit index math (the launcher checks n * total columns < 2^31): a 64-bit divide per element
   // was most of this kernel's time
   const unsigned tid = blockIdx.x * blockDim.x + threadIdx.x;
@@ -341,6 +349,65 @@ __global__ __launch_bounds__(256) void adam_kernel(AdamArgs a) {
   a.v[k][j] = v;
   const float denom = sqrtf(v) / bc2_sqrt + a.eps;
   a.p[k][j] = a.p[k][j] - step_size * m / denom;
+}
+
+// Adam over the tensors of up to two optimisers in one launch (the twin update's policy and value
+// steps): tensor k belongs to group grp[k] with its own lr and device step counter (the count BEFORE
+// this step: the kernel takes t = count + 1, as torch.optim.Adam's step() does after its increment);
+// gradients are scaled by gscale (the data-parallel mean, 1 / world size). The last block to finish
+// advances every group's counter (and an optional device counter `ctr`, the graphs' minibatch
+// index), so no separate increment launch: every block reads the counters before it arrives at the
+// completion counter, and the last arrival writes after all have.
+constexpr int kAdamMultiMaxT = 24;
+constexpr int kAdamMaxGroups = 2;
+struct AdamMultiArgs {
+  float* p[kAdamMultiMaxT];
+  const float* g[kAdamMultiMaxT];
+  float* m[kAdamMultiMaxT];
+  float* v[kAdamMultiMaxT];
+  long long numel[kAdamMultiMaxT];
+  int blk[kAdamMultiMaxT + 1];  // first block of each tensor (a block covers 256 elements of one tensor)
+  int grp[kAdamMultiMaxT];
+  int nt, ngroups;
+  float lr[kAdamMaxGroups];
+  float* step[kAdamMaxGroups];
+  float b1, b2, eps, gscale;
+  int* done;
+  int* ctr;
+};
+__global__ __launch_bounds__(256) void adam_multi_kernel(AdamMultiArgs a) {
+  // the block's tensor from the block index: uniform, so the argument arrays are read with scalar
+  // loads (a per-thread search over element offsets indexed them per lane)
+  const int b = blockIdx.x;
+  int k = 0;
+  while (k + 1 < a.nt && b >= a.blk[k + 1]) k++;
+  const long long j = (long long)(b - a.blk[k]) * blockDim.x + threadIdx.x;
+  if (j < a.numel[k]) {
+    if (a.g[k]) {
+      const int gi = a.grp[k];
+      const float t = *a.step[gi] + 1.f;
+      const float step_size = a.lr[gi] / (1.f - powf(a.b1, t));
+      const float bc2_sqrt = sqrtf(1.f - powf(a.b2, t));
+      const float g = a.g[k][j] * a.gscale;
+      const float m = a.b1 * a.m[k][j] + (1.f - a.b1) * g;
+      const float v = a.b2 * a.v[k][j] + (1.f - a.b2) * g * g;
+      a.m[k][j] = m;
+      a.v[k][j] = v;
+      const float denom = sqrtf(v) / bc2_sqrt + a.eps;
+      a.p[k][j] = a.p[k][j] - step_size * m / denom;
+    }
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    __threadfence();
+    const int prev = atomicAdd(a.done, 1);
+    if (prev == (int)gridDim.x - 1) {
+      for (int gi = 0; gi < a.ngroups; gi++) *a.step[gi] += 1.f;
+      if (a.ctr) *a.ctr += 1;
+      *a.done = 0;
+      __threadfence();
+    }
+  }
 }
 
 }  // namespace mjl

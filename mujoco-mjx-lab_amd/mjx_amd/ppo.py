@@ -619,8 +619,23 @@ def value_loss(value, obs, returns):
     return torch.mean((v - returns) ** 2)
 
 
-def _gather_minibatch(idx, *arrays):
-    """arrays[k][idx] for every k, as one native launch (mjl_gather_rows) on the GPU."""
+def _gather_minibatch(idx, *arrays, row: Optional[torch.Tensor] = None):
+    """arrays[k][idx] for every k, as one native launch (mjl_gather_rows) on the GPU. With `row` (a
+    device int32), idx is an [n_minibatches, rows] table and the launch gathers row *row of it, read
+    when the launch runs (a captured minibatch step; mjl_gather_rows_indexed)."""
+    if row is not None:
+        import ctypes
+        from ._lib import check, lib
+        n = idx.shape[1]
+        outs = tuple(torch.empty((n,) + tuple(a.shape[1:]), dtype=a.dtype, device=a.device) for a in arrays)
+        k = len(arrays)
+        check(lib().mjl_gather_rows_indexed(idx.data_ptr(), ctypes.c_void_p(row.data_ptr()), n,
+                                            min(a.shape[0] for a in arrays), k,
+                                            (ctypes.c_void_p * k)(*[a.data_ptr() for a in arrays]),
+                                            (ctypes.c_void_p * k)(*[o.data_ptr() for o in outs]),
+                                            (ctypes.c_int * k)(*[max(1, a[0].numel()) for a in arrays]),
+                                            torch.cuda.current_stream(idx.device).cuda_stream))
+        return outs
     if not (idx.is_cuda and idx.dtype == torch.int64 and len(arrays) <= 5
             and all(a.is_cuda and a.dtype == torch.float32 and a.is_contiguous() for a in arrays)):
         return tuple(a[idx] for a in arrays)
@@ -693,11 +708,12 @@ def adam_state_from_torch(d: dict, shapes: list):
 
 class NativeAdam:
     """torch.optim.Adam (betas, eps; no weight decay) for CUDA float32 parameters as one native
-    launch per step (mjl_adam_dev: the fused update of every tensor), where torch's fused Adam took
-    ≈42 µs for the 151K-parameter policy. The step count lives on the device and is advanced by a
-    launch inside step(), so a hipGraph that captured step() takes each replay's own bias
-    corrections (a host int baked into the capture made replays drift from eager).
-    state_dict / load_state_dict use torch.optim.Adam's layout (checkpoints interchange)."""
+    launch per step (mjl_adam_multi: the fused update of every tensor), where torch's fused Adam took
+    ≈42 µs for the 151K-parameter policy. The step count lives on the device and the launch itself
+    advances it, so a hipGraph that captured step() takes each replay's own bias corrections (a host
+    int baked into the capture made replays drift from eager). adam_steps() takes
+    several optimisers' steps in one launch. state_dict / load_state_dict use torch.optim.Adam's
+    layout (checkpoints interchange)."""
 
     def __init__(self, params, lr: float, betas=(0.9, 0.999), eps: float = 1e-8):
         self.params = [p for p in params]
@@ -708,6 +724,7 @@ class NativeAdam:
         self.m = [torch.zeros_like(p) for p in self.params]
         self.v = [torch.zeros_like(p) for p in self.params]
         self.step_t = torch.zeros(1, dtype=torch.float32, device=self.params[0].device)
+        self.done = torch.zeros(1, dtype=torch.int32, device=self.params[0].device)  # the launch's completion count
 
     @property
     def t(self) -> int:
@@ -723,20 +740,7 @@ class NativeAdam:
     @torch.no_grad()
     def step(self, grads: Optional[List[torch.Tensor]] = None):
         """One Adam step with `grads` (default: the parameters' .grad)."""
-        import ctypes
-        from ._lib import check, lib
-        k = len(self.params)
-        src = [p.grad for p in self.params] if grads is None else list(grads)
-        grads = [g if g is None else g.contiguous() for g in src]
-        self.step_t.add_(1.0)
-        vp = ctypes.c_void_p * k
-        check(lib().mjl_adam_dev(k, vp(*[p.data_ptr() for p in self.params]),
-                                 vp(*[None if g is None else g.data_ptr() for g in grads]),
-                                 vp(*[x.data_ptr() for x in self.m]), vp(*[x.data_ptr() for x in self.v]),
-                                 (ctypes.c_longlong * k)(*[p.numel() for p in self.params]), self.lr, self.betas[0],
-                                 self.betas[1], self.eps, ctypes.c_void_p(self.step_t.data_ptr()),
-                                 torch.cuda.current_stream(self.params[0].device).cuda_stream))
-        self._keep = grads  # the launch reads them asynchronously
+        adam_steps([(self, grads)])
 
     def state_dict(self):
         return adam_state_to_torch(float(self.step_t.item()), self.m, self.v, self.lr, self.betas, self.eps)
@@ -746,6 +750,38 @@ class NativeAdam:
         self.step_t.fill_(step)
         for dst, src in zip(self.m + self.v, (m + v) if m is not None else [torch.zeros_like(x) for x in self.m + self.v]):
             dst.copy_(src)
+
+
+@torch.no_grad()
+def adam_steps(pairs, gscale: float = 1.0, ctr: Optional[torch.Tensor] = None):
+    """One Adam step of each (NativeAdam, grads or None for the parameters' .grad) in ONE launch
+    (mjl_adam_multi, up to 2 optimisers with the same betas / eps), gradients scaled by gscale; `ctr`
+    (device int32, optional) is advanced by the launch with the step counters."""
+    import ctypes
+    from ._lib import check, lib
+    o0 = pairs[0][0]
+    if len(pairs) > 2 or any(o.betas != o0.betas or o.eps != o0.eps for o, _ in pairs):
+        raise ValueError("adam_steps: at most 2 optimisers with equal betas and eps")
+    ps, gs, ms, vs, ns, grp = [], [], [], [], [], []
+    for gi, (opt, grads) in enumerate(pairs):
+        src = [p.grad for p in opt.params] if grads is None else list(grads)
+        if len(src) != len(opt.params):
+            raise ValueError("adam_steps: one gradient per parameter")
+        for p, g, m, v in zip(opt.params, src, opt.m, opt.v):
+            ps.append(p); gs.append(None if g is None else g.contiguous()); ms.append(m); vs.append(v)
+            ns.append(p.numel()); grp.append(gi)
+    k = len(ps)
+    vp = ctypes.c_void_p * k
+    dev = o0.params[0].device
+    check(lib().mjl_adam_multi(k, vp(*[p.data_ptr() for p in ps]), vp(*[None if g is None else g.data_ptr() for g in gs]),
+                               vp(*[x.data_ptr() for x in ms]), vp(*[x.data_ptr() for x in vs]),
+                               (ctypes.c_longlong * k)(*ns), (ctypes.c_int * k)(*grp), len(pairs),
+                               (ctypes.c_float * len(pairs))(*[o.lr for o, _ in pairs]), o0.betas[0], o0.betas[1],
+                               o0.eps, float(gscale), (ctypes.c_void_p * len(pairs))(*[o.step_t.data_ptr() for o, _ in pairs]),
+                               ctypes.c_void_p(o0.done.data_ptr()), None if ctr is None else ctypes.c_void_p(ctr.data_ptr()),
+                               torch.cuda.current_stream(dev).cuda_stream))
+    for opt, _ in pairs:
+        opt._keep = gs  # the launch reads the gradients asynchronously
 
 
 def _adam(params, lr):
@@ -881,18 +917,20 @@ class PPOUpdater:
         return sum(p.numel() for p in self.pp + self.vp)
 
     # ------------------------------------------------------------------ bodies
-    def _body_a(self, idx, src, st):
+    def _body_a(self, idx, src, st, row: Optional[torch.Tensor] = None):
         """Gather the minibatch; forward + backward of both nets (and, single-process, both Adam
-        steps). Data-parallel: leaves both nets' gradients in the all-reduce buffer."""
+        steps). Data-parallel: leaves both nets' gradients in the all-reduce buffer. With `row` (twin
+        graphs), idx and st are the whole update's [n_minibatches, ...] tables, read at row *row, which
+        the Adam launch advances: the replays need no per-minibatch host copies."""
         cfg, opt_p, opt_v = self.cfg, self.opt_p, self.opt_v
-        o, a, ol, r, ad = _gather_minibatch(idx, *src)
+        o, a, ol, r, ad = _gather_minibatch(idx, *src, row=row)
         dp = self.dist is not None
         if self._tw:
             tw = self.twin
-            tw.forward_backward(o, a, ol, r, ad, st, cfg.clip_eps, cfg.ent_coef, min(64, o.shape[0] // SPLIT_ROWS))
-            if not dp:
-                opt_p.step(grads=tw.grads_p)
-                opt_v.step(grads=tw.grads_v)
+            tw.forward_backward(o, a, ol, r, ad, st, cfg.clip_eps, cfg.ent_coef, min(64, o.shape[0] // SPLIT_ROWS),
+                                stats_row=row)
+            if not dp:  # both nets' Adam steps in one launch
+                adam_steps([(opt_p, tw.grads_p), (opt_v, tw.grads_v)], ctr=row)
             return
         if self.side is not None:
             cur = torch.cuda.current_stream(o.device)
@@ -921,12 +959,13 @@ class PPOUpdater:
             opt_p.step()
             opt_v.step()
 
-    def _body_b(self):
-        """Data-parallel: the all-reduced gradient sum -> mean, then both Adam steps."""
-        if self._tw:
-            self.twin.grad.div_(self.world)
-            self.opt_p.step(grads=self.twin.grads_p)
-            self.opt_v.step(grads=self.twin.grads_v)
+    def _body_b(self, row: Optional[torch.Tensor] = None):
+        """Data-parallel: the all-reduced gradient sum -> mean, then both Adam steps (advancing the
+        twin graphs' minibatch row)."""
+        if isinstance(self.opt_p, NativeAdam) and isinstance(self.opt_v, NativeAdam):
+            # the all-reduced sum -> mean inside the one Adam launch of both nets
+            gp, gv = (self.twin.grads_p, self.twin.grads_v) if self._tw else (self.views_p, self.views_v)
+            adam_steps([(self.opt_p, gp), (self.opt_v, gv)], gscale=1.0 / self.world, ctr=row)
             return
         self.flat.div_(self.world)
         if isinstance(self.opt_p, NativeAdam):
@@ -987,6 +1026,9 @@ class PPOUpdater:
             self._ga = self._gb = None
         for dst, x in zip(self._src, src):  # the graphs read the static copies
             dst.copy_(x)
+        if self._tw:  # the twin graphs read the update's index / statistics tables at a device row
+            self._run_twin_graphs(index_batches, stats, events)
+            return
         for i in range(index_batches.shape[0]):
             self._idx.copy_(index_batches[i])
             if stats is not None:
@@ -999,6 +1041,36 @@ class PPOUpdater:
                     self._gb = torch.cuda.CUDAGraph()
                     with torch.cuda.graph(self._gb):
                         self._body_b()
+            self._ga.replay()
+            if self.dist is not None:
+                self._allreduce(events)
+                self._gb.replay()
+
+
+    def _run_twin_graphs(self, index_batches, stats, events):
+        """The twin path's replays: the whole update's index table (and, data-parallel, its advantage
+        statistics) copied once, a device row counter that the captured Adam launch advances, so a
+        minibatch step is graph A (+ the all-reduce + graph B) with no host copy in between."""
+        nmb = index_batches.shape[0]
+        if getattr(self, "_idx_all", None) is None or self._idx_all.shape != index_batches.shape:
+            self._idx_all = torch.empty_like(index_batches, memory_format=torch.contiguous_format)
+            self._st_all = torch.zeros((nmb, 2), device=index_batches.device)
+            self._row = torch.zeros(1, dtype=torch.int32, device=index_batches.device)
+            self._ga = self._gb = None
+        self._idx_all.copy_(index_batches)
+        if stats is not None:
+            self._st_all.copy_(stats)
+        self._row.zero_()
+        st = self._st_all if stats is not None else None
+        for _ in range(nmb):
+            if self._ga is None:
+                self._ga = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(self._ga):
+                    self._body_a(self._idx_all, self._src, st, row=self._row)
+                if self.dist is not None:
+                    self._gb = torch.cuda.CUDAGraph()
+                    with torch.cuda.graph(self._gb):
+                        self._body_b(row=self._row)
             self._ga.replay()
             if self.dist is not None:
                 self._allreduce(events)

@@ -107,12 +107,20 @@ class TwinNets:
         self.grads_p: List[torch.Tensor] = [gview[id(p)] for p in policy.parameters()]
         self.grads_v: List[torch.Tensor] = [gview[id(p)] for p in value.parameters()]
         self._scr = {}
+        self._done = {}  # per stream: the single-launch column sums' completion counter (kept zero)
 
     def owns_storage(self) -> bool:
         """Whether the modules' parameters still are views of the stacked storage (a load_state_dict
         copies into them and keeps it; re-assigning .data would not)."""
         pm = self.policy.mlp
         return all(l.weight.data_ptr() == self.W[i][0].data_ptr() for i, l in enumerate(pm.layers))
+
+    def _counter(self) -> torch.Tensor:
+        st = torch.cuda.current_stream(self.grad.device).cuda_stream
+        t = self._done.get(st)
+        if t is None:
+            t = self._done[st] = torch.zeros(1, dtype=torch.int32, device=self.grad.device)
+        return t
 
     def _scratch(self, key, floats: int) -> torch.Tensor:
         st = torch.cuda.current_stream(self.grad.device).cuda_stream
@@ -122,9 +130,12 @@ class TwinNets:
             t = self._scr[k] = torch.empty(max(floats, 4), device=self.grad.device)
         return t
 
-    def forward_backward(self, o, acts, old_logp, ret, adv, adv_stats, clip_eps: float, ent_coef: float, splits: int):
+    def forward_backward(self, o, acts, old_logp, ret, adv, adv_stats, clip_eps: float, ent_coef: float, splits: int,
+                         want_value_loss: bool = False, stats_row=None):
         """Both nets' losses and gradients for one minibatch (o [M, K0], acts [M, A], old_logp / ret /
-        adv [M]); the gradients into self.grad. Returns (policy loss, value loss) device scalars."""
+        adv [M]); the gradients into self.grad. Returns (policy loss, value loss) device scalars (the
+        value loss only with want_value_loss: the update does not need it). stats_row: adv_stats is the
+        [n_minibatches, 2] table, read at that device row."""
         L = lib()
         dev = o.device
         st = torch.cuda.current_stream(dev).cuda_stream
@@ -147,27 +158,34 @@ class TwinNets:
         gm = torch.empty((M, A), device=dev)
         scr = self._scratch("loss", int(L.mjl_ppo_loss_scratch(M, A)))
         check(L.mjl_ppo_surrogate_clipped(mean.data_ptr(), log_std.data_ptr(), acts.data_ptr(), old_logp.data_ptr(),
-                                          adv.data_ptr(), None if adv_stats is None else adv_stats.data_ptr(), M, A,
+                                          adv.data_ptr(), None if adv_stats is None else adv_stats.data_ptr(),
+                                          None if stats_row is None else stats_row.data_ptr(), M, A,
                                           float(clip_eps), float(ent_coef), -20.0, 2.0, scr.data_ptr(),
                                           loss_p.data_ptr(), gm.data_ptr(), self.g_log_std.data_ptr(), st))
-        gv = torch.empty(M, device=dev)
-        scr_v = self._scratch("mse", M // 256 + 1)
-        check(L.mjl_mse_strided(z[1].data_ptr(), A, ret.data_ptr(), M, scr_v.data_ptr(), loss_v.data_ptr(),
-                                gv.data_ptr(), st))
-        # ---- backward
+        if want_value_loss:  # (reporting only: the value gradient comes from the head kernel below)
+            gv = torch.empty(M, device=dev)
+            scr_v = self._scratch("mse", M // 256 + 1)
+            check(L.mjl_mse_strided(z[1].data_ptr(), A, ret.data_ptr(), M, scr_v.data_ptr(), loss_v.data_ptr(),
+                                    gv.data_ptr(), st))
+        # ---- backward: dZ of both output layers, the value's 2 (v - ret) / M formed in the same pass
         dz = torch.empty((2, M, A), device=dev)
-        check(L.mjl_twin_head_bwd(gm.data_ptr(), mean.data_ptr(), gv.data_ptr(), M, A, dz.data_ptr(), st))
+        check(L.mjl_twin_head_bwd(gm.data_ptr(), mean.data_ptr(), z[1].data_ptr(), A, ret.data_ptr(), M, A,
+                                  dz.data_ptr(), st))
         ncs = int(L.mjl_colsum_batched_scratch(2, M, max(A, self.W[0].shape[1])))
         cs = self._scratch("colsum", ncs)
-        check(L.mjl_colsum_batched(dz.data_ptr(), 2, M, A, cs.data_ptr(), self.gb[nl - 1].data_ptr(), st))
+        done = self._counter().data_ptr()  # column sums in one launch each (the last block finishes)
+        check(L.mjl_colsum_batched(dz.data_ptr(), 2, M, A, cs.data_ptr(), self.gb[nl - 1].data_ptr(), done, st))
         g = dz
         for l in range(nl - 1, -1, -1):
             N, K = self.W[l].shape[1], self.W[l].shape[2]
             xin = hs[l]  # the layer's input: H_{l-1}, or the observations for l = 0
+            # split-K slices of the weight gradient: the thin layers (the 21 / 1-unit outputs, the 54-wide
+            # input) are a few output tiles per slice, so they take more, shorter slices
+            s = splits if (N >= 64 and K >= 64) else max(splits, min(64, M // 256))
             if l < nl - 1:  # tanh layer: dZ = dH (1 - H^2) and the bias gradient in one pass
                 dzl = torch.empty_like(g)
                 check(L.mjl_tanh_bwd_colsum_batched(g.data_ptr(), hs[l + 1].data_ptr(), 2, M, N, dzl.data_ptr(),
-                                                    cs.data_ptr(), self.gb[l].data_ptr(), st))
+                                                    cs.data_ptr(), self.gb[l].data_ptr(), done, st))
             else:
                 dzl = g
             if l == 0:  # the shared observations: [2, M, K0] with batch stride 0 -> per split, both nets

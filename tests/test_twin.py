@@ -42,7 +42,8 @@ def test_twin_gradients_match_float64_autograd(n):
     assert twin.TwinNets.eligible(pol, val)
     tw = twin.TwinNets(pol, val)
     o, a, ol, r, ad = _data(n)
-    lp, lv = tw.forward_backward(o, a, ol, r, ad, None, cfg.clip_eps, cfg.ent_coef, min(64, n // ppo.SPLIT_ROWS))
+    lp, lv = tw.forward_backward(o, a, ol, r, ad, None, cfg.clip_eps, cfg.ent_coef, min(64, n // ppo.SPLIT_ROWS),
+                                 want_value_loss=True)
     torch.cuda.synchronize()
     old = ppo.NATIVE_LOSSES
     ppo.NATIVE_LOSSES = False

@@ -1,0 +1,25 @@
+# round 4: twin update with the uniform-block Adam, single-launch column sums and more split-K slices
+# for the thin layers: tests, TunableOp tuning of the new GEMM shapes (extending the shipped table),
+# A/B, C5 phase split; then the APG / solver-timing / Hessian-variant probes (tools/r4/gpu_e.sh)
+set -o pipefail
+export TMPDIR=/tmp
+O=gpurun_out/r4g
+mkdir -p $O
+timeout -k 10 600 python -u -m pytest -x -q --timeout 400 --timeout-method thread -m gpu tests/test_twin.py tests/test_ppo_graph.py tests/test_ppo.py tests/test_dp_gpu.py > $O/pytest.log 2>&1
+rc=$?; echo "pytest rc=$rc"; tail -3 $O/pytest.log
+if [ $rc -ne 0 ]; then grep -v amdgpu.ids $O/pytest.log | grep -B5 -A40 "^____" | head -80; exit $rc; fi
+cp mujoco-mjx-lab_amd/mjx_amd/tuning/gfx950_tunableop.csv $O/tunableop_results0.csv
+( export PYTORCH_TUNABLEOP_ENABLED=1 PYTORCH_TUNABLEOP_TUNING=1 PYTORCH_TUNABLEOP_FILENAME=$O/tunableop_results%d.csv
+  timeout -k 10 400 python -u tools/ppo_update_probe.py twin > $O/tune.txt 2>&1 ) || exit $?
+wc -l $O/tunableop_results0.csv
+cp $O/tunableop_results0.csv mujoco-mjx-lab_amd/mjx_amd/tuning/gfx950_tunableop.csv
+timeout -k 10 200 python -u tools/ppo_update_probe.py twin > $O/ab.txt 2>&1 || exit $?
+grep -v amdgpu.ids $O/ab.txt
+for T in 1 0; do
+  MJL_TWIN_UPDATE=$T PROBE_DP=nccl PROBE_MB=8192 timeout -k 10 300 python -u tools/ppo_phase_probe.py > $O/phase_c5_nccl_twin$T.json 2> $O/phase_c5_nccl_twin$T.err || exit $?
+  MJL_TWIN_UPDATE=$T timeout -k 10 300 python -u tools/ppo_phase_probe.py > $O/phase_c3_twin$T.json 2> $O/phase_c3_twin$T.err || exit $?
+  grep -h '^{' $O/phase_c5_nccl_twin$T.json $O/phase_c3_twin$T.json
+done
+PROBE_DP=nccl PROBE_MB=8192 timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof_c5 -o t -- python tools/ppo_phase_probe.py > $O/prof_c5.log 2>&1 || exit $?
+echo ALL_OK_G
+bash tools/r4/gpu_e.sh
