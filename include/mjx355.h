@@ -400,13 +400,11 @@ int mjl_tanh_inplace(float* x, long long n, void* stream);
  * as one batched GEMM per layer, train_ppo.py:233-252 taking both nets' steps per minibatch):
  * x [nb][n][d] -> out [nb][d], each matrix summed in mjl_colsum's order; for nb > 1, n must be a
  * multiple of the 128-row chunk (n > 256). scratch: mjl_colsum_batched_scratch(nb, n, d) floats.
- * done (device int, zero before the first call, left zero; or NULL): one launch instead of two, the
- * last block of the first stage summing the chunk rows.
  * mjl_slice_sum_batched: out[b][e] = sum over s < ns of x[(b * ns + s) * m + e]. */
 long long mjl_colsum_batched_scratch(int nb, int n, int d);
-int mjl_colsum_batched(const float* x, int nb, int n, int d, float* scratch, float* out, int* done, void* stream);
+int mjl_colsum_batched(const float* x, int nb, int n, int d, float* scratch, float* out, void* stream);
 int mjl_tanh_bwd_colsum_batched(const float* g, const float* y, int nb, int n, int d, float* dz, float* scratch,
-                                float* colsum_out, int* done, void* stream);
+                                float* colsum_out, void* stream);
 int mjl_slice_sum_batched(const float* x, int nb, int ns, long long m, float* out, void* stream);
 /* The twin update's output-layer backward: mean [M, A] = tanh of the policy's last Dense (networks.py:
  * 103), g_mean [M, A] = d loss / d mean (mjl_ppo_surrogate), v[r] = v[r * vstride] the value net's
@@ -468,13 +466,12 @@ int mjl_adam_dev(int nt, float* const* p, const float* const* g, float* const* m
 
 /* Adam over nt <= 24 tensors of up to 2 optimisers in one launch (the PPO update's policy and value
  * steps, train_ppo.py:246-251): tensor k uses group[k]'s lr and device step counter step[group[k]]
- * (float, the count before this step: the launch takes step + 1 and advances every group's counter
- * by one when it completes); g is scaled by gscale (the data-parallel mean: 1 / world size); ctr
- * (device int, or NULL) is advanced with the counters; done is a device int that must be zero before
- * the first launch (the kernel leaves it zero). Same arithmetic as mjl_adam_dev. */
+ * (float, the count before this step: the step takes step + 1, and every group's counter is advanced
+ * by one after it); g is scaled by gscale (the data-parallel mean: 1 / world size); ctr (device int,
+ * or NULL) is advanced with the counters. Same arithmetic as mjl_adam_dev. */
 int mjl_adam_multi(int nt, float* const* p, const float* const* g, float* const* m, float* const* v,
                    const long long* numel, const int* group, int ngroups, const float* lr, float beta1, float beta2,
-                   float eps, float gscale, float* const* step, int* done, int* ctr, void* stream);
+                   float eps, float gscale, float* const* step, int* ctr, void* stream);
 
 /* PPO update dense layers (train_ppo.py:204-252: value_and_grad of ppo_loss_fn / value_loss_fn
  * through the src/networks.py:22-61 MLPs), fp32 on the matrix cores, torch nn.Linear layouts

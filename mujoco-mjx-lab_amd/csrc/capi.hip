@@ -1005,8 +1005,7 @@ extern "C" long long mjl_colsum_batched_scratch(int nb, int n, int d) {
   return p.R > 1 ? (long long)nb * p.R * d : 0;
 }
 
-extern "C" int mjl_colsum_batched(const float* x, int nb, int n, int d, float* scratch, float* out, int* done,
-                                  void* stream) {
+extern "C" int mjl_colsum_batched(const float* x, int nb, int n, int d, float* scratch, float* out, void* stream) {
   if ((!x && n > 0) || !out || nb <= 0 || n < 0 || d <= 0) return fail(MJL_ERR_ARG, "bad argument");
   hipStream_t s = (hipStream_t)stream;
   if (n == 0) {
@@ -1017,25 +1016,24 @@ extern "C" int mjl_colsum_batched(const float* x, int nb, int n, int d, float* s
   if (!batched_plan_ok(nb, n, p)) return fail(MJL_ERR_ARG, "colsum_batched: n must be a multiple of %d", p.chunk);
   if (p.R > 1 && !scratch) return fail(MJL_ERR_ARG, "colsum needs mjl_colsum_batched_scratch(nb, n, d) floats of scratch");
   const unsigned tiles1 = (unsigned)((d + p.dc1 - 1) / p.dc1);
-  int* one = p.R > 1 ? done : nullptr;  // single launch: the last block sums the chunk rows
   hipLaunchKernelGGL(colsum_kernel, dim3(tiles1, (unsigned)(p.R * nb)), dim3(256), 0, s, x, n * nb, d, p.dc1, p.chunk,
-                     p.R > 1 ? scratch : out, nb, p.R, out, one);
+                     p.R > 1 ? scratch : out);
   HIPCHK(hipGetLastError());
-  if (p.R > 1 && !one) {
+  if (p.R > 1) {
     const unsigned tiles2 = (unsigned)((d + p.dc2 - 1) / p.dc2);
     hipLaunchKernelGGL(colsum_kernel, dim3(tiles2, (unsigned)nb), dim3(256), 0, s, scratch, p.R * nb, d, p.dc2, p.R,
-                       out, 0, 0, (float*)nullptr, (int*)nullptr);
+                       out);
     HIPCHK(hipGetLastError());
   }
   return MJL_OK;
 }
 
 extern "C" int mjl_colsum(const float* x, int n, int d, float* scratch, float* out, void* stream) {
-  return mjl_colsum_batched(x, 1, n, d, scratch, out, nullptr, stream);
+  return mjl_colsum_batched(x, 1, n, d, scratch, out, stream);
 }
 
 extern "C" int mjl_tanh_bwd_colsum_batched(const float* g, const float* y, int nb, int n, int d, float* dz,
-                                           float* scratch, float* colsum_out, int* done, void* stream) {
+                                           float* scratch, float* colsum_out, void* stream) {
   if (!g || !y || !dz || !colsum_out || nb <= 0 || n <= 0 || d <= 0) return fail(MJL_ERR_ARG, "bad argument");
   if (d % 4 || ((uintptr_t)g | (uintptr_t)y | (uintptr_t)dz | (uintptr_t)colsum_out) % 16)
     return fail(MJL_ERR_ARG, "tanh_bwd_colsum: d divisible by 4 and 16-byte aligned rows expected");
@@ -1046,14 +1044,13 @@ extern "C" int mjl_tanh_bwd_colsum_batched(const float* g, const float* y, int n
     return fail(MJL_ERR_ARG, "tanh_bwd_colsum needs mjl_colsum_batched_scratch(nb, n, d) floats of 16-byte aligned scratch");
   const int dq = d / 4 < 64 ? d / 4 : 64;
   const unsigned tiles1 = (unsigned)((d / 4 + dq - 1) / dq);
-  int* one = p.R > 1 ? done : nullptr;
   hipLaunchKernelGGL(tanh_bwd_colsum_kernel, dim3(tiles1, (unsigned)(p.R * nb)), dim3(256), 0, s, g, y, n * nb, d, dq,
-                     p.chunk, dz, p.R > 1 ? scratch : colsum_out, nb, p.R, colsum_out, one);
+                     p.chunk, dz, p.R > 1 ? scratch : colsum_out);
   HIPCHK(hipGetLastError());
-  if (p.R > 1 && !one) {
+  if (p.R > 1) {
     const unsigned tiles2 = (unsigned)((d + p.dc2 - 1) / p.dc2);
     hipLaunchKernelGGL(colsum_kernel, dim3(tiles2, (unsigned)nb), dim3(256), 0, s, scratch, p.R * nb, d, p.dc2, p.R,
-                       colsum_out, 0, 0, (float*)nullptr, (int*)nullptr);
+                       colsum_out);
     HIPCHK(hipGetLastError());
   }
   return MJL_OK;
@@ -1061,7 +1058,7 @@ extern "C" int mjl_tanh_bwd_colsum_batched(const float* g, const float* y, int n
 
 extern "C" int mjl_tanh_bwd_colsum(const float* g, const float* y, int n, int d, float* dz, float* scratch,
                                    float* colsum_out, void* stream) {
-  return mjl_tanh_bwd_colsum_batched(g, y, 1, n, d, dz, scratch, colsum_out, nullptr, stream);
+  return mjl_tanh_bwd_colsum_batched(g, y, 1, n, d, dz, scratch, colsum_out, stream);
 }
 
 extern "C" int mjl_slice_sum_batched(const float* x, int nb, int ns, long long m, float* out, void* stream) {
@@ -1352,10 +1349,9 @@ extern "C" int mjl_adam_dev(int nt, float* const* p, const float* const* g, floa
 
 extern "C" int mjl_adam_multi(int nt, float* const* p, const float* const* g, float* const* m, float* const* v,
                               const long long* numel, const int* group, int ngroups, const float* lr, float beta1,
-                              float beta2, float eps, float gscale, float* const* step, int* done, int* ctr,
-                              void* stream) {
+                              float beta2, float eps, float gscale, float* const* step, int* ctr, void* stream) {
   if (nt < 1 || nt > kAdamMultiMaxT || ngroups < 1 || ngroups > kAdamMaxGroups || !p || !g || !m || !v || !numel ||
-      !group || !lr || !step || !done)
+      !group || !lr || !step)
     return fail(MJL_ERR_ARG, "bad argument");
   AdamMultiArgs a;
   std::memset(&a, 0, sizeof(a));
@@ -1375,9 +1371,10 @@ extern "C" int mjl_adam_multi(int nt, float* const* p, const float* const* g, fl
     a.lr[gi] = lr[gi]; a.step[gi] = step[gi];
   }
   a.b1 = beta1; a.b2 = beta2; a.eps = eps; a.gscale = gscale;
-  a.done = done; a.ctr = ctr;
-  const unsigned blocks = (unsigned)(a.blk[nt] > 0 ? a.blk[nt] : 1);  // >= 1: the counters advance
-  hipLaunchKernelGGL(adam_multi_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, a);
+  if (a.blk[nt] > 0)
+    hipLaunchKernelGGL(adam_multi_kernel, dim3((unsigned)a.blk[nt]), dim3(256), 0, (hipStream_t)stream, a);
+  hipLaunchKernelGGL(step_counters_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream, step[0],
+                     ngroups > 1 ? step[1] : nullptr, ctr);
   HIPCHK(hipGetLastError());
   return MJL_OK;
 }

@@ -219,34 +219,6 @@ __global__ __launch_bounds__(64 * MJL_POL_WAVES) void policy_rollout_kernel(cons
 }
 #pragma clang fp contract(on)
 
-// Single-launch finish of a two-stage column sum: every block of the stage-1 grid arrives at a
-// device counter after writing its partial row; the last to arrive sums the partial rows
-// part[nbm][R][d] into fin[nbm][d] (rows in order, four interleaved partial sums per column) and
-// re-arms the counter. Deterministic: the order does not depend on which block is last.
-__device__ __forceinline__ void colsum_last_block(const float* part, int nbm, int R, int d, float* fin, int* done) {
-  __shared__ int last;
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    __threadfence();
-    last = atomicAdd(done, 1) == (int)(gridDim.x * gridDim.y) - 1;
-  }
-  __syncthreads();
-  if (!last) return;
-  __threadfence();
-  for (int c = threadIdx.x; c < nbm * d; c += blockDim.x) {
-    const int b = c / d, col = c - b * d;
-    const float* p = part + (size_t)b * R * d + col;
-    float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
-    int r = 0;
-    for (; r + 3 < R; r += 4) {
-      s0 += p[(size_t)r * d]; s1 += p[(size_t)(r + 1) * d]; s2 += p[(size_t)(r + 2) * d]; s3 += p[(size_t)(r + 3) * d];
-    }
-    for (; r < R; r++) s0 += p[(size_t)r * d];
-    fin[c] = (s0 + s1) + (s2 + s3);
-  }
-  if (threadIdx.x == 0) *done = 0;
-}
-
 // Column sums of a row-major [n, d] matrix (the PPO update's bias gradients dY.sum(0) over a
 // 65,536-row minibatch, and the split-K weight-gradient sum over its splits), in a fixed order.
 // A 256-thread block covers a tile of dc = min(d, tile) columns with G = 256 / dc row groups;
@@ -256,7 +228,7 @@ __device__ __forceinline__ void colsum_last_block(const float* part, int nbm, in
 // caller reduces those rows again when there is more than one). torch's sum(0) takes 33 us for
 // [65536, 256] and 169 us for [65536, 21] on MI355X (tools/colsum_probe.py).
 __global__ __launch_bounds__(256) void colsum_kernel(const float* __restrict__ x, int n, int d, int dc, int chunk,
-                                                     float* __restrict__ out, int nbm, int R, float* fin, int* done) {
+                                                     float* __restrict__ out) {
   __shared__ float red[256];
   const int G = 256 / dc, t = threadIdx.x, g = t / dc, c = t - g * dc;
   const int col = blockIdx.x * dc + c;
@@ -282,7 +254,6 @@ __global__ __launch_bounds__(256) void colsum_kernel(const float* __restrict__ x
     for (int q = 1; q < G; q++) acc += red[q * dc + t];
     out[(size_t)blockIdx.y * d + col] = acc;
   }
-  if (done) colsum_last_block(out, nbm, R, d, fin, done);  // (the single-launch form: out = partial rows)
 }
 
 // launch geometry shared by mjl_colsum and mjl_colsum_scratch: stage 1 over the rows in chunks of
@@ -308,8 +279,7 @@ struct ColsumPlan {
 // in group order (fixed order: deterministic).
 __global__ __launch_bounds__(256) void tanh_bwd_colsum_kernel(const float* __restrict__ g, const float* __restrict__ y,
                                                               int n, int d, int dq, int chunk, float* __restrict__ dz,
-                                                              float* __restrict__ out, int nbm, int R, float* fin,
-                                                              int* done) {
+                                                              float* __restrict__ out) {
   __shared__ float4 red[256];
   const int G = 256 / dq, t = threadIdx.x, grp = t / dq, q = t - grp * dq;
   const int col = (blockIdx.x * dq + q) * 4;
@@ -351,7 +321,6 @@ __global__ __launch_bounds__(256) void tanh_bwd_colsum_kernel(const float* __res
     }
     *reinterpret_cast<float4*>(out + (size_t)blockIdx.y * d + col) = acc;
   }
-  if (done) colsum_last_block(out, nbm, R, d, fin, done);
 }
 
 }  // namespace mjl

@@ -128,14 +128,14 @@ def lib() -> C.CDLL:
     L.mjl_tanh_inplace.argtypes = [f32p, C.c_longlong, vp]
     L.mjl_colsum_batched_scratch.argtypes = [i32, i32, i32]
     L.mjl_colsum_batched_scratch.restype = C.c_longlong
-    L.mjl_colsum_batched.argtypes = [f32p, i32, i32, i32, f32p, f32p, vp, vp]
-    L.mjl_tanh_bwd_colsum_batched.argtypes = [f32p, f32p, i32, i32, i32, f32p, f32p, f32p, vp, vp]
+    L.mjl_colsum_batched.argtypes = [f32p, i32, i32, i32, f32p, f32p, vp]
+    L.mjl_tanh_bwd_colsum_batched.argtypes = [f32p, f32p, i32, i32, i32, f32p, f32p, f32p, vp]
     L.mjl_slice_sum_batched.argtypes = [f32p, i32, i32, C.c_longlong, f32p, vp]
     L.mjl_twin_head_bwd.argtypes = [f32p, f32p, f32p, i32, f32p, i32, i32, f32p, vp]
     L.mjl_mse_strided.argtypes = [vp, i32, vp, i32, vp, vp, vp, vp]
     L.mjl_bias_act.argtypes = [vp, vp, i32, C.c_longlong, i32, C.c_uint, vp]
     L.mjl_adam_multi.argtypes = [i32, vp, vp, vp, vp, vp, vp, i32, vp, C.c_float, C.c_float, C.c_float, C.c_float,
-                                 vp, vp, vp, vp]
+                                 vp, vp, vp]
     L.mjl_ppo_surrogate_clipped.argtypes = [vp, vp, vp, vp, vp, vp, vp, i32, i32, C.c_float, C.c_float, C.c_float,
                                             C.c_float, vp, vp, vp, vp, vp]
     L.mjl_gather_rows_indexed.argtypes = [vp, vp, i32, C.c_longlong, i32, vp, vp, vp, vp]

@@ -390,7 +390,8 @@ class APGTrainer:
         g = g * torch.clamp(cfg.grad_clip / (gnorm + 1e-16), max=1.0).to(g.dtype)  # optax.clip_by_global_norm
         _set_grads(params, g)
         self.opt.step()
-        if cfg.normalize_observations and step % cfg.rms_update_every == 0:
+        frozen = getattr(cfg, "rms_freeze_after", None) is not None and step > cfg.rms_freeze_after
+        if cfg.normalize_observations and step % cfg.rms_update_every == 0 and not frozen:
             obs, in_loss = obs_traj
             flat = obs.reshape(-1, obs.shape[-1])
             keep = torch.isfinite(flat).all(1)

@@ -11,7 +11,7 @@ from __future__ import annotations
 import json
 import os
 from dataclasses import dataclass, field, fields
-from typing import List, Tuple
+from typing import List, Optional, Tuple
 
 _RIGHT_ACT = [3, 4, 5, 6, 7, 8, 15, 16, 17]
 _LEFT_ACT = [9, 10, 11, 12, 13, 14, 18, 19, 20]
@@ -92,6 +92,11 @@ class APGConfig(BaseConfig):
     # and, included, their variance swamps the statistics: when normalisation starts at update 100 every
     # policy input collapses to ~const and the return drops from ~-130 to ~-416 (DESIGN.md "APG C4").
     rms_in_loss_only: bool = False
+    # not in the reference (opt-in, train_apg.py --rms-freeze-after N): no observation-statistics updates
+    # after update N. At C4 the statistics' drift under a fixed policy is what undoes the learning after
+    # normalisation starts: frozen after update 100 the return rises -82 -> -56 over updates 100-300
+    # where the drifting statistics take it -101 -> -120 (same resets, DESIGN.md "APG at C4").
+    rms_freeze_after: Optional[int] = None
 
 
 @dataclass

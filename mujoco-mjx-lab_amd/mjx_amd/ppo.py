@@ -709,9 +709,9 @@ def adam_state_from_torch(d: dict, shapes: list):
 class NativeAdam:
     """torch.optim.Adam (betas, eps; no weight decay) for CUDA float32 parameters as one native
     launch per step (mjl_adam_multi: the fused update of every tensor), where torch's fused Adam took
-    ≈42 µs for the 151K-parameter policy. The step count lives on the device and the launch itself
-    advances it, so a hipGraph that captured step() takes each replay's own bias corrections (a host
-    int baked into the capture made replays drift from eager). adam_steps() takes
+    ≈42 µs for the 151K-parameter policy. The step count lives on the device and is advanced on the
+    device after the step, so a hipGraph that captured step() takes each replay's own bias corrections
+    (a host int baked into the capture made replays drift from eager). adam_steps() takes
     several optimisers' steps in one launch. state_dict / load_state_dict use torch.optim.Adam's
     layout (checkpoints interchange)."""
 
@@ -724,7 +724,6 @@ class NativeAdam:
         self.m = [torch.zeros_like(p) for p in self.params]
         self.v = [torch.zeros_like(p) for p in self.params]
         self.step_t = torch.zeros(1, dtype=torch.float32, device=self.params[0].device)
-        self.done = torch.zeros(1, dtype=torch.int32, device=self.params[0].device)  # the launch's completion count
 
     @property
     def t(self) -> int:
@@ -755,8 +754,9 @@ class NativeAdam:
 @torch.no_grad()
 def adam_steps(pairs, gscale: float = 1.0, ctr: Optional[torch.Tensor] = None):
     """One Adam step of each (NativeAdam, grads or None for the parameters' .grad) in ONE launch
-    (mjl_adam_multi, up to 2 optimisers with the same betas / eps), gradients scaled by gscale; `ctr`
-    (device int32, optional) is advanced by the launch with the step counters."""
+    (mjl_adam_multi, up to 2 optimisers with the same betas / eps; plus a one-thread launch advancing
+    the step counters), gradients scaled by gscale; `ctr` (device int32, optional) is advanced with
+    the step counters."""
     import ctypes
     from ._lib import check, lib
     o0 = pairs[0][0]
@@ -778,7 +778,7 @@ def adam_steps(pairs, gscale: float = 1.0, ctr: Optional[torch.Tensor] = None):
                                (ctypes.c_longlong * k)(*ns), (ctypes.c_int * k)(*grp), len(pairs),
                                (ctypes.c_float * len(pairs))(*[o.lr for o, _ in pairs]), o0.betas[0], o0.betas[1],
                                o0.eps, float(gscale), (ctypes.c_void_p * len(pairs))(*[o.step_t.data_ptr() for o, _ in pairs]),
-                               ctypes.c_void_p(o0.done.data_ptr()), None if ctr is None else ctypes.c_void_p(ctr.data_ptr()),
+                               None if ctr is None else ctypes.c_void_p(ctr.data_ptr()),
                                torch.cuda.current_stream(dev).cuda_stream))
     for opt, _ in pairs:
         opt._keep = gs  # the launch reads the gradients asynchronously

@@ -107,20 +107,12 @@ class TwinNets:
         self.grads_p: List[torch.Tensor] = [gview[id(p)] for p in policy.parameters()]
         self.grads_v: List[torch.Tensor] = [gview[id(p)] for p in value.parameters()]
         self._scr = {}
-        self._done = {}  # per stream: the single-launch column sums' completion counter (kept zero)
 
     def owns_storage(self) -> bool:
         """Whether the modules' parameters still are views of the stacked storage (a load_state_dict
         copies into them and keeps it; re-assigning .data would not)."""
         pm = self.policy.mlp
         return all(l.weight.data_ptr() == self.W[i][0].data_ptr() for i, l in enumerate(pm.layers))
-
-    def _counter(self) -> torch.Tensor:
-        st = torch.cuda.current_stream(self.grad.device).cuda_stream
-        t = self._done.get(st)
-        if t is None:
-            t = self._done[st] = torch.zeros(1, dtype=torch.int32, device=self.grad.device)
-        return t
 
     def _scratch(self, key, floats: int) -> torch.Tensor:
         st = torch.cuda.current_stream(self.grad.device).cuda_stream
@@ -173,8 +165,7 @@ class TwinNets:
                                   dz.data_ptr(), st))
         ncs = int(L.mjl_colsum_batched_scratch(2, M, max(A, self.W[0].shape[1])))
         cs = self._scratch("colsum", ncs)
-        done = self._counter().data_ptr()  # column sums in one launch each (the last block finishes)
-        check(L.mjl_colsum_batched(dz.data_ptr(), 2, M, A, cs.data_ptr(), self.gb[nl - 1].data_ptr(), done, st))
+        check(L.mjl_colsum_batched(dz.data_ptr(), 2, M, A, cs.data_ptr(), self.gb[nl - 1].data_ptr(), st))
         g = dz
         for l in range(nl - 1, -1, -1):
             N, K = self.W[l].shape[1], self.W[l].shape[2]
@@ -185,7 +176,7 @@ class TwinNets:
             if l < nl - 1:  # tanh layer: dZ = dH (1 - H^2) and the bias gradient in one pass
                 dzl = torch.empty_like(g)
                 check(L.mjl_tanh_bwd_colsum_batched(g.data_ptr(), hs[l + 1].data_ptr(), 2, M, N, dzl.data_ptr(),
-                                                    cs.data_ptr(), self.gb[l].data_ptr(), done, st))
+                                                    cs.data_ptr(), self.gb[l].data_ptr(), st))
             else:
                 dzl = g
             if l == 0:  # the shared observations: [2, M, K0] with batch stride 0 -> per split, both nets

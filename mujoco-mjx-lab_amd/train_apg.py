@@ -58,6 +58,9 @@ def main():
                          "(APGConfig.rms_in_loss_only; not the reference's rule, which takes every rollout "
                          "observation, train_apg.py:290-292 -- the default)")
     ap.add_argument("--rms-all-obs", action="store_true", help="the default (kept for old command lines)")
+    ap.add_argument("--rms-freeze-after", type=int, default=None,
+                    help="no observation-statistics updates after this update (APGConfig.rms_freeze_after; not "
+                         "the reference's rule, which updates them every 10 updates, train_apg.py:290-292)")
     a = ap.parse_args()
 
     cfg = APGConfig()
@@ -69,6 +72,7 @@ def main():
     if a.results_dir:
         cfg.results_dir = a.results_dir
     cfg.rms_in_loss_only = bool(a.rms_in_loss_only) and not a.rms_all_obs
+    cfg.rms_freeze_after = a.rms_freeze_after
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank, local = int(os.environ.get("RANK", "0")), int(os.environ.get("LOCAL_RANK", "0"))

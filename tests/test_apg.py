@@ -141,6 +141,19 @@ def test_obs_statistics_from_in_loss_observations(in_loss_only):
     assert (float(tr.rms.var.max()) < 1e3) == in_loss_only
 
 
+def test_obs_statistics_freeze_after():
+    """cfg.rms_freeze_after = N (opt-in): the observation statistics update every rms_update_every
+    updates up to update N and never after."""
+    cfg = _cfg(rms_update_every=1, rms_freeze_after=1)
+    tr = apg.APGTrainer(cfg, DiffPointEnv(cfg.batch_size, 3), device="cpu")
+    tr.policy.double()
+    counts = []
+    for step in range(4):
+        tr.update(step)
+        counts.append(float(tr.rms.count))
+    assert counts[1] > counts[0] and counts[2] == counts[1] and counts[3] == counts[1]
+
+
 def _port():
     s = socket.socket()
     s.bind(("127.0.0.1", 0))

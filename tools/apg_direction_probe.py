@@ -7,7 +7,11 @@ Per probed update it also logs the envs in the loss per step (first / last step 
 per-env action-cotangent energy sum_t |dL/da_t|^2 (quantiles: the per-env gradient's size
 through the policy) and the gradient norm before the clip. One JSON line per probed update.
 
-python tools/apg_direction_probe.py VJP UPDATES [--rms-in-loss-only] [--probe 0,25,...]"""
+python tools/apg_direction_probe.py VJP UPDATES [--rms-in-loss-only] [--probe 0,25,...] [--env-seed S]
+    [--freeze-rms-after N] [--all-updates]
+--all-updates: at EVERY update, the loss after the step on that update's own resets (one extra
+rollout per update) beside the loss before it: the same-batch improvement rate; --freeze-rms-after N:
+no observation-statistics updates after update N (is the decline the statistics' drift?)."""
 import argparse
 import json
 import os
@@ -32,17 +36,38 @@ def main():
     ap.add_argument("--probe", default="0,10,50,99,100,110,150,200,250,299")
     ap.add_argument("--envs", type=int, default=2048)
     ap.add_argument("--horizon", type=int, default=128)
+    ap.add_argument("--env-seed", type=int, default=None, help="env reset seed (default cfg.seed; train_apg.py "
+                    "uses cfg.seed * 7919)")
+    ap.add_argument("--freeze-rms-after", type=int, default=None)
+    ap.add_argument("--all-updates", action="store_true")
     a = ap.parse_args()
     probe = {int(x) for x in a.probe.split(",") if x}
     cfg = APGConfig()
     cfg.batch_size, cfg.horizon = a.envs, a.horizon
     cfg.rms_in_loss_only = bool(a.rms_in_loss_only)
     m = apg_model(cfg, solver="cg")
-    env = HumanoidEnv(mjx.put_model(m), resolve_ids(m, EnvConfig()), cfg.batch_size, seed=cfg.seed)
+    env = HumanoidEnv(mjx.put_model(m), resolve_ids(m, EnvConfig()), cfg.batch_size,
+                      seed=cfg.seed if a.env_seed is None else a.env_seed)
     aenv = HumanoidAPGEnv(env, a.vjp)
     tr = APGTrainer(cfg, aenv, device="cuda", use_graph=False)
     params = list(tr.policy.parameters())
     for it in range(a.updates):
+        if a.freeze_rms_after is not None and it > a.freeze_rms_after:
+            cfg.rms_update_every = 10 ** 9
+        if a.all_updates and it not in probe:  # the step's effect on its own batch
+            c0 = env.counter
+            rms0 = (tr.rms.mean.clone(), tr.rms.var.clone(), tr.rms.count.clone())
+            met = tr.update(it)
+            rms1 = (tr.rms.mean, tr.rms.var, tr.rms.count)
+            use_norm = it >= cfg.obs_warmup_steps and cfg.normalize_observations
+            tr.rms.mean, tr.rms.var, tr.rms.count = rms0
+            env.counter = c0
+            with torch.no_grad(), torch.enable_grad():
+                after = float(tr.loss_and_grad(use_norm)[0])
+            tr.rms.mean, tr.rms.var, tr.rms.count = rms1
+            print(json.dumps({"update": it, "return": met["return"], "loss_before": met["loss"], "loss_after": after,
+                              "improved": after < met["loss"]}), flush=True)
+            continue
         if it not in probe:
             tr.update(it)
             continue
