@@ -402,10 +402,17 @@ int mjl_tanh_inplace(float* x, long long n, void* stream);
  * multiple of the 128-row chunk (n > 256). scratch: mjl_colsum_batched_scratch(nb, n, d) floats.
  * mjl_slice_sum_batched: out[b][e] = sum over s < ns of x[(b * ns + s) * m + e]. */
 long long mjl_colsum_batched_scratch(int nb, int n, int d);
+/* (out / colsum_out NULL: the first stage only, its chunk partials [nb][R = n / 128][d] left in scratch
+ * for mjl_slice_sum_multi; n a multiple of 128 above 256.) */
 int mjl_colsum_batched(const float* x, int nb, int n, int d, float* scratch, float* out, void* stream);
 int mjl_tanh_bwd_colsum_batched(const float* g, const float* y, int nb, int n, int d, float* dz, float* scratch,
                                 float* colsum_out, void* stream);
 int mjl_slice_sum_batched(const float* x, int nb, int ns, long long m, float* out, void* stream);
+/* nseg <= 16 slice sums in one launch: out_k[b][e] = sum over s < ns[k] (in order) of
+ * x_k[(b * ns[k] + s) * m[k] + e], b < nb[k] (the twin update's weight-gradient slices and column-sum
+ * partials of every layer, reduced together at the end of its backward). */
+int mjl_slice_sum_multi(int nseg, const float* const* x, float* const* out, const int* nb, const int* ns,
+                        const long long* m, void* stream);
 /* The twin update's output-layer backward: mean [M, A] = tanh of the policy's last Dense (networks.py:
  * 103), g_mean [M, A] = d loss / d mean (mjl_ppo_surrogate), v[r] = v[r * vstride] the value net's
  * output and ret [M] its targets (train_ppo.py:218-220, value loss mean (v - ret)^2);

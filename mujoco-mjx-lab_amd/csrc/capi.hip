@@ -1006,6 +1006,14 @@ extern "C" long long mjl_colsum_batched_scratch(int nb, int n, int d) {
 }
 
 extern "C" int mjl_colsum_batched(const float* x, int nb, int n, int d, float* scratch, float* out, void* stream) {
+  if (!out) {  // stage 1 only: the chunk partials [nb][R][d] stay in scratch (mjl_slice_sum_multi sums them)
+    const ColsumPlan p(n > 0 ? n : 1, d);
+    if (!x || !scratch || nb <= 0 || n <= 256 || d <= 0 || n % p.chunk) return fail(MJL_ERR_ARG, "bad argument");
+    hipLaunchKernelGGL(colsum_kernel, dim3((unsigned)((d + p.dc1 - 1) / p.dc1), (unsigned)(p.R * nb)), dim3(256), 0,
+                       (hipStream_t)stream, x, n * nb, d, p.dc1, p.chunk, scratch);
+    HIPCHK(hipGetLastError());
+    return MJL_OK;
+  }
   if ((!x && n > 0) || !out || nb <= 0 || n < 0 || d <= 0) return fail(MJL_ERR_ARG, "bad argument");
   hipStream_t s = (hipStream_t)stream;
   if (n == 0) {
@@ -1034,7 +1042,17 @@ extern "C" int mjl_colsum(const float* x, int n, int d, float* scratch, float* o
 
 extern "C" int mjl_tanh_bwd_colsum_batched(const float* g, const float* y, int nb, int n, int d, float* dz,
                                            float* scratch, float* colsum_out, void* stream) {
-  if (!g || !y || !dz || !colsum_out || nb <= 0 || n <= 0 || d <= 0) return fail(MJL_ERR_ARG, "bad argument");
+  if (!g || !y || !dz || nb <= 0 || n <= 0 || d <= 0) return fail(MJL_ERR_ARG, "bad argument");
+  if (!colsum_out) {  // stage 1 only: the chunk partials [nb][R][d] stay in scratch
+    const ColsumPlan p(n, d);
+    if (d % 4 || n <= 256 || n % p.chunk || !scratch || ((uintptr_t)g | (uintptr_t)y | (uintptr_t)dz | (uintptr_t)scratch) % 16)
+      return fail(MJL_ERR_ARG, "tanh_bwd_colsum (stage 1): d % 4 == 0, n a multiple of %d above 256, aligned", p.chunk);
+    const int dq = d / 4 < 64 ? d / 4 : 64;
+    hipLaunchKernelGGL(tanh_bwd_colsum_kernel, dim3((unsigned)((d / 4 + dq - 1) / dq), (unsigned)(p.R * nb)), dim3(256),
+                       0, (hipStream_t)stream, g, y, n * nb, d, dq, p.chunk, dz, scratch);
+    HIPCHK(hipGetLastError());
+    return MJL_OK;
+  }
   if (d % 4 || ((uintptr_t)g | (uintptr_t)y | (uintptr_t)dz | (uintptr_t)colsum_out) % 16)
     return fail(MJL_ERR_ARG, "tanh_bwd_colsum: d divisible by 4 and 16-byte aligned rows expected");
   hipStream_t s = (hipStream_t)stream;
@@ -1068,6 +1086,26 @@ extern "C" int mjl_slice_sum_batched(const float* x, int nb, int ns, long long m
   const long long q = m / 4;
   hipLaunchKernelGGL(slice_sum_kernel, dim3((unsigned)((q + 255) / 256), (unsigned)nb), dim3(256), 0,
                      (hipStream_t)stream, x, ns, m, out);
+  HIPCHK(hipGetLastError());
+  return MJL_OK;
+}
+
+extern "C" int mjl_slice_sum_multi(int nseg, const float* const* x, float* const* out, const int* nb, const int* ns,
+                                   const long long* m, void* stream) {
+  if (nseg < 1 || nseg > kSliceSegMax || !x || !out || !nb || !ns || !m) return fail(MJL_ERR_ARG, "bad argument");
+  SliceSegs sg;
+  std::memset(&sg, 0, sizeof(sg));
+  sg.nseg = nseg;
+  for (int k = 0; k < nseg; k++) {
+    if (!x[k] || !out[k] || nb[k] <= 0 || ns[k] <= 0 || m[k] <= 0) return fail(MJL_ERR_ARG, "bad argument");
+    sg.x[k] = x[k]; sg.out[k] = out[k]; sg.m[k] = m[k]; sg.ns[k] = ns[k]; sg.nb[k] = nb[k];
+    sg.vec[k] = (m[k] % 4 == 0 && ((uintptr_t)x[k] | (uintptr_t)out[k]) % 16 == 0) ? 1 : 0;
+    const long long units = sg.vec[k] ? m[k] / 4 : m[k];
+    const long long blocks = (long long)nb[k] * ((units + 255) / 256);
+    if (sg.blk[k] + blocks >= (1LL << 30)) return fail(MJL_ERR_ARG, "slice_sum_multi: too many elements");
+    sg.blk[k + 1] = sg.blk[k] + (int)blocks;
+  }
+  hipLaunchKernelGGL(slice_sum_multi_kernel, dim3((unsigned)sg.blk[nseg]), dim3(256), 0, (hipStream_t)stream, sg);
   HIPCHK(hipGetLastError());
   return MJL_OK;
 }

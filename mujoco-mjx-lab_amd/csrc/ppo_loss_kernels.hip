@@ -231,6 +231,49 @@ __global__ __launch_bounds__(256) void slice_sum_kernel(const float* __restrict_
   reinterpret_cast<float4*>(out)[q] = acc;
 }
 
+// Several slice sums in one launch (the twin update's backward: every layer's split-K weight-gradient
+// slices and every column sum's chunk partials, reduced together once the backward has produced them
+// all): segment k sums x_k[b][s][e] over s < ns_k in order into out_k[b][e] for b < nb_k, e < m_k.
+// A block covers 256 float4 groups (vec) or 256 floats of one (segment, b) row, found from the block
+// index (uniform: the segment table is read with scalar loads).
+constexpr int kSliceSegMax = 16;
+struct SliceSegs {
+  const float* x[kSliceSegMax];
+  float* out[kSliceSegMax];
+  long long m[kSliceSegMax];
+  int ns[kSliceSegMax], nb[kSliceSegMax], vec[kSliceSegMax];
+  int blk[kSliceSegMax + 1];  // first block of each segment (nb rows x blocks per row)
+  int nseg;
+};
+__global__ __launch_bounds__(256) void slice_sum_multi_kernel(SliceSegs sg) {
+  const int blk = blockIdx.x;
+  int k = 0;
+  while (k + 1 < sg.nseg && blk >= sg.blk[k + 1]) k++;
+  const long long m = sg.m[k];
+  const int ns = sg.ns[k], vec = sg.vec[k];
+  const long long units = vec ? m / 4 : m;
+  const int per_row = (int)((units + 255) / 256);
+  const int rb = blk - sg.blk[k], b = rb / per_row;
+  const long long q = (long long)(rb - b * per_row) * 256 + threadIdx.x;
+  if (q >= units) return;
+  const float* x = sg.x[k] + (size_t)b * ns * m;
+  float* out = sg.out[k] + (size_t)b * m;
+  if (vec) {
+    const float4* src = reinterpret_cast<const float4*>(x) + q;
+    const long long stride = m / 4;
+    float4 acc = src[0];
+    for (int s = 1; s < ns; s++) {
+      const float4 a = src[s * stride];
+      acc.x += a.x; acc.y += a.y; acc.z += a.z; acc.w += a.w;
+    }
+    reinterpret_cast<float4*>(out)[q] = acc;
+  } else {
+    float acc = x[q];
+    for (int s = 1; s < ns; s++) acc += x[s * m + q];
+    out[q] = acc;
+  }
+}
+
 // The twin update's output-layer backward (twin.py): the policy's mean = tanh(z) sits in out[0]
 // ([M, A]), the value in column 0 of out[1] (v[r] = v[r * vstride]); g_mean = d loss / d mean
 // (mjl_ppo_surrogate). dz[0] = g_mean (1 - mean^2); dz[1][:, 0] = d mean((v - ret)^2) / d v =

@@ -32,7 +32,7 @@ EXPORTS = [
     "mjl_adam_dev", "mjl_mlp_fwd", "mjl_mlp_colpart_rows", "mjl_mlp_bwd",
     "mjl_colsum_batched_scratch", "mjl_colsum_batched", "mjl_tanh_bwd_colsum_batched", "mjl_slice_sum_batched",
     "mjl_twin_head_bwd", "mjl_mse_strided", "mjl_ppo_surrogate_clipped", "mjl_bias_act", "mjl_adam_multi",
-    "mjl_gather_rows_indexed",
+    "mjl_gather_rows_indexed", "mjl_slice_sum_multi",
 ]
 
 _lib = None
@@ -139,6 +139,7 @@ def lib() -> C.CDLL:
     L.mjl_ppo_surrogate_clipped.argtypes = [vp, vp, vp, vp, vp, vp, vp, i32, i32, C.c_float, C.c_float, C.c_float,
                                             C.c_float, vp, vp, vp, vp, vp]
     L.mjl_gather_rows_indexed.argtypes = [vp, vp, i32, C.c_longlong, i32, vp, vp, vp, vp]
+    L.mjl_slice_sum_multi.argtypes = [i32, vp, vp, vp, vp, vp, vp]
     L.mjl_small_mlp_fwd.argtypes = [vp, i32, i32, i32, vp, vp, vp, vp, vp]
     L.mjl_small_mlp_bwd_input.argtypes = [vp, i32, i32, i32, vp, vp, vp, vp, vp]
     L.mjl_step_vjp.argtypes = [vp, f32p, f32p, f32p, f32p, f32p, vp]

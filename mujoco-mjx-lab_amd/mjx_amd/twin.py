@@ -17,12 +17,13 @@ which is also the data-parallel all-reduce buffer (no concatenation).
 
 Forward: H_l = tanh(H_{l-1} W_lᵀ + b_l) as a bias-less torch.bmm + one native bias-and-tanh pass
 (mjl_bias_act; baddbmm would first copy the broadcast bias into its output); Z = H W_outᵀ + b_out;
-mean = tanh(Z[0]); v = Z[1][:, 0]. Losses: mjl_ppo_surrogate_clipped (log_std clipped in the kernel),
-mjl_mse_strided on v. Backward, by hand in the order autograd takes: mjl_twin_head_bwd forms
-dZ; each layer's weight gradient is the split-K batched GEMM dZᵀ X over both nets (2 x splits
-slices, summed in order by mjl_slice_sum_batched), its bias gradient the fixed-order column sums
-(mjl_colsum_batched / mjl_tanh_bwd_colsum_batched, which also forms dZ_l = dH (1 - H²)), dH =
-dZ W as one batched GEMM. Same formulas as the per-net path (ppo.py _SplitKLinear /
+mean = tanh(Z[0]); v = Z[1][:, 0]. Losses: mjl_ppo_surrogate_clipped (log_std clipped in the kernel);
+the value's gradient 2 (v - ret) / M inside the head backward. Backward, by hand in the order
+autograd takes: mjl_twin_head_bwd forms dZ; each layer's weight gradient is the split-K batched GEMM
+dZᵀ X over both nets (2 x splits slices), its bias gradient the fixed-order column sums' first stage
+(mjl_colsum_batched / mjl_tanh_bwd_colsum_batched, which also forms dZ_l = dH (1 - H²)), dH = dZ W
+as one batched GEMM; the second stages — every layer's slices and chunk partials, summed in order —
+run together in one launch at the end (mjl_slice_sum_multi). Same formulas as the per-net path (ppo.py _SplitKLinear /
 _TanhSplitKLinear + the native losses); the GEMMs are the library's batched kernels instead of its
 single ones, so results agree to rounding, not bit for bit (tests/test_twin.py)."""
 from __future__ import annotations
@@ -163,9 +164,13 @@ class TwinNets:
         dz = torch.empty((2, M, A), device=dev)
         check(L.mjl_twin_head_bwd(gm.data_ptr(), mean.data_ptr(), z[1].data_ptr(), A, ret.data_ptr(), M, A,
                                   dz.data_ptr(), st))
-        ncs = int(L.mjl_colsum_batched_scratch(2, M, max(A, self.W[0].shape[1])))
-        cs = self._scratch("colsum", ncs)
-        check(L.mjl_colsum_batched(dz.data_ptr(), 2, M, A, cs.data_ptr(), self.gb[nl - 1].data_ptr(), st))
+        # every reduction's first stage here; their second stages (column-sum chunk partials, split-K
+        # weight-gradient slices) all in ONE launch after the last layer (mjl_slice_sum_multi)
+        segs = []  # (x, out, nb, ns, m)
+        R = M // 128  # column-sum chunk rows per matrix (ColsumPlan)
+        cs = self._scratch(f"cs{nl - 1}", int(L.mjl_colsum_batched_scratch(2, M, A)))
+        check(L.mjl_colsum_batched(dz.data_ptr(), 2, M, A, cs.data_ptr(), None, st))
+        segs.append((cs, self.gb[nl - 1], 2, R, A))
         g = dz
         for l in range(nl - 1, -1, -1):
             N, K = self.W[l].shape[1], self.W[l].shape[2]
@@ -173,10 +178,12 @@ class TwinNets:
             # split-K slices of the weight gradient: the thin layers (the 21 / 1-unit outputs, the 54-wide
             # input) are a few output tiles per slice, so they take more, shorter slices
             s = splits if (N >= 64 and K >= 64) else max(splits, min(64, M // 256))
-            if l < nl - 1:  # tanh layer: dZ = dH (1 - H^2) and the bias gradient in one pass
+            if l < nl - 1:  # tanh layer: dZ = dH (1 - H^2) and the bias gradient's partials in one pass
                 dzl = torch.empty_like(g)
+                cs = self._scratch(f"cs{l}", int(L.mjl_colsum_batched_scratch(2, M, N)))
                 check(L.mjl_tanh_bwd_colsum_batched(g.data_ptr(), hs[l + 1].data_ptr(), 2, M, N, dzl.data_ptr(),
-                                                    cs.data_ptr(), self.gb[l].data_ptr(), st))
+                                                    cs.data_ptr(), None, st))
+                segs.append((cs, self.gb[l], 2, R, N))
             else:
                 dzl = g
             if l == 0:  # the shared observations: [2, M, K0] with batch stride 0 -> per split, both nets
@@ -184,9 +191,17 @@ class TwinNets:
             else:
                 xs = xin.view(2 * s, M // s, K)
             part = torch.bmm(dzl.view(2 * s, M // s, N).transpose(1, 2), xs)  # [2s, N, K]
-            check(L.mjl_slice_sum_batched(part.data_ptr(), 2, s, N * K, self.gW[l].data_ptr(), st))
+            segs.append((part, self.gW[l], 2, s, N * K))
             if l > 0:
                 g = torch.bmm(dzl, self.W[l])  # [2, M, K]
+        import ctypes
+        k = len(segs)
+        check(L.mjl_slice_sum_multi(k, (ctypes.c_void_p * k)(*[x.data_ptr() for x, *_ in segs]),
+                                    (ctypes.c_void_p * k)(*[o.data_ptr() for _, o, *_ in segs]),
+                                    (ctypes.c_int * k)(*[nb for _, _, nb, _, _ in segs]),
+                                    (ctypes.c_int * k)(*[ns for _, _, _, ns, _ in segs]),
+                                    (ctypes.c_longlong * k)(*[m for *_, m in segs]), st))
+        self._keep = segs  # the launch reads the partial buffers asynchronously
         return loss_p, loss_v
 
 
