@@ -1100,8 +1100,12 @@ extern "C" int mjl_slice_sum_multi(int nseg, const float* const* x, float* const
     if (!x[k] || !out[k] || nb[k] <= 0 || ns[k] <= 0 || m[k] <= 0) return fail(MJL_ERR_ARG, "bad argument");
     sg.x[k] = x[k]; sg.out[k] = out[k]; sg.m[k] = m[k]; sg.ns[k] = ns[k]; sg.nb[k] = nb[k];
     sg.vec[k] = (m[k] % 4 == 0 && ((uintptr_t)x[k] | (uintptr_t)out[k]) % 16 == 0) ? 1 : 0;
+    int lanes = 1;  // lanes per output: about 8 slices each, at most a wave
+    while (lanes < 64 && ns[k] >= 16 * lanes) lanes *= 2;
+    sg.lanes[k] = lanes;
     const long long units = sg.vec[k] ? m[k] / 4 : m[k];
-    const long long blocks = (long long)nb[k] * ((units + 255) / 256);
+    const long long outs = 256 / lanes;
+    const long long blocks = (long long)nb[k] * ((units + outs - 1) / outs);
     if (sg.blk[k] + blocks >= (1LL << 30)) return fail(MJL_ERR_ARG, "slice_sum_multi: too many elements");
     sg.blk[k + 1] = sg.blk[k] + (int)blocks;
   }

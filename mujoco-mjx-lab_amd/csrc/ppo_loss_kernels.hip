@@ -233,44 +233,55 @@ __global__ __launch_bounds__(256) void slice_sum_kernel(const float* __restrict_
 
 // Several slice sums in one launch (the twin update's backward: every layer's split-K weight-gradient
 // slices and every column sum's chunk partials, reduced together once the backward has produced them
-// all): segment k sums x_k[b][s][e] over s < ns_k in order into out_k[b][e] for b < nb_k, e < m_k.
-// A block covers 256 float4 groups (vec) or 256 floats of one (segment, b) row, found from the block
-// index (uniform: the segment table is read with scalar loads).
+// all): segment k sums x_k[b][s][e] over s < ns_k into out_k[b][e] for b < nb_k, e < m_k. A long sum
+// (the column sums' 64-512 chunk rows) is split over S_k adjacent lanes, lane j taking the slices
+// [j c, (j + 1) c) in order, the S_k partials then combined by a fixed xor butterfly (deterministic).
+// A block covers 256 / S_k outputs (float4 groups when vec) of one (segment, b) row, found from the
+// block index (uniform: the segment table is read with scalar loads).
 constexpr int kSliceSegMax = 16;
 struct SliceSegs {
   const float* x[kSliceSegMax];
   float* out[kSliceSegMax];
   long long m[kSliceSegMax];
-  int ns[kSliceSegMax], nb[kSliceSegMax], vec[kSliceSegMax];
+  int ns[kSliceSegMax], nb[kSliceSegMax], vec[kSliceSegMax], lanes[kSliceSegMax];
   int blk[kSliceSegMax + 1];  // first block of each segment (nb rows x blocks per row)
   int nseg;
 };
+__device__ __forceinline__ float4 f4add(float4 a, float4 b) {
+  return make_float4(a.x + b.x, a.y + b.y, a.z + b.z, a.w + b.w);
+}
 __global__ __launch_bounds__(256) void slice_sum_multi_kernel(SliceSegs sg) {
   const int blk = blockIdx.x;
   int k = 0;
   while (k + 1 < sg.nseg && blk >= sg.blk[k + 1]) k++;
   const long long m = sg.m[k];
-  const int ns = sg.ns[k], vec = sg.vec[k];
+  const int ns = sg.ns[k], vec = sg.vec[k], S = sg.lanes[k];
   const long long units = vec ? m / 4 : m;
-  const int per_row = (int)((units + 255) / 256);
+  const int outs = 256 / S;  // outputs per block
+  const int per_row = (int)((units + outs - 1) / outs);
   const int rb = blk - sg.blk[k], b = rb / per_row;
-  const long long q = (long long)(rb - b * per_row) * 256 + threadIdx.x;
-  if (q >= units) return;
+  const int t = threadIdx.x, o = t / S, j = t - o * S;
+  const long long q = (long long)(rb - b * per_row) * outs + o;
+  const bool ok = q < units;
+  const int c = (ns + S - 1) / S, s0 = j * c, s1 = min(ns, s0 + c);
   const float* x = sg.x[k] + (size_t)b * ns * m;
   float* out = sg.out[k] + (size_t)b * m;
   if (vec) {
-    const float4* src = reinterpret_cast<const float4*>(x) + q;
+    const float4* src = reinterpret_cast<const float4*>(x) + (ok ? q : 0);
     const long long stride = m / 4;
-    float4 acc = src[0];
-    for (int s = 1; s < ns; s++) {
-      const float4 a = src[s * stride];
-      acc.x += a.x; acc.y += a.y; acc.z += a.z; acc.w += a.w;
-    }
-    reinterpret_cast<float4*>(out)[q] = acc;
+    float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (ok)
+      for (int s = s0; s < s1; s++) acc = f4add(acc, src[s * stride]);
+    for (int off = S / 2; off > 0; off >>= 1)
+      acc = f4add(acc, make_float4(__shfl_xor(acc.x, off), __shfl_xor(acc.y, off), __shfl_xor(acc.z, off),
+                                   __shfl_xor(acc.w, off)));
+    if (ok && j == 0) reinterpret_cast<float4*>(out)[q] = acc;
   } else {
-    float acc = x[q];
-    for (int s = 1; s < ns; s++) acc += x[s * m + q];
-    out[q] = acc;
+    float acc = 0.f;
+    if (ok)
+      for (int s = s0; s < s1; s++) acc += x[s * m + q];
+    for (int off = S / 2; off > 0; off >>= 1) acc += __shfl_xor(acc, off);
+    if (ok && j == 0) out[q] = acc;
   }
 }
 
