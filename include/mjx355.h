@@ -402,8 +402,12 @@ int mjl_tanh_inplace(float* x, long long n, void* stream);
  * multiple of the 128-row chunk (n > 256). scratch: mjl_colsum_batched_scratch(nb, n, d) floats.
  * mjl_slice_sum_batched: out[b][e] = sum over s < ns of x[(b * ns + s) * m + e]. */
 long long mjl_colsum_batched_scratch(int nb, int n, int d);
-/* (out / colsum_out NULL: the first stage only, its chunk partials [nb][R = n / 128][d] left in scratch
- * for mjl_slice_sum_multi; n a multiple of 128 above 256.) */
+/* The first stages alone, with the caller's row chunk: partials [nb][n / chunk][d] = each chunk's
+ * column sums (of x, or of dz = g (1 - y^2), which is also written out), for mjl_slice_sum_multi to
+ * finish. n % chunk == 0; the tanh form needs d % 4 == 0 and 16-byte aligned buffers. */
+int mjl_colsum_partials(const float* x, int nb, int n, int d, int chunk, float* partials, void* stream);
+int mjl_tanh_bwd_colsum_partials(const float* g, const float* y, int nb, int n, int d, int chunk, float* dz,
+                                 float* partials, void* stream);
 int mjl_colsum_batched(const float* x, int nb, int n, int d, float* scratch, float* out, void* stream);
 int mjl_tanh_bwd_colsum_batched(const float* g, const float* y, int nb, int n, int d, float* dz, float* scratch,
                                 float* colsum_out, void* stream);
@@ -493,6 +497,19 @@ int mjl_mlp_fwd(const float* x, int ldx, const float* w, const float* b, int M, 
 long long mjl_mlp_colpart_rows(int M);
 int mjl_mlp_bwd(const float* g, const float* y, int M, int N, const float* w, int K, int act, float* dz, float* dx,
                 float* colpart, void* stream);
+/* The twin PPO update's stacked dense layers (mjx_amd/twin.py; train_ppo.py:204-252 through both
+ * src/networks.py MLPs at once): nb problems per launch.
+ * mjl_twin_dense_fwd: y[z] = act_z(x[z] w[z]^T + b[z]), x at z * x_bstride (0: shared observations)
+ *   [M, K], w [nb, N, K], b [nb, N], y [nb, M, N]; act_z = tanh when bit z of act_mask is set.
+ * mjl_twin_dense_dx_tanh: dz[z] = (g[z] w[z]) (1 - y[z]^2): g [nb, M, N] (this layer's dZ), w [nb, N, K],
+ *   y [nb, M, K] (the tanh output feeding the layer), dz [nb, M, K] (the lower layer's dZ); partials
+ *   [nb][mjl_twin_dense_partial_rows(M)][K] = its column sums per 128-row block (fixed order).
+ *   K % 4 == 0, 16-byte aligned w / y / dz. */
+int mjl_twin_dense_fwd(const float* x, long long x_bstride, const float* w, const float* b, int nb, int M, int N,
+                       int K, unsigned act_mask, float* y, void* stream);
+long long mjl_twin_dense_partial_rows(int M);
+int mjl_twin_dense_dx_tanh(const float* g, const float* w, const float* y, int nb, int M, int N, int K, float* dz,
+                           float* partials, void* stream);
 
 #ifdef __cplusplus
 }

@@ -1005,15 +1005,32 @@ extern "C" long long mjl_colsum_batched_scratch(int nb, int n, int d) {
   return p.R > 1 ? (long long)nb * p.R * d : 0;
 }
 
+// first stages only, with the caller's chunk: partials [nb][n / chunk][d] (the twin update reduces
+// every layer's partials together afterwards, mjl_slice_sum_multi; 32-row chunks give its 8,192-row
+// minibatch 512 blocks per pass where the two-stage plan's 128-row chunks gave 128 for 256 CUs)
+extern "C" int mjl_colsum_partials(const float* x, int nb, int n, int d, int chunk, float* partials, void* stream) {
+  if (!x || !partials || nb <= 0 || n <= 0 || d <= 0 || chunk <= 0 || n % chunk) return fail(MJL_ERR_ARG, "bad argument");
+  const int dc = d < 256 ? d : 256;
+  hipLaunchKernelGGL(colsum_kernel, dim3((unsigned)((d + dc - 1) / dc), (unsigned)(n / chunk * nb)), dim3(256), 0,
+                     (hipStream_t)stream, x, n * nb, d, dc, chunk, partials);
+  HIPCHK(hipGetLastError());
+  return MJL_OK;
+}
+
+extern "C" int mjl_tanh_bwd_colsum_partials(const float* g, const float* y, int nb, int n, int d, int chunk, float* dz,
+                                            float* partials, void* stream) {
+  if (!g || !y || !dz || !partials || nb <= 0 || n <= 0 || d <= 0 || chunk <= 0 || n % chunk)
+    return fail(MJL_ERR_ARG, "bad argument");
+  if (d % 4 || ((uintptr_t)g | (uintptr_t)y | (uintptr_t)dz | (uintptr_t)partials) % 16)
+    return fail(MJL_ERR_ARG, "tanh_bwd_colsum_partials: d divisible by 4 and 16-byte aligned rows expected");
+  const int dq = d / 4 < 64 ? d / 4 : 64;
+  hipLaunchKernelGGL(tanh_bwd_colsum_kernel, dim3((unsigned)((d / 4 + dq - 1) / dq), (unsigned)(n / chunk * nb)),
+                     dim3(256), 0, (hipStream_t)stream, g, y, n * nb, d, dq, chunk, dz, partials);
+  HIPCHK(hipGetLastError());
+  return MJL_OK;
+}
+
 extern "C" int mjl_colsum_batched(const float* x, int nb, int n, int d, float* scratch, float* out, void* stream) {
-  if (!out) {  // stage 1 only: the chunk partials [nb][R][d] stay in scratch (mjl_slice_sum_multi sums them)
-    const ColsumPlan p(n > 0 ? n : 1, d);
-    if (!x || !scratch || nb <= 0 || n <= 256 || d <= 0 || n % p.chunk) return fail(MJL_ERR_ARG, "bad argument");
-    hipLaunchKernelGGL(colsum_kernel, dim3((unsigned)((d + p.dc1 - 1) / p.dc1), (unsigned)(p.R * nb)), dim3(256), 0,
-                       (hipStream_t)stream, x, n * nb, d, p.dc1, p.chunk, scratch);
-    HIPCHK(hipGetLastError());
-    return MJL_OK;
-  }
   if ((!x && n > 0) || !out || nb <= 0 || n < 0 || d <= 0) return fail(MJL_ERR_ARG, "bad argument");
   hipStream_t s = (hipStream_t)stream;
   if (n == 0) {
@@ -1042,17 +1059,7 @@ extern "C" int mjl_colsum(const float* x, int n, int d, float* scratch, float* o
 
 extern "C" int mjl_tanh_bwd_colsum_batched(const float* g, const float* y, int nb, int n, int d, float* dz,
                                            float* scratch, float* colsum_out, void* stream) {
-  if (!g || !y || !dz || nb <= 0 || n <= 0 || d <= 0) return fail(MJL_ERR_ARG, "bad argument");
-  if (!colsum_out) {  // stage 1 only: the chunk partials [nb][R][d] stay in scratch
-    const ColsumPlan p(n, d);
-    if (d % 4 || n <= 256 || n % p.chunk || !scratch || ((uintptr_t)g | (uintptr_t)y | (uintptr_t)dz | (uintptr_t)scratch) % 16)
-      return fail(MJL_ERR_ARG, "tanh_bwd_colsum (stage 1): d % 4 == 0, n a multiple of %d above 256, aligned", p.chunk);
-    const int dq = d / 4 < 64 ? d / 4 : 64;
-    hipLaunchKernelGGL(tanh_bwd_colsum_kernel, dim3((unsigned)((d / 4 + dq - 1) / dq), (unsigned)(p.R * nb)), dim3(256),
-                       0, (hipStream_t)stream, g, y, n * nb, d, dq, p.chunk, dz, scratch);
-    HIPCHK(hipGetLastError());
-    return MJL_OK;
-  }
+  if (!g || !y || !dz || !colsum_out || nb <= 0 || n <= 0 || d <= 0) return fail(MJL_ERR_ARG, "bad argument");
   if (d % 4 || ((uintptr_t)g | (uintptr_t)y | (uintptr_t)dz | (uintptr_t)colsum_out) % 16)
     return fail(MJL_ERR_ARG, "tanh_bwd_colsum: d divisible by 4 and 16-byte aligned rows expected");
   hipStream_t s = (hipStream_t)stream;
@@ -1431,14 +1438,103 @@ extern "C" int mjl_mlp_fwd(const float* x, int ldx, const float* w, const float*
   if (M == 0) return MJL_OK;
   hipStream_t s = (hipStream_t)stream;
   const bool vec = K % 4 == 0 && ldx % 4 == 0 && aligned16(x) && aligned16(w);
+  const unsigned am = act == MLP_ACT_TANH ? 1u : 0u;
   if (N <= 32) {  // the heads (21 actions, 1 value): 256 x 32 tiles, 4 waves of 64 x 32
     dim3 grid(1, (M + 255) / 256);
-    if (vec) hipLaunchKernelGGL((mlp_fwd_kernel<256, 32, 4, 1, true>), grid, dim3(256), 0, s, x, ldx, w, K, b, y, N, M, N, K, act);
-    else hipLaunchKernelGGL((mlp_fwd_kernel<256, 32, 4, 1, false>), grid, dim3(256), 0, s, x, ldx, w, K, b, y, N, M, N, K, act);
+    if (vec) hipLaunchKernelGGL((mlp_fwd_kernel<256, 32, 4, 1, true>), grid, dim3(256), 0, s, x, ldx, 0LL, w, K, 0LL, b, 0, y, N, 0LL, M, N, K, am);
+    else hipLaunchKernelGGL((mlp_fwd_kernel<256, 32, 4, 1, false>), grid, dim3(256), 0, s, x, ldx, 0LL, w, K, 0LL, b, 0, y, N, 0LL, M, N, K, am);
   } else {  // 128 x 128 tiles, 4 waves of 64 x 64; a row block's column tiles are neighbours in launch order
     dim3 grid((N + 127) / 128, (M + 127) / 128);
-    if (vec) hipLaunchKernelGGL((mlp_fwd_kernel<128, 128, 2, 2, true>), grid, dim3(256), 0, s, x, ldx, w, K, b, y, N, M, N, K, act);
-    else hipLaunchKernelGGL((mlp_fwd_kernel<128, 128, 2, 2, false>), grid, dim3(256), 0, s, x, ldx, w, K, b, y, N, M, N, K, act);
+    if (vec) hipLaunchKernelGGL((mlp_fwd_kernel<128, 128, 2, 2, true>), grid, dim3(256), 0, s, x, ldx, 0LL, w, K, 0LL, b, 0, y, N, 0LL, M, N, K, am);
+    else hipLaunchKernelGGL((mlp_fwd_kernel<128, 128, 2, 2, false>), grid, dim3(256), 0, s, x, ldx, 0LL, w, K, 0LL, b, 0, y, N, 0LL, M, N, K, am);
+  }
+  HIPCHK(hipGetLastError());
+  return MJL_OK;
+}
+
+// ---- the twin update's stacked dense layers (mjx_amd/twin.py): nb problems per launch (blockIdx.z)
+// (tile-shape experiments: MJL_DENSE_CFG selects the dense kernels' tiles; 0 = 128 x 128)
+template <auto F> struct KPtr { static constexpr auto value = F; };
+static int dense_cfg() {
+  static const int c = [] { const char* e = getenv("MJL_DENSE_CFG"); return e ? atoi(e) : 0; }();
+  return c;
+}
+
+extern "C" int mjl_twin_dense_fwd(const float* x, long long x_bstride, const float* w, const float* b, int nb, int M,
+                                  int N, int K, unsigned act_mask, float* y, void* stream) {
+  if (!x || !w || !b || !y || nb <= 0 || nb > 32 || M < 0 || N <= 0 || K <= 0 || x_bstride < 0)
+    return fail(MJL_ERR_ARG, "bad argument");
+  if (M == 0) return MJL_OK;
+  if ((long long)nb * M * (N > K ? N : K) >= (1LL << 31)) return fail(MJL_ERR_ARG, "twin_dense_fwd: stack too large");
+  hipStream_t s = (hipStream_t)stream;
+  const bool vec = K % 4 == 0 && x_bstride % 4 == 0 && aligned16(x) && aligned16(w);
+  const long long sw = (long long)N * K, sy = (long long)M * N;
+  if (N <= 32) {  // the heads: 64 x 32 tiles, one wave each (4 x the blocks of the 256-row tiles)
+    dim3 grid(1, (M + 63) / 64, nb);
+    if (vec) hipLaunchKernelGGL((mlp_fwd_kernel<64, 32, 1, 1, true>), grid, dim3(64), 0, s, x, K, x_bstride, w, K, sw, b, N, y, N, sy, M, N, K, act_mask);
+    else hipLaunchKernelGGL((mlp_fwd_kernel<64, 32, 1, 1, false>), grid, dim3(64), 0, s, x, K, x_bstride, w, K, sw, b, N, y, N, sy, M, N, K, act_mask);
+  } else {
+    auto go = [&](auto kv, auto kn, int BM, int BN) {
+      dim3 grid((N + BN - 1) / BN, (M + BM - 1) / BM, nb);
+      hipLaunchKernelGGL(decltype(kv)::value, grid, dim3(256), 0, s, x, K, x_bstride, w, K, sw, b, N, y, N, sy, M, N, K, act_mask);
+      (void)kn;
+    };
+    switch (dense_cfg()) {
+      case 1:
+        if (vec) go(KPtr<mlp_fwd_kernel<128, 64, 2, 2, true>>{}, 0, 128, 64);
+        else go(KPtr<mlp_fwd_kernel<128, 64, 2, 2, false>>{}, 0, 128, 64);
+        break;
+      case 2:
+        if (vec) go(KPtr<mlp_fwd_kernel<64, 128, 2, 2, true>>{}, 0, 64, 128);
+        else go(KPtr<mlp_fwd_kernel<64, 128, 2, 2, false>>{}, 0, 64, 128);
+        break;
+      case 3:
+        if (vec) go(KPtr<mlp_fwd_kernel<128, 64, 2, 2, true, 16>>{}, 0, 128, 64);
+        else go(KPtr<mlp_fwd_kernel<128, 64, 2, 2, false, 16>>{}, 0, 128, 64);
+        break;
+      case 4:
+        if (vec) go(KPtr<mlp_fwd_kernel<64, 64, 2, 2, true>>{}, 0, 64, 64);
+        else go(KPtr<mlp_fwd_kernel<64, 64, 2, 2, false>>{}, 0, 64, 64);
+        break;
+      default:
+        if (vec) go(KPtr<mlp_fwd_kernel<128, 128, 2, 2, true>>{}, 0, 128, 128);
+        else go(KPtr<mlp_fwd_kernel<128, 128, 2, 2, false>>{}, 0, 128, 128);
+    }
+  }
+  HIPCHK(hipGetLastError());
+  return MJL_OK;
+}
+
+extern "C" long long mjl_twin_dense_partial_rows(int M) { return M > 0 ? (M + 127) / 128 : 0; }
+
+extern "C" int mjl_twin_dense_dx_tanh(const float* g, const float* w, const float* y, int nb, int M, int N, int K,
+                                      float* dz, float* partials, void* stream) {
+  if (!g || !w || !y || !dz || !partials || nb <= 0 || nb > 32 || M < 0 || N <= 0 || K <= 0 || K % 4)
+    return fail(MJL_ERR_ARG, "bad argument");
+  if (M == 0) return MJL_OK;
+  if ((long long)nb * M * (N > K ? N : K) >= (1LL << 31)) return fail(MJL_ERR_ARG, "twin_dense_dx_tanh: stack too large");
+  if (!(aligned16(w) && aligned16(y) && aligned16(dz))) return fail(MJL_ERR_ARG, "twin_dense_dx_tanh: 16-byte alignment");
+  hipStream_t s = (hipStream_t)stream;
+  const bool vec = N % 4 == 0 && aligned16(g);
+  const long long sg = (long long)M * N, sw = (long long)N * K, sy = (long long)M * K;
+  auto go = [&](auto kv, int BN) {  // 128-row blocks always: the partial rows are per 128 rows
+    dim3 grid((K + BN - 1) / BN, (M + 127) / 128, nb);
+    hipLaunchKernelGGL(decltype(kv)::value, grid, dim3(256), 0, s, g, sg, w, sw, y, sy, dz, partials, M, N, K);
+  };
+  switch (dense_cfg()) {
+    case 1:
+    case 2:
+    case 4:
+      if (vec) go(KPtr<mlp_dx_tanh_kernel<128, 64, 2, 2, true>>{}, 64);
+      else go(KPtr<mlp_dx_tanh_kernel<128, 64, 2, 2, false>>{}, 64);
+      break;
+    case 3:
+      if (vec) go(KPtr<mlp_dx_tanh_kernel<128, 64, 2, 2, true, 16>>{}, 64);
+      else go(KPtr<mlp_dx_tanh_kernel<128, 64, 2, 2, false, 16>>{}, 64);
+      break;
+    default:
+      if (vec) go(KPtr<mlp_dx_tanh_kernel<128, 128, 2, 2, true>>{}, 128);
+      else go(KPtr<mlp_dx_tanh_kernel<128, 128, 2, 2, false>>{}, 128);
   }
   HIPCHK(hipGetLastError());
   return MJL_OK;

@@ -3,6 +3,8 @@
 // fp32 matrix cores (v_mfma_f32_32x32x2_f32: exact f32, a k-ordered fma chain per output).
 //
 //  mlp_fwd_kernel   Y = act(X W^T + b)          bias + tanh in the epilogue (no separate pass over Y)
+//  mlp_dx_tanh_kernel  D = (G W) (1 - Y^2)     the input gradient with the lower layer's tanh' and its
+//                   bias gradient's column-sum partials in the epilogue (the twin update's backward)
 //  mlp_bwd_kernel   dZ = act'(G, Y) = G (1 - Y^2) (tanh) or G (identity), formed while the A tile is
 //                   staged; writes dZ (for the weight gradient), its per-row-block column sums (the bias
 //                   gradient, reduced in a fixed order by mjl_colsum) and dX = dZ W
@@ -133,12 +135,20 @@ __device__ __forceinline__ void mlp_mma_step(const float* As, const float* Bs, i
   }
 }
 
-// Y[M, N] = act(X[M, K] W[N, K]^T + b[N])
+// Y[M, N] = act(X[M, K] W[N, K]^T + b[N]); blockIdx.z selects one of a stack of such problems (the
+// twin update's two nets: X at z * sx — sx = 0 for the shared observations —, W at z * sw, b at
+// z * sbias, Y at z * sy; act = tanh when bit z of act_mask is set)
 template <int BM, int BN, int WM, int WN, bool VECX, int BK = 32>
-__global__ __launch_bounds__(WM * WN * 64) void mlp_fwd_kernel(const float* __restrict__ X, int ldx,
-                                                               const float* __restrict__ W, int ldw,
-                                                               const float* __restrict__ bias, float* __restrict__ Y,
-                                                               int ldy, int M, int N, int K, int act) {
+__global__ __launch_bounds__(WM * WN * 64) void mlp_fwd_kernel(const float* __restrict__ X, int ldx, long long sx,
+                                                               const float* __restrict__ W, int ldw, long long sw,
+                                                               const float* __restrict__ bias, int sbias,
+                                                               float* __restrict__ Y, int ldy, long long sy, int M,
+                                                               int N, int K, unsigned act_mask) {
+  X += blockIdx.z * sx;
+  W += blockIdx.z * sw;
+  bias += blockIdx.z * sbias;
+  Y += blockIdx.z * sy;
+  const int act = (act_mask >> blockIdx.z) & 1u ? MLP_ACT_TANH : MLP_ACT_NONE;
   constexpr int T = WM * WN * 64, TM = BM / WM / 32, TN = BN / WN / 32;
   constexpr int SA = BM * (BK + kMlpPad), SB = BN * (BK + kMlpPad);
   __shared__ __attribute__((aligned(16))) float lds[2 * (SA + SB)];
@@ -306,6 +316,98 @@ __global__ __launch_bounds__(WM * WN * 64) void mlp_bwd_kernel(const float* __re
           if (row < M && col < K) dX[(size_t)row * lddx + col] = acc[tm][tn][r];
         }
       }
+  }
+}
+
+// The backward's input-gradient GEMM with the tanh derivative of the layer below in its epilogue:
+// D = (G W) (1 - Y^2) over a stack of problems (blockIdx.z): G [M, N] = dZ of this layer, W [N, K],
+// Y [M, K] = the tanh output feeding this layer, D [M, K] = dZ of that layer (the dH = G W of autograd
+// never reaches memory: the separate tanh-backward pass re-read it and Y). part[z][blockIdx.y][K]: the
+// column sums of D over the block's BM rows (the lower layer's bias gradient, first stage): each lane
+// sums its rows in order, the two half-waves pair up, then the WM row waves in order through LDS.
+template <int BM, int BN, int WM, int WN, bool VECG, int BK = 32>
+__global__ __launch_bounds__(WM * WN * 64) void mlp_dx_tanh_kernel(const float* __restrict__ G, long long sg,
+                                                                   const float* __restrict__ W, long long sw,
+                                                                   const float* __restrict__ Y, long long sy,
+                                                                   float* __restrict__ D, float* __restrict__ part,
+                                                                   int M, int N, int K) {
+  G += blockIdx.z * sg;
+  W += blockIdx.z * sw;
+  Y += blockIdx.z * sy;
+  D += blockIdx.z * sy;
+  part += ((size_t)blockIdx.z * gridDim.y + blockIdx.y) * K;
+  constexpr int T = WM * WN * 64, TM = BM / WM / 32, TN = BN / WN / 32;
+  constexpr int SA = BM * (BK + kMlpPad), SB = BK * (BN + kMlpPad);
+  __shared__ __attribute__((aligned(16))) float lds[2 * (SA + SB)];
+  __shared__ float red[WM][BN];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int i0 = blockIdx.y * BM, j0 = blockIdx.x * BN;
+  const int wr = wave / WN, wi = wr * (BM / WM), wj = (wave % WN) * (BN / WN);
+  f32x16 acc[TM][TN];
+#pragma unroll
+  for (int tm = 0; tm < TM; tm++)
+#pragma unroll
+    for (int tn = 0; tn < TN; tn++) acc[tm][tn] = f32x16{};
+  typedef Stage<BM, T, VECG, BK> SG;
+  typedef StageK<BN, T, BK> SW;
+  SG sa[2];
+  SW sb[2];
+  const int nk = (N + BK - 1) / BK;
+  sa[0].load(G, N, i0, M, 0, N, tid);
+  sb[0].load(W, K, 0, N, j0, K, tid);
+  if (nk > 1) {
+    sa[1].load(G, N, i0, M, BK, N, tid);
+    sb[1].load(W, K, BK, N, j0, K, tid);
+  }
+  sa[0].store(lds, tid);
+  sb[0].store(lds + SA, tid);
+  __syncthreads();
+  auto step = [&](int s, SG& na, SW& nb, SG& la, SW& lb) {
+    const float* As = lds + (s & 1) * (SA + SB);
+    if (s + 2 < nk) {
+      la.load(G, N, i0, M, (s + 2) * BK, N, tid);
+      lb.load(W, K, (s + 2) * BK, N, j0, K, tid);
+    }
+    mlp_mma_step<BK, BN, TM, TN, false>(As, As + SA, wi, wj, lane, acc);
+    if (s + 1 < nk) {
+      float* nx = lds + ((s + 1) & 1) * (SA + SB);
+      na.store(nx, tid);
+      nb.store(nx + SA, tid);
+    }
+    __syncthreads();
+  };
+  for (int s = 0; s < nk; s += 2) {
+    step(s, sa[1], sb[1], sa[0], sb[0]);
+    if (s + 1 < nk) step(s + 1, sa[0], sb[0], sa[1], sb[1]);
+  }
+  float cs[TN];
+#pragma unroll
+  for (int tn = 0; tn < TN; tn++) {
+    cs[tn] = 0.f;
+    const int col = j0 + wj + tn * 32 + (lane & 31);
+#pragma unroll
+    for (int tm = 0; tm < TM; tm++)
+#pragma unroll
+      for (int r = 0; r < 16; r++) {
+        const int row = i0 + wi + tm * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+        if (row < M && col < K) {
+          const size_t o = (size_t)row * K + col;
+          const float y = Y[o];
+          const float d = acc[tm][tn][r] * (1.f - y * y);
+          D[o] = d;
+          cs[tn] += d;
+        }
+      }
+    cs[tn] += __shfl_xor(cs[tn], 32);
+    if (lane < 32) red[wr][wj + tn * 32 + lane] = cs[tn];
+  }
+  __syncthreads();
+  for (int c = tid; c < BN; c += T) {
+    if (j0 + c >= K) continue;
+    float s = red[0][c];
+#pragma unroll
+    for (int q = 1; q < WM; q++) s += red[q][c];
+    part[j0 + c] = s;
   }
 }
 

@@ -32,7 +32,8 @@ EXPORTS = [
     "mjl_adam_dev", "mjl_mlp_fwd", "mjl_mlp_colpart_rows", "mjl_mlp_bwd",
     "mjl_colsum_batched_scratch", "mjl_colsum_batched", "mjl_tanh_bwd_colsum_batched", "mjl_slice_sum_batched",
     "mjl_twin_head_bwd", "mjl_mse_strided", "mjl_ppo_surrogate_clipped", "mjl_bias_act", "mjl_adam_multi",
-    "mjl_gather_rows_indexed", "mjl_slice_sum_multi",
+    "mjl_gather_rows_indexed", "mjl_slice_sum_multi", "mjl_colsum_partials", "mjl_tanh_bwd_colsum_partials",
+    "mjl_twin_dense_fwd", "mjl_twin_dense_partial_rows", "mjl_twin_dense_dx_tanh",
 ]
 
 _lib = None
@@ -140,6 +141,12 @@ def lib() -> C.CDLL:
                                             C.c_float, vp, vp, vp, vp, vp]
     L.mjl_gather_rows_indexed.argtypes = [vp, vp, i32, C.c_longlong, i32, vp, vp, vp, vp]
     L.mjl_slice_sum_multi.argtypes = [i32, vp, vp, vp, vp, vp, vp]
+    L.mjl_colsum_partials.argtypes = [vp, i32, i32, i32, i32, vp, vp]
+    L.mjl_twin_dense_fwd.argtypes = [vp, C.c_longlong, vp, vp, i32, i32, i32, i32, C.c_uint, vp, vp]
+    L.mjl_twin_dense_partial_rows.argtypes = [i32]
+    L.mjl_twin_dense_partial_rows.restype = C.c_longlong
+    L.mjl_twin_dense_dx_tanh.argtypes = [vp, vp, vp, i32, i32, i32, i32, vp, vp, vp]
+    L.mjl_tanh_bwd_colsum_partials.argtypes = [vp, vp, i32, i32, i32, i32, vp, vp, vp]
     L.mjl_small_mlp_fwd.argtypes = [vp, i32, i32, i32, vp, vp, vp, vp, vp]
     L.mjl_small_mlp_bwd_input.argtypes = [vp, i32, i32, i32, vp, vp, vp, vp, vp]
     L.mjl_step_vjp.argtypes = [vp, f32p, f32p, f32p, f32p, f32p, vp]

@@ -36,6 +36,12 @@ import torch
 from ._lib import check, lib
 
 TWIN_UPDATE = os.environ.get("MJL_TWIN_UPDATE", "1") != "0"
+# rows per column-sum partial (first stage) of the output layer's bias gradient
+COLSUM_CHUNK = int(os.environ.get("MJL_TWIN_COLSUM_CHUNK", "32"))
+# the layers on the native dense kernels (mjl_twin_dense_fwd / mjl_twin_dense_dx_tanh: bias + tanh in
+# the forward GEMM's epilogue, tanh' and the bias-gradient partials in the input-gradient GEMM's);
+# 0: bias-less torch.bmm + the separate bias/tanh and tanh-backward passes
+DENSE = os.environ.get("MJL_TWIN_DENSE", "0") == "1"
 
 
 def _align4(n: int) -> int:
@@ -134,15 +140,24 @@ class TwinNets:
         st = torch.cuda.current_stream(dev).cuda_stream
         M, A, nl = o.shape[0], self.A, self.nl
         s = splits
-        # ---- forward: bias-less batched GEMMs, the bias and tanh in one native pass (mjl_bias_act)
+        dense = DENSE and o.is_contiguous()
+        # ---- forward: bias and tanh in the GEMM's epilogue (dense), or bias-less batched GEMMs + one
+        # native bias/tanh pass (mjl_bias_act)
         x = o.unsqueeze(0).expand(2, M, self.K0)  # both nets read the same observations (batch stride 0)
         hs = [x]
-        for l in range(nl - 1):
-            h = torch.bmm(hs[-1], self.W[l].transpose(1, 2))
-            check(L.mjl_bias_act(h.data_ptr(), self.b[l].data_ptr(), 2, M, h.shape[2], 3, st))
+        for l in range(nl):
+            N, K = self.W[l].shape[1], self.W[l].shape[2]
+            mask = 3 if l < nl - 1 else 1  # the output layer: tanh for the policy's mean, linear value
+            if dense:
+                h = torch.empty((2, M, N), device=dev)
+                xs = hs[-1]
+                check(L.mjl_twin_dense_fwd(xs.data_ptr(), 0 if l == 0 else M * K, self.W[l].data_ptr(),
+                                           self.b[l].data_ptr(), 2, M, N, K, mask, h.data_ptr(), st))
+            else:
+                h = torch.bmm(hs[-1], self.W[l].transpose(1, 2))
+                check(L.mjl_bias_act(h.data_ptr(), self.b[l].data_ptr(), 2, M, N, mask, st))
             hs.append(h)
-        z = torch.bmm(hs[-1], self.W[nl - 1].transpose(1, 2))  # [2, M, A]
-        check(L.mjl_bias_act(z.data_ptr(), self.b[nl - 1].data_ptr(), 2, M, A, 1, st))  # tanh: the policy's mean
+        z = hs.pop()  # [2, M, A]
         mean = z[0]
         # ---- losses (networks.py:103 clips log_std to [-20, 2]: in the kernel, with its gradient mask)
         log_std = self.policy.log_std
@@ -167,24 +182,26 @@ class TwinNets:
         # every reduction's first stage here; their second stages (column-sum chunk partials, split-K
         # weight-gradient slices) all in ONE launch after the last layer (mjl_slice_sum_multi)
         segs = []  # (x, out, nb, ns, m)
-        R = M // 128  # column-sum chunk rows per matrix (ColsumPlan)
-        cs = self._scratch(f"cs{nl - 1}", int(L.mjl_colsum_batched_scratch(2, M, A)))
-        check(L.mjl_colsum_batched(dz.data_ptr(), 2, M, A, cs.data_ptr(), None, st))
+        ch = COLSUM_CHUNK if M % COLSUM_CHUNK == 0 else M
+        R = M // ch  # column-sum partial rows per matrix
+        cs = self._scratch(f"cs{nl - 1}", 2 * R * A)
+        check(L.mjl_colsum_partials(dz.data_ptr(), 2, M, A, ch, cs.data_ptr(), st))
         segs.append((cs, self.gb[nl - 1], 2, R, A))
         g = dz
+        Rd = int(L.mjl_twin_dense_partial_rows(M))
         for l in range(nl - 1, -1, -1):
             N, K = self.W[l].shape[1], self.W[l].shape[2]
             xin = hs[l]  # the layer's input: H_{l-1}, or the observations for l = 0
             # split-K slices of the weight gradient: the thin layers (the 21 / 1-unit outputs, the 54-wide
             # input) are a few output tiles per slice, so they take more, shorter slices
             s = splits if (N >= 64 and K >= 64) else max(splits, min(64, M // 256))
-            if l < nl - 1:  # tanh layer: dZ = dH (1 - H^2) and the bias gradient's partials in one pass
+            if l < nl - 1 and not dense:  # tanh layer: dZ = dH (1 - H^2) and the bias gradient's partials
                 dzl = torch.empty_like(g)
-                cs = self._scratch(f"cs{l}", int(L.mjl_colsum_batched_scratch(2, M, N)))
-                check(L.mjl_tanh_bwd_colsum_batched(g.data_ptr(), hs[l + 1].data_ptr(), 2, M, N, dzl.data_ptr(),
-                                                    cs.data_ptr(), None, st))
+                cs = self._scratch(f"cs{l}", 2 * R * N)
+                check(L.mjl_tanh_bwd_colsum_partials(g.data_ptr(), hs[l + 1].data_ptr(), 2, M, N, ch, dzl.data_ptr(),
+                                                     cs.data_ptr(), st))
                 segs.append((cs, self.gb[l], 2, R, N))
-            else:
+            else:  # the output layer's dZ, or (dense) the one the layer above's input-gradient GEMM formed
                 dzl = g
             if l == 0:  # the shared observations: [2, M, K0] with batch stride 0 -> per split, both nets
                 xs = o.view(1, s, M // s, K).expand(2, s, M // s, K).reshape(2 * s, M // s, K)
@@ -192,7 +209,13 @@ class TwinNets:
                 xs = xin.view(2 * s, M // s, K)
             part = torch.bmm(dzl.view(2 * s, M // s, N).transpose(1, 2), xs)  # [2s, N, K]
             segs.append((part, self.gW[l], 2, s, N * K))
-            if l > 0:
+            if l > 0 and dense:  # dZ of the layer below = (dZ W) (1 - H^2), its bias partials on the way
+                g = torch.empty((2, M, K), device=dev)
+                cs = self._scratch(f"csd{l - 1}", 2 * Rd * K)
+                check(L.mjl_twin_dense_dx_tanh(dzl.data_ptr(), self.W[l].data_ptr(), xin.data_ptr(), 2, M, N, K,
+                                               g.data_ptr(), cs.data_ptr(), st))
+                segs.append((cs, self.gb[l - 1], 2, Rd, K))
+            elif l > 0:
                 g = torch.bmm(dzl, self.W[l])  # [2, M, K]
         import ctypes
         k = len(segs)

@@ -31,8 +31,10 @@ def _data(n, seed=1):
             torch.randn(n, generator=gd, device="cuda"), torch.randn(n, generator=gd, device="cuda"))
 
 
+@pytest.mark.parametrize("dense", [True, False])
 @pytest.mark.parametrize("n", [8192, 65536])
-def test_twin_gradients_match_float64_autograd(n):
+def test_twin_gradients_match_float64_autograd(n, dense, monkeypatch):
+    monkeypatch.setattr(twin, "DENSE", dense)
     cfg = reference_ppo_config()
     pol, val = _nets(cfg)
     ref_p = ppo.GaussianPolicy(54, 21, cfg.policy_hidden_layer_specs).cuda().double()

@@ -143,6 +143,44 @@ def shard_twin(reps: int = 5, envs: int = 1024):
                   f"wall median {1e3 * w[len(w) // 2]:.2f} ms (min {1e3 * w[0]:.2f}, max {1e3 * w[-1]:.2f})", flush=True)
 
 
+def twin_chunk(reps: int = 5, envs: int = 1024, chunks=(128, 64, 32), mbs=(8192, 65536), attr="COLSUM_CHUNK"):
+    """Graph-replayed twin updates at several values of a twin-module setting (attr: twin.COLSUM_CHUNK,
+    the column-sum partial chunk, or twin.DENSE; read when a minibatch step is captured), interleaved:
+    C5's per-rank shard and C3's single-process update."""
+    from mjx_amd import twin
+    cfg = reference_ppo_config()
+    N = envs * 256
+    gd = torch.Generator(device="cuda").manual_seed(1)
+    obs, act = torch.randn((N, 54), generator=gd, device="cuda"), torch.randn((N, 21), generator=gd, device="cuda").clamp(-1, 1)
+    logp, ret, adv = (torch.randn(N, generator=gd, device="cuda") for _ in range(3))
+    for mb, dist in ((8192, _NoComm()), (65536, None)):
+        if mb not in mbs:
+            continue
+        cfg.minibatch_size = mb
+        ups = {}
+        for c in chunks:
+            g = torch.Generator().manual_seed(0)
+            pol = ppo.GaussianPolicy(54, 21, cfg.policy_hidden_layer_specs, cfg.log_std_init, g).cuda()
+            val = ppo.ValueNet(54, cfg.value_hidden_layer_specs, g).cuda()
+            op, ov = ppo._adam(pol.parameters(), 3e-4), ppo._adam(val.parameters(), 3e-4)
+            ups[c] = ppo.PPOUpdater(pol, val, op, ov, cfg, dist, 1, use_graph=True)
+        ts = {c: [] for c in chunks}
+        for r in range(reps + 2):
+            idx = ppo.make_index_batches(N, mb, cfg.epochs, torch.Generator(device="cuda").manual_seed(r), "cuda")
+            for c in chunks:
+                setattr(twin, attr, c)
+                torch.cuda.synchronize()
+                t0 = time.time()
+                ups[c].run(obs, act, logp, ret, adv, idx)
+                torch.cuda.synchronize()
+                if r >= 2:
+                    ts[c].append(time.time() - t0)
+        for c in chunks:
+            w = sorted(ts[c])
+            print(f"{'dp-shard' if dist is not None else 'single'} minibatch={mb} steps={idx.shape[0]} {attr}={c}: "
+                  f"wall median {1e3 * w[len(w) // 2]:.2f} ms (min {1e3 * w[0]:.2f}, max {1e3 * w[-1]:.2f})", flush=True)
+
+
 def shard(reps: int = 5, minibatch: int = 8192, envs: int = 1024):
     """One rank's update in the C5 configuration on 8 GPUs (1024 envs x 256 steps, 4 epochs of
     8,192-row minibatches: 128 minibatch steps) through PPOUpdater's data-parallel bodies with the
@@ -209,6 +247,15 @@ if __name__ == "__main__":
         sys.exit(0)
     if len(sys.argv) > 1 and sys.argv[1] == "shard":
         shard()
+        sys.exit(0)
+    if len(sys.argv) > 1 and sys.argv[1] == "c5twin":  # the C5-shape twin update alone (for kernel traces)
+        twin_chunk(chunks=(32,), mbs=(8192,))
+        sys.exit(0)
+    if len(sys.argv) > 1 and sys.argv[1] == "dense":
+        twin_chunk(chunks=(True, False), attr="DENSE")
+        sys.exit(0)
+    if len(sys.argv) > 1 and sys.argv[1] == "chunk":
+        twin_chunk()
         sys.exit(0)
     if len(sys.argv) > 1 and sys.argv[1] == "twin":
         shard_twin()
