@@ -421,9 +421,12 @@ int mjl_slice_sum_multi(int nseg, const float* const* x, float* const* out, cons
  * 103), g_mean [M, A] = d loss / d mean (mjl_ppo_surrogate), v[r] = v[r * vstride] the value net's
  * output and ret [M] its targets (train_ppo.py:218-220, value loss mean (v - ret)^2);
  * dz4 [2][M][A]: dz4[0] = g_mean (1 - mean^2), dz4[1][:, 0] = 2 (v - ret) / M, dz4[1][:, 1:] = 0 (the
- * value net's output layer is padded to A rows). */
+ * value net's output layer is padded to A rows); A <= 32. partials (or NULL): [2][mjl_twin_head_partial_rows(M)][A]
+ * = dz4's column sums per 32-row chunk (fixed order), the output biases' gradient before the sum over
+ * chunks (mjl_slice_sum_multi). */
+long long mjl_twin_head_partial_rows(int M);
 int mjl_twin_head_bwd(const float* g_mean, const float* mean, const float* v, int vstride, const float* ret, int M,
-                      int A, float* dz4, void* stream);
+                      int A, float* dz4, float* partials, void* stream);
 /* x[b][r][j] = act_b(x[b][r][j] + bias[b][j]) in place over nb stacked row-major [rows, n] matrices,
  * act_b = tanh when bit b of act_mask is set, else the identity (the twin update's dense-layer
  * epilogue, src/networks.py:55-61, after a bias-less batched GEMM). */
@@ -438,7 +441,7 @@ int mjl_bias_act(float* x, const float* bias, int nb, long long rows, int n, uns
  *   g_log_std [A] are d loss / d mean and d loss / d log_std (torch.minimum / clamp conventions for
  *   ties and bounds). mjl_mse: loss = mean (v - r)^2, g_v = 2 (v - r) / n. scratch:
  *   mjl_ppo_loss_scratch(n, A) floats (mjl_mse needs n / 256 + 1). A <= 32.
- * mjl_gather_rows: dst_k[r, :] = src_k[idx[r], :] for narr <= 5 row-major float arrays of nsrc rows
+ * mjl_gather_rows: dst_k[r, :] = src_k[idx[r], :] for narr <= 8 row-major float arrays of nsrc rows
  *   and cols[k] columns (the minibatch gather of train_ppo.py:237-241), idx int64 [n]; one launch;
  *   an index outside [0, nsrc) gives a NaN row; n x (total columns) must be below 2^31. */
 long long mjl_ppo_loss_scratch(int n, int A);
@@ -449,11 +452,15 @@ int mjl_mse(const float* v, const float* r, int n, float* scratch, float* loss, 
 /* mjl_ppo_surrogate with log_std clipped to [log_std_lo, log_std_hi] on read (networks.py:103 clips it
  * to [-20, 2]) and g_log_std zero where the raw value lies outside (torch.clamp's backward, bounds
  * inclusive); +-INFINITY bounds = mjl_ppo_surrogate. stats_row (device int, or NULL): adv_stats is an
- * [n_minibatches, 2] table read at that row (a captured minibatch step reads its row at run time). */
+ * [n_minibatches, 2] table read at that row (a captured minibatch step reads its row at run time).
+ * step0 / step1 / ctr (each device float / float / int, or NULL): advanced by one after every read of
+ * the minibatch row (the captured update's counters: mjl_adam_multi with advanced = 1 then takes the
+ * step counts as they are). */
 int mjl_ppo_surrogate_clipped(const float* mean, const float* log_std, const float* act, const float* old_logp,
                               const float* adv, const float* adv_stats, const int* stats_row, int n, int A,
                               float clip_eps, float ent_coef, float log_std_lo, float log_std_hi, float* scratch,
-                              float* loss, float* g_mean, float* g_log_std, void* stream);
+                              float* loss, float* g_mean, float* g_log_std, float* step0, float* step1, int* ctr,
+                              void* stream);
 /* mjl_mse with v[i] read at v + i * vstride (the value column of the twin update's padded output). */
 int mjl_mse_strided(const float* v, int vstride, const float* r, int n, float* scratch, float* loss, float* g_v,
                     void* stream);
@@ -479,37 +486,12 @@ int mjl_adam_dev(int nt, float* const* p, const float* const* g, float* const* m
  * steps, train_ppo.py:246-251): tensor k uses group[k]'s lr and device step counter step[group[k]]
  * (float, the count before this step: the step takes step + 1, and every group's counter is advanced
  * by one after it); g is scaled by gscale (the data-parallel mean: 1 / world size); ctr (device int,
- * or NULL) is advanced with the counters. Same arithmetic as mjl_adam_dev. */
+ * or NULL) is advanced with the counters. advanced = 1: the counters were advanced earlier in the
+ * minibatch step (mjl_ppo_surrogate_clipped's step0 / step1 / ctr): the step takes step as it is and
+ * nothing is advanced here. Same arithmetic as mjl_adam_dev. */
 int mjl_adam_multi(int nt, float* const* p, const float* const* g, float* const* m, float* const* v,
                    const long long* numel, const int* group, int ngroups, const float* lr, float beta1, float beta2,
-                   float eps, float gscale, float* const* step, int* ctr, void* stream);
-
-/* PPO update dense layers (train_ppo.py:204-252: value_and_grad of ppo_loss_fn / value_loss_fn
- * through the src/networks.py:22-61 MLPs), fp32 on the matrix cores, torch nn.Linear layouts
- * (row-major x [M, K] with row stride ldx, w [N, K], b [N], y [M, N]); act: 0 none, 1 tanh.
- * mjl_mlp_fwd: y = act(x w^T + b), bias and tanh in the GEMM's epilogue.
- * mjl_mlp_bwd: dz = g (1 - y^2) (tanh; g for none) [M, N] written out, dx = dz w [M, K] (dx may be NULL:
- *   the first layer), and colpart [mjl_mlp_colpart_rows(M), N] = dz's column sums per 128-row block
- *   (the bias gradient is their column sum, mjl_colsum: fixed order). The weight gradient dz^T x is a
- *   batched GEMM outside. Device pointers; w / dx 16-byte aligned and K % 4 == 0 when dx is given. */
-int mjl_mlp_fwd(const float* x, int ldx, const float* w, const float* b, int M, int N, int K, int act, float* y,
-                void* stream);
-long long mjl_mlp_colpart_rows(int M);
-int mjl_mlp_bwd(const float* g, const float* y, int M, int N, const float* w, int K, int act, float* dz, float* dx,
-                float* colpart, void* stream);
-/* The twin PPO update's stacked dense layers (mjx_amd/twin.py; train_ppo.py:204-252 through both
- * src/networks.py MLPs at once): nb problems per launch.
- * mjl_twin_dense_fwd: y[z] = act_z(x[z] w[z]^T + b[z]), x at z * x_bstride (0: shared observations)
- *   [M, K], w [nb, N, K], b [nb, N], y [nb, M, N]; act_z = tanh when bit z of act_mask is set.
- * mjl_twin_dense_dx_tanh: dz[z] = (g[z] w[z]) (1 - y[z]^2): g [nb, M, N] (this layer's dZ), w [nb, N, K],
- *   y [nb, M, K] (the tanh output feeding the layer), dz [nb, M, K] (the lower layer's dZ); partials
- *   [nb][mjl_twin_dense_partial_rows(M)][K] = its column sums per 128-row block (fixed order).
- *   K % 4 == 0, 16-byte aligned w / y / dz. */
-int mjl_twin_dense_fwd(const float* x, long long x_bstride, const float* w, const float* b, int nb, int M, int N,
-                       int K, unsigned act_mask, float* y, void* stream);
-long long mjl_twin_dense_partial_rows(int M);
-int mjl_twin_dense_dx_tanh(const float* g, const float* w, const float* y, int nb, int M, int N, int K, float* dz,
-                           float* partials, void* stream);
+                   float eps, float gscale, float* const* step, int* ctr, int advanced, void* stream);
 
 #ifdef __cplusplus
 }

@@ -15,7 +15,6 @@
 #include "ppo_kernels.hip"
 #include "apg_kernels.hip"
 #include "ppo_loss_kernels.hip"
-#include "mlp_kernels.hip"
 
 using namespace mjl;
 
@@ -1130,7 +1129,7 @@ extern "C" int mjl_bias_act(float* x, const float* bias, int nb, long long rows,
   if (!x || !bias || nb <= 0 || rows < 0 || n <= 0) return fail(MJL_ERR_ARG, "bad argument");
   if (rows == 0) return MJL_OK;
   if ((long long)nb * rows * n >= (1LL << 31)) return fail(MJL_ERR_ARG, "bias_act: at most 2^31 elements");
-  const bool v4 = n % 4 == 0 && (uintptr_t)x % 16 == 0;
+  const bool v4 = n % 4 == 0 && (uintptr_t)x % 16 == 0 && (uintptr_t)bias % 16 == 0;
   const long long groups = (long long)nb * rows * n / (v4 ? 4 : 1);
   const dim3 grid((unsigned)((groups + 255) / 256));
   if (v4)
@@ -1141,13 +1140,15 @@ extern "C" int mjl_bias_act(float* x, const float* bias, int nb, long long rows,
   return MJL_OK;
 }
 
+extern "C" long long mjl_twin_head_partial_rows(int M) { return M > 0 ? (M + kHeadChunk - 1) / kHeadChunk : 0; }
+
 extern "C" int mjl_twin_head_bwd(const float* g_mean, const float* mean, const float* v, int vstride, const float* ret,
-                                 int M, int A, float* dz4, void* stream) {
-  if (!g_mean || !mean || !v || !ret || !dz4 || M <= 0 || A <= 0 || vstride <= 0) return fail(MJL_ERR_ARG, "bad argument");
-  const long long n = 2LL * M * A;
-  if (n >= (1LL << 31)) return fail(MJL_ERR_ARG, "twin_head_bwd: 2 M A must be below 2^31");
-  hipLaunchKernelGGL(twin_head_bwd_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, (hipStream_t)stream,
-                     g_mean, mean, v, vstride, ret, M, A, dz4);
+                                 int M, int A, float* dz4, float* partials, void* stream) {
+  if (!g_mean || !mean || !v || !ret || !dz4 || M <= 0 || A <= 0 || A > 32 || vstride <= 0)
+    return fail(MJL_ERR_ARG, "bad argument");
+  if (2LL * M * A >= (1LL << 31)) return fail(MJL_ERR_ARG, "twin_head_bwd: 2 M A must be below 2^31");
+  hipLaunchKernelGGL(twin_head_bwd_kernel, dim3((unsigned)((M + kHeadChunk - 1) / kHeadChunk), 2), dim3(256), 0,
+                     (hipStream_t)stream, g_mean, mean, v, vstride, ret, M, A, dz4, partials);
   HIPCHK(hipGetLastError());
   return MJL_OK;
 }
@@ -1281,29 +1282,39 @@ extern "C" int mjl_apg_obs_vjp(int B, int nq, int nv, const float* o, const uint
 }
 
 // ---------------------------------------------------------------- PPO update losses
+constexpr int kSurrRows = 64;  // rows per ppo_surrogate_kernel block
 extern "C" long long mjl_ppo_loss_scratch(int n, int A) {
   if (n <= 0 || A <= 0) return 0;
-  const long long nb = (n + kLossT - 1) / kLossT;
-  return 3 * nb + nb * (A + 1);
+  const long long nb = (n + kLossT - 1) / kLossT, nbs = (n + kSurrRows - 1) / kSurrRows;
+  return 3 * nb + nbs * (A + 1);
 }
 
 extern "C" int mjl_ppo_surrogate_clipped(const float* mean, const float* log_std, const float* act,
                                          const float* old_logp, const float* adv, const float* adv_stats,
                                          const int* stats_row, int n, int A, float clip_eps, float ent_coef,
                                          float log_std_lo, float log_std_hi, float* scratch, float* loss,
-                                         float* g_mean, float* g_log_std, void* stream) {
+                                         float* g_mean, float* g_log_std, float* step0, float* step1, int* ctr,
+                                         void* stream) {
   if (!mean || !log_std || !act || !old_logp || !adv || !scratch || !loss || !g_mean || !g_log_std || n <= 0 || A <= 0)
     return fail(MJL_ERR_ARG, "bad argument");
   if (A > kLossMaxA) return fail(MJL_ERR_UNSUPPORTED, "ppo surrogate: at most %d action columns", kLossMaxA);
   hipStream_t s = (hipStream_t)stream;
-  const int nb = (n + kLossT - 1) / kLossT;
+  static const int rb = [] { const char* e = getenv("MJL_SURR_ROWS"); return e ? atoi(e) : kSurrRows; }();
+  const int nb_adv = (n + kLossT - 1) / kLossT, nb = (n + rb - 1) / rb;
   float* adv_part = scratch;
-  float* part = scratch + 3 * (size_t)nb;
-  if (!adv_stats) hipLaunchKernelGGL(adv_stats_kernel, dim3(nb), dim3(kLossT), 0, s, adv, n, adv_part);
-  hipLaunchKernelGGL(ppo_surrogate_kernel, dim3(nb), dim3(kLossT), 0, s, mean, log_std, act, old_logp, adv, n, A,
-                     clip_eps, adv_part, nb, adv_stats, g_mean, part, log_std_lo, log_std_hi, stats_row);
+  float* part = scratch + 3 * (size_t)nb_adv;
+  if (!adv_stats) hipLaunchKernelGGL(adv_stats_kernel, dim3(nb_adv), dim3(kLossT), 0, s, adv, n, adv_part);
+  if (rb == 256)
+    hipLaunchKernelGGL(ppo_surrogate_kernel<256>, dim3(nb), dim3(256), 0, s, mean, log_std, act, old_logp,
+                       adv, n, A, clip_eps, adv_part, nb_adv, adv_stats, g_mean, part, log_std_lo, log_std_hi, stats_row);
+  else if (rb == 128)
+    hipLaunchKernelGGL(ppo_surrogate_kernel<128>, dim3(nb), dim3(128), 0, s, mean, log_std, act, old_logp,
+                       adv, n, A, clip_eps, adv_part, nb_adv, adv_stats, g_mean, part, log_std_lo, log_std_hi, stats_row);
+  else
+    hipLaunchKernelGGL(ppo_surrogate_kernel<64>, dim3(nb), dim3(64), 0, s, mean, log_std, act, old_logp,
+                       adv, n, A, clip_eps, adv_part, nb_adv, adv_stats, g_mean, part, log_std_lo, log_std_hi, stats_row);
   hipLaunchKernelGGL(ppo_surrogate_final_kernel, dim3(A + 1), dim3(64), 0, s, part, nb, n, A, log_std, ent_coef, loss,
-                     g_log_std, log_std_lo, log_std_hi);
+                     g_log_std, log_std_lo, log_std_hi, step0, step1, ctr);
   HIPCHK(hipGetLastError());
   return MJL_OK;
 }
@@ -1313,7 +1324,8 @@ extern "C" int mjl_ppo_surrogate(const float* mean, const float* log_std, const 
                                  float ent_coef, float* scratch, float* loss, float* g_mean, float* g_log_std,
                                  void* stream) {
   return mjl_ppo_surrogate_clipped(mean, log_std, act, old_logp, adv, adv_stats, nullptr, n, A, clip_eps, ent_coef,
-                                   -INFINITY, INFINITY, scratch, loss, g_mean, g_log_std, stream);
+                                   -INFINITY, INFINITY, scratch, loss, g_mean, g_log_std, nullptr, nullptr, nullptr,
+                                   stream);
 }
 
 extern "C" int mjl_mse_strided(const float* v, int vstride, const float* r, int n, float* scratch, float* loss,
@@ -1333,7 +1345,8 @@ extern "C" int mjl_mse(const float* v, const float* r, int n, float* scratch, fl
 
 extern "C" int mjl_gather_rows_indexed(const long long* idx, const int* idx_row, int n, long long nsrc, int narr,
                                        const float* const* src, float* const* dst, const int* cols, void* stream) {
-  if (!idx || n < 0 || nsrc < 0 || narr < 1 || narr > 5 || !src || !dst || !cols) return fail(MJL_ERR_ARG, "bad argument");
+  if (!idx || n < 0 || nsrc < 0 || narr < 1 || narr > kGatherMax || !src || !dst || !cols)
+    return fail(MJL_ERR_ARG, "bad argument");
   GatherArgs g;
   std::memset(&g, 0, sizeof(g));
   g.narr = narr;
@@ -1398,7 +1411,8 @@ extern "C" int mjl_adam_dev(int nt, float* const* p, const float* const* g, floa
 
 extern "C" int mjl_adam_multi(int nt, float* const* p, const float* const* g, float* const* m, float* const* v,
                               const long long* numel, const int* group, int ngroups, const float* lr, float beta1,
-                              float beta2, float eps, float gscale, float* const* step, int* ctr, void* stream) {
+                              float beta2, float eps, float gscale, float* const* step, int* ctr, int advanced,
+                              void* stream) {
   if (nt < 1 || nt > kAdamMultiMaxT || ngroups < 1 || ngroups > kAdamMaxGroups || !p || !g || !m || !v || !numel ||
       !group || !lr || !step)
     return fail(MJL_ERR_ARG, "bad argument");
@@ -1420,147 +1434,12 @@ extern "C" int mjl_adam_multi(int nt, float* const* p, const float* const* g, fl
     a.lr[gi] = lr[gi]; a.step[gi] = step[gi];
   }
   a.b1 = beta1; a.b2 = beta2; a.eps = eps; a.gscale = gscale;
+  a.tadd = advanced ? 0.f : 1.f;
   if (a.blk[nt] > 0)
     hipLaunchKernelGGL(adam_multi_kernel, dim3((unsigned)a.blk[nt]), dim3(256), 0, (hipStream_t)stream, a);
-  hipLaunchKernelGGL(step_counters_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream, step[0],
-                     ngroups > 1 ? step[1] : nullptr, ctr);
-  HIPCHK(hipGetLastError());
-  return MJL_OK;
-}
-
-// ---------------------------------------------------------------- PPO update dense layers
-static bool aligned16(const void* p) { return ((uintptr_t)p & 15) == 0; }
-
-extern "C" int mjl_mlp_fwd(const float* x, int ldx, const float* w, const float* b, int M, int N, int K, int act,
-                           float* y, void* stream) {
-  if (!x || !w || !b || !y || M < 0 || N <= 0 || K <= 0 || ldx < K || (act != MLP_ACT_NONE && act != MLP_ACT_TANH))
-    return fail(MJL_ERR_ARG, "bad argument");
-  if (M == 0) return MJL_OK;
-  hipStream_t s = (hipStream_t)stream;
-  const bool vec = K % 4 == 0 && ldx % 4 == 0 && aligned16(x) && aligned16(w);
-  const unsigned am = act == MLP_ACT_TANH ? 1u : 0u;
-  if (N <= 32) {  // the heads (21 actions, 1 value): 256 x 32 tiles, 4 waves of 64 x 32
-    dim3 grid(1, (M + 255) / 256);
-    if (vec) hipLaunchKernelGGL((mlp_fwd_kernel<256, 32, 4, 1, true>), grid, dim3(256), 0, s, x, ldx, 0LL, w, K, 0LL, b, 0, y, N, 0LL, M, N, K, am);
-    else hipLaunchKernelGGL((mlp_fwd_kernel<256, 32, 4, 1, false>), grid, dim3(256), 0, s, x, ldx, 0LL, w, K, 0LL, b, 0, y, N, 0LL, M, N, K, am);
-  } else {  // 128 x 128 tiles, 4 waves of 64 x 64; a row block's column tiles are neighbours in launch order
-    dim3 grid((N + 127) / 128, (M + 127) / 128);
-    if (vec) hipLaunchKernelGGL((mlp_fwd_kernel<128, 128, 2, 2, true>), grid, dim3(256), 0, s, x, ldx, 0LL, w, K, 0LL, b, 0, y, N, 0LL, M, N, K, am);
-    else hipLaunchKernelGGL((mlp_fwd_kernel<128, 128, 2, 2, false>), grid, dim3(256), 0, s, x, ldx, 0LL, w, K, 0LL, b, 0, y, N, 0LL, M, N, K, am);
-  }
-  HIPCHK(hipGetLastError());
-  return MJL_OK;
-}
-
-// ---- the twin update's stacked dense layers (mjx_amd/twin.py): nb problems per launch (blockIdx.z)
-// (tile-shape experiments: MJL_DENSE_CFG selects the dense kernels' tiles; 0 = 128 x 128)
-template <auto F> struct KPtr { static constexpr auto value = F; };
-static int dense_cfg() {
-  static const int c = [] { const char* e = getenv("MJL_DENSE_CFG"); return e ? atoi(e) : 0; }();
-  return c;
-}
-
-extern "C" int mjl_twin_dense_fwd(const float* x, long long x_bstride, const float* w, const float* b, int nb, int M,
-                                  int N, int K, unsigned act_mask, float* y, void* stream) {
-  if (!x || !w || !b || !y || nb <= 0 || nb > 32 || M < 0 || N <= 0 || K <= 0 || x_bstride < 0)
-    return fail(MJL_ERR_ARG, "bad argument");
-  if (M == 0) return MJL_OK;
-  if ((long long)nb * M * (N > K ? N : K) >= (1LL << 31)) return fail(MJL_ERR_ARG, "twin_dense_fwd: stack too large");
-  hipStream_t s = (hipStream_t)stream;
-  const bool vec = K % 4 == 0 && x_bstride % 4 == 0 && aligned16(x) && aligned16(w);
-  const long long sw = (long long)N * K, sy = (long long)M * N;
-  if (N <= 32) {  // the heads: 64 x 32 tiles, one wave each (4 x the blocks of the 256-row tiles)
-    dim3 grid(1, (M + 63) / 64, nb);
-    if (vec) hipLaunchKernelGGL((mlp_fwd_kernel<64, 32, 1, 1, true>), grid, dim3(64), 0, s, x, K, x_bstride, w, K, sw, b, N, y, N, sy, M, N, K, act_mask);
-    else hipLaunchKernelGGL((mlp_fwd_kernel<64, 32, 1, 1, false>), grid, dim3(64), 0, s, x, K, x_bstride, w, K, sw, b, N, y, N, sy, M, N, K, act_mask);
-  } else {
-    auto go = [&](auto kv, auto kn, int BM, int BN) {
-      dim3 grid((N + BN - 1) / BN, (M + BM - 1) / BM, nb);
-      hipLaunchKernelGGL(decltype(kv)::value, grid, dim3(256), 0, s, x, K, x_bstride, w, K, sw, b, N, y, N, sy, M, N, K, act_mask);
-      (void)kn;
-    };
-    switch (dense_cfg()) {
-      case 1:
-        if (vec) go(KPtr<mlp_fwd_kernel<128, 64, 2, 2, true>>{}, 0, 128, 64);
-        else go(KPtr<mlp_fwd_kernel<128, 64, 2, 2, false>>{}, 0, 128, 64);
-        break;
-      case 2:
-        if (vec) go(KPtr<mlp_fwd_kernel<64, 128, 2, 2, true>>{}, 0, 64, 128);
-        else go(KPtr<mlp_fwd_kernel<64, 128, 2, 2, false>>{}, 0, 64, 128);
-        break;
-      case 3:
-        if (vec) go(KPtr<mlp_fwd_kernel<128, 64, 2, 2, true, 16>>{}, 0, 128, 64);
-        else go(KPtr<mlp_fwd_kernel<128, 64, 2, 2, false, 16>>{}, 0, 128, 64);
-        break;
-      case 4:
-        if (vec) go(KPtr<mlp_fwd_kernel<64, 64, 2, 2, true>>{}, 0, 64, 64);
-        else go(KPtr<mlp_fwd_kernel<64, 64, 2, 2, false>>{}, 0, 64, 64);
-        break;
-      default:
-        if (vec) go(KPtr<mlp_fwd_kernel<128, 128, 2, 2, true>>{}, 0, 128, 128);
-        else go(KPtr<mlp_fwd_kernel<128, 128, 2, 2, false>>{}, 0, 128, 128);
-    }
-  }
-  HIPCHK(hipGetLastError());
-  return MJL_OK;
-}
-
-extern "C" long long mjl_twin_dense_partial_rows(int M) { return M > 0 ? (M + 127) / 128 : 0; }
-
-extern "C" int mjl_twin_dense_dx_tanh(const float* g, const float* w, const float* y, int nb, int M, int N, int K,
-                                      float* dz, float* partials, void* stream) {
-  if (!g || !w || !y || !dz || !partials || nb <= 0 || nb > 32 || M < 0 || N <= 0 || K <= 0 || K % 4)
-    return fail(MJL_ERR_ARG, "bad argument");
-  if (M == 0) return MJL_OK;
-  if ((long long)nb * M * (N > K ? N : K) >= (1LL << 31)) return fail(MJL_ERR_ARG, "twin_dense_dx_tanh: stack too large");
-  if (!(aligned16(w) && aligned16(y) && aligned16(dz))) return fail(MJL_ERR_ARG, "twin_dense_dx_tanh: 16-byte alignment");
-  hipStream_t s = (hipStream_t)stream;
-  const bool vec = N % 4 == 0 && aligned16(g);
-  const long long sg = (long long)M * N, sw = (long long)N * K, sy = (long long)M * K;
-  auto go = [&](auto kv, int BN) {  // 128-row blocks always: the partial rows are per 128 rows
-    dim3 grid((K + BN - 1) / BN, (M + 127) / 128, nb);
-    hipLaunchKernelGGL(decltype(kv)::value, grid, dim3(256), 0, s, g, sg, w, sw, y, sy, dz, partials, M, N, K);
-  };
-  switch (dense_cfg()) {
-    case 1:
-    case 2:
-    case 4:
-      if (vec) go(KPtr<mlp_dx_tanh_kernel<128, 64, 2, 2, true>>{}, 64);
-      else go(KPtr<mlp_dx_tanh_kernel<128, 64, 2, 2, false>>{}, 64);
-      break;
-    case 3:
-      if (vec) go(KPtr<mlp_dx_tanh_kernel<128, 64, 2, 2, true, 16>>{}, 64);
-      else go(KPtr<mlp_dx_tanh_kernel<128, 64, 2, 2, false, 16>>{}, 64);
-      break;
-    default:
-      if (vec) go(KPtr<mlp_dx_tanh_kernel<128, 128, 2, 2, true>>{}, 128);
-      else go(KPtr<mlp_dx_tanh_kernel<128, 128, 2, 2, false>>{}, 128);
-  }
-  HIPCHK(hipGetLastError());
-  return MJL_OK;
-}
-
-extern "C" long long mjl_mlp_colpart_rows(int M) { return M > 0 ? (M + 127) / 128 : 0; }
-
-extern "C" int mjl_mlp_bwd(const float* g, const float* y, int M, int N, const float* w, int K, int act, float* dz,
-                           float* dx, float* colpart, void* stream) {
-  if (!g || !y || !dz || !colpart || M < 0 || N <= 0 || (dx && (!w || K <= 0 || K % 4 != 0)) ||
-      (act != MLP_ACT_NONE && act != MLP_ACT_TANH))
-    return fail(MJL_ERR_ARG, "bad argument");
-  if (M == 0) return MJL_OK;
-  hipStream_t s = (hipStream_t)stream;
-  const bool vec = N % 4 == 0 && aligned16(g) && aligned16(y) && aligned16(dz);
-  if (dx && !(aligned16(w) && aligned16(dx))) return fail(MJL_ERR_ARG, "mlp_bwd: 16-byte aligned w and dx expected");
-  const dim3 blk(256);
-  if (dx) {
-    dim3 grid((K + 127) / 128, (M + 127) / 128);
-    if (vec) hipLaunchKernelGGL((mlp_bwd_kernel<128, 128, 2, 2, true, true>), grid, blk, 0, s, g, y, N, w, K, dz, dx, K, colpart, M, N, K, act);
-    else hipLaunchKernelGGL((mlp_bwd_kernel<128, 128, 2, 2, true, false>), grid, blk, 0, s, g, y, N, w, K, dz, dx, K, colpart, M, N, K, act);
-  } else {
-    dim3 grid(1, (M + 127) / 128);
-    if (vec) hipLaunchKernelGGL((mlp_bwd_kernel<128, 128, 2, 2, false, true>), grid, blk, 0, s, g, y, N, w, 0, dz, nullptr, 0, colpart, M, N, 0, act);
-    else hipLaunchKernelGGL((mlp_bwd_kernel<128, 128, 2, 2, false, false>), grid, blk, 0, s, g, y, N, w, 0, dz, nullptr, 0, colpart, M, N, 0, act);
-  }
+  if (!advanced)
+    hipLaunchKernelGGL(step_counters_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream, step[0],
+                       ngroups > 1 ? step[1] : nullptr, ctr);
   HIPCHK(hipGetLastError());
   return MJL_OK;
 }

@@ -83,19 +83,21 @@ __device__ __forceinline__ void adv_merge_wave(const float* __restrict__ part, i
 // act and mean (contiguous: rows x A floats) come in through LDS with coalesced loads, and g_mean goes
 // out the same way (a thread per row striding A floats touched 64 lines per load); the partials are
 // per-wave butterfly sums, then the block's waves in order through LDS (one barrier for all A + 1).
-__global__ __launch_bounds__(kLossT) void ppo_surrogate_kernel(
+// RB rows (threads) per block.
+template <int RB>
+__global__ __launch_bounds__(RB) void ppo_surrogate_kernel(
     const float* __restrict__ mean, const float* __restrict__ log_std, const float* __restrict__ act,
     const float* __restrict__ old_logp, const float* __restrict__ adv, int n, int A, float clip_eps,
-    const float* __restrict__ adv_part, int nb, const float* __restrict__ adv_stats, float* __restrict__ gmean,
+    const float* __restrict__ adv_part, int nb_adv, const float* __restrict__ adv_stats, float* __restrict__ gmean,
     float* __restrict__ part, float ls_lo, float ls_hi, const int* __restrict__ stats_row) {
-  constexpr int NW = kLossT / 64;
-  __shared__ float sd[kLossT * kLossMaxA];  // a - m of the block's rows, row-major
-  __shared__ float sdl[kLossT];             // d logp per row
+  constexpr int NW = RB / 64;
+  __shared__ float sd[RB * kLossMaxA];  // a - m of the block's rows, row-major
+  __shared__ float sdl[RB];             // d logp per row
   __shared__ float wred[NW][kLossMaxA + 1];
   __shared__ float ivs[kLossMaxA], lsd[kLossMaxA], lss;
   __shared__ float mu_s, sd_s;
-  const int t = threadIdx.x, lane = t & 63, w = t >> 6, r0 = blockIdx.x * kLossT, i = r0 + t;
-  const int rows = min(kLossT, n - r0), cnt = rows * A;
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6, r0 = blockIdx.x * RB, i = r0 + t;
+  const int rows = min(RB, n - r0), cnt = rows * A;
   const size_t base = (size_t)r0 * A;
   // the row's own scalars first, then the staging loads 8 deep per thread (one load and LDS store
   // per trip left each thread ~42 dependent HBM round trips at 8,192 rows: 32 blocks, 13 us)
@@ -104,27 +106,27 @@ __global__ __launch_bounds__(kLossT) void ppo_surrogate_kernel(
   {
     constexpr int U = 8;
     int e = t;
-    for (; e + (U - 1) * kLossT < cnt; e += U * kLossT) {
+    for (; e + (U - 1) * RB < cnt; e += U * RB) {
       float d[U];
 #pragma unroll
-      for (int u = 0; u < U; u++) d[u] = act[base + e + u * kLossT] - mean[base + e + u * kLossT];
+      for (int u = 0; u < U; u++) d[u] = act[base + e + u * RB] - mean[base + e + u * RB];
 #pragma unroll
-      for (int u = 0; u < U; u++) sd[e + u * kLossT] = d[u];
+      for (int u = 0; u < U; u++) sd[e + u * RB] = d[u];
     }
-    for (; e < cnt; e += kLossT) sd[e] = act[base + e] - mean[base + e];
+    for (; e < cnt; e += RB) sd[e] = act[base + e] - mean[base + e];
   }
   if (t < A) {
     const float ls = fminf(fmaxf(log_std[t], ls_lo), ls_hi);  // networks.py:103's clip (bounds +-inf: none)
     lsd[t] = ls;
     ivs[t] = expf(-2.f * ls);
   }
-  if (w == 1) {  // the advantage statistics, beside the staging loads
+  if (w == (NW > 1 ? 1 : 0)) {  // the advantage statistics, beside the staging loads
     float mu, sdv;
     if (adv_stats) {  // global statistics (data-parallel); row *stats_row of a [n_minibatches, 2] table
       const float* st = adv_stats + (stats_row ? 2 * (size_t)*stats_row : 0);
       mu = st[0]; sdv = st[1];
     }
-    else adv_merge_wave(adv_part, nb, lane, mu, sdv);
+    else adv_merge_wave(adv_part, nb_adv, lane, mu, sdv);
     if (lane == 0) { mu_s = mu; sd_s = sdv; }
   }
   __syncthreads();
@@ -162,7 +164,7 @@ __global__ __launch_bounds__(kLossT) void ppo_surrogate_kernel(
     if (lane == 0) wred[w][1 + j] = c;
   }
   __syncthreads();
-  for (int e = t; e < cnt; e += kLossT) {
+  for (int e = t; e < cnt; e += RB) {
     const int r = e / A, j = e - r * A;
     gmean[base + e] = sdl[r] * sd[e] * ivs[j];
   }
@@ -182,8 +184,16 @@ __global__ __launch_bounds__(kLossT) void ppo_surrogate_kernel(
 __global__ __launch_bounds__(64) void ppo_surrogate_final_kernel(const float* __restrict__ part, int nb, int n, int A,
                                                                  const float* __restrict__ log_std, float ent_coef,
                                                                  float* __restrict__ loss, float* __restrict__ glog_std,
-                                                                 float ls_lo, float ls_hi) {
+                                                                 float ls_lo, float ls_hi, float* step0, float* step1,
+                                                                 int* ctr) {
   const int lane = threadIdx.x, col = blockIdx.x;
+  // the update graph's minibatch counters, advanced here (every read of the row in this minibatch
+  // step — gather, statistics — precedes this launch; Adam then takes the advanced step counts)
+  if (col == 0 && lane == 0) {
+    if (step0) *step0 += 1.f;
+    if (step1) *step1 += 1.f;
+    if (ctr) *ctr += 1;
+  }
   float s = 0.f;
   for (int b = lane; b < nb; b += 64) s += part[(size_t)b * (A + 1) + col];
   s = wave_sum(s);
@@ -303,23 +313,42 @@ __global__ __launch_bounds__(256) void slice_sum_multi_kernel(SliceSegs sg) {
 // ([M, A]), the value in column 0 of out[1] (v[r] = v[r * vstride]); g_mean = d loss / d mean
 // (mjl_ppo_surrogate). dz[0] = g_mean (1 - mean^2); dz[1][:, 0] = d mean((v - ret)^2) / d v =
 // 2 (v - ret) / M (mse_kernel's gradient: the value loss itself is not needed by the update);
-// dz[1][:, 1:] = 0 (the value's padded output rows get no gradient). 32-bit indices (M A < 2^30).
+// dz[1][:, 1:] = 0 (the value's padded output rows get no gradient). partials (or NULL): the output
+// biases' gradient, first stage — each net's dZ column sums per kHeadChunk-row chunk, [2][chunks][A].
+constexpr int kHeadChunk = 32;  // 512 blocks at the 8,192-row minibatch
 __global__ __launch_bounds__(256) void twin_head_bwd_kernel(const float* __restrict__ g_mean,
                                                             const float* __restrict__ mean,
                                                             const float* __restrict__ v, int vstride,
                                                             const float* __restrict__ ret, int M, int A,
-                                                            float* __restrict__ dz4) {
-  const unsigned i = blockIdx.x * blockDim.x + threadIdx.x;
-  const unsigned n = (unsigned)M * (unsigned)A;
-  if (i >= 2 * n) return;
-  if (i < n) {
-    const float y = mean[i];
-    dz4[i] = g_mean[i] * (1.f - y * y);
-  } else {
-    const unsigned j = i - n, r = j / (unsigned)A;
-    float g = 0.f;
-    if (j - r * (unsigned)A == 0) g = 2.f * (v[(size_t)r * vstride] - ret[r]) / (float)M;
-    dz4[i] = g;
+                                                            float* __restrict__ dz4, float* __restrict__ partials) {
+  // block (chunk c = blockIdx.x, net = blockIdx.y): rows [c * kHeadChunk, ...) of one net's dZ, thread t
+  // = row group t / A (every G-th row of the chunk, in order) x column t % A; then the groups in order
+  __shared__ float red[256];
+  const int net = blockIdx.y, G = 256 / A, t = threadIdx.x, grp = t / A, j = t - grp * A;
+  const int r0 = blockIdx.x * kHeadChunk, r1 = min(M, r0 + kHeadChunk);
+  float s = 0.f;
+  if (grp < G) {
+    float* out = dz4 + (size_t)net * M * A;
+    for (int r = r0 + grp; r < r1; r += G) {
+      const size_t o = (size_t)r * A + j;
+      float d;
+      if (net == 0) {
+        const float y = mean[o];
+        d = g_mean[o] * (1.f - y * y);
+      } else {
+        d = j == 0 ? 2.f * (v[(size_t)r * vstride] - ret[r]) / (float)M : 0.f;
+      }
+      out[o] = d;
+      s += d;
+    }
+  }
+  if (!partials) return;  // (uniform over the launch)
+  red[t] = s;
+  __syncthreads();
+  if (t < A) {
+    float acc = red[t];
+    for (int q = 1; q < G; q++) acc += red[q * A + t];
+    partials[((size_t)net * gridDim.x + blockIdx.x) * A + t] = acc;
   }
 }
 
@@ -339,9 +368,10 @@ __global__ __launch_bounds__(256) void bias_act_kernel(float* __restrict__ x, co
   const int j = (int)(e % (unsigned)n);
   const bool th = (act_mask >> b) & 1u;
   const float* bb = bias + (size_t)b * n + j;
-  if constexpr (V == 4) {
+  if constexpr (V == 4) {  // (the launcher checks 16-byte alignment of x and bias)
     float4 v = reinterpret_cast<float4*>(x)[q];
-    v.x += bb[0]; v.y += bb[1]; v.z += bb[2]; v.w += bb[3];
+    const float4 c = *reinterpret_cast<const float4*>(bb);
+    v.x += c.x; v.y += c.y; v.z += c.z; v.w += c.w;
     if (th) { v.x = tanhf(v.x); v.y = tanhf(v.y); v.z = tanhf(v.z); v.w = tanhf(v.w); }
     reinterpret_cast<float4*>(x)[q] = v;
   } else {
@@ -361,10 +391,11 @@ __global__ __launch_bounds__(256) void tanh_inplace_kernel(float* __restrict__ x
 }
 
 // minibatch gather: dst_k[r] = src_k[idx[r]] for up to 5 row-major arrays of `cols_k` columns
+constexpr int kGatherMax = 8;
 struct GatherArgs {
-  const float* src[5];
-  float* dst[5];
-  int cols[5];
+  const float* src[kGatherMax];
+  float* dst[kGatherMax];
+  int cols[kGatherMax];
   int narr;
 };
 __global__ __launch_bounds__(256) void gather_rows_kernel(const long long* __restrict__ idx, int n, long long nsrc,
@@ -440,6 +471,7 @@ struct AdamMultiArgs {
   float lr[kAdamMaxGroups];
   const float* step[kAdamMaxGroups];
   float b1, b2, eps, gscale;
+  float tadd;  // t = *step + tadd: 1, or 0 when the counters were advanced before this launch
 };
 __global__ __launch_bounds__(256) void adam_multi_kernel(AdamMultiArgs a) {
   const int b = blockIdx.x;
@@ -448,7 +480,7 @@ __global__ __launch_bounds__(256) void adam_multi_kernel(AdamMultiArgs a) {
   const long long j = (long long)(b - a.blk[k]) * blockDim.x + threadIdx.x;
   if (j >= a.numel[k] || !a.g[k]) return;
   const int gi = a.grp[k];
-  const float t = *a.step[gi] + 1.f;
+  const float t = *a.step[gi] + a.tadd;
   const float step_size = a.lr[gi] / (1.f - powf(a.b1, t));
   const float bc2_sqrt = sqrtf(1.f - powf(a.b2, t));
   const float g = a.g[k][j] * a.gscale;

@@ -29,11 +29,11 @@ EXPORTS = [
     "mjl_step_vjp_full", "mjl_env_step_vjp_full", "mjl_env_fill_reset_pool",
     "mjl_apg_obs", "mjl_apg_post", "mjl_apg_obs_vjp", "mjl_env_step_record", "mjl_env_step_vjp_replay",
     "mjl_ppo_loss_scratch", "mjl_ppo_surrogate", "mjl_mse", "mjl_gather_rows", "mjl_adam",
-    "mjl_adam_dev", "mjl_mlp_fwd", "mjl_mlp_colpart_rows", "mjl_mlp_bwd",
+    "mjl_adam_dev",
     "mjl_colsum_batched_scratch", "mjl_colsum_batched", "mjl_tanh_bwd_colsum_batched", "mjl_slice_sum_batched",
     "mjl_twin_head_bwd", "mjl_mse_strided", "mjl_ppo_surrogate_clipped", "mjl_bias_act", "mjl_adam_multi",
     "mjl_gather_rows_indexed", "mjl_slice_sum_multi", "mjl_colsum_partials", "mjl_tanh_bwd_colsum_partials",
-    "mjl_twin_dense_fwd", "mjl_twin_dense_partial_rows", "mjl_twin_dense_dx_tanh",
+    "mjl_twin_head_partial_rows",
 ]
 
 _lib = None
@@ -99,10 +99,6 @@ def lib() -> C.CDLL:
     L.mjl_gather_rows.argtypes = [vp, i32, C.c_longlong, i32, vp, vp, vp, vp]
     L.mjl_adam.argtypes = [i32, vp, vp, vp, vp, vp, C.c_float, C.c_float, C.c_float, C.c_float, i32, vp]
     L.mjl_adam_dev.argtypes = [i32, vp, vp, vp, vp, vp, C.c_float, C.c_float, C.c_float, C.c_float, vp, vp]
-    L.mjl_mlp_fwd.argtypes = [vp, i32, vp, vp, i32, i32, i32, i32, vp, vp]
-    L.mjl_mlp_colpart_rows.argtypes = [i32]
-    L.mjl_mlp_colpart_rows.restype = C.c_longlong
-    L.mjl_mlp_bwd.argtypes = [vp, vp, i32, i32, vp, i32, i32, vp, vp, vp, vp]
     L.mjl_env_step_record.argtypes = [vp, i32, vp, vp, vp, vp, vp, vp]
     L.mjl_env_step_vjp_replay.argtypes = [vp, i32] + [vp] * 12 + [vp]
     L.mjl_apg_obs.argtypes = [vp, vp, vp, vp, i32, vp, vp, vp, vp]
@@ -132,20 +128,18 @@ def lib() -> C.CDLL:
     L.mjl_colsum_batched.argtypes = [f32p, i32, i32, i32, f32p, f32p, vp]
     L.mjl_tanh_bwd_colsum_batched.argtypes = [f32p, f32p, i32, i32, i32, f32p, f32p, f32p, vp]
     L.mjl_slice_sum_batched.argtypes = [f32p, i32, i32, C.c_longlong, f32p, vp]
-    L.mjl_twin_head_bwd.argtypes = [f32p, f32p, f32p, i32, f32p, i32, i32, f32p, vp]
+    L.mjl_twin_head_bwd.argtypes = [f32p, f32p, f32p, i32, f32p, i32, i32, f32p, vp, vp]
+    L.mjl_twin_head_partial_rows.argtypes = [i32]
+    L.mjl_twin_head_partial_rows.restype = C.c_longlong
     L.mjl_mse_strided.argtypes = [vp, i32, vp, i32, vp, vp, vp, vp]
     L.mjl_bias_act.argtypes = [vp, vp, i32, C.c_longlong, i32, C.c_uint, vp]
     L.mjl_adam_multi.argtypes = [i32, vp, vp, vp, vp, vp, vp, i32, vp, C.c_float, C.c_float, C.c_float, C.c_float,
-                                 vp, vp, vp]
+                                 vp, vp, i32, vp]
     L.mjl_ppo_surrogate_clipped.argtypes = [vp, vp, vp, vp, vp, vp, vp, i32, i32, C.c_float, C.c_float, C.c_float,
-                                            C.c_float, vp, vp, vp, vp, vp]
+                                            C.c_float, vp, vp, vp, vp, vp, vp, vp, vp]
     L.mjl_gather_rows_indexed.argtypes = [vp, vp, i32, C.c_longlong, i32, vp, vp, vp, vp]
     L.mjl_slice_sum_multi.argtypes = [i32, vp, vp, vp, vp, vp, vp]
     L.mjl_colsum_partials.argtypes = [vp, i32, i32, i32, i32, vp, vp]
-    L.mjl_twin_dense_fwd.argtypes = [vp, C.c_longlong, vp, vp, i32, i32, i32, i32, C.c_uint, vp, vp]
-    L.mjl_twin_dense_partial_rows.argtypes = [i32]
-    L.mjl_twin_dense_partial_rows.restype = C.c_longlong
-    L.mjl_twin_dense_dx_tanh.argtypes = [vp, vp, vp, i32, i32, i32, i32, vp, vp, vp]
     L.mjl_tanh_bwd_colsum_partials.argtypes = [vp, vp, i32, i32, i32, i32, vp, vp, vp]
     L.mjl_small_mlp_fwd.argtypes = [vp, i32, i32, i32, vp, vp, vp, vp, vp]
     L.mjl_small_mlp_bwd_input.argtypes = [vp, i32, i32, i32, vp, vp, vp, vp, vp]

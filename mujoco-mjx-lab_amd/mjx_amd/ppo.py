@@ -169,89 +169,12 @@ def _linear(lin: nn.Linear, x: torch.Tensor) -> torch.Tensor:
     return lin(x)
 
 
-# the dense layers on mjl_mlp_fwd / mjl_mlp_bwd (MJL_FUSED_MLP=1): off by default — measured against
-# hipBLASLt + torch's elementwise passes: equal at the 65,536-row minibatch (26.1 vs
-# 26.3 ms per C3 update), slower at the 8,192-row per-rank minibatch of C5 on 8 GPUs (64.5 vs 53.9 ms)
-FUSED_MLP = os.environ.get("MJL_FUSED_MLP", "0") == "1"
-_MLP_ACT = {"tanh": 1, "linear": 0, "none": 0}
-
-
-class _FusedMLP(torch.autograd.Function):
-    """A whole MLP (src/networks.py:55-61: Dense + activation per layer) on the native dense-layer
-    kernels: forward y_l = act_l(y_{l-1} W_l^T + b_l) with bias and tanh in the GEMM epilogue
-    (mjl_mlp_fwd); backward per layer, from the top, dz_l = g (1 - y_l^2) fused into the GEMM
-    dx = dz_l W_l with the bias gradient's per-block column sums on the way (mjl_mlp_bwd), the weight
-    gradient dz_l^T y_{l-1} as split-K batched GEMMs + a sum (as _SplitKLinear), the bias gradient a
-    fixed-order column sum. Where torch ran a GEMM, a tanh pass and, in the backward, a tanh-backward
-    pass and a column-sum pass per layer."""
-
-    @staticmethod
-    def forward(ctx, x, acts, *params):
-        from ._lib import check, lib
-        L = lib()
-        st = torch.cuda.current_stream(x.device).cuda_stream
-        h = x.contiguous()
-        M = h.shape[0]
-        ys = []
-        for l, act in enumerate(acts):
-            w, b = params[2 * l], params[2 * l + 1]
-            N, K = w.shape
-            y = torch.empty((M, N), dtype=torch.float32, device=x.device)
-            check(L.mjl_mlp_fwd(h.data_ptr(), K, w.data_ptr(), b.data_ptr(), M, N, K, act, y.data_ptr(), st))
-            ys.append(y)
-            h = y
-        ctx.acts = acts
-        ctx.save_for_backward(x.contiguous(), *params, *ys)
-        return h
-
-    @staticmethod
-    def backward(ctx, g):
-        from ._lib import check, lib
-        L = lib()
-        acts = ctx.acts
-        nl = len(acts)
-        saved = ctx.saved_tensors
-        x, params, ys = saved[0], saved[1:1 + 2 * nl], saved[1 + 2 * nl:]
-        st = torch.cuda.current_stream(x.device).cuda_stream
-        M = x.shape[0]
-        rows = int(L.mjl_mlp_colpart_rows(M))
-        grads = [None] * (2 * nl)
-        g = g.contiguous()
-        gx = None
-        for l in range(nl - 1, -1, -1):
-            w = params[2 * l]
-            N, K = w.shape
-            xin = x if l == 0 else ys[l - 1]
-            dz = torch.empty((M, N), dtype=torch.float32, device=x.device)
-            part = torch.empty((rows, N), dtype=torch.float32, device=x.device)
-            want_dx = l > 0 or ctx.needs_input_grad[0]
-            dx = torch.empty((M, K), dtype=torch.float32, device=x.device) if want_dx else None
-            check(L.mjl_mlp_bwd(g.data_ptr(), ys[l].data_ptr(), M, N, w.data_ptr() if want_dx else None, K, acts[l],
-                                dz.data_ptr(), dx.data_ptr() if want_dx else None, part.data_ptr(), st))
-            s = min(64, max(1, M // SPLIT_ROWS))
-            if M % s:
-                s = 1
-            grads[2 * l] = slice_sum_native(torch.bmm(dz.reshape(s, M // s, N).transpose(1, 2), xin.reshape(s, M // s, K)))
-            grads[2 * l + 1] = colsum_native(part) if N > 1 else part.sum(0)
-            g = dx
-            if l == 0:
-                gx = dx
-        return (gx, None, *grads)
-
-
-def _fused_ok(mlp, x) -> bool:
-    return (FUSED_MLP and x.is_cuda and x.dim() == 2 and x.shape[0] >= UPDATE_MIN_ROWS and x.dtype == torch.float32
-            and all(a in _MLP_ACT for a in mlp.acts)
-            and all(p.dtype == torch.float32 and p.is_contiguous() for p in mlp.parameters())
-            and all(lin.out_features % 4 == 0 or lin is mlp.layers[-1] for lin in mlp.layers)
-            and (not x.requires_grad or mlp.layers[0].in_features % 4 == 0))
-
-
 class MLP(nn.Module):
     """src/networks.py:22-61: layers of (features, activation); Glorot-normal weights
     N(0, 2/(in+out)), zero biases (networks.py:32-53). Unknown activations fall back to tanh.
     Batches of >= UPDATE_MIN_ROWS rows on the GPU (the PPO update's minibatches, the value pass over
-    the rollout) run on the native dense-layer kernels (_FusedMLP)."""
+    the rollout) take the split-K weight gradient and the native tanh-backward + bias-gradient pass
+    (_TanhSplitKLinear)."""
 
     def __init__(self, in_dim: int, layer_specs: Sequence[Tuple[int, str]], generator: Optional[torch.Generator] = None):
         super().__init__()
@@ -268,14 +191,6 @@ class MLP(nn.Module):
 
     def forward(self, x, out_tanh: bool = False):
         """out_tanh: a tanh after the last layer (GaussianPolicy's mean, networks.py:103)."""
-        if _fused_ok(self, x):
-            acts = tuple(_MLP_ACT[a] for a in self.acts)
-            if out_tanh:
-                if acts[-1] != 0:
-                    raise ValueError("out_tanh after an activated last layer")
-                acts = acts[:-1] + (1,)
-            params = [t for lin in self.layers for t in (lin.weight, lin.bias)]
-            return _FusedMLP.apply(x, acts, *params)
         last = len(self.layers) - 1
         for l, (lin, a) in enumerate(zip(self.layers, self.acts)):
             act = ACTIVATIONS.get(a, torch.tanh)
@@ -619,24 +534,32 @@ def value_loss(value, obs, returns):
     return torch.mean((v - returns) ** 2)
 
 
-def _gather_minibatch(idx, *arrays, row: Optional[torch.Tensor] = None):
+def _gather_minibatch(idx, *arrays, row: Optional[torch.Tensor] = None, twice_first: bool = False):
     """arrays[k][idx] for every k, as one native launch (mjl_gather_rows) on the GPU. With `row` (a
     device int32), idx is an [n_minibatches, rows] table and the launch gathers row *row of it, read
-    when the launch runs (a captured minibatch step; mjl_gather_rows_indexed)."""
+    when the launch runs (a captured minibatch step; mjl_gather_rows_indexed). twice_first (with
+    row): the first array's rows are written twice, as one [2, rows, ...] block (the twin update's
+    observations, one copy per net)."""
     if row is not None:
         import ctypes
         from ._lib import check, lib
         n = idx.shape[1]
-        outs = tuple(torch.empty((n,) + tuple(a.shape[1:]), dtype=a.dtype, device=a.device) for a in arrays)
-        k = len(arrays)
+        outs = [torch.empty((n,) + tuple(a.shape[1:]), dtype=a.dtype, device=a.device) for a in arrays]
+        dsts, srcs = list(outs), list(arrays)
+        if twice_first:
+            a0 = arrays[0]
+            outs[0] = torch.empty((2, n) + tuple(a0.shape[1:]), dtype=a0.dtype, device=a0.device)
+            dsts = [outs[0][0], outs[0][1]] + outs[1:]
+            srcs = [a0] + list(arrays)
+        k = len(srcs)
         check(lib().mjl_gather_rows_indexed(idx.data_ptr(), ctypes.c_void_p(row.data_ptr()), n,
                                             min(a.shape[0] for a in arrays), k,
-                                            (ctypes.c_void_p * k)(*[a.data_ptr() for a in arrays]),
-                                            (ctypes.c_void_p * k)(*[o.data_ptr() for o in outs]),
-                                            (ctypes.c_int * k)(*[max(1, a[0].numel()) for a in arrays]),
+                                            (ctypes.c_void_p * k)(*[a.data_ptr() for a in srcs]),
+                                            (ctypes.c_void_p * k)(*[o.data_ptr() for o in dsts]),
+                                            (ctypes.c_int * k)(*[max(1, a[0].numel()) for a in srcs]),
                                             torch.cuda.current_stream(idx.device).cuda_stream))
-        return outs
-    if not (idx.is_cuda and idx.dtype == torch.int64 and len(arrays) <= 5
+        return tuple(outs)
+    if not (idx.is_cuda and idx.dtype == torch.int64 and len(arrays) <= 8
             and all(a.is_cuda and a.dtype == torch.float32 and a.is_contiguous() for a in arrays)):
         return tuple(a[idx] for a in arrays)
     import ctypes
@@ -752,11 +675,12 @@ class NativeAdam:
 
 
 @torch.no_grad()
-def adam_steps(pairs, gscale: float = 1.0, ctr: Optional[torch.Tensor] = None):
+def adam_steps(pairs, gscale: float = 1.0, ctr: Optional[torch.Tensor] = None, advanced: bool = False):
     """One Adam step of each (NativeAdam, grads or None for the parameters' .grad) in ONE launch
     (mjl_adam_multi, up to 2 optimisers with the same betas / eps; plus a one-thread launch advancing
     the step counters), gradients scaled by gscale; `ctr` (device int32, optional) is advanced with
-    the step counters."""
+    the step counters. advanced: the counters (and ctr) were already advanced in this minibatch step
+    (the twin update's loss launch does it in the captured graphs): no counter launch."""
     import ctypes
     from ._lib import check, lib
     o0 = pairs[0][0]
@@ -778,7 +702,7 @@ def adam_steps(pairs, gscale: float = 1.0, ctr: Optional[torch.Tensor] = None):
                                (ctypes.c_longlong * k)(*ns), (ctypes.c_int * k)(*grp), len(pairs),
                                (ctypes.c_float * len(pairs))(*[o.lr for o, _ in pairs]), o0.betas[0], o0.betas[1],
                                o0.eps, float(gscale), (ctypes.c_void_p * len(pairs))(*[o.step_t.data_ptr() for o, _ in pairs]),
-                               None if ctr is None else ctypes.c_void_p(ctr.data_ptr()),
+                               None if ctr is None else ctypes.c_void_p(ctr.data_ptr()), int(advanced),
                                torch.cuda.current_stream(dev).cuda_stream))
     for opt, _ in pairs:
         opt._keep = gs  # the launch reads the gradients asynchronously
@@ -923,14 +847,17 @@ class PPOUpdater:
         graphs), idx and st are the whole update's [n_minibatches, ...] tables, read at row *row, which
         the Adam launch advances: the replays need no per-minibatch host copies."""
         cfg, opt_p, opt_v = self.cfg, self.opt_p, self.opt_v
-        o, a, ol, r, ad = _gather_minibatch(idx, *src, row=row)
+        o, a, ol, r, ad = _gather_minibatch(idx, *src, row=row, twice_first=self._tw and row is not None)
         dp = self.dist is not None
         if self._tw:
             tw = self.twin
-            tw.forward_backward(o, a, ol, r, ad, st, cfg.clip_eps, cfg.ent_coef, min(64, o.shape[0] // SPLIT_ROWS),
-                                stats_row=row)
+            # captured (row given): the loss launch advances the step counters and the row, Adam
+            # takes them as they are
+            ctrs = (opt_p.step_t, opt_v.step_t, row) if row is not None else None
+            tw.forward_backward(o, a, ol, r, ad, st, cfg.clip_eps, cfg.ent_coef, min(64, o.shape[-2] // SPLIT_ROWS),
+                                stats_row=row, counters=ctrs)
             if not dp:  # both nets' Adam steps in one launch
-                adam_steps([(opt_p, tw.grads_p), (opt_v, tw.grads_v)], ctr=row)
+                adam_steps([(opt_p, tw.grads_p), (opt_v, tw.grads_v)], advanced=ctrs is not None)
             return
         if self.side is not None:
             cur = torch.cuda.current_stream(o.device)
@@ -965,7 +892,10 @@ class PPOUpdater:
         if isinstance(self.opt_p, NativeAdam) and isinstance(self.opt_v, NativeAdam):
             # the all-reduced sum -> mean inside the one Adam launch of both nets
             gp, gv = (self.twin.grads_p, self.twin.grads_v) if self._tw else (self.views_p, self.views_v)
-            adam_steps([(self.opt_p, gp), (self.opt_v, gv)], gscale=1.0 / self.world, ctr=row)
+            if row is not None and self._tw:  # (the twin loss launch advanced the counters and the row)
+                adam_steps([(self.opt_p, gp), (self.opt_v, gv)], gscale=1.0 / self.world, advanced=True)
+            else:
+                adam_steps([(self.opt_p, gp), (self.opt_v, gv)], gscale=1.0 / self.world, ctr=row)
             return
         self.flat.div_(self.world)
         if isinstance(self.opt_p, NativeAdam):

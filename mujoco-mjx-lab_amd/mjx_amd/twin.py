@@ -36,12 +36,8 @@ import torch
 from ._lib import check, lib
 
 TWIN_UPDATE = os.environ.get("MJL_TWIN_UPDATE", "1") != "0"
-# rows per column-sum partial (first stage) of the output layer's bias gradient
-COLSUM_CHUNK = int(os.environ.get("MJL_TWIN_COLSUM_CHUNK", "32"))
-# the layers on the native dense kernels (mjl_twin_dense_fwd / mjl_twin_dense_dx_tanh: bias + tanh in
-# the forward GEMM's epilogue, tanh' and the bias-gradient partials in the input-gradient GEMM's);
-# 0: bias-less torch.bmm + the separate bias/tanh and tanh-backward passes
-DENSE = os.environ.get("MJL_TWIN_DENSE", "0") == "1"
+# rows per column-sum partial (the bias gradients' first stage); 32 and 64 measured no faster
+COLSUM_CHUNK = int(os.environ.get("MJL_TWIN_COLSUM_CHUNK", "128"))
 
 
 def _align4(n: int) -> int:
@@ -130,32 +126,28 @@ class TwinNets:
         return t
 
     def forward_backward(self, o, acts, old_logp, ret, adv, adv_stats, clip_eps: float, ent_coef: float, splits: int,
-                         want_value_loss: bool = False, stats_row=None):
-        """Both nets' losses and gradients for one minibatch (o [M, K0], acts [M, A], old_logp / ret /
-        adv [M]); the gradients into self.grad. Returns (policy loss, value loss) device scalars (the
-        value loss only with want_value_loss: the update does not need it). stats_row: adv_stats is the
-        [n_minibatches, 2] table, read at that device row."""
+                         want_value_loss: bool = False, stats_row=None, counters=None):
+        """Both nets' losses and gradients for one minibatch (o [M, K0] — or [2, M, K0], the same rows
+        twice, as the update's gather writes them —, acts [M, A], old_logp / ret / adv [M]); the
+        gradients into self.grad. Returns (policy loss, value loss) device scalars (the value loss only
+        with want_value_loss: the update does not need it). stats_row: adv_stats is the
+        [n_minibatches, 2] table, read at that device row. counters: (policy step, value step, row)
+        device counters that the loss launch advances (the captured update; Adam then runs with
+        advanced=True)."""
         L = lib()
         dev = o.device
         st = torch.cuda.current_stream(dev).cuda_stream
-        M, A, nl = o.shape[0], self.A, self.nl
+        M, A, nl = o.shape[-2], self.A, self.nl
         s = splits
-        dense = DENSE and o.is_contiguous()
-        # ---- forward: bias and tanh in the GEMM's epilogue (dense), or bias-less batched GEMMs + one
-        # native bias/tanh pass (mjl_bias_act)
-        x = o.unsqueeze(0).expand(2, M, self.K0)  # both nets read the same observations (batch stride 0)
+        # ---- forward: bias-less batched GEMMs, the bias and tanh in one native pass (mjl_bias_act).
+        # Both nets read the same observations: a batch-stride-0 view, or the gathered copy per net
+        # (which the first layer's weight-gradient slices can then read without an expand copy)
+        x = o if o.dim() == 3 else o.unsqueeze(0).expand(2, M, self.K0)
         hs = [x]
         for l in range(nl):
-            N, K = self.W[l].shape[1], self.W[l].shape[2]
+            h = torch.bmm(hs[-1], self.W[l].transpose(1, 2))
             mask = 3 if l < nl - 1 else 1  # the output layer: tanh for the policy's mean, linear value
-            if dense:
-                h = torch.empty((2, M, N), device=dev)
-                xs = hs[-1]
-                check(L.mjl_twin_dense_fwd(xs.data_ptr(), 0 if l == 0 else M * K, self.W[l].data_ptr(),
-                                           self.b[l].data_ptr(), 2, M, N, K, mask, h.data_ptr(), st))
-            else:
-                h = torch.bmm(hs[-1], self.W[l].transpose(1, 2))
-                check(L.mjl_bias_act(h.data_ptr(), self.b[l].data_ptr(), 2, M, N, mask, st))
+            check(L.mjl_bias_act(h.data_ptr(), self.b[l].data_ptr(), 2, M, h.shape[2], mask, st))
             hs.append(h)
         z = hs.pop()  # [2, M, A]
         mean = z[0]
@@ -165,57 +157,55 @@ class TwinNets:
         loss_v = torch.empty((), device=dev)
         gm = torch.empty((M, A), device=dev)
         scr = self._scratch("loss", int(L.mjl_ppo_loss_scratch(M, A)))
+        c0, c1, c2 = (None, None, None) if counters is None else (c.data_ptr() for c in counters)
         check(L.mjl_ppo_surrogate_clipped(mean.data_ptr(), log_std.data_ptr(), acts.data_ptr(), old_logp.data_ptr(),
                                           adv.data_ptr(), None if adv_stats is None else adv_stats.data_ptr(),
                                           None if stats_row is None else stats_row.data_ptr(), M, A,
                                           float(clip_eps), float(ent_coef), -20.0, 2.0, scr.data_ptr(),
-                                          loss_p.data_ptr(), gm.data_ptr(), self.g_log_std.data_ptr(), st))
+                                          loss_p.data_ptr(), gm.data_ptr(), self.g_log_std.data_ptr(), c0, c1, c2, st))
         if want_value_loss:  # (reporting only: the value gradient comes from the head kernel below)
             gv = torch.empty(M, device=dev)
             scr_v = self._scratch("mse", M // 256 + 1)
             check(L.mjl_mse_strided(z[1].data_ptr(), A, ret.data_ptr(), M, scr_v.data_ptr(), loss_v.data_ptr(),
                                     gv.data_ptr(), st))
-        # ---- backward: dZ of both output layers, the value's 2 (v - ret) / M formed in the same pass
-        dz = torch.empty((2, M, A), device=dev)
-        check(L.mjl_twin_head_bwd(gm.data_ptr(), mean.data_ptr(), z[1].data_ptr(), A, ret.data_ptr(), M, A,
-                                  dz.data_ptr(), st))
-        # every reduction's first stage here; their second stages (column-sum chunk partials, split-K
-        # weight-gradient slices) all in ONE launch after the last layer (mjl_slice_sum_multi)
+        # ---- backward: dZ of both output layers, the value's 2 (v - ret) / M formed in the same pass,
+        # with the output biases' column-sum partials.
+        # Every reduction's first stage comes here; their second stages (column-sum chunk partials,
+        # split-K weight-gradient slices) all in ONE launch after the last layer (mjl_slice_sum_multi)
         segs = []  # (x, out, nb, ns, m)
-        ch = COLSUM_CHUNK if M % COLSUM_CHUNK == 0 else M
+        dz = torch.empty((2, M, A), device=dev)
+        Rh = int(L.mjl_twin_head_partial_rows(M))
+        cs = self._scratch(f"cs{nl - 1}", 2 * Rh * A)
+        check(L.mjl_twin_head_bwd(gm.data_ptr(), mean.data_ptr(), z[1].data_ptr(), A, ret.data_ptr(), M, A,
+                                  dz.data_ptr(), cs.data_ptr(), st))
+        segs.append((cs, self.gb[nl - 1], 2, Rh, A))
+        # (32-row chunks — 4x the blocks — where the minibatch is small: 8.4 against 9.0 us per pass
+        # at 8,192 rows; at 65,536 the 4x partials cost more than they gain)
+        ch = COLSUM_CHUNK if M > 16384 else 32
+        ch = ch if M % ch == 0 else M
         R = M // ch  # column-sum partial rows per matrix
-        cs = self._scratch(f"cs{nl - 1}", 2 * R * A)
-        check(L.mjl_colsum_partials(dz.data_ptr(), 2, M, A, ch, cs.data_ptr(), st))
-        segs.append((cs, self.gb[nl - 1], 2, R, A))
         g = dz
-        Rd = int(L.mjl_twin_dense_partial_rows(M))
         for l in range(nl - 1, -1, -1):
             N, K = self.W[l].shape[1], self.W[l].shape[2]
             xin = hs[l]  # the layer's input: H_{l-1}, or the observations for l = 0
             # split-K slices of the weight gradient: the thin layers (the 21 / 1-unit outputs, the 54-wide
             # input) are a few output tiles per slice, so they take more, shorter slices
             s = splits if (N >= 64 and K >= 64) else max(splits, min(64, M // 256))
-            if l < nl - 1 and not dense:  # tanh layer: dZ = dH (1 - H^2) and the bias gradient's partials
+            if l < nl - 1:  # tanh layer: dZ = dH (1 - H^2) and the bias gradient's partials in one pass
                 dzl = torch.empty_like(g)
                 cs = self._scratch(f"cs{l}", 2 * R * N)
                 check(L.mjl_tanh_bwd_colsum_partials(g.data_ptr(), hs[l + 1].data_ptr(), 2, M, N, ch, dzl.data_ptr(),
                                                      cs.data_ptr(), st))
                 segs.append((cs, self.gb[l], 2, R, N))
-            else:  # the output layer's dZ, or (dense) the one the layer above's input-gradient GEMM formed
+            else:
                 dzl = g
-            if l == 0:  # the shared observations: [2, M, K0] with batch stride 0 -> per split, both nets
+            if l == 0 and o.dim() == 2:  # batch stride 0 -> per split, both nets (an expand copy)
                 xs = o.view(1, s, M // s, K).expand(2, s, M // s, K).reshape(2 * s, M // s, K)
             else:
                 xs = xin.view(2 * s, M // s, K)
             part = torch.bmm(dzl.view(2 * s, M // s, N).transpose(1, 2), xs)  # [2s, N, K]
             segs.append((part, self.gW[l], 2, s, N * K))
-            if l > 0 and dense:  # dZ of the layer below = (dZ W) (1 - H^2), its bias partials on the way
-                g = torch.empty((2, M, K), device=dev)
-                cs = self._scratch(f"csd{l - 1}", 2 * Rd * K)
-                check(L.mjl_twin_dense_dx_tanh(dzl.data_ptr(), self.W[l].data_ptr(), xin.data_ptr(), 2, M, N, K,
-                                               g.data_ptr(), cs.data_ptr(), st))
-                segs.append((cs, self.gb[l - 1], 2, Rd, K))
-            elif l > 0:
+            if l > 0:
                 g = torch.bmm(dzl, self.W[l])  # [2, M, K]
         import ctypes
         k = len(segs)

@@ -31,10 +31,11 @@ def _data(n, seed=1):
             torch.randn(n, generator=gd, device="cuda"), torch.randn(n, generator=gd, device="cuda"))
 
 
-@pytest.mark.parametrize("dense", [True, False])
+@pytest.mark.parametrize("dup", [False, True])
 @pytest.mark.parametrize("n", [8192, 65536])
-def test_twin_gradients_match_float64_autograd(n, dense, monkeypatch):
-    monkeypatch.setattr(twin, "DENSE", dense)
+def test_twin_gradients_match_float64_autograd(n, dup):
+    """dup: the observations handed over as the [2, M, K0] block the graphed update's gather writes
+    (one copy per net) instead of one [M, K0] matrix read through a batch-stride-0 view."""
     cfg = reference_ppo_config()
     pol, val = _nets(cfg)
     ref_p = ppo.GaussianPolicy(54, 21, cfg.policy_hidden_layer_specs).cuda().double()
@@ -44,7 +45,7 @@ def test_twin_gradients_match_float64_autograd(n, dense, monkeypatch):
     assert twin.TwinNets.eligible(pol, val)
     tw = twin.TwinNets(pol, val)
     o, a, ol, r, ad = _data(n)
-    lp, lv = tw.forward_backward(o, a, ol, r, ad, None, cfg.clip_eps, cfg.ent_coef, min(64, n // ppo.SPLIT_ROWS),
+    lp, lv = tw.forward_backward(o.unsqueeze(0).expand(2, n, 54).contiguous() if dup else o, a, ol, r, ad, None, cfg.clip_eps, cfg.ent_coef, min(64, n // ppo.SPLIT_ROWS),
                                  want_value_loss=True)
     torch.cuda.synchronize()
     old = ppo.NATIVE_LOSSES

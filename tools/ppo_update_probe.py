@@ -145,7 +145,7 @@ def shard_twin(reps: int = 5, envs: int = 1024):
 
 def twin_chunk(reps: int = 5, envs: int = 1024, chunks=(128, 64, 32), mbs=(8192, 65536), attr="COLSUM_CHUNK"):
     """Graph-replayed twin updates at several values of a twin-module setting (attr: twin.COLSUM_CHUNK,
-    the column-sum partial chunk, or twin.DENSE; read when a minibatch step is captured), interleaved:
+    the column-sum partial chunk; read when a minibatch step is captured), interleaved:
     C5's per-rank shard and C3's single-process update."""
     from mjx_amd import twin
     cfg = reference_ppo_config()
@@ -248,11 +248,11 @@ if __name__ == "__main__":
     if len(sys.argv) > 1 and sys.argv[1] == "shard":
         shard()
         sys.exit(0)
-    if len(sys.argv) > 1 and sys.argv[1] == "c5twin":  # the C5-shape twin update alone (for kernel traces)
-        twin_chunk(chunks=(32,), mbs=(8192,))
+    if len(sys.argv) > 1 and sys.argv[1] == "twinonly":  # the twin update alone at C5's and C3's shapes
+        twin_chunk(chunks=(128,))
         sys.exit(0)
-    if len(sys.argv) > 1 and sys.argv[1] == "dense":
-        twin_chunk(chunks=(True, False), attr="DENSE")
+    if len(sys.argv) > 1 and sys.argv[1] == "c5twin":  # the C5-shape twin update alone (for kernel traces)
+        twin_chunk(chunks=(128,), mbs=(8192,))
         sys.exit(0)
     if len(sys.argv) > 1 and sys.argv[1] == "chunk":
         twin_chunk()
