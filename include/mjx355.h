@@ -402,10 +402,9 @@ int mjl_tanh_inplace(float* x, long long n, void* stream);
  * multiple of the 128-row chunk (n > 256). scratch: mjl_colsum_batched_scratch(nb, n, d) floats.
  * mjl_slice_sum_batched: out[b][e] = sum over s < ns of x[(b * ns + s) * m + e]. */
 long long mjl_colsum_batched_scratch(int nb, int n, int d);
-/* The first stages alone, with the caller's row chunk: partials [nb][n / chunk][d] = each chunk's
- * column sums (of x, or of dz = g (1 - y^2), which is also written out), for mjl_slice_sum_multi to
- * finish. n % chunk == 0; the tanh form needs d % 4 == 0 and 16-byte aligned buffers. */
-int mjl_colsum_partials(const float* x, int nb, int n, int d, int chunk, float* partials, void* stream);
+/* The first stage alone, with the caller's row chunk: dz = g (1 - y^2) written out and partials
+ * [nb][n / chunk][d] = each chunk's column sums of dz, for mjl_slice_sum_multi to finish.
+ * n % chunk == 0, d % 4 == 0, 16-byte aligned buffers. */
 int mjl_tanh_bwd_colsum_partials(const float* g, const float* y, int nb, int n, int d, int chunk, float* dz,
                                  float* partials, void* stream);
 int mjl_colsum_batched(const float* x, int nb, int n, int d, float* scratch, float* out, void* stream);
@@ -414,19 +413,27 @@ int mjl_tanh_bwd_colsum_batched(const float* g, const float* y, int nb, int n, i
 int mjl_slice_sum_batched(const float* x, int nb, int ns, long long m, float* out, void* stream);
 /* nseg <= 16 slice sums in one launch: out_k[b][e] = sum over s < ns[k] (in order) of
  * x_k[(b * ns[k] + s) * m[k] + e], b < nb[k] (the twin update's weight-gradient slices and column-sum
- * partials of every layer, reduced together at the end of its backward). */
+ * partials of every layer, reduced together at the end of its backward). step0 / step1 / ctr (device
+ * float / float / int, each or NULL) are advanced by one in the same launch: the captured update's
+ * step counters and minibatch row, after their last read in the step (mjl_adam_multi then runs with
+ * advanced = 1). */
 int mjl_slice_sum_multi(int nseg, const float* const* x, float* const* out, const int* nb, const int* ns,
-                        const long long* m, void* stream);
-/* The twin update's output-layer backward: mean [M, A] = tanh of the policy's last Dense (networks.py:
- * 103), g_mean [M, A] = d loss / d mean (mjl_ppo_surrogate), v[r] = v[r * vstride] the value net's
- * output and ret [M] its targets (train_ppo.py:218-220, value loss mean (v - ret)^2);
- * dz4 [2][M][A]: dz4[0] = g_mean (1 - mean^2), dz4[1][:, 0] = 2 (v - ret) / M, dz4[1][:, 1:] = 0 (the
- * value net's output layer is padded to A rows); A <= 32. partials (or NULL): [2][mjl_twin_head_partial_rows(M)][A]
- * = dz4's column sums per 32-row chunk (fixed order), the output biases' gradient before the sum over
- * chunks (mjl_slice_sum_multi). */
-long long mjl_twin_head_partial_rows(int M);
-int mjl_twin_head_bwd(const float* g_mean, const float* mean, const float* v, int vstride, const float* ret, int M,
-                      int A, float* dz4, float* partials, void* stream);
+                        const long long* m, float* step0, float* step1, int* ctr, void* stream);
+/* The twin update's losses and output-layer backward in one pass (train_ppo.py:204-220 for both nets):
+ * z [2][n][A], z[0] = the policy's mean (tanh of its last Dense, networks.py:103), z[1][:, 0] = the
+ * value (the value net's output layer padded to A rows); the clipped surrogate as
+ * mjl_ppo_surrogate_clipped (advantages normalised by adv_stats — a [n_minibatches, 2] table read at
+ * *stats_row when stats_row is given — or over the n rows when adv_stats is NULL), the value loss
+ * mean (v - ret)^2 (train_ppo.py:218-220). Writes dz [2][n][A]: dz[0] = d loss / d mean (1 - mean^2),
+ * dz[1][:, 0] = 2 (v - ret) / n, dz[1][:, 1:] = 0; and per block b < mjl_twin_loss_head_blocks(n) the
+ * partials whose in-order sums over b (mjl_slice_sum_multi) are the results: lossp [nb] -> the policy
+ * loss, glsp [nb][A] -> d loss / d log_std (clip mask included), biasp [2][nb][A] -> both output
+ * biases' gradients. scratch: mjl_ppo_loss_scratch(n, A) floats. A <= 32. */
+long long mjl_twin_loss_head_blocks(int n);
+int mjl_twin_loss_head(const float* z, const float* log_std, const float* act, const float* old_logp, const float* adv,
+                       const float* ret, const float* adv_stats, const int* stats_row, int n, int A, float clip_eps,
+                       float ent_coef, float log_std_lo, float log_std_hi, float* scratch, float* dz, float* lossp,
+                       float* glsp, float* biasp, void* stream);
 /* x[b][r][j] = act_b(x[b][r][j] + bias[b][j]) in place over nb stacked row-major [rows, n] matrices,
  * act_b = tanh when bit b of act_mask is set, else the identity (the twin update's dense-layer
  * epilogue, src/networks.py:55-61, after a bias-less batched GEMM). */
@@ -452,15 +459,11 @@ int mjl_mse(const float* v, const float* r, int n, float* scratch, float* loss, 
 /* mjl_ppo_surrogate with log_std clipped to [log_std_lo, log_std_hi] on read (networks.py:103 clips it
  * to [-20, 2]) and g_log_std zero where the raw value lies outside (torch.clamp's backward, bounds
  * inclusive); +-INFINITY bounds = mjl_ppo_surrogate. stats_row (device int, or NULL): adv_stats is an
- * [n_minibatches, 2] table read at that row (a captured minibatch step reads its row at run time).
- * step0 / step1 / ctr (each device float / float / int, or NULL): advanced by one after every read of
- * the minibatch row (the captured update's counters: mjl_adam_multi with advanced = 1 then takes the
- * step counts as they are). */
+ * [n_minibatches, 2] table read at that row (a captured minibatch step reads its row at run time). */
 int mjl_ppo_surrogate_clipped(const float* mean, const float* log_std, const float* act, const float* old_logp,
                               const float* adv, const float* adv_stats, const int* stats_row, int n, int A,
                               float clip_eps, float ent_coef, float log_std_lo, float log_std_hi, float* scratch,
-                              float* loss, float* g_mean, float* g_log_std, float* step0, float* step1, int* ctr,
-                              void* stream);
+                              float* loss, float* g_mean, float* g_log_std, void* stream);
 /* mjl_mse with v[i] read at v + i * vstride (the value column of the twin update's padded output). */
 int mjl_mse_strided(const float* v, int vstride, const float* r, int n, float* scratch, float* loss, float* g_v,
                     void* stream);
@@ -487,7 +490,7 @@ int mjl_adam_dev(int nt, float* const* p, const float* const* g, float* const* m
  * (float, the count before this step: the step takes step + 1, and every group's counter is advanced
  * by one after it); g is scaled by gscale (the data-parallel mean: 1 / world size); ctr (device int,
  * or NULL) is advanced with the counters. advanced = 1: the counters were advanced earlier in the
- * minibatch step (mjl_ppo_surrogate_clipped's step0 / step1 / ctr): the step takes step as it is and
+ * minibatch step (mjl_slice_sum_multi's step0 / step1 / ctr): the step takes step as it is and
  * nothing is advanced here. Same arithmetic as mjl_adam_dev. */
 int mjl_adam_multi(int nt, float* const* p, const float* const* g, float* const* m, float* const* v,
                    const long long* numel, const int* group, int ngroups, const float* lr, float beta1, float beta2,

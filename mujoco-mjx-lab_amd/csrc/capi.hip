@@ -1007,15 +1007,6 @@ extern "C" long long mjl_colsum_batched_scratch(int nb, int n, int d) {
 // first stages only, with the caller's chunk: partials [nb][n / chunk][d] (the twin update reduces
 // every layer's partials together afterwards, mjl_slice_sum_multi; 32-row chunks give its 8,192-row
 // minibatch 512 blocks per pass where the two-stage plan's 128-row chunks gave 128 for 256 CUs)
-extern "C" int mjl_colsum_partials(const float* x, int nb, int n, int d, int chunk, float* partials, void* stream) {
-  if (!x || !partials || nb <= 0 || n <= 0 || d <= 0 || chunk <= 0 || n % chunk) return fail(MJL_ERR_ARG, "bad argument");
-  const int dc = d < 256 ? d : 256;
-  hipLaunchKernelGGL(colsum_kernel, dim3((unsigned)((d + dc - 1) / dc), (unsigned)(n / chunk * nb)), dim3(256), 0,
-                     (hipStream_t)stream, x, n * nb, d, dc, chunk, partials);
-  HIPCHK(hipGetLastError());
-  return MJL_OK;
-}
-
 extern "C" int mjl_tanh_bwd_colsum_partials(const float* g, const float* y, int nb, int n, int d, int chunk, float* dz,
                                             float* partials, void* stream) {
   if (!g || !y || !dz || !partials || nb <= 0 || n <= 0 || d <= 0 || chunk <= 0 || n % chunk)
@@ -1097,11 +1088,12 @@ extern "C" int mjl_slice_sum_batched(const float* x, int nb, int ns, long long m
 }
 
 extern "C" int mjl_slice_sum_multi(int nseg, const float* const* x, float* const* out, const int* nb, const int* ns,
-                                   const long long* m, void* stream) {
+                                   const long long* m, float* step0, float* step1, int* ctr, void* stream) {
   if (nseg < 1 || nseg > kSliceSegMax || !x || !out || !nb || !ns || !m) return fail(MJL_ERR_ARG, "bad argument");
   SliceSegs sg;
   std::memset(&sg, 0, sizeof(sg));
   sg.nseg = nseg;
+  sg.step0 = step0; sg.step1 = step1; sg.ctr = ctr;
   for (int k = 0; k < nseg; k++) {
     if (!x[k] || !out[k] || nb[k] <= 0 || ns[k] <= 0 || m[k] <= 0) return fail(MJL_ERR_ARG, "bad argument");
     sg.x[k] = x[k]; sg.out[k] = out[k]; sg.m[k] = m[k]; sg.ns[k] = ns[k]; sg.nb[k] = nb[k];
@@ -1136,19 +1128,6 @@ extern "C" int mjl_bias_act(float* x, const float* bias, int nb, long long rows,
     hipLaunchKernelGGL(bias_act_kernel<4>, grid, dim3(256), 0, (hipStream_t)stream, x, bias, nb, rows, n, act_mask);
   else
     hipLaunchKernelGGL(bias_act_kernel<1>, grid, dim3(256), 0, (hipStream_t)stream, x, bias, nb, rows, n, act_mask);
-  HIPCHK(hipGetLastError());
-  return MJL_OK;
-}
-
-extern "C" long long mjl_twin_head_partial_rows(int M) { return M > 0 ? (M + kHeadChunk - 1) / kHeadChunk : 0; }
-
-extern "C" int mjl_twin_head_bwd(const float* g_mean, const float* mean, const float* v, int vstride, const float* ret,
-                                 int M, int A, float* dz4, float* partials, void* stream) {
-  if (!g_mean || !mean || !v || !ret || !dz4 || M <= 0 || A <= 0 || A > 32 || vstride <= 0)
-    return fail(MJL_ERR_ARG, "bad argument");
-  if (2LL * M * A >= (1LL << 31)) return fail(MJL_ERR_ARG, "twin_head_bwd: 2 M A must be below 2^31");
-  hipLaunchKernelGGL(twin_head_bwd_kernel, dim3((unsigned)((M + kHeadChunk - 1) / kHeadChunk), 2), dim3(256), 0,
-                     (hipStream_t)stream, g_mean, mean, v, vstride, ret, M, A, dz4, partials);
   HIPCHK(hipGetLastError());
   return MJL_OK;
 }
@@ -1282,7 +1261,9 @@ extern "C" int mjl_apg_obs_vjp(int B, int nq, int nv, const float* o, const uint
 }
 
 // ---------------------------------------------------------------- PPO update losses
-constexpr int kSurrRows = 64;  // rows per ppo_surrogate_kernel block
+// rows per ppo_surrogate_kernel / twin_loss_head_kernel block (128: 0.2-0.3 ms per C5 per-rank
+// update ahead of 64 and 256, profiles/r4/surrogate_rows_ab.txt)
+constexpr int kSurrRows = 128;
 extern "C" long long mjl_ppo_loss_scratch(int n, int A) {
   if (n <= 0 || A <= 0) return 0;
   const long long nb = (n + kLossT - 1) / kLossT, nbs = (n + kSurrRows - 1) / kSurrRows;
@@ -1293,28 +1274,19 @@ extern "C" int mjl_ppo_surrogate_clipped(const float* mean, const float* log_std
                                          const float* old_logp, const float* adv, const float* adv_stats,
                                          const int* stats_row, int n, int A, float clip_eps, float ent_coef,
                                          float log_std_lo, float log_std_hi, float* scratch, float* loss,
-                                         float* g_mean, float* g_log_std, float* step0, float* step1, int* ctr,
-                                         void* stream) {
+                                         float* g_mean, float* g_log_std, void* stream) {
   if (!mean || !log_std || !act || !old_logp || !adv || !scratch || !loss || !g_mean || !g_log_std || n <= 0 || A <= 0)
     return fail(MJL_ERR_ARG, "bad argument");
   if (A > kLossMaxA) return fail(MJL_ERR_UNSUPPORTED, "ppo surrogate: at most %d action columns", kLossMaxA);
   hipStream_t s = (hipStream_t)stream;
-  static const int rb = [] { const char* e = getenv("MJL_SURR_ROWS"); return e ? atoi(e) : kSurrRows; }();
-  const int nb_adv = (n + kLossT - 1) / kLossT, nb = (n + rb - 1) / rb;
+  const int nb_adv = (n + kLossT - 1) / kLossT, nb = (n + kSurrRows - 1) / kSurrRows;
   float* adv_part = scratch;
   float* part = scratch + 3 * (size_t)nb_adv;
   if (!adv_stats) hipLaunchKernelGGL(adv_stats_kernel, dim3(nb_adv), dim3(kLossT), 0, s, adv, n, adv_part);
-  if (rb == 256)
-    hipLaunchKernelGGL(ppo_surrogate_kernel<256>, dim3(nb), dim3(256), 0, s, mean, log_std, act, old_logp,
-                       adv, n, A, clip_eps, adv_part, nb_adv, adv_stats, g_mean, part, log_std_lo, log_std_hi, stats_row);
-  else if (rb == 128)
-    hipLaunchKernelGGL(ppo_surrogate_kernel<128>, dim3(nb), dim3(128), 0, s, mean, log_std, act, old_logp,
-                       adv, n, A, clip_eps, adv_part, nb_adv, adv_stats, g_mean, part, log_std_lo, log_std_hi, stats_row);
-  else
-    hipLaunchKernelGGL(ppo_surrogate_kernel<64>, dim3(nb), dim3(64), 0, s, mean, log_std, act, old_logp,
-                       adv, n, A, clip_eps, adv_part, nb_adv, adv_stats, g_mean, part, log_std_lo, log_std_hi, stats_row);
+  hipLaunchKernelGGL(ppo_surrogate_kernel<kSurrRows>, dim3(nb), dim3(kSurrRows), 0, s, mean, log_std, act, old_logp,
+                     adv, n, A, clip_eps, adv_part, nb_adv, adv_stats, g_mean, part, log_std_lo, log_std_hi, stats_row);
   hipLaunchKernelGGL(ppo_surrogate_final_kernel, dim3(A + 1), dim3(64), 0, s, part, nb, n, A, log_std, ent_coef, loss,
-                     g_log_std, log_std_lo, log_std_hi, step0, step1, ctr);
+                     g_log_std, log_std_lo, log_std_hi);
   HIPCHK(hipGetLastError());
   return MJL_OK;
 }
@@ -1324,8 +1296,27 @@ extern "C" int mjl_ppo_surrogate(const float* mean, const float* log_std, const 
                                  float ent_coef, float* scratch, float* loss, float* g_mean, float* g_log_std,
                                  void* stream) {
   return mjl_ppo_surrogate_clipped(mean, log_std, act, old_logp, adv, adv_stats, nullptr, n, A, clip_eps, ent_coef,
-                                   -INFINITY, INFINITY, scratch, loss, g_mean, g_log_std, nullptr, nullptr, nullptr,
-                                   stream);
+                                   -INFINITY, INFINITY, scratch, loss, g_mean, g_log_std, stream);
+}
+
+extern "C" long long mjl_twin_loss_head_blocks(int n) { return n > 0 ? (n + kSurrRows - 1) / kSurrRows : 0; }
+
+extern "C" int mjl_twin_loss_head(const float* z, const float* log_std, const float* act, const float* old_logp,
+                                  const float* adv, const float* ret, const float* adv_stats, const int* stats_row,
+                                  int n, int A, float clip_eps, float ent_coef, float log_std_lo, float log_std_hi,
+                                  float* scratch, float* dz, float* lossp, float* glsp, float* biasp, void* stream) {
+  if (!z || !log_std || !act || !old_logp || !adv || !ret || !scratch || !dz || !lossp || !glsp || !biasp || n <= 0 ||
+      A <= 0)
+    return fail(MJL_ERR_ARG, "bad argument");
+  if (A > kLossMaxA || 2 * A + 2 > kSurrRows) return fail(MJL_ERR_UNSUPPORTED, "twin_loss_head: at most %d action columns", kLossMaxA);
+  hipStream_t s = (hipStream_t)stream;
+  const int nb_adv = (n + kLossT - 1) / kLossT, nb = (n + kSurrRows - 1) / kSurrRows;
+  if (!adv_stats) hipLaunchKernelGGL(adv_stats_kernel, dim3(nb_adv), dim3(kLossT), 0, s, adv, n, scratch);
+  hipLaunchKernelGGL(twin_loss_head_kernel<kSurrRows>, dim3(nb), dim3(kSurrRows), 0, s, z, log_std, act, old_logp, adv,
+                     ret, n, A, clip_eps, ent_coef, scratch, nb_adv, adv_stats, stats_row, log_std_lo, log_std_hi, dz,
+                     lossp, glsp, biasp);
+  HIPCHK(hipGetLastError());
+  return MJL_OK;
 }
 
 extern "C" int mjl_mse_strided(const float* v, int vstride, const float* r, int n, float* scratch, float* loss,
@@ -1359,8 +1350,17 @@ extern "C" int mjl_gather_rows_indexed(const long long* idx, const int* idx_row,
   const long long work = (long long)n * tot;
   if (work == 0) return MJL_OK;
   if (work + 255 >= (1ll << 31)) return fail(MJL_ERR_ARG, "gather_rows: rows x total columns must be below 2^31");
-  hipLaunchKernelGGL(gather_rows_kernel, dim3((unsigned)((work + 255) / 256)), dim3(256), 0, (hipStream_t)stream, idx,
-                     n, nsrc, g, idx_row);
+  if (tot <= kGatherWaveCols) {
+    GatherMap map;
+    int q = 0;
+    for (int k = 0; k < narr; k++)
+      for (int c = 0; c < cols[k]; c++, q++) { map.k[q] = (unsigned char)k; map.c[q] = (unsigned char)c; }
+    hipLaunchKernelGGL(gather_rows_wave_kernel, dim3((unsigned)((n + 3) / 4)), dim3(256), 0, (hipStream_t)stream, idx,
+                       n, nsrc, g, map, (int)tot, idx_row);
+  } else {
+    hipLaunchKernelGGL(gather_rows_kernel, dim3((unsigned)((work + 255) / 256)), dim3(256), 0, (hipStream_t)stream, idx,
+                       n, nsrc, g, idx_row);
+  }
   HIPCHK(hipGetLastError());
   return MJL_OK;
 }

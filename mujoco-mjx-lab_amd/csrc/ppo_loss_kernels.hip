@@ -184,16 +184,8 @@ __global__ __launch_bounds__(RB) void ppo_surrogate_kernel(
 __global__ __launch_bounds__(64) void ppo_surrogate_final_kernel(const float* __restrict__ part, int nb, int n, int A,
                                                                  const float* __restrict__ log_std, float ent_coef,
                                                                  float* __restrict__ loss, float* __restrict__ glog_std,
-                                                                 float ls_lo, float ls_hi, float* step0, float* step1,
-                                                                 int* ctr) {
+                                                                 float ls_lo, float ls_hi) {
   const int lane = threadIdx.x, col = blockIdx.x;
-  // the update graph's minibatch counters, advanced here (every read of the row in this minibatch
-  // step — gather, statistics — precedes this launch; Adam then takes the advanced step counts)
-  if (col == 0 && lane == 0) {
-    if (step0) *step0 += 1.f;
-    if (step1) *step1 += 1.f;
-    if (ctr) *ctr += 1;
-  }
   float s = 0.f;
   for (int b = lane; b < nb; b += 64) s += part[(size_t)b * (A + 1) + col];
   s = wave_sum(s);
@@ -204,6 +196,137 @@ __global__ __launch_bounds__(64) void ppo_surrogate_final_kernel(const float* __
     const float ls = log_std[col - 1];
     glog_std[col - 1] = (ls >= ls_lo && ls <= ls_hi) ? s - ent_coef / (float)A : 0.f;
   }
+}
+
+// The twin update's losses and output-layer backward in one pass (train_ppo.py:204-220 for both
+// nets; mjx_amd/twin.py). z [2][n][A]: z[0] = the policy's mean (tanh applied), z[1][:, 0] = the
+// value. Per row the clipped surrogate exactly as ppo_surrogate_kernel; then dZ of both output
+// layers, dz[0] = d loss / d mean (1 - mean^2) and dz[1][:, 0] = 2 (v - ret) / n (dz[1][:, 1:] = 0,
+// the value's padded rows); and the block's partial sums, pre-scaled so that the blocks summed in
+// order (mjl_slice_sum_multi) ARE the results: lossp[b] = -(sum surr) / n (block 0 adds -ent_coef x
+// entropy), glsp[b][j] = sum over rows of dlogp (q_j - 1) (block 0 adds -ent_coef / A; 0 where
+// log_std_j lies outside [lo, hi]: torch.clamp's backward), biasp[net][b][j] = the column sums of
+// dz[net] (the output biases' gradients). Where the per-net path took the surrogate, its final
+// reduction and a head backward with its column sums as separate launches. RB >= 2 A + 2.
+template <int RB>
+__global__ __launch_bounds__(RB) void twin_loss_head_kernel(
+    const float* __restrict__ z, const float* __restrict__ log_std, const float* __restrict__ act,
+    const float* __restrict__ old_logp, const float* __restrict__ adv, const float* __restrict__ ret, int n, int A,
+    float clip_eps, float ent_coef, const float* __restrict__ adv_part, int nb_adv,
+    const float* __restrict__ adv_stats, const int* __restrict__ stats_row, float ls_lo, float ls_hi,
+    float* __restrict__ dz, float* __restrict__ lossp, float* __restrict__ glsp, float* __restrict__ biasp) {
+  constexpr int NW = RB / 64;
+  __shared__ float sd[RB * kLossMaxA];  // a - mean of the block's rows, row-major; then dz[0]
+  __shared__ float sm[RB * kLossMaxA];  // mean
+  __shared__ float sgv[RB];             // dz[1][:, 0]
+  __shared__ float wred[NW][2 * kLossMaxA + 2];
+  __shared__ float ivs[kLossMaxA], lsd[kLossMaxA], lss;
+  __shared__ float mu_s, sd_s;
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6, r0 = blockIdx.x * RB, i = r0 + t;
+  const int rows = min(RB, n - r0), cnt = rows * A;
+  const size_t base = (size_t)r0 * A;
+  const float* mean = z;
+  const float* v = z + (size_t)n * A;
+  const bool in = t < rows;
+  const float olp = in ? old_logp[i] : 0.f, adv_i = in ? adv[i] : 0.f;
+  const float gv = in ? 2.f * (v[(size_t)i * A] - ret[i]) / (float)n : 0.f;
+  {
+    constexpr int U = 8;
+    int e = t;
+    for (; e + (U - 1) * RB < cnt; e += U * RB) {
+      float a[U], m[U];
+#pragma unroll
+      for (int u = 0; u < U; u++) { a[u] = act[base + e + u * RB]; m[u] = mean[base + e + u * RB]; }
+#pragma unroll
+      for (int u = 0; u < U; u++) { sm[e + u * RB] = m[u]; sd[e + u * RB] = a[u] - m[u]; }
+    }
+    for (; e < cnt; e += RB) {
+      const float m = mean[base + e];
+      sm[e] = m;
+      sd[e] = act[base + e] - m;
+    }
+  }
+  sgv[t] = gv;
+  if (t < A) {
+    const float ls = fminf(fmaxf(log_std[t], ls_lo), ls_hi);  // networks.py:103's clip
+    lsd[t] = ls;
+    ivs[t] = expf(-2.f * ls);
+  }
+  if (w == (NW > 1 ? 1 : 0)) {  // the advantage statistics
+    float mu, sdv;
+    if (adv_stats) {
+      const float* st = adv_stats + (stats_row ? 2 * (size_t)*stats_row : 0);
+      mu = st[0]; sdv = st[1];
+    }
+    else adv_merge_wave(adv_part, nb_adv, lane, mu, sdv);
+    if (lane == 0) { mu_s = mu; sd_s = sdv; }
+  }
+  __syncthreads();
+  if (t == 0) {
+    float s = 0.f;
+    for (int j = 0; j < A; j++) s += 2.f * lsd[j] + kLog2Pi;
+    lss = s;
+  }
+  __syncthreads();
+  float* dr = sd + (in ? t : 0) * A;
+  const float* mr = sm + (in ? t : 0) * A;
+  float qs = 0.f;
+  for (int j = 0; j < A; j++) qs += dr[j] * dr[j] * ivs[j];
+  float surr = 0.f, dlogp = 0.f;
+  if (in) {
+    const float logp = -0.5f * (qs + lss);
+    const float ratio = expf(logp - olp);
+    const float an = (adv_i - mu_s) / (sd_s + 1e-8f);
+    const float lo = 1.f - clip_eps, hi = 1.f + clip_eps;
+    const float rc = fminf(fmaxf(ratio, lo), hi);
+    const float t1 = ratio * an, t2 = rc * an;
+    surr = fminf(t1, t2);
+    const float w1 = t1 < t2 ? 1.f : (t1 == t2 ? 0.5f : 0.f);
+    const float w2 = t2 < t1 ? 1.f : (t1 == t2 ? 0.5f : 0.f);
+    const float dratio = (-1.f / (float)n) * (w1 * an + ((ratio >= lo && ratio <= hi) ? w2 * an : 0.f));
+    dlogp = dratio * ratio;
+  }
+  const float ssum = wave_sum(surr);
+  if (lane == 0) wred[w][0] = ssum;
+  for (int j = 0; j < A; j++) {
+    const float d = dr[j], m = mr[j];
+    const float c = wave_sum(in ? dlogp * (d * d * ivs[j] - 1.f) : 0.f);  // d logp / d s_j = q_j - 1
+    const float g = in ? dlogp * d * ivs[j] * (1.f - m * m) : 0.f;          // d loss / d z_j
+    const float cz = wave_sum(g);
+    if (in) dr[j] = g;  // (row t's a - mean is read by thread t only)
+    if (lane == 0) { wred[w][1 + j] = c; wred[w][1 + A + j] = cz; }
+  }
+  const float gsum = wave_sum(gv);
+  if (lane == 0) wred[w][1 + 2 * A] = gsum;
+  __syncthreads();
+  float* dz0 = dz + base;
+  float* dz1 = dz + (size_t)n * A + base;
+  for (int e = t; e < cnt; e += RB) {
+    const int r = e / A, j = e - r * A;
+    dz0[e] = sd[e];
+    dz1[e] = j == 0 ? sgv[r] : 0.f;
+  }
+  const int nb = gridDim.x, b = blockIdx.x;
+  if (t <= 2 * A + 1) {
+    float acc = wred[0][t];
+#pragma unroll
+    for (int k = 1; k < NW; k++) acc += wred[k][t];
+    if (t == 0) {
+      float val = -acc / (float)n;
+      if (b == 0) val -= ent_coef * (0.5f * ((float)A + lss) / (float)A);  // entropy, train_ppo.py:215
+      lossp[b] = val;
+    } else if (t <= A) {
+      const int j = t - 1;
+      const float ls = log_std[j];
+      const float val = b == 0 ? acc - ent_coef / (float)A : acc;
+      glsp[(size_t)b * A + j] = (ls >= ls_lo && ls <= ls_hi) ? val : 0.f;
+    } else if (t <= 2 * A) {
+      biasp[(size_t)b * A + (t - 1 - A)] = acc;
+    } else {
+      biasp[((size_t)nb + b) * A] = acc;
+    }
+  }
+  if (t >= 1 && t < A) biasp[((size_t)nb + b) * A + t] = 0.f;
 }
 
 // value MSE: per block sum of (v - r)^2 and d/dv = 2 (v - r) / n (v[i] at v + i * vstride: the value
@@ -270,12 +393,20 @@ struct SliceSegs {
   int ns[kSliceSegMax], nb[kSliceSegMax], vec[kSliceSegMax], lanes[kSliceSegMax];
   int blk[kSliceSegMax + 1];  // first block of each segment (nb rows x blocks per row)
   int nseg;
+  float* step0;  // device counters advanced by one (block 0, thread 0; or NULL): the captured
+  float* step1;  // update's step counts and minibatch row, after their last read in the step
+  int* ctr;
 };
 __device__ __forceinline__ float4 f4add(float4 a, float4 b) {
   return make_float4(a.x + b.x, a.y + b.y, a.z + b.z, a.w + b.w);
 }
 __global__ __launch_bounds__(256) void slice_sum_multi_kernel(SliceSegs sg) {
   const int blk = blockIdx.x;
+  if (blk == 0 && threadIdx.x == 0) {
+    if (sg.step0) *sg.step0 += 1.f;
+    if (sg.step1) *sg.step1 += 1.f;
+    if (sg.ctr) *sg.ctr += 1;
+  }
   int k = 0;
   while (k + 1 < sg.nseg && blk >= sg.blk[k + 1]) k++;
   const long long m = sg.m[k];
@@ -306,49 +437,6 @@ __global__ __launch_bounds__(256) void slice_sum_multi_kernel(SliceSegs sg) {
       for (int s = s0; s < s1; s++) acc += x[s * m + q];
     for (int off = S / 2; off > 0; off >>= 1) acc += __shfl_xor(acc, off);
     if (ok && j == 0) out[q] = acc;
-  }
-}
-
-// The twin update's output-layer backward (twin.py): the policy's mean = tanh(z) sits in out[0]
-// ([M, A]), the value in column 0 of out[1] (v[r] = v[r * vstride]); g_mean = d loss / d mean
-// (mjl_ppo_surrogate). dz[0] = g_mean (1 - mean^2); dz[1][:, 0] = d mean((v - ret)^2) / d v =
-// 2 (v - ret) / M (mse_kernel's gradient: the value loss itself is not needed by the update);
-// dz[1][:, 1:] = 0 (the value's padded output rows get no gradient). partials (or NULL): the output
-// biases' gradient, first stage — each net's dZ column sums per kHeadChunk-row chunk, [2][chunks][A].
-constexpr int kHeadChunk = 32;  // 512 blocks at the 8,192-row minibatch
-__global__ __launch_bounds__(256) void twin_head_bwd_kernel(const float* __restrict__ g_mean,
-                                                            const float* __restrict__ mean,
-                                                            const float* __restrict__ v, int vstride,
-                                                            const float* __restrict__ ret, int M, int A,
-                                                            float* __restrict__ dz4, float* __restrict__ partials) {
-  // block (chunk c = blockIdx.x, net = blockIdx.y): rows [c * kHeadChunk, ...) of one net's dZ, thread t
-  // = row group t / A (every G-th row of the chunk, in order) x column t % A; then the groups in order
-  __shared__ float red[256];
-  const int net = blockIdx.y, G = 256 / A, t = threadIdx.x, grp = t / A, j = t - grp * A;
-  const int r0 = blockIdx.x * kHeadChunk, r1 = min(M, r0 + kHeadChunk);
-  float s = 0.f;
-  if (grp < G) {
-    float* out = dz4 + (size_t)net * M * A;
-    for (int r = r0 + grp; r < r1; r += G) {
-      const size_t o = (size_t)r * A + j;
-      float d;
-      if (net == 0) {
-        const float y = mean[o];
-        d = g_mean[o] * (1.f - y * y);
-      } else {
-        d = j == 0 ? 2.f * (v[(size_t)r * vstride] - ret[r]) / (float)M : 0.f;
-      }
-      out[o] = d;
-      s += d;
-    }
-  }
-  if (!partials) return;  // (uniform over the launch)
-  red[t] = s;
-  __syncthreads();
-  if (t < A) {
-    float acc = red[t];
-    for (int q = 1; q < G; q++) acc += red[q * A + t];
-    partials[((size_t)net * gridDim.x + blockIdx.x) * A + t] = acc;
   }
 }
 
@@ -412,6 +500,29 @@ __global__ __launch_bounds__(256) void gather_rows_kernel(const long long* __res
   while (c >= g.cols[k]) { c -= g.cols[k]; k++; }
   const long long s = idx[r];  // an index outside [0, nsrc) yields NaN rows, not an out-of-bounds read
   g.dst[k][(size_t)r * g.cols[k] + c] = (s >= 0 && s < nsrc) ? g.src[k][(size_t)s * g.cols[k] + c] : __builtin_nanf("");
+}
+
+// The same gather, one wave per row (total columns <= kGatherWaveCols): the row's index is loaded
+// once, lane l copies columns l, l + 64, ... of the concatenated row through a column -> (array,
+// column) table, so every array's row segment is read and written contiguously. (The element-per-
+// thread kernel above paid a divide, an array search and an index load per element.)
+constexpr int kGatherWaveCols = 192;
+struct GatherMap {
+  unsigned char k[kGatherWaveCols];
+  unsigned char c[kGatherWaveCols];
+};
+__global__ __launch_bounds__(256) void gather_rows_wave_kernel(const long long* __restrict__ idx, int n, long long nsrc,
+                                                               GatherArgs g, GatherMap map, int tot,
+                                                               const int* __restrict__ idx_row) {
+  if (idx_row) idx += (size_t)*idx_row * n;
+  const int r = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+  if (r >= n) return;
+  const long long s = idx[r];
+  const bool ok = s >= 0 && s < nsrc;
+  for (int q = lane; q < tot; q += 64) {
+    const int k = map.k[q], c = map.c[q], w = g.cols[k];
+    g.dst[k][(size_t)r * w + c] = ok ? g.src[k][(size_t)s * w + c] : __builtin_nanf("");
+  }
 }
 
 // Adam over up to 16 tensors in one launch (torch.optim.Adam's fused update, fp32): m = b1 m +

@@ -31,9 +31,8 @@ EXPORTS = [
     "mjl_ppo_loss_scratch", "mjl_ppo_surrogate", "mjl_mse", "mjl_gather_rows", "mjl_adam",
     "mjl_adam_dev",
     "mjl_colsum_batched_scratch", "mjl_colsum_batched", "mjl_tanh_bwd_colsum_batched", "mjl_slice_sum_batched",
-    "mjl_twin_head_bwd", "mjl_mse_strided", "mjl_ppo_surrogate_clipped", "mjl_bias_act", "mjl_adam_multi",
-    "mjl_gather_rows_indexed", "mjl_slice_sum_multi", "mjl_colsum_partials", "mjl_tanh_bwd_colsum_partials",
-    "mjl_twin_head_partial_rows",
+    "mjl_mse_strided", "mjl_ppo_surrogate_clipped", "mjl_bias_act", "mjl_adam_multi",
+    "mjl_gather_rows_indexed", "mjl_slice_sum_multi", "mjl_tanh_bwd_colsum_partials", "mjl_twin_loss_head_blocks", "mjl_twin_loss_head",
 ]
 
 _lib = None
@@ -128,18 +127,18 @@ def lib() -> C.CDLL:
     L.mjl_colsum_batched.argtypes = [f32p, i32, i32, i32, f32p, f32p, vp]
     L.mjl_tanh_bwd_colsum_batched.argtypes = [f32p, f32p, i32, i32, i32, f32p, f32p, f32p, vp]
     L.mjl_slice_sum_batched.argtypes = [f32p, i32, i32, C.c_longlong, f32p, vp]
-    L.mjl_twin_head_bwd.argtypes = [f32p, f32p, f32p, i32, f32p, i32, i32, f32p, vp, vp]
-    L.mjl_twin_head_partial_rows.argtypes = [i32]
-    L.mjl_twin_head_partial_rows.restype = C.c_longlong
     L.mjl_mse_strided.argtypes = [vp, i32, vp, i32, vp, vp, vp, vp]
     L.mjl_bias_act.argtypes = [vp, vp, i32, C.c_longlong, i32, C.c_uint, vp]
     L.mjl_adam_multi.argtypes = [i32, vp, vp, vp, vp, vp, vp, i32, vp, C.c_float, C.c_float, C.c_float, C.c_float,
                                  vp, vp, i32, vp]
     L.mjl_ppo_surrogate_clipped.argtypes = [vp, vp, vp, vp, vp, vp, vp, i32, i32, C.c_float, C.c_float, C.c_float,
-                                            C.c_float, vp, vp, vp, vp, vp, vp, vp, vp]
+                                            C.c_float, vp, vp, vp, vp, vp]
     L.mjl_gather_rows_indexed.argtypes = [vp, vp, i32, C.c_longlong, i32, vp, vp, vp, vp]
-    L.mjl_slice_sum_multi.argtypes = [i32, vp, vp, vp, vp, vp, vp]
-    L.mjl_colsum_partials.argtypes = [vp, i32, i32, i32, i32, vp, vp]
+    L.mjl_slice_sum_multi.argtypes = [i32, vp, vp, vp, vp, vp, vp, vp, vp, vp]
+    L.mjl_twin_loss_head_blocks.argtypes = [i32]
+    L.mjl_twin_loss_head_blocks.restype = C.c_longlong
+    L.mjl_twin_loss_head.argtypes = [vp, vp, vp, vp, vp, vp, vp, vp, i32, i32, C.c_float, C.c_float, C.c_float,
+                                     C.c_float, vp, vp, vp, vp, vp, vp]
     L.mjl_tanh_bwd_colsum_partials.argtypes = [vp, vp, i32, i32, i32, i32, vp, vp, vp]
     L.mjl_small_mlp_fwd.argtypes = [vp, i32, i32, i32, vp, vp, vp, vp, vp]
     L.mjl_small_mlp_bwd_input.argtypes = [vp, i32, i32, i32, vp, vp, vp, vp, vp]

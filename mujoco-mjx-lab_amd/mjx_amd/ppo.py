@@ -851,8 +851,8 @@ class PPOUpdater:
         dp = self.dist is not None
         if self._tw:
             tw = self.twin
-            # captured (row given): the loss launch advances the step counters and the row, Adam
-            # takes them as they are
+            # captured (row given): the backward's final reduction launch advances the step counters
+            # and the row, Adam takes them as they are
             ctrs = (opt_p.step_t, opt_v.step_t, row) if row is not None else None
             tw.forward_backward(o, a, ol, r, ad, st, cfg.clip_eps, cfg.ent_coef, min(64, o.shape[-2] // SPLIT_ROWS),
                                 stats_row=row, counters=ctrs)
@@ -892,7 +892,7 @@ class PPOUpdater:
         if isinstance(self.opt_p, NativeAdam) and isinstance(self.opt_v, NativeAdam):
             # the all-reduced sum -> mean inside the one Adam launch of both nets
             gp, gv = (self.twin.grads_p, self.twin.grads_v) if self._tw else (self.views_p, self.views_v)
-            if row is not None and self._tw:  # (the twin loss launch advanced the counters and the row)
+            if row is not None and self._tw:  # (the twin backward advanced the counters and the row)
                 adam_steps([(self.opt_p, gp), (self.opt_v, gv)], gscale=1.0 / self.world, advanced=True)
             else:
                 adam_steps([(self.opt_p, gp), (self.opt_v, gv)], gscale=1.0 / self.world, ctr=row)

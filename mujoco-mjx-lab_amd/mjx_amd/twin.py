@@ -17,13 +17,14 @@ which is also the data-parallel all-reduce buffer (no concatenation).
 
 Forward: H_l = tanh(H_{l-1} W_lᵀ + b_l) as a bias-less torch.bmm + one native bias-and-tanh pass
 (mjl_bias_act; baddbmm would first copy the broadcast bias into its output); Z = H W_outᵀ + b_out;
-mean = tanh(Z[0]); v = Z[1][:, 0]. Losses: mjl_ppo_surrogate_clipped (log_std clipped in the kernel);
-the value's gradient 2 (v - ret) / M inside the head backward. Backward, by hand in the order
-autograd takes: mjl_twin_head_bwd forms dZ; each layer's weight gradient is the split-K batched GEMM
-dZᵀ X over both nets (2 x splits slices), its bias gradient the fixed-order column sums' first stage
-(mjl_colsum_batched / mjl_tanh_bwd_colsum_batched, which also forms dZ_l = dH (1 - H²)), dH = dZ W
-as one batched GEMM; the second stages — every layer's slices and chunk partials, summed in order —
-run together in one launch at the end (mjl_slice_sum_multi). Same formulas as the per-net path (ppo.py _SplitKLinear /
+mean = tanh(Z[0]); v = Z[1][:, 0]. Losses and the output layers' dZ in one launch (mjl_twin_loss_head:
+the clipped surrogate with log_std clipped in the kernel, the value's gradient 2 (v - ret) / M).
+Backward, by hand in the order autograd takes: each layer's weight gradient is the split-K batched
+GEMM dZᵀ X over both nets (2 x splits slices), its bias gradient the fixed-order column sums' first
+stage (mjl_tanh_bwd_colsum_partials, which also forms dZ_l = dH (1 - H²)), dH = dZ W as one batched
+GEMM; the second stages — every layer's slices and partials, the loss and d loss / d log_std
+partials, summed in order — run together in one launch at the end (mjl_slice_sum_multi, which also
+advances the captured update's counters). Same formulas as the per-net path (ppo.py _SplitKLinear /
 _TanhSplitKLinear + the native losses); the GEMMs are the library's batched kernels instead of its
 single ones, so results agree to rounding, not bit for bit (tests/test_twin.py)."""
 from __future__ import annotations
@@ -132,8 +133,8 @@ class TwinNets:
         gradients into self.grad. Returns (policy loss, value loss) device scalars (the value loss only
         with want_value_loss: the update does not need it). stats_row: adv_stats is the
         [n_minibatches, 2] table, read at that device row. counters: (policy step, value step, row)
-        device counters that the loss launch advances (the captured update; Adam then runs with
-        advanced=True)."""
+        device counters that the final reduction launch advances (the captured update; Adam then runs
+        with advanced=True)."""
         L = lib()
         dev = o.device
         st = torch.cuda.current_stream(dev).cuda_stream
@@ -149,36 +150,32 @@ class TwinNets:
             mask = 3 if l < nl - 1 else 1  # the output layer: tanh for the policy's mean, linear value
             check(L.mjl_bias_act(h.data_ptr(), self.b[l].data_ptr(), 2, M, h.shape[2], mask, st))
             hs.append(h)
-        z = hs.pop()  # [2, M, A]
-        mean = z[0]
-        # ---- losses (networks.py:103 clips log_std to [-20, 2]: in the kernel, with its gradient mask)
+        z = hs.pop()  # [2, M, A]: the policy's mean, the value in column 0 of z[1]
+        # ---- losses and the output layers' dZ in one launch (networks.py:103 clips log_std to [-20, 2]:
+        # in the kernel, with its gradient mask); the value loss itself only for reporting.
+        # Every reduction's first stage comes here (block partials of the loss, d loss / d log_std and
+        # the output biases' gradients; the column-sum chunk partials and split-K weight-gradient slices
+        # below); their second stages all in ONE launch after the last layer (mjl_slice_sum_multi)
         log_std = self.policy.log_std
         loss_p = torch.empty((), device=dev)
         loss_v = torch.empty((), device=dev)
-        gm = torch.empty((M, A), device=dev)
-        scr = self._scratch("loss", int(L.mjl_ppo_loss_scratch(M, A)))
-        c0, c1, c2 = (None, None, None) if counters is None else (c.data_ptr() for c in counters)
-        check(L.mjl_ppo_surrogate_clipped(mean.data_ptr(), log_std.data_ptr(), acts.data_ptr(), old_logp.data_ptr(),
-                                          adv.data_ptr(), None if adv_stats is None else adv_stats.data_ptr(),
-                                          None if stats_row is None else stats_row.data_ptr(), M, A,
-                                          float(clip_eps), float(ent_coef), -20.0, 2.0, scr.data_ptr(),
-                                          loss_p.data_ptr(), gm.data_ptr(), self.g_log_std.data_ptr(), c0, c1, c2, st))
-        if want_value_loss:  # (reporting only: the value gradient comes from the head kernel below)
+        if want_value_loss:
             gv = torch.empty(M, device=dev)
             scr_v = self._scratch("mse", M // 256 + 1)
             check(L.mjl_mse_strided(z[1].data_ptr(), A, ret.data_ptr(), M, scr_v.data_ptr(), loss_v.data_ptr(),
                                     gv.data_ptr(), st))
-        # ---- backward: dZ of both output layers, the value's 2 (v - ret) / M formed in the same pass,
-        # with the output biases' column-sum partials.
-        # Every reduction's first stage comes here; their second stages (column-sum chunk partials,
-        # split-K weight-gradient slices) all in ONE launch after the last layer (mjl_slice_sum_multi)
         segs = []  # (x, out, nb, ns, m)
         dz = torch.empty((2, M, A), device=dev)
-        Rh = int(L.mjl_twin_head_partial_rows(M))
-        cs = self._scratch(f"cs{nl - 1}", 2 * Rh * A)
-        check(L.mjl_twin_head_bwd(gm.data_ptr(), mean.data_ptr(), z[1].data_ptr(), A, ret.data_ptr(), M, A,
-                                  dz.data_ptr(), cs.data_ptr(), st))
-        segs.append((cs, self.gb[nl - 1], 2, Rh, A))
+        nbk = int(L.mjl_twin_loss_head_blocks(M))
+        scr = self._scratch("loss", int(L.mjl_ppo_loss_scratch(M, A)))
+        part = self._scratch("lossparts", nbk * (1 + 3 * A))
+        lossp, glsp, biasp = part[:nbk], part[nbk:nbk * (1 + A)], part[nbk * (1 + A):nbk * (1 + 3 * A)]
+        check(L.mjl_twin_loss_head(z.data_ptr(), log_std.data_ptr(), acts.data_ptr(), old_logp.data_ptr(),
+                                   adv.data_ptr(), ret.data_ptr(), None if adv_stats is None else adv_stats.data_ptr(),
+                                   None if stats_row is None else stats_row.data_ptr(), M, A, float(clip_eps),
+                                   float(ent_coef), -20.0, 2.0, scr.data_ptr(), dz.data_ptr(), lossp.data_ptr(),
+                                   glsp.data_ptr(), biasp.data_ptr(), st))
+        segs += [(lossp, loss_p, 1, nbk, 1), (glsp, self.g_log_std, 1, nbk, A), (biasp, self.gb[nl - 1], 2, nbk, A)]
         # (32-row chunks — 4x the blocks — where the minibatch is small: 8.4 against 9.0 us per pass
         # at 8,192 rows; at 65,536 the 4x partials cost more than they gain)
         ch = COLSUM_CHUNK if M > 16384 else 32
@@ -209,11 +206,12 @@ class TwinNets:
                 g = torch.bmm(dzl, self.W[l])  # [2, M, K]
         import ctypes
         k = len(segs)
+        c0, c1, c2 = (None, None, None) if counters is None else (c.data_ptr() for c in counters)
         check(L.mjl_slice_sum_multi(k, (ctypes.c_void_p * k)(*[x.data_ptr() for x, *_ in segs]),
                                     (ctypes.c_void_p * k)(*[o.data_ptr() for _, o, *_ in segs]),
                                     (ctypes.c_int * k)(*[nb for _, _, nb, _, _ in segs]),
                                     (ctypes.c_int * k)(*[ns for _, _, _, ns, _ in segs]),
-                                    (ctypes.c_longlong * k)(*[m for *_, m in segs]), st))
+                                    (ctypes.c_longlong * k)(*[m for *_, m in segs]), c0, c1, c2, st))
         self._keep = segs  # the launch reads the partial buffers asynchronously
         return loss_p, loss_v
 

@@ -617,3 +617,28 @@ def test_gather_rows_bounds():
     ok = torch.tensor([True, True, True, False, False, True], device="cuda")
     assert torch.equal(oa[ok], a[idx[ok]]) and torch.equal(ob[ok], b[idx[ok]])
     assert bool(torch.isnan(oa[~ok]).all()) and bool(torch.isnan(ob[~ok]).all())
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("cols", [(54, 54, 21, 1, 1, 1), (200,), (150, 60)])
+def test_gather_rows_indexed_wide_and_twice(cols):
+    """mjl_gather_rows_indexed through both kernels (a wave per row up to 192 total columns, an
+    element per thread beyond), row *idx_row of an index table; and the twin update's form (the
+    first array written twice into one [2, rows, ...] block)."""
+    g = torch.Generator(device="cuda").manual_seed(len(cols))
+    arrs = [torch.randn((300, c) if c > 1 else (300,), generator=g, device="cuda") for c in cols]
+    table = torch.randint(0, 300, (3, 77), generator=g, device="cuda", dtype=torch.int64)
+    table[1, 5] = 300  # out of range: a NaN row
+    row = torch.tensor([1], dtype=torch.int32, device="cuda")
+    outs = ppo._gather_minibatch(table, *arrs, row=row)
+    idx = table[1]
+    ok = idx < 300
+    for o, a in zip(outs, arrs):
+        assert torch.equal(o[ok], a[idx[ok]]) and bool(torch.isnan(o[~ok]).all())
+    if len(arrs) + 1 <= 8:
+        tw = ppo._gather_minibatch(table, *arrs, row=row, twice_first=True)
+        assert tw[0].shape == (2,) + outs[0].shape
+        assert torch.equal(tw[0][0][ok], tw[0][1][ok]) and torch.equal(tw[0][0][ok], outs[0][ok])
+        assert bool(torch.isnan(tw[0][:, ~ok]).all())
+        for o, t in zip(outs[1:], tw[1:]):
+            assert torch.equal(o[ok], t[ok])

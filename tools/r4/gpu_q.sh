@@ -1,0 +1,14 @@
+# round 4: twin losses + output-layer backward in one launch, counters in the final reduction, wave-per-row gather
+# gathered once per net (no layer-0 expand copy); unrolled surrogate staging; tests + timing + trace
+set -o pipefail
+export TMPDIR=/tmp
+O=gpurun_out/r4q
+mkdir -p $O
+timeout -k 10 600 python -u -m pytest -x -q --timeout 300 --timeout-method thread -m gpu tests/test_twin.py tests/test_ppo_graph.py tests/test_update_kernels.py tests/test_ppo.py tests/test_dp_gpu.py > $O/pytest.log 2>&1
+rc=$?; echo "pytest rc=$rc"; tail -2 $O/pytest.log
+if [ $rc -ne 0 ]; then grep -v amdgpu.ids $O/pytest.log | grep -B5 -A40 "^____" | head -100; exit $rc; fi
+timeout -k 10 300 python -u tools/ppo_update_probe.py twinonly > $O/ab.txt 2>&1 || exit $?
+grep -v amdgpu.ids $O/ab.txt
+timeout -k 10 300 rocprofv3 --kernel-trace --output-format csv -d $O/prof -o run -- python -u tools/ppo_update_probe.py c5twin > $O/prof.txt 2>&1 || exit $?
+f=$(find $O/prof -name '*kernel_trace.csv' | head -1)
+python tools/trace_by_grid.py "$f" 30 > $O/by_grid.txt && cat $O/by_grid.txt && rm -rf $O/prof
