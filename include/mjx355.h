@@ -428,12 +428,14 @@ int mjl_slice_sum_multi(int nseg, const float* const* x, float* const* out, cons
  * dz[1][:, 0] = 2 (v - ret) / n, dz[1][:, 1:] = 0; and per block b < mjl_twin_loss_head_blocks(n) the
  * partials whose in-order sums over b (mjl_slice_sum_multi) are the results: lossp [nb] -> the policy
  * loss, glsp [nb][A] -> d loss / d log_std (clip mask included), biasp [2][nb][A] -> both output
- * biases' gradients. scratch: mjl_ppo_loss_scratch(n, A) floats. A <= 32. */
+ * biases' gradients. bias (or NULL): z holds the output layers' pre-activations and bias [2][A] their
+ * biases — mean = tanh(z[0] + bias[0]), v = z[1][:, 0] + bias[1][0]. scratch: mjl_ppo_loss_scratch(n, A)
+ * floats. A <= 32. */
 long long mjl_twin_loss_head_blocks(int n);
 int mjl_twin_loss_head(const float* z, const float* log_std, const float* act, const float* old_logp, const float* adv,
                        const float* ret, const float* adv_stats, const int* stats_row, int n, int A, float clip_eps,
-                       float ent_coef, float log_std_lo, float log_std_hi, float* scratch, float* dz, float* lossp,
-                       float* glsp, float* biasp, void* stream);
+                       float ent_coef, float log_std_lo, float log_std_hi, const float* bias, float* scratch,
+                       float* dz, float* lossp, float* glsp, float* biasp, void* stream);
 /* x[b][r][j] = act_b(x[b][r][j] + bias[b][j]) in place over nb stacked row-major [rows, n] matrices,
  * act_b = tanh when bit b of act_mask is set, else the identity (the twin update's dense-layer
  * epilogue, src/networks.py:55-61, after a bias-less batched GEMM). */

@@ -1304,7 +1304,8 @@ extern "C" long long mjl_twin_loss_head_blocks(int n) { return n > 0 ? (n + kSur
 extern "C" int mjl_twin_loss_head(const float* z, const float* log_std, const float* act, const float* old_logp,
                                   const float* adv, const float* ret, const float* adv_stats, const int* stats_row,
                                   int n, int A, float clip_eps, float ent_coef, float log_std_lo, float log_std_hi,
-                                  float* scratch, float* dz, float* lossp, float* glsp, float* biasp, void* stream) {
+                                  const float* bias, float* scratch, float* dz, float* lossp, float* glsp, float* biasp,
+                                  void* stream) {
   if (!z || !log_std || !act || !old_logp || !adv || !ret || !scratch || !dz || !lossp || !glsp || !biasp || n <= 0 ||
       A <= 0)
     return fail(MJL_ERR_ARG, "bad argument");
@@ -1313,8 +1314,8 @@ extern "C" int mjl_twin_loss_head(const float* z, const float* log_std, const fl
   const int nb_adv = (n + kLossT - 1) / kLossT, nb = (n + kSurrRows - 1) / kSurrRows;
   if (!adv_stats) hipLaunchKernelGGL(adv_stats_kernel, dim3(nb_adv), dim3(kLossT), 0, s, adv, n, scratch);
   hipLaunchKernelGGL(twin_loss_head_kernel<kSurrRows>, dim3(nb), dim3(kSurrRows), 0, s, z, log_std, act, old_logp, adv,
-                     ret, n, A, clip_eps, ent_coef, scratch, nb_adv, adv_stats, stats_row, log_std_lo, log_std_hi, dz,
-                     lossp, glsp, biasp);
+                     ret, n, A, clip_eps, ent_coef, scratch, nb_adv, adv_stats, stats_row, log_std_lo, log_std_hi, bias,
+                     dz, lossp, glsp, biasp);
   HIPCHK(hipGetLastError());
   return MJL_OK;
 }

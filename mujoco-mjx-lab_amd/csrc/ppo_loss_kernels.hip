@@ -45,6 +45,26 @@ __device__ __forceinline__ float wave_sum(float v) {
   return v;
 }
 
+// sum over the 64 lanes of a wave without LDS traffic: DPP quad permutes and row rotates leave every
+// lane of each 16-lane row with its row's sum, then the four rows are read out (v_readlane) and added
+// in a fixed order; the result is wave-uniform. (__shfl_xor is a ds_bpermute round trip per step: a
+// chain of 42 six-step butterflies made that the longest part of twin_loss_head_kernel.)
+template <int CTRL>
+__device__ __forceinline__ float dpp_f(float v) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xf, 0xf, false));
+}
+__device__ __forceinline__ float wave_sum_dpp(float v) {
+  v += dpp_f<0xb1>(v);   // quad_perm [1, 0, 3, 2]
+  v += dpp_f<0x4e>(v);   // quad_perm [2, 3, 0, 1]
+  v += dpp_f<0x124>(v);  // row_ror:4
+  v += dpp_f<0x128>(v);  // row_ror:8
+  const float r0 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 0));
+  const float r1 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 16));
+  const float r2 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 32));
+  const float r3 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 48));
+  return (r0 + r1) + (r2 + r3);
+}
+
 // Chan et al. pairwise merge of (count, mean, M2) partials
 __device__ __forceinline__ void chan_merge(float& c, float& m, float& M2, float cb, float mb, float M2b) {
   if (cb == 0.f) return;
@@ -207,17 +227,21 @@ __global__ __launch_bounds__(64) void ppo_surrogate_final_kernel(const float* __
 // entropy), glsp[b][j] = sum over rows of dlogp (q_j - 1) (block 0 adds -ent_coef / A; 0 where
 // log_std_j lies outside [lo, hi]: torch.clamp's backward), biasp[net][b][j] = the column sums of
 // dz[net] (the output biases' gradients). Where the per-net path took the surrogate, its final
-// reduction and a head backward with its column sums as separate launches. RB >= 2 A + 2.
+// reduction and a head backward with its column sums as separate launches. bias (or NULL): z holds
+// the output layers' pre-activations and bias [2][A] their biases (mean = tanh(z[0] + bias[0]), v =
+// z[1][:, 0] + bias[1][0]: the head's bias + tanh pass folded in). RB >= 2 A + 2.
 template <int RB>
 __global__ __launch_bounds__(RB) void twin_loss_head_kernel(
     const float* __restrict__ z, const float* __restrict__ log_std, const float* __restrict__ act,
     const float* __restrict__ old_logp, const float* __restrict__ adv, const float* __restrict__ ret, int n, int A,
     float clip_eps, float ent_coef, const float* __restrict__ adv_part, int nb_adv,
     const float* __restrict__ adv_stats, const int* __restrict__ stats_row, float ls_lo, float ls_hi,
-    float* __restrict__ dz, float* __restrict__ lossp, float* __restrict__ glsp, float* __restrict__ biasp) {
+    const float* __restrict__ bias, float* __restrict__ dz, float* __restrict__ lossp, float* __restrict__ glsp,
+    float* __restrict__ biasp) {
   constexpr int NW = RB / 64;
-  __shared__ float sd[RB * kLossMaxA];  // a - mean of the block's rows, row-major; then dz[0]
-  __shared__ float sm[RB * kLossMaxA];  // mean
+  __shared__ float sd[RB * kLossMaxA];  // a, then a - mean of the block's rows (row-major), then dz[0]
+  __shared__ float sm[RB * kLossMaxA];  // z, then the mean
+  __shared__ float sb[kLossMaxA + 1];   // the output biases (bias given)
   __shared__ float sgv[RB];             // dz[1][:, 0]
   __shared__ float wred[NW][2 * kLossMaxA + 2];
   __shared__ float ivs[kLossMaxA], lsd[kLossMaxA], lss;
@@ -229,7 +253,7 @@ __global__ __launch_bounds__(RB) void twin_loss_head_kernel(
   const float* v = z + (size_t)n * A;
   const bool in = t < rows;
   const float olp = in ? old_logp[i] : 0.f, adv_i = in ? adv[i] : 0.f;
-  const float gv = in ? 2.f * (v[(size_t)i * A] - ret[i]) / (float)n : 0.f;
+  const float gv = in ? 2.f * (v[(size_t)i * A] + (bias ? bias[A] : 0.f) - ret[i]) / (float)n : 0.f;
   {
     constexpr int U = 8;
     int e = t;
@@ -238,15 +262,15 @@ __global__ __launch_bounds__(RB) void twin_loss_head_kernel(
 #pragma unroll
       for (int u = 0; u < U; u++) { a[u] = act[base + e + u * RB]; m[u] = mean[base + e + u * RB]; }
 #pragma unroll
-      for (int u = 0; u < U; u++) { sm[e + u * RB] = m[u]; sd[e + u * RB] = a[u] - m[u]; }
+      for (int u = 0; u < U; u++) { sm[e + u * RB] = m[u]; sd[e + u * RB] = a[u]; }
     }
     for (; e < cnt; e += RB) {
-      const float m = mean[base + e];
-      sm[e] = m;
-      sd[e] = act[base + e] - m;
+      sm[e] = mean[base + e];
+      sd[e] = act[base + e];
     }
   }
   sgv[t] = gv;
+  if (t < A) sb[t] = bias ? bias[t] : 0.f;
   if (t < A) {
     const float ls = fminf(fmaxf(log_std[t], ls_lo), ls_hi);  // networks.py:103's clip
     lsd[t] = ls;
@@ -269,9 +293,16 @@ __global__ __launch_bounds__(RB) void twin_loss_head_kernel(
   }
   __syncthreads();
   float* dr = sd + (in ? t : 0) * A;
-  const float* mr = sm + (in ? t : 0) * A;
+  float* mr = sm + (in ? t : 0) * A;
   float qs = 0.f;
-  for (int j = 0; j < A; j++) qs += dr[j] * dr[j] * ivs[j];
+  // bias given: z is the output layer's pre-activation, the mean tanh(z + b) (the head's bias + tanh
+  // pass folded in); row t's staged values are read and rewritten by thread t only
+  for (int j = 0; j < A; j++) {
+    const float m = bias ? tanhf(mr[j] + sb[j]) : mr[j];
+    const float d = dr[j] - m;
+    if (in) { mr[j] = m; dr[j] = d; }
+    qs += d * d * ivs[j];
+  }
   float surr = 0.f, dlogp = 0.f;
   if (in) {
     const float logp = -0.5f * (qs + lss);
@@ -286,17 +317,17 @@ __global__ __launch_bounds__(RB) void twin_loss_head_kernel(
     const float dratio = (-1.f / (float)n) * (w1 * an + ((ratio >= lo && ratio <= hi) ? w2 * an : 0.f));
     dlogp = dratio * ratio;
   }
-  const float ssum = wave_sum(surr);
+  const float ssum = wave_sum_dpp(surr);
   if (lane == 0) wred[w][0] = ssum;
   for (int j = 0; j < A; j++) {
     const float d = dr[j], m = mr[j];
-    const float c = wave_sum(in ? dlogp * (d * d * ivs[j] - 1.f) : 0.f);  // d logp / d s_j = q_j - 1
+    const float c = wave_sum_dpp(in ? dlogp * (d * d * ivs[j] - 1.f) : 0.f);  // d logp / d s_j = q_j - 1
     const float g = in ? dlogp * d * ivs[j] * (1.f - m * m) : 0.f;          // d loss / d z_j
-    const float cz = wave_sum(g);
+    const float cz = wave_sum_dpp(g);
     if (in) dr[j] = g;  // (row t's a - mean is read by thread t only)
     if (lane == 0) { wred[w][1 + j] = c; wred[w][1 + A + j] = cz; }
   }
-  const float gsum = wave_sum(gv);
+  const float gsum = wave_sum_dpp(gv);
   if (lane == 0) wred[w][1 + 2 * A] = gsum;
   __syncthreads();
   float* dz0 = dz + base;

@@ -138,7 +138,7 @@ def lib() -> C.CDLL:
     L.mjl_twin_loss_head_blocks.argtypes = [i32]
     L.mjl_twin_loss_head_blocks.restype = C.c_longlong
     L.mjl_twin_loss_head.argtypes = [vp, vp, vp, vp, vp, vp, vp, vp, i32, i32, C.c_float, C.c_float, C.c_float,
-                                     C.c_float, vp, vp, vp, vp, vp, vp]
+                                     C.c_float, vp, vp, vp, vp, vp, vp, vp]
     L.mjl_tanh_bwd_colsum_partials.argtypes = [vp, vp, i32, i32, i32, i32, vp, vp, vp]
     L.mjl_small_mlp_fwd.argtypes = [vp, i32, i32, i32, vp, vp, vp, vp, vp]
     L.mjl_small_mlp_bwd_input.argtypes = [vp, i32, i32, i32, vp, vp, vp, vp, vp]

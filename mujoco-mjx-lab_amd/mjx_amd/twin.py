@@ -145,12 +145,16 @@ class TwinNets:
         # (which the first layer's weight-gradient slices can then read without an expand copy)
         x = o if o.dim() == 3 else o.unsqueeze(0).expand(2, M, self.K0)
         hs = [x]
+        # (the output layer's bias and tanh go into the loss launch unless the value loss is wanted)
+        fold = not want_value_loss
         for l in range(nl):
             h = torch.bmm(hs[-1], self.W[l].transpose(1, 2))
             mask = 3 if l < nl - 1 else 1  # the output layer: tanh for the policy's mean, linear value
-            check(L.mjl_bias_act(h.data_ptr(), self.b[l].data_ptr(), 2, M, h.shape[2], mask, st))
+            if l < nl - 1 or not fold:
+                check(L.mjl_bias_act(h.data_ptr(), self.b[l].data_ptr(), 2, M, h.shape[2], mask, st))
             hs.append(h)
-        z = hs.pop()  # [2, M, A]: the policy's mean, the value in column 0 of z[1]
+        z = hs.pop()  # [2, M, A]: the policy's mean and the value in column 0 of z[1] (fold: before the
+        # output bias and the mean's tanh)
         # ---- losses and the output layers' dZ in one launch (networks.py:103 clips log_std to [-20, 2]:
         # in the kernel, with its gradient mask); the value loss itself only for reporting.
         # Every reduction's first stage comes here (block partials of the loss, d loss / d log_std and
@@ -173,7 +177,8 @@ class TwinNets:
         check(L.mjl_twin_loss_head(z.data_ptr(), log_std.data_ptr(), acts.data_ptr(), old_logp.data_ptr(),
                                    adv.data_ptr(), ret.data_ptr(), None if adv_stats is None else adv_stats.data_ptr(),
                                    None if stats_row is None else stats_row.data_ptr(), M, A, float(clip_eps),
-                                   float(ent_coef), -20.0, 2.0, scr.data_ptr(), dz.data_ptr(), lossp.data_ptr(),
+                                   float(ent_coef), -20.0, 2.0, self.b[nl - 1].data_ptr() if fold else None,
+                                   scr.data_ptr(), dz.data_ptr(), lossp.data_ptr(),
                                    glsp.data_ptr(), biasp.data_ptr(), st))
         segs += [(lossp, loss_p, 1, nbk, 1), (glsp, self.g_log_std, 1, nbk, A), (biasp, self.gb[nl - 1], 2, nbk, A)]
         # (32-row chunks — 4x the blocks — where the minibatch is small: 8.4 against 9.0 us per pass

@@ -45,9 +45,16 @@ def test_twin_gradients_match_float64_autograd(n, dup):
     assert twin.TwinNets.eligible(pol, val)
     tw = twin.TwinNets(pol, val)
     o, a, ol, r, ad = _data(n)
-    lp, lv = tw.forward_backward(o.unsqueeze(0).expand(2, n, 54).contiguous() if dup else o, a, ol, r, ad, None, cfg.clip_eps, cfg.ent_coef, min(64, n // ppo.SPLIT_ROWS),
-                                 want_value_loss=True)
+    ob = o.unsqueeze(0).expand(2, n, 54).contiguous() if dup else o
+    splits = min(64, n // ppo.SPLIT_ROWS)
+    # the update's form first (the output layer's bias and tanh folded into the loss launch), then the
+    # reporting form (bias + tanh pass, the value loss too): the same gradients to rounding
+    tw.forward_backward(ob, a, ol, r, ad, None, cfg.clip_eps, cfg.ent_coef, splits)
+    g_fold = [g.clone() for g in tw.grads_p + tw.grads_v]
+    lp, lv = tw.forward_backward(ob, a, ol, r, ad, None, cfg.clip_eps, cfg.ent_coef, splits, want_value_loss=True)
     torch.cuda.synchronize()
+    for gf, gu in zip(g_fold, tw.grads_p + tw.grads_v):
+        assert float((gf - gu).abs().max()) <= 1e-5 * (float(gu.abs().max()) + 1e-12)
     old = ppo.NATIVE_LOSSES
     ppo.NATIVE_LOSSES = False
     try:

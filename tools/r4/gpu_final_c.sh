@@ -16,3 +16,5 @@ bash tools/r4/profile.sh || exit $?
 echo PROFILE_OK
 MJL_BENCH_REHEARSAL=1 timeout -k 10 500 python bench.py --gpus 2 --no-cpu --steps 20 > gpurun_out/prof4/rehearsal_n2.json 2> gpurun_out/prof4/rehearsal_n2.err || exit $?
 tail -c 600 gpurun_out/prof4/rehearsal_n2.json
+timeout -k 10 300 python -u tools/ppo_update_probe.py twinonly > $O/twin_update.txt 2>&1 || exit $?
+grep -v amdgpu.ids $O/twin_update.txt
