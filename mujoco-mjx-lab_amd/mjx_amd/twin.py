@@ -37,6 +37,9 @@ import torch
 from ._lib import check, lib
 
 TWIN_UPDATE = os.environ.get("MJL_TWIN_UPDATE", "1") != "0"
+# the output layers' bias + tanh inside the loss launch (mjl_twin_loss_head's bias argument) instead
+# of a separate mjl_bias_act pass
+FOLD_HEAD = os.environ.get("MJL_TWIN_FOLD_HEAD", "1") != "0"
 # rows per column-sum partial (the bias gradients' first stage); 32 and 64 measured no faster
 COLSUM_CHUNK = int(os.environ.get("MJL_TWIN_COLSUM_CHUNK", "128"))
 
@@ -146,7 +149,7 @@ class TwinNets:
         x = o if o.dim() == 3 else o.unsqueeze(0).expand(2, M, self.K0)
         hs = [x]
         # (the output layer's bias and tanh go into the loss launch unless the value loss is wanted)
-        fold = not want_value_loss
+        fold = FOLD_HEAD and not want_value_loss
         for l in range(nl):
             h = torch.bmm(hs[-1], self.W[l].transpose(1, 2))
             mask = 3 if l < nl - 1 else 1  # the output layer: tanh for the policy's mean, linear value
