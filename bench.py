@@ -575,6 +575,58 @@ def policy_roofline(tr, local) -> dict:
                     "HIP events around a replayed hipGraph of 100 launches"}
 
 
+class _IdentityComm:
+    """A one-rank stand-in for torch.distributed: all_reduce is the identity (the per-rank C5 update
+    below runs the data-parallel graphs with the collective taken out)."""
+
+    @staticmethod
+    def all_reduce(t, op=None):
+        return t
+
+    @staticmethod
+    def get_world_size():
+        return 1
+
+
+def c5_rank_update(local, reps: int = 3) -> dict:
+    """One rank's PPO update at BASELINE C5's per-rank shape on 8 GPUs (1024 envs x 256 steps, 4 epochs
+    of 8,192-row minibatches = 128 minibatch steps) through PPOUpdater's data-parallel graphs with the
+    all-reduce replaced by the identity: the update's compute per rank (synthetic rollout data,
+    random-init reference-size nets). The collective itself is measured at --gpus N > 1."""
+    from mjx_amd import ppo
+    from mjx_amd.config import reference_ppo_config
+    dev = f"cuda:{local}"
+    cfg = reference_ppo_config()
+    cfg.minibatch_size = 8192
+    g = torch.Generator().manual_seed(0)
+    pol = ppo.GaussianPolicy(54, 21, cfg.policy_hidden_layer_specs, cfg.log_std_init, g).to(dev)
+    val = ppo.ValueNet(54, cfg.value_hidden_layer_specs, g).to(dev)
+    op, ov = ppo._adam(pol.parameters(), cfg.lr_policy), ppo._adam(val.parameters(), cfg.lr_value)
+    up = ppo.PPOUpdater(pol, val, op, ov, cfg, _IdentityComm(), 1, use_graph=True)
+    n = 1024 * 256
+    gd = torch.Generator(device=dev).manual_seed(1)
+    obs = torch.randn((n, 54), generator=gd, device=dev)
+    act = torch.randn((n, 21), generator=gd, device=dev).clamp(-1, 1)
+    logp, ret, adv = (torch.randn(n, generator=gd, device=dev) for _ in range(3))
+    ts = []
+    for r in range(reps + 2):
+        idx = ppo.make_index_batches(n, cfg.minibatch_size, cfg.epochs, torch.Generator(device=dev).manual_seed(r), dev)
+        sync(dev)
+        t0 = time.perf_counter()
+        up.run(obs, act, logp, ret, adv, idx)
+        sync(dev)
+        if r >= 2:
+            ts.append(time.perf_counter() - t0)
+    steps = int(idx.shape[0])
+    out = {"ppo_c5_rank_update_ms": 1e3 * sorted(ts)[len(ts) // 2], "ppo_c5_rank_update_steps": steps,
+           "ppo_c5_rank_update_twin": up.twin is not None,
+           "ppo_c5_rank_update_note": "one rank of C5 on 8 GPUs: 1024 envs x 256 steps, 4 epochs x 32 minibatches "
+                                      "of 8,192 rows, the data-parallel update graphs with an identity collective; "
+                                      "median of 3 synced runs after 2 (capture)"}
+    del up, pol, val, op, ov
+    return out
+
+
 def ppo_c3(args, local) -> dict:
     """C3: src/config.json PPO at 1024 envs on one GPU, throughput and return@iter (seed 42)."""
     tr = ppo_trainer(args, args.ppo_envs, None, 0, local, eval_envs=32)
@@ -596,6 +648,8 @@ def ppo_c3(args, local) -> dict:
     from mjx_amd import tunable
     out["tuned_gemm_table"] = tunable.table_loaded()
     del tr
+    free_gpu()
+    out.update(c5_rank_update(local))
     free_gpu()
     return out
 
