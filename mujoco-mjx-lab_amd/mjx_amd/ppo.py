@@ -534,26 +534,23 @@ def value_loss(value, obs, returns):
     return torch.mean((v - returns) ** 2)
 
 
-def _gather_minibatch(idx, *arrays, row: Optional[torch.Tensor] = None, twice_first: bool = False, outs=None):
+def _gather_minibatch(idx, *arrays, row: Optional[torch.Tensor] = None, twice_first: bool = False):
     """arrays[k][idx] for every k, as one native launch (mjl_gather_rows) on the GPU. With `row` (a
     device int32), idx is an [n_minibatches, rows] table and the launch gathers row *row of it, read
     when the launch runs (a captured minibatch step; mjl_gather_rows_indexed). twice_first (with
     row): the first array's rows are written twice, as one [2, rows, ...] block (the twin update's
-    observations, one copy per net). outs (with row): write into these tensors (the same layout)."""
+    observations, one copy per net)."""
     if row is not None:
         import ctypes
         from ._lib import check, lib
         n = idx.shape[1]
-        if outs is None:
-            outs = [torch.empty((n,) + tuple(a.shape[1:]), dtype=a.dtype, device=a.device) for a in arrays]
-            if twice_first:
-                a0 = arrays[0]
-                outs[0] = torch.empty((2, n) + tuple(a0.shape[1:]), dtype=a0.dtype, device=a0.device)
-        outs = list(outs)
+        outs = [torch.empty((n,) + tuple(a.shape[1:]), dtype=a.dtype, device=a.device) for a in arrays]
         dsts, srcs = list(outs), list(arrays)
         if twice_first:
+            a0 = arrays[0]
+            outs[0] = torch.empty((2, n) + tuple(a0.shape[1:]), dtype=a0.dtype, device=a0.device)
             dsts = [outs[0][0], outs[0][1]] + outs[1:]
-            srcs = [arrays[0]] + list(arrays)
+            srcs = [a0] + list(arrays)
         k = len(srcs)
         check(lib().mjl_gather_rows_indexed(idx.data_ptr(), ctypes.c_void_p(row.data_ptr()), n,
                                             min(a.shape[0] for a in arrays), k,
@@ -733,9 +730,6 @@ def _set_grads(params: List[torch.Tensor], flat: torch.Tensor):
 
 
 TWO_STREAM_UPDATE = os.environ.get("MJL_TWO_STREAM", "1") != "0"  # value net on a side stream in ppo_update
-# twin graphs: the next minibatch gathered on a side stream during the current step, into the other of
-# two buffer sets (one graph per parity), instead of at the head of each step
-TWIN_PREFETCH = os.environ.get("MJL_TWIN_PREFETCH", "0") == "1"
 _SIDE_STREAMS = {}
 
 
@@ -847,36 +841,21 @@ class PPOUpdater:
         return sum(p.numel() for p in self.pp + self.vp)
 
     # ------------------------------------------------------------------ bodies
-    def _body_a(self, idx, src, st, row: Optional[torch.Tensor] = None, mb=None, prefetch=None):
+    def _body_a(self, idx, src, st, row: Optional[torch.Tensor] = None):
         """Gather the minibatch; forward + backward of both nets (and, single-process, both Adam
         steps). Data-parallel: leaves both nets' gradients in the all-reduce buffer. With `row` (twin
         graphs), idx and st are the whole update's [n_minibatches, ...] tables, read at row *row, which
-        the Adam launch advances: the replays need no per-minibatch host copies. mb / prefetch (twin
-        graphs): this step's gathered minibatch, and (index table one row ahead, the other buffer set)
-        for the next step's gather on the side stream."""
+        the Adam launch advances: the replays need no per-minibatch host copies."""
         cfg, opt_p, opt_v = self.cfg, self.opt_p, self.opt_v
+        o, a, ol, r, ad = _gather_minibatch(idx, *src, row=row, twice_first=self._tw and row is not None)
         dp = self.dist is not None
-        join = None
-        if mb is not None:  # twin graphs with prefetch: this step's minibatch is already in mb
-            o, a, ol, r, ad = mb
-            nxt_idx, nxt = prefetch
-            cur = torch.cuda.current_stream(o.device)
-            side = _side_stream(o.device)
-            side.wait_stream(cur)
-            with torch.cuda.stream(side):  # the next step's rows (index table one row ahead)
-                _gather_minibatch(nxt_idx, *src, row=row, twice_first=True, outs=nxt)
-
-            def join():  # before the launch that advances the row
-                cur.wait_stream(side)
-        else:
-            o, a, ol, r, ad = _gather_minibatch(idx, *src, row=row, twice_first=self._tw and row is not None)
         if self._tw:
             tw = self.twin
             # captured (row given): the backward's final reduction launch advances the step counters
             # and the row, Adam takes them as they are
             ctrs = (opt_p.step_t, opt_v.step_t, row) if row is not None else None
             tw.forward_backward(o, a, ol, r, ad, st, cfg.clip_eps, cfg.ent_coef, min(64, o.shape[-2] // SPLIT_ROWS),
-                                stats_row=row, counters=ctrs, join=join)
+                                stats_row=row, counters=ctrs)
             if not dp:  # both nets' Adam steps in one launch
                 adam_steps([(opt_p, tw.grads_p), (opt_v, tw.grads_v)], advanced=ctrs is not None)
             return
@@ -1002,45 +981,27 @@ class PPOUpdater:
         """The twin path's replays: the whole update's index table (and, data-parallel, its advantage
         statistics) copied once, a device row counter that the captured Adam launch advances, so a
         minibatch step is graph A (+ the all-reduce + graph B) with no host copy in between."""
-        nmb, M = index_batches.shape
-        dev = index_batches.device
-        if getattr(self, "_idx_all", None) is None or self._idx_all.shape[0] != nmb + 1 or self._idx_all.shape[1] != M:
-            # one spare row: the last step's prefetch reads it (index 0 rows, never used)
-            self._idx_all = torch.zeros((nmb + 1, M), dtype=index_batches.dtype, device=dev)
-            self._st_all = torch.zeros((nmb, 2), device=dev)
-            self._row = torch.zeros(1, dtype=torch.int32, device=dev)
+        nmb = index_batches.shape[0]
+        if getattr(self, "_idx_all", None) is None or self._idx_all.shape != index_batches.shape:
+            self._idx_all = torch.empty_like(index_batches, memory_format=torch.contiguous_format)
+            self._st_all = torch.zeros((nmb, 2), device=index_batches.device)
+            self._row = torch.zeros(1, dtype=torch.int32, device=index_batches.device)
             self._ga = self._gb = None
-        if self._ga is None:
-            self._gas = [None, None]
-            o0, a0 = self._src[0], self._src[1]
-            self._mbs = [(torch.empty((2, M) + tuple(o0.shape[1:]), device=dev),
-                          torch.empty((M,) + tuple(a0.shape[1:]), device=dev),
-                          *(torch.empty(M, device=dev) for _ in range(3))) for _ in range(2)]
-        self._idx_all[:nmb].copy_(index_batches)
+        self._idx_all.copy_(index_batches)
         if stats is not None:
             self._st_all.copy_(stats)
         self._row.zero_()
         st = self._st_all if stats is not None else None
-        pf = TWIN_PREFETCH
-        if pf:  # step 0's minibatch; each step then gathers the next one into the other buffer set
-            _gather_minibatch(self._idx_all, *self._src, row=self._row, twice_first=True, outs=self._mbs[0])
-        for k in range(nmb):
-            p = k % 2 if pf else 0
-            if self._gas[p] is None:
-                g = torch.cuda.CUDAGraph()
-                with torch.cuda.graph(g):
-                    if pf:
-                        self._body_a(self._idx_all, self._src, st, row=self._row, mb=self._mbs[p],
-                                     prefetch=(self._idx_all[1:], self._mbs[1 - p]))
-                    else:
-                        self._body_a(self._idx_all, self._src, st, row=self._row)
-                self._gas[p] = g
-                self._ga = self._gas[0]
-                if self.dist is not None and self._gb is None:
+        for _ in range(nmb):
+            if self._ga is None:
+                self._ga = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(self._ga):
+                    self._body_a(self._idx_all, self._src, st, row=self._row)
+                if self.dist is not None:
                     self._gb = torch.cuda.CUDAGraph()
                     with torch.cuda.graph(self._gb):
                         self._body_b(row=self._row)
-            self._gas[p].replay()
+            self._ga.replay()
             if self.dist is not None:
                 self._allreduce(events)
                 self._gb.replay()

@@ -130,15 +130,14 @@ class TwinNets:
         return t
 
     def forward_backward(self, o, acts, old_logp, ret, adv, adv_stats, clip_eps: float, ent_coef: float, splits: int,
-                         want_value_loss: bool = False, stats_row=None, counters=None, join=None):
+                         want_value_loss: bool = False, stats_row=None, counters=None):
         """Both nets' losses and gradients for one minibatch (o [M, K0] — or [2, M, K0], the same rows
         twice, as the update's gather writes them —, acts [M, A], old_logp / ret / adv [M]); the
         gradients into self.grad. Returns (policy loss, value loss) device scalars (the value loss only
         with want_value_loss: the update does not need it). stats_row: adv_stats is the
         [n_minibatches, 2] table, read at that device row. counters: (policy step, value step, row)
         device counters that the final reduction launch advances (the captured update; Adam then runs
-        with advanced=True). join: called right before that launch (the caller's side-stream work that
-        reads the row joins there)."""
+        with advanced=True)."""
         L = lib()
         dev = o.device
         st = torch.cuda.current_stream(dev).cuda_stream
@@ -216,8 +215,6 @@ class TwinNets:
         import ctypes
         k = len(segs)
         c0, c1, c2 = (None, None, None) if counters is None else (c.data_ptr() for c in counters)
-        if join is not None:
-            join()
         check(L.mjl_slice_sum_multi(k, (ctypes.c_void_p * k)(*[x.data_ptr() for x, *_ in segs]),
                                     (ctypes.c_void_p * k)(*[o.data_ptr() for _, o, *_ in segs]),
                                     (ctypes.c_int * k)(*[nb for _, _, nb, _, _ in segs]),

@@ -143,8 +143,7 @@ def shard_twin(reps: int = 5, envs: int = 1024):
                   f"wall median {1e3 * w[len(w) // 2]:.2f} ms (min {1e3 * w[0]:.2f}, max {1e3 * w[-1]:.2f})", flush=True)
 
 
-def twin_chunk(reps: int = 5, envs: int = 1024, chunks=(128, 64, 32), mbs=(8192, 65536), attr="COLSUM_CHUNK",
-               mod=None):
+def twin_chunk(reps: int = 5, envs: int = 1024, chunks=(128, 64, 32), mbs=(8192, 65536), attr="COLSUM_CHUNK"):
     """Graph-replayed twin updates at several values of a twin-module setting (attr: twin.COLSUM_CHUNK,
     the column-sum partial chunk; read when a minibatch step is captured), interleaved:
     C5's per-rank shard and C3's single-process update."""
@@ -169,7 +168,7 @@ def twin_chunk(reps: int = 5, envs: int = 1024, chunks=(128, 64, 32), mbs=(8192,
         for r in range(reps + 2):
             idx = ppo.make_index_batches(N, mb, cfg.epochs, torch.Generator(device="cuda").manual_seed(r), "cuda")
             for c in chunks:
-                setattr(mod if mod is not None else twin, attr, c)
+                setattr(twin, attr, c)
                 torch.cuda.synchronize()
                 t0 = time.time()
                 ups[c].run(obs, act, logp, ret, adv, idx)
@@ -248,9 +247,6 @@ if __name__ == "__main__":
         sys.exit(0)
     if len(sys.argv) > 1 and sys.argv[1] == "shard":
         shard()
-        sys.exit(0)
-    if len(sys.argv) > 1 and sys.argv[1] == "prefetch":  # the next minibatch gathered during the current step
-        twin_chunk(reps=8, chunks=(True, False), attr="TWIN_PREFETCH", mod=ppo)
         sys.exit(0)
     if len(sys.argv) > 1 and sys.argv[1] == "fold":  # the head's bias + tanh folded into the loss launch or not
         twin_chunk(reps=8, chunks=(True, False), attr="FOLD_HEAD")
