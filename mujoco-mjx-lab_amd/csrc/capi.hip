@@ -1313,7 +1313,7 @@ extern "C" int mjl_twin_loss_head(const float* z, const float* log_std, const fl
   hipStream_t s = (hipStream_t)stream;
   const int nb_adv = (n + kLossT - 1) / kLossT, nb = (n + kSurrRows - 1) / kSurrRows;
   if (!adv_stats) hipLaunchKernelGGL(adv_stats_kernel, dim3(nb_adv), dim3(kLossT), 0, s, adv, n, scratch);
-  hipLaunchKernelGGL(twin_loss_head_kernel<kSurrRows>, dim3(nb), dim3(kSurrRows), 0, s, z, log_std, act, old_logp, adv,
+  hipLaunchKernelGGL(twin_loss_head_kernel<kSurrRows>, dim3(nb), dim3(2 * kSurrRows), 0, s, z, log_std, act, old_logp, adv,
                      ret, n, A, clip_eps, ent_coef, scratch, nb_adv, adv_stats, stats_row, log_std_lo, log_std_hi, bias,
                      dz, lossp, glsp, biasp);
   HIPCHK(hipGetLastError());

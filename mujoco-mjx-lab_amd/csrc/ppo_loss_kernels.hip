@@ -231,17 +231,19 @@ __global__ __launch_bounds__(64) void ppo_surrogate_final_kernel(const float* __
 // the output layers' pre-activations and bias [2][A] their biases (mean = tanh(z[0] + bias[0]), v =
 // z[1][:, 0] + bias[1][0]: the head's bias + tanh pass folded in). RB >= 2 A + 2.
 template <int RB>
-__global__ __launch_bounds__(RB) void twin_loss_head_kernel(
+__global__ __launch_bounds__(2 * RB) void twin_loss_head_kernel(
     const float* __restrict__ z, const float* __restrict__ log_std, const float* __restrict__ act,
     const float* __restrict__ old_logp, const float* __restrict__ adv, const float* __restrict__ ret, int n, int A,
     float clip_eps, float ent_coef, const float* __restrict__ adv_part, int nb_adv,
     const float* __restrict__ adv_stats, const int* __restrict__ stats_row, float ls_lo, float ls_hi,
     const float* __restrict__ bias, float* __restrict__ dz, float* __restrict__ lossp, float* __restrict__ glsp,
     float* __restrict__ biasp) {
-  constexpr int NW = RB / 64;
-  __shared__ float sd[RB * kLossMaxA];  // a, then a - mean of the block's rows (row-major), then dz[0]
-  __shared__ float sm[RB * kLossMaxA];  // z, then the mean
-  __shared__ float sb[kLossMaxA + 1];   // the output biases (bias given)
+  // 2 RB threads: all of them stage the block's rows element-wise (and, bias given, form the means:
+  // half the per-thread chain of tanh's a thread-per-row pass had); the row passes run on the first
+  // RB (waves 0 .. NW - 1), thread t = row t
+  constexpr int NW = RB / 64, TB = 2 * RB;
+  __shared__ float sd[RB * kLossMaxA];  // a - mean of the block's rows (row-major), then dz[0]
+  __shared__ float sm[RB * kLossMaxA];  // the mean
   __shared__ float sgv[RB];             // dz[1][:, 0]
   __shared__ float wred[NW][2 * kLossMaxA + 2];
   __shared__ float ivs[kLossMaxA], lsd[kLossMaxA], lss;
@@ -251,26 +253,40 @@ __global__ __launch_bounds__(RB) void twin_loss_head_kernel(
   const size_t base = (size_t)r0 * A;
   const float* mean = z;
   const float* v = z + (size_t)n * A;
-  const bool in = t < rows;
+  const bool in = t < RB && t < rows;
   const float olp = in ? old_logp[i] : 0.f, adv_i = in ? adv[i] : 0.f;
   const float gv = in ? 2.f * (v[(size_t)i * A] + (bias ? bias[A] : 0.f) - ret[i]) / (float)n : 0.f;
   {
-    constexpr int U = 8;
-    int e = t;
-    for (; e + (U - 1) * RB < cnt; e += U * RB) {
+    // element e = t + k TB: its column advances by TB mod A per trip (no divide per element)
+    const int step = TB % A;
+    int e = t, j = t % A;
+    auto col_next = [&](int c) { c += step; return c >= A ? c - A : c; };
+    constexpr int U = 4;
+    for (; e + (U - 1) * TB < cnt; e += U * TB) {
       float a[U], m[U];
+      int jj[U];
 #pragma unroll
-      for (int u = 0; u < U; u++) { a[u] = act[base + e + u * RB]; m[u] = mean[base + e + u * RB]; }
+      for (int u = 0; u < U; u++) {
+        a[u] = act[base + e + u * TB];
+        m[u] = mean[base + e + u * TB];
+        jj[u] = j;
+        j = col_next(j);
+      }
 #pragma unroll
-      for (int u = 0; u < U; u++) { sm[e + u * RB] = m[u]; sd[e + u * RB] = a[u]; }
+      for (int u = 0; u < U; u++) {
+        const float mu = bias ? tanhf(m[u] + bias[jj[u]]) : m[u];
+        sm[e + u * TB] = mu;
+        sd[e + u * TB] = a[u] - mu;
+      }
     }
-    for (; e < cnt; e += RB) {
-      sm[e] = mean[base + e];
-      sd[e] = act[base + e];
+    for (; e < cnt; e += TB) {
+      const float mu = bias ? tanhf(mean[base + e] + bias[j]) : mean[base + e];
+      sm[e] = mu;
+      sd[e] = act[base + e] - mu;
+      j = col_next(j);
     }
   }
-  sgv[t] = gv;
-  if (t < A) sb[t] = bias ? bias[t] : 0.f;
+  if (t < RB) sgv[t] = gv;
   if (t < A) {
     const float ls = fminf(fmaxf(log_std[t], ls_lo), ls_hi);  // networks.py:103's clip
     lsd[t] = ls;
@@ -293,16 +309,9 @@ __global__ __launch_bounds__(RB) void twin_loss_head_kernel(
   }
   __syncthreads();
   float* dr = sd + (in ? t : 0) * A;
-  float* mr = sm + (in ? t : 0) * A;
+  const float* mr = sm + (in ? t : 0) * A;
   float qs = 0.f;
-  // bias given: z is the output layer's pre-activation, the mean tanh(z + b) (the head's bias + tanh
-  // pass folded in); row t's staged values are read and rewritten by thread t only
-  for (int j = 0; j < A; j++) {
-    const float m = bias ? tanhf(mr[j] + sb[j]) : mr[j];
-    const float d = dr[j] - m;
-    if (in) { mr[j] = m; dr[j] = d; }
-    qs += d * d * ivs[j];
-  }
+  for (int j = 0; j < A; j++) qs += dr[j] * dr[j] * ivs[j];
   float surr = 0.f, dlogp = 0.f;
   if (in) {
     const float logp = -0.5f * (qs + lss);
@@ -317,6 +326,7 @@ __global__ __launch_bounds__(RB) void twin_loss_head_kernel(
     const float dratio = (-1.f / (float)n) * (w1 * an + ((ratio >= lo && ratio <= hi) ? w2 * an : 0.f));
     dlogp = dratio * ratio;
   }
+  if (w < NW) {  // the row waves
   const float ssum = wave_sum_dpp(surr);
   if (lane == 0) wred[w][0] = ssum;
   for (int j = 0; j < A; j++) {
@@ -329,13 +339,20 @@ __global__ __launch_bounds__(RB) void twin_loss_head_kernel(
   }
   const float gsum = wave_sum_dpp(gv);
   if (lane == 0) wred[w][1 + 2 * A] = gsum;
+  }
   __syncthreads();
   float* dz0 = dz + base;
   float* dz1 = dz + (size_t)n * A + base;
-  for (int e = t; e < cnt; e += RB) {
-    const int r = e / A, j = e - r * A;
-    dz0[e] = sd[e];
-    dz1[e] = j == 0 ? sgv[r] : 0.f;
+  {
+    const int rstep = TB / A, cstep = TB % A;
+    int r = t / A, c = t - (t / A) * A;
+    for (int e = t; e < cnt; e += TB) {
+      dz0[e] = sd[e];
+      dz1[e] = c == 0 ? sgv[r] : 0.f;
+      r += rstep;
+      c += cstep;
+      if (c >= A) { c -= A; r++; }
+    }
   }
   const int nb = gridDim.x, b = blockIdx.x;
   if (t <= 2 * A + 1) {
