@@ -40,8 +40,10 @@ TWIN_UPDATE = os.environ.get("MJL_TWIN_UPDATE", "1") != "0"
 # the output layers' bias + tanh inside the loss launch (mjl_twin_loss_head's bias argument) instead
 # of a separate mjl_bias_act pass
 FOLD_HEAD = os.environ.get("MJL_TWIN_FOLD_HEAD", "1") != "0"
-# split-K slices of the 256-wide layers' weight gradients (None: the caller's splits)
+# split-K slices of the 256-wide layers' weight gradients (None: the caller's splits), and of the thin
+# ones (the 21-wide output, the 54-wide input; None: M / 256, at most 64)
 HIDDEN_SPLITS = None
+THIN_SPLITS = None
 # rows per column-sum partial (the bias gradients' first stage); 32 and 64 measured no faster
 COLSUM_CHUNK = int(os.environ.get("MJL_TWIN_COLSUM_CHUNK", "128"))
 
@@ -197,7 +199,7 @@ class TwinNets:
             xin = hs[l]  # the layer's input: H_{l-1}, or the observations for l = 0
             # split-K slices of the weight gradient: the thin layers (the 21 / 1-unit outputs, the 54-wide
             # input) are a few output tiles per slice, so they take more, shorter slices
-            s = (HIDDEN_SPLITS or splits) if (N >= 64 and K >= 64) else max(splits, min(64, M // 256))
+            s = (HIDDEN_SPLITS or splits) if (N >= 64 and K >= 64) else max(splits, THIN_SPLITS or min(64, M // 256))
             if l < nl - 1:  # tanh layer: dZ = dH (1 - H^2) and the bias gradient's partials in one pass
                 dzl = torch.empty_like(g)
                 cs = self._scratch(f"cs{l}", 2 * R * N)

@@ -248,6 +248,9 @@ if __name__ == "__main__":
     if len(sys.argv) > 1 and sys.argv[1] == "shard":
         shard()
         sys.exit(0)
+    if len(sys.argv) > 1 and sys.argv[1] == "thin":  # split-K slices of the thin layers' weight gradients
+        twin_chunk(reps=6, chunks=(None, 8, 16), attr="THIN_SPLITS", mbs=(8192,))
+        sys.exit(0)
     if len(sys.argv) > 1 and sys.argv[1] == "splits":  # split-K slices of the hidden layers' weight gradients
         twin_chunk(reps=6, chunks=(None, 2, 8), attr="HIDDEN_SPLITS", mbs=(8192,))
         sys.exit(0)
