@@ -37,6 +37,9 @@ import torch  # noqa: E402
 
 REF_DEVICE_STEPS_PER_S = 72618.0  # HUMANOID_MJX device steps/s (README.md:77), batch 4096
 REF_HUMANOID_XML_STEPS_PER_S = 6176.0  # README.md:76 HUMANOID row (humanoid.xml)
+REF_SPHERE_STEPS_PER_S = 5957372.0     # README.md:78 SPHERE row
+SPHERE_XML = ("<mujoco><worldbody><body><freejoint/><geom size='.15' mass='1' type='sphere'/></body></worldbody>"
+              "</mujoco>")               # mjx_humanoid_speed_test.py:29-40
 HBM_PEAK_GBS = 8000.0             # MI355X_MICROARCH.md: HBM3E peak 8.0 TB/s (spec)
 F32_PEAK_TFLOPS = 157.3           # MI355X_MICROARCH.md: peak FP32 matrix (dense) = FP32 vector
 SPEEDTEST_KERNEL = "step_kernel<mjl::Dims<27, 17, 22, 20, 48, 16>, 2, 2>"  # rocprofv3 kernel name
@@ -424,6 +427,30 @@ def speedtest_extras(args, model, sys_, local):
     ex["speedtest_humanoid_xml_kernel_ms"] = hk
     ex["speedtest_humanoid_xml_vs_readme"] = ex["speedtest_humanoid_xml_steps_per_s"] / REF_HUMANOID_XML_STEPS_PER_S
     del dh
+    # ... and at the README's own batch of 4096 (mjx_humanoid_speed_test.py:140)
+    dh = mjx.make_data(sh, 4096, device=local)
+    dh.set_option(0, 0)
+    vh = torch.linspace(0.0, 1.0, 4096, device=dev)
+    oh = torch.empty_like(vh)
+    hw, hk = timed_launches(lambda: mjx.speedtest_step(sh, dh, vh, oh), args.steps, args.warmup, None)
+    ex["speedtest_humanoid_xml_b4096_steps_per_s"] = 4096 * args.steps / hw
+    ex["speedtest_humanoid_xml_b4096_kernel_ms"] = hk
+    ex["speedtest_humanoid_xml_b4096_vs_readme"] = 4096 * args.steps / hw / REF_HUMANOID_XML_STEPS_PER_S
+    del dh
+    # the README's SPHERE row (mjx_humanoid_speed_test.py:29-40,142, README.md:78: 5,957,372 steps/s):
+    # one free sphere, no floor, default options (Euler, dt 0.002), batch 4096, fresh state per step
+    from mjx_amd import mjcf
+    ms = mjcf.compile_xml_string(SPHERE_XML)
+    ss = mjx.put_model(ms)
+    dsp = mjx.make_data(ss, 4096, device=local)
+    dsp.set_option(0, 0)
+    vs = torch.linspace(0.0, 1.0, 4096, device=dev)
+    osp = torch.empty_like(vs)
+    sw, sk = timed_launches(lambda: mjx.speedtest_step(ss, dsp, vs, osp), args.steps, args.warmup, None)
+    ex["speedtest_sphere_b4096_steps_per_s"] = 4096 * args.steps / sw
+    ex["speedtest_sphere_b4096_kernel_ms"] = sk
+    ex["speedtest_sphere_b4096_vs_readme"] = 4096 * args.steps / sw / REF_SPHERE_STEPS_PER_S
+    del dsp
     # the reference's own batch size for the README row
     d4 = mjx.make_data(sys_, 4096, device=local)
     v4 = torch.linspace(0.0, 1.0, 4096, device=dev)

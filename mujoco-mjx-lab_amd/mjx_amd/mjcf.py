@@ -437,8 +437,11 @@ def compile_xml_string(text: str, name_hint: str = "", sha: str = "") -> Compile
                 for o in ("euler", "axisangle", "xyaxes"):
                     if o in a:
                         raise MJCFError(f"geom orientation '{o}' not supported")
+                # an explicit mass sets the density (mjCGeom::SetInertia: density = mass / volume)
+                dens = float(a["density"])
                 if "mass" in a:
-                    raise MJCFError("explicit geom mass not supported")
+                    vol, _ = _geom_inertia(gtype, size, 1.0)
+                    dens = float(a["mass"]) / vol
                 frv = _floats(a["friction"])  # missing trailing values keep MuJoCo's defaults
                 fr = (frv + [1.0, 0.005, 0.0001][len(frv):])[:3]
                 gid = len(geoms)
@@ -447,7 +450,7 @@ def compile_xml_string(text: str, name_hint: str = "", sha: str = "") -> Compile
                               "condim": int(a["condim"]), "friction": np.array(fr),
                               "solref": _floats(a["solref"]), "solimp": _pad_solimp(_floats(a["solimp"])),
                               "solmix": float(a["solmix"]), "margin": float(a["margin"]), "gap": float(a["gap"]),
-                              "density": float(a["density"]), "priority": int(a["priority"])})
+                              "density": dens, "priority": int(a["priority"])})
                 geom_names.append(child.get("name", ""))
                 b["geoms"].append(gid)
             elif tag == "site":

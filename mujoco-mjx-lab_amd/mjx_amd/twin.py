@@ -48,6 +48,14 @@ THIN_SPLITS = None
 COLSUM_CHUNK = int(os.environ.get("MJL_TWIN_COLSUM_CHUNK", "128"))
 
 
+# launch caps of the twin step's fused launches (csrc/ppo_loss_kernels.hip): mjl_adam_multi takes at most
+# ADAM_MULTI_MAX_T tensors (the pair has 4 nl + 1: log_std plus a weight and a bias per layer of each
+# net), mjl_slice_sum_multi at most SLICE_SEG_MAX segments (the pair has 2 nl + 2); deeper nets take
+# the per-net path (tests/test_twin.py checks these against the kernel source)
+ADAM_MULTI_MAX_T = 24
+SLICE_SEG_MAX = 16
+
+
 def _align4(n: int) -> int:
     return (n + 3) // 4 * 4
 
@@ -59,7 +67,8 @@ class TwinNets:
     @staticmethod
     def eligible(policy, value) -> bool:
         pm, vm = policy.mlp, value.mlp
-        if len(pm.layers) != len(vm.layers) or len(pm.layers) < 2:
+        nl = len(pm.layers)
+        if len(vm.layers) != nl or nl < 2 or 4 * nl + 1 > ADAM_MULTI_MAX_T or 2 * nl + 2 > SLICE_SEG_MAX:
             return False
         if not all(a == "tanh" for a in pm.acts[:-1]) or not all(a == "tanh" for a in vm.acts[:-1]):
             return False
@@ -120,10 +129,18 @@ class TwinNets:
         self._scr = {}
 
     def owns_storage(self) -> bool:
-        """Whether the modules' parameters still are views of the stacked storage (a load_state_dict
-        copies into them and keeps it; re-assigning .data would not)."""
-        pm = self.policy.mlp
-        return all(l.weight.data_ptr() == self.W[i][0].data_ptr() for i, l in enumerate(pm.layers))
+        """Whether every parameter of both modules still is its view of the stacked storage (a
+        load_state_dict copies into them and keeps it; re-assigning .data, load_state_dict(assign=True)
+        or another TwinNets over the same modules would not): the update's forward reads the stacked
+        tensors and Adam writes the modules' parameters, so both must be the same memory."""
+        pm, vm = self.policy.mlp, self.value.mlp
+        for l, (lp, lv) in enumerate(zip(pm.layers, vm.layers)):
+            n_v = lv.out_features
+            if (lp.weight.data_ptr() != self.W[l][0].data_ptr() or lp.bias.data_ptr() != self.b[l][0].data_ptr()
+                    or lv.weight.data_ptr() != self.W[l][1, :n_v].data_ptr()
+                    or lv.bias.data_ptr() != self.b[l][1, :n_v].data_ptr()):
+                return False
+        return True
 
     def _scratch(self, key, floats: int) -> torch.Tensor:
         st = torch.cuda.current_stream(self.grad.device).cuda_stream
@@ -229,7 +246,15 @@ class TwinNets:
 
 
 def twin_for(policy, value) -> Optional[TwinNets]:
-    """A TwinNets over (policy, value) when MJL_TWIN_UPDATE is on and the pair is eligible."""
-    if TWIN_UPDATE and TwinNets.eligible(policy, value):
-        return TwinNets(policy, value)
-    return None
+    """A TwinNets over (policy, value) when MJL_TWIN_UPDATE is on and the pair is eligible. The pair's
+    TwinNets is kept on the policy module and reused while it still owns both modules' storage: a
+    second TwinNets over the same modules would re-point their parameters and leave the first one's
+    holder (a trainer's updater) on stale storage."""
+    if not (TWIN_UPDATE and TwinNets.eligible(policy, value)):
+        return None
+    tw = getattr(policy, "_twin_nets", None)
+    if tw is not None and tw.value is value and tw.owns_storage():
+        return tw
+    tw = TwinNets(policy, value)
+    object.__setattr__(policy, "_twin_nets", tw)  # a plain attribute (not a registered submodule)
+    return tw

@@ -166,3 +166,13 @@ def test_flip_tables_involution():
     y = x[op] * osg
     z = y[op] * osg
     assert np.allclose(z, x)
+
+
+def test_explicit_geom_mass_sets_density():
+    """mjx_humanoid_speed_test.py:29-40's SPHERE model gives its geom mass="1": MuJoCo then takes
+    density = mass / volume (mjCGeom::SetInertia), so body mass 1 and inertia 2/5 m r^2."""
+    from mjx_amd import mjcf
+    m = mjcf.compile_xml_string("<mujoco><worldbody><body><freejoint/><geom size='.15' mass='1' type='sphere'/>"
+                                "</body></worldbody></mujoco>")
+    assert m.body_mass[1] == pytest.approx(1.0, rel=1e-12)
+    assert m.body_inertia[1][:3] == pytest.approx([0.4 * 0.15 ** 2] * 3, rel=1e-12)

@@ -105,3 +105,38 @@ def test_twin_update_matches_per_net_update():
         off = err > 2e-6 + 2e-5 * b.abs()
         assert off.float().mean().item() <= 1e-3, f"{int(off.sum())} of {off.numel()} entries off"
         assert err.max().item() <= 2 * 3e-4 * 4
+
+
+def test_deep_nets_take_the_per_net_path():
+    """the twin step's fused launches have caps (mjl_adam_multi 24 tensors, the pair needs
+    4 nl + 1; mjl_slice_sum_multi 16 segments, the pair needs 2 nl + 2). Five hidden layers (nl = 6)
+    exceed them: the pair is not eligible, and an update over them runs on the per-net path."""
+    cfg = reference_ppo_config()
+    cfg.policy_hidden_layer_specs = cfg.value_hidden_layer_specs = [(64, "tanh")] * 5
+    cfg.minibatch_size, cfg.epochs = 8192, 1
+    pol, val = _nets(cfg)
+    assert not twin.TwinNets.eligible(pol, val)
+    op, ov = ppo._adam(pol.parameters(), cfg.lr_policy), ppo._adam(val.parameters(), cfg.lr_value)
+    up = ppo.PPOUpdater(pol, val, op, ov, cfg, use_graph=False)
+    assert up.twin is None
+    before = [p.detach().clone() for p in pol.parameters()]
+    idx = ppo.make_index_batches(8192, 8192, 1, torch.Generator(device="cuda").manual_seed(3), "cuda")
+    up.run(*_data(8192), idx)
+    torch.cuda.synchronize()
+    assert all(torch.isfinite(p).all() for p in pol.parameters())
+    assert any(float((p - b).abs().max()) > 0 for p, b in zip(pol.parameters(), before))
+
+
+def test_twin_storage_reused_and_repointing_detected():
+    """a second updater over the same modules reuses their TwinNets (no re-stacking that
+    would strand the first holder), and re-pointing any value parameter ends ownership."""
+    cfg = reference_ppo_config()
+    pol, val = _nets(cfg)
+    a = twin.twin_for(pol, val)
+    b = twin.twin_for(pol, val)
+    assert a is b and a.owns_storage()
+    with torch.no_grad():
+        val.mlp.layers[1].bias.data = val.mlp.layers[1].bias.data.clone()
+    assert not a.owns_storage()
+    c = twin.twin_for(pol, val)
+    assert c is not a and c.owns_storage()
