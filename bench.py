@@ -607,8 +607,8 @@ class _IdentityComm:
     below runs the data-parallel graphs with the collective taken out)."""
 
     @staticmethod
-    def all_reduce(t, op=None):
-        return t
+    def all_reduce(t, op=None, async_op=False):
+        return None
 
     @staticmethod
     def get_world_size():

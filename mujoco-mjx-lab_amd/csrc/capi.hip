@@ -45,32 +45,7 @@ struct mjlModel {
   mjlModelDesc desc;
   ModelF mf;
   int nefc_max, ncon_max, nvc;  // nvc: 0 = DHum kernels, 1 = DGen kernels
-  int tree;                     // nvc 0 and the primal step kernels run tree-ordered (DHumT): see tree_ok
 };
-
-// The tree-ordered step kernels (DHumT, step_kernels.hip tree_factor_solve) need the reference
-// humanoids' dof tree, Newton (CG's preconditioner reads the stored dense factor of M, which the tree
-// path does not write), and every limited tendon's dofs on one body chain (its row then keeps the
-// Hessian's tree pattern; contacts are checked per env in the kernel). Off unless MJL_TREE=1: measured
-// no faster than the dense panels inside the step kernel at two waves per SIMD.
-static bool tree_ok(const mjlModelDesc* d) {
-  static const bool on = [] { const char* e = std::getenv("MJL_TREE"); return e && e[0] == '1'; }();
-  if (!on || d->nv != HumTree::NV || d->solver != MJL_SOLVER_NEWTON) return false;
-  for (int v = 0; v < d->nv; v++)
-    if (d->dof_parentid[v] != HumTree::parent(v)) return false;
-  auto on_chain = [&](int a, int b) {  // dof a is b or one of b's ancestors, or the other way round
-    for (int x = b; x >= 0; x = d->dof_parentid[x]) if (x == a) return true;
-    for (int x = a; x >= 0; x = d->dof_parentid[x]) if (x == b) return true;
-    return false;
-  };
-  for (int t = 0; t < d->ntendon; t++) {
-    if (!d->tendon_limited[t]) continue;
-    for (int u = 0; u < d->tendon_num[t]; u++)
-      for (int w = u + 1; w < d->tendon_num[t]; w++)
-        if (!on_chain(d->jnt_dofadr[d->tendon_jnt[t][u]], d->jnt_dofadr[d->tendon_jnt[t][w]])) return false;
-  }
-  return true;
-}
 
 struct mjlBatch {
   const mjlModel* model;
@@ -378,7 +353,6 @@ int mjl_model_create(const mjlModelDesc* d, mjlModel** out) {
   M->ncon_max = ncon_max;
   // compact kernel instantiation when the model fits the humanoid capacities, generic otherwise
   M->nvc = (d->nv <= DHum::NV && d->nbody <= DHum::NB && d->njnt <= DHum::NJ && d->ngeom <= DHum::NG) ? 0 : 1;
-  M->tree = (M->nvc == 0 && tree_ok(d)) ? 1 : 0;
   *out = M;
   return MJL_OK;
 }
@@ -659,12 +633,7 @@ template <int MODE> static int launch(mjlBatch* B, const KParams& P, void* strea
   HIPCHK(hipSetDevice(B->device));
   dim3 grid(B->nenv), block(64);
   constexpr bool kOneWave = MODE == MODE_ENV_STEP;
-  const bool tree = B->model->nvc == 0 && B->model->tree;
-  if (tree && kOneWave && one_wave_launch(B))
-    hipLaunchKernelGGL((step_kernel<DHumT, MODE, kOneWave ? 1 : MJL_MINWAVES>), grid, block, 0, (hipStream_t)stream, P);
-  else if (tree)
-    hipLaunchKernelGGL((step_kernel<DHumT, MODE>), grid, block, 0, (hipStream_t)stream, P);
-  else if (B->model->nvc == 0 && kOneWave && one_wave_launch(B))
+  if (B->model->nvc == 0 && kOneWave && one_wave_launch(B))
     hipLaunchKernelGGL((step_kernel<DHum, MODE, kOneWave ? 1 : MJL_MINWAVES>), grid, block, 0, (hipStream_t)stream, P);
   else if (B->model->nvc == 0)
     hipLaunchKernelGGL((step_kernel<DHum, MODE>), grid, block, 0, (hipStream_t)stream, P);

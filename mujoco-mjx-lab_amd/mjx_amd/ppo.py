@@ -730,6 +730,10 @@ def _set_grads(params: List[torch.Tensor], flat: torch.Tensor):
 
 
 TWO_STREAM_UPDATE = os.environ.get("MJL_TWO_STREAM", "1") != "0"  # value net on a side stream in ppo_update
+# data-parallel twin update: the gradient all-reduce in two buckets, the top layers' (and log_std's) in
+# flight while the lower layers' backward runs (PPOUpdater._allreduce_buckets); MJL_DP_BUCKETS=0: one
+# all-reduce after the whole backward
+DP_BUCKETS = os.environ.get("MJL_DP_BUCKETS", "1") != "0"
 _SIDE_STREAMS = {}
 
 
@@ -886,6 +890,44 @@ class PPOUpdater:
             opt_p.step()
             opt_v.step()
 
+    def _bucketed(self) -> bool:
+        """Data-parallel twin runs all-reduce the gradient in two buckets, the first overlapping the
+        lower layers' backward (DP_BUCKETS; needs a hidden-hidden layer below the top two)."""
+        return DP_BUCKETS and self.dist is not None and self._tw and self.twin.nl > 2
+
+    def _body_a_phases(self, idx, src, st, row: Optional[torch.Tensor] = None):
+        """_body_a of the data-parallel twin path in two phases (a generator): the gather, forward, loss
+        head and the top two layers' backward, after which bucket 1 of the gradient is final (yield);
+        then the layers below, finishing bucket 2 (and advancing the captured counters)."""
+        cfg, opt_p, opt_v = self.cfg, self.opt_p, self.opt_v
+        o, a, ol, r, ad = _gather_minibatch(idx, *src, row=row, twice_first=row is not None)
+        ctrs = (opt_p.step_t, opt_v.step_t, row) if row is not None else None
+        gen = self.twin.forward_backward_phases(o, a, ol, r, ad, st, cfg.clip_eps, cfg.ent_coef,
+                                                min(64, o.shape[-2] // SPLIT_ROWS), stats_row=row, counters=ctrs)
+        next(gen)
+        yield
+        next(gen)
+        self._keep_phase = (o, a, ol, r, ad, gen)
+
+    def _allreduce_buckets(self, run_phase2, events):
+        """Bucket 1's all-reduce in flight while run_phase2() enqueues the lower layers' backward, then
+        bucket 2's; both joined into the current stream. `events` gets one pair per minibatch around the
+        exposed part: from the end of phase 2's compute to the end of both collectives."""
+        b1, b2 = self.twin.buckets()
+        w1 = self.dist.all_reduce(b1, async_op=True)
+        run_phase2()
+        ev = None
+        if events is not None:
+            ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+            ev[0].record()
+        w2 = self.dist.all_reduce(b2, async_op=True)
+        for w in (w1, w2):
+            if w is not None and hasattr(w, "wait"):
+                w.wait()
+        if ev is not None:
+            ev[1].record()
+            events.append(ev)
+
     def _body_b(self, row: Optional[torch.Tensor] = None):
         """Data-parallel: the all-reduced gradient sum -> mean, then both Adam steps (advancing the
         twin graphs' minibatch row)."""
@@ -943,6 +985,12 @@ class PPOUpdater:
         self.runs += 1
         if not use_graph:
             for i in range(index_batches.shape[0]):
+                if self._bucketed():
+                    gen = self._body_a_phases(index_batches[i], src, None if stats is None else stats[i])
+                    next(gen)
+                    self._allreduce_buckets(lambda: next(gen, None), events)
+                    self._body_b()
+                    continue
                 self._body_a(index_batches[i], src, None if stats is None else stats[i])
                 if self.dist is not None:
                     self._allreduce(events)
@@ -992,17 +1040,31 @@ class PPOUpdater:
             self._st_all.copy_(stats)
         self._row.zero_()
         st = self._st_all if stats is not None else None
+        bucketed = self._bucketed()
         for _ in range(nmb):
             if self._ga is None:
                 self._ga = torch.cuda.CUDAGraph()
-                with torch.cuda.graph(self._ga):
-                    self._body_a(self._idx_all, self._src, st, row=self._row)
+                if bucketed:  # graph A in two parts around bucket 1's all-reduce, one memory pool
+                    pool = torch.cuda.graph_pool_handle()
+                    with torch.cuda.graph(self._ga, pool=pool):
+                        gen = self._body_a_phases(self._idx_all, self._src, st, row=self._row)
+                        next(gen)
+                    self._ga2 = torch.cuda.CUDAGraph()
+                    with torch.cuda.graph(self._ga2, pool=pool):
+                        next(gen, None)
+                    self._gen_keep = gen  # phase 1's tensors, read by phase 2's replays
+                else:
+                    with torch.cuda.graph(self._ga):
+                        self._body_a(self._idx_all, self._src, st, row=self._row)
                 if self.dist is not None:
                     self._gb = torch.cuda.CUDAGraph()
                     with torch.cuda.graph(self._gb):
                         self._body_b(row=self._row)
             self._ga.replay()
-            if self.dist is not None:
+            if bucketed:
+                self._allreduce_buckets(self._ga2.replay, events)
+                self._gb.replay()
+            elif self.dist is not None:
                 self._allreduce(events)
                 self._gb.replay()
 

@@ -150,6 +150,14 @@ class TwinNets:
             t = self._scr[k] = torch.empty(max(floats, 4), device=self.grad.device)
         return t
 
+    def buckets(self):
+        """The data-parallel all-reduce buffer in two buckets, in the order the backward completes them:
+        bucket 1 = the top two layers of both nets and log_std (grad[o:], finished mid-backward), bucket
+        2 = the layers below (grad[:o])."""
+        o = self.gW[self.nl - 2].data_ptr() - self.grad.data_ptr()
+        o //= self.grad.element_size()
+        return self.grad[o:], self.grad[:o]
+
     def forward_backward(self, o, acts, old_logp, ret, adv, adv_stats, clip_eps: float, ent_coef: float, splits: int,
                          want_value_loss: bool = False, stats_row=None, counters=None):
         """Both nets' losses and gradients for one minibatch (o [M, K0] — or [2, M, K0], the same rows
@@ -159,6 +167,19 @@ class TwinNets:
         [n_minibatches, 2] table, read at that device row. counters: (policy step, value step, row)
         device counters that the final reduction launch advances (the captured update; Adam then runs
         with advanced=True)."""
+        for out in self.forward_backward_phases(o, acts, old_logp, ret, adv, adv_stats, clip_eps, ent_coef, splits,
+                                                want_value_loss, stats_row, counters, split=False):
+            pass
+        return out
+
+    def forward_backward_phases(self, o, acts, old_logp, ret, adv, adv_stats, clip_eps: float, ent_coef: float,
+                                splits: int, want_value_loss: bool = False, stats_row=None, counters=None,
+                                split: bool = True):
+        """forward_backward as a generator. split: it yields None once bucket 1 of buckets() is final
+        (the top two layers' weight-gradient slices and column-sum partials, the loss head's partials,
+        summed in one launch), so the caller can start that bucket's all-reduce while the lower layers'
+        backward runs (the data-parallel update's overlap); its last item is (policy loss, value
+        loss) once bucket 2 -- and, with counters, the captured update's counters -- are final."""
         L = lib()
         dev = o.device
         st = torch.cuda.current_stream(dev).cuda_stream
@@ -233,16 +254,24 @@ class TwinNets:
             segs.append((part, self.gW[l], 2, s, N * K))
             if l > 0:
                 g = torch.bmm(dzl, self.W[l])  # [2, M, K]
+            if split and l == nl - 2:  # bucket 1 complete: its second stages now, then the caller's turn
+                self._slice_sum(segs, None, st)
+                self._keep1 = (segs, hs, g)  # read by the launches in flight (and, captured, by the replays)
+                segs = []
+                yield None
+        self._slice_sum(segs, counters, st)
+        yield loss_p, loss_v
+
+    def _slice_sum(self, segs, counters, st):
         import ctypes
         k = len(segs)
         c0, c1, c2 = (None, None, None) if counters is None else (c.data_ptr() for c in counters)
-        check(L.mjl_slice_sum_multi(k, (ctypes.c_void_p * k)(*[x.data_ptr() for x, *_ in segs]),
-                                    (ctypes.c_void_p * k)(*[o.data_ptr() for _, o, *_ in segs]),
-                                    (ctypes.c_int * k)(*[nb for _, _, nb, _, _ in segs]),
-                                    (ctypes.c_int * k)(*[ns for _, _, _, ns, _ in segs]),
-                                    (ctypes.c_longlong * k)(*[m for *_, m in segs]), c0, c1, c2, st))
+        check(lib().mjl_slice_sum_multi(k, (ctypes.c_void_p * k)(*[x.data_ptr() for x, *_ in segs]),
+                                        (ctypes.c_void_p * k)(*[o.data_ptr() for _, o, *_ in segs]),
+                                        (ctypes.c_int * k)(*[nb for _, _, nb, _, _ in segs]),
+                                        (ctypes.c_int * k)(*[ns for _, _, _, ns, _ in segs]),
+                                        (ctypes.c_longlong * k)(*[m for *_, m in segs]), c0, c1, c2, st))
         self._keep = segs  # the launch reads the partial buffers asynchronously
-        return loss_p, loss_v
 
 
 def twin_for(policy, value) -> Optional[TwinNets]:

@@ -249,3 +249,44 @@ def test_qpos_history_dump(tmp_path):
     for t in range(10):
         s, aux, *_ = o.env_step(cfg_c, s, aux, d["act"][t].astype(np.float64))
         np.testing.assert_allclose(d["qpos"][t], state_arrays(m, s)["qpos"], atol=1e-3)
+
+
+def test_apg_c4_step_descends_after_normalisation():
+    """the C4 update's direction at full size (2048 x 128, CG 4/4, implicit VJP), probed
+    at the first post-normalisation update (100, train_apg.py:256,262). On that update's own resets,
+    with the observation statistics held at their pre-update values, the clipped Adam step lowers the
+    loss at 1 and 10 learning-rate steps: loss(theta0 + eps (theta1 - theta0)) < loss(theta0) for eps
+    in {1, 10}. Statistics from the observations in the loss (--rms-in-loss-only: under the reference's
+    rule, every rollout observation, the statistics collapse at this update and the gradient is not
+    finite, DESIGN.md "APG at C4"). Deterministic: the same run gives the same losses (measured round
+    4, tools/apg_direction_probe.py: 101.11 -> 99.94 / 99.46)."""
+    from mjx_amd import apg
+    from train_apg import apg_model
+    cfg = APGConfig()
+    cfg.batch_size, cfg.horizon = 2048, 128
+    cfg.rms_in_loss_only = True
+    m = apg_model(cfg, solver="cg")
+    env = HumanoidEnv(mjx.put_model(m), resolve_ids(m, EnvConfig()), cfg.batch_size, seed=cfg.seed)
+    tr = apg.APGTrainer(cfg, apg.HumanoidAPGEnv(env, "implicit"), device="cuda", use_graph=False)
+    for it in range(100):
+        tr.update(it)
+    params = list(tr.policy.parameters())
+    c0 = env.counter
+    rms0 = (tr.rms.mean.clone(), tr.rms.var.clone(),
+            tr.rms.count.clone() if torch.is_tensor(tr.rms.count) else float(tr.rms.count))
+    th0 = [p.detach().clone() for p in params]
+    met = tr.update(100)
+    assert np.isfinite(met["grad_norm"]) and met["reverse_nonfinite_envs"] == 0, met
+    th1 = [p.detach().clone() for p in params]
+    tr.rms.mean, tr.rms.var, tr.rms.count = rms0
+    losses = {}
+    with torch.no_grad():
+        for eps in (0.0, 1.0, 10.0):
+            for p, x0, x1 in zip(params, th0, th1):
+                p.copy_(x0 + eps * (x1 - x0))
+            env.counter = c0
+            with torch.enable_grad():
+                losses[eps] = float(tr.loss_and_grad(True)[0])
+    print("APG C4 update 100 losses at eps 0 / 1 / 10:", losses)
+    assert losses[0.0] == pytest.approx(met["loss"], rel=1e-5)
+    assert losses[1.0] < losses[0.0] and losses[10.0] < losses[0.0]

@@ -98,8 +98,8 @@ class _NoComm:
     """A one-rank stand-in for torch.distributed in the probe: all_reduce is the identity."""
 
     @staticmethod
-    def all_reduce(t, op=None):
-        return t
+    def all_reduce(t, op=None, async_op=False):
+        return None
 
     @staticmethod
     def get_world_size():

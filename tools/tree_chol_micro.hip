@@ -13,6 +13,194 @@
 #include <cstdlib>
 #include <vector>
 
+#include <type_traits>
+
+namespace mjl {
+// compile-time loop: f(std::integral_constant<int, i>) for i in [B, E)
+template <int B, int E, class F> INL void static_for(F&& f) {
+  if constexpr (B < E) {
+    f(std::integral_constant<int, B>{});
+    static_for<B + 1, E>(f);
+  }
+}
+
+
+// ---------------------------------------------------------------------------------------------
+// tree-ordered factor + solve (the two reference humanoids' dof tree). Measured in the step kernel
+// in round 5 (MJL_TREE=1 instantiation, profiles/r5/): no faster than the dense panels there --
+// speed test 58.13 vs 58.27 us, pooled env step 90.5 vs 88.2 us at 2048 envs, 79.6 vs 78.3 us at
+// 1024 -- so it lives here, not in the product ("tree-ordered factor").
+// ---------------------------------------------------------------------------------------------
+// The dof tree of humanoid.xml / humanoid_mjx.xml (dof_parentid): a trunk of 9 dofs (the free
+// joint's 6, then abdomen z, y, x) and four chains hanging off it -- the legs (6 dofs each, parent
+// dof 8) and the arms (3 each, parent dof 5). The mass matrix has exactly the tree's pattern (entry
+// (i, j) is nonzero only when one dof is an ancestor of the other), so do M + dt diag(damping) and
+// the Newton Hessian M + J'DJ whenever no active row couples two branches (every row's J lies on one
+// body chain: floor contacts, joint limits, the hamstring tendons). Eliminating the dofs leaves
+// first (MuJoCo's mj_factorM order, M = L' D L) makes no fill, and the four chains are independent:
+// 15 dependent columns instead of 27.
+struct HumTree {
+  static constexpr int NV = 27, TN = 9, NBR = 4;
+  static constexpr int bs[NBR] = {9, 15, 21, 24};   // first dof of each chain
+  static constexpr int be[NBR] = {15, 21, 24, 27};  // one past its last dof
+  static constexpr int bp[NBR] = {8, 8, 5, 5};      // the trunk dof it hangs off
+  static constexpr int len(int b) { return be[b] - bs[b]; }
+  static constexpr int parent(int d) {  // dof_parentid of this tree
+    if (d < TN) return d - 1;
+    for (int b = 0; b < NBR; b++)
+      if (d == bs[b]) return bp[b];
+    return d - 1;
+  }
+};
+
+// L' D L = S (S: the tree-patterned SPD matrix in LDS at src, stride LD; ADD: plus the symmetric
+// MFMA-layout addend C, as chol_aug_factor_solve), returns S^-1 rhs with row i's value in lanes i
+// and i + 32; `scratch` (LD floats of LDS) carries the forward substitution's result between lanes.
+// Nothing is stored: the callers that use it only need the solution (the Newton direction,
+// qacc_smooth, the implicit-integration update).
+//
+// Layout: lane l holds row l & 31 of S in registers a[0..LD) (the whole row, both triangles), and
+// the right-hand side rides along as one more row R = NV (lane R: a[j] = rhs_j). Eliminating dof k
+// (pivot d_k = S'[k][k], broadcast of row k by v_readlane) updates S'[i][j] -= S'[i][k] S'[k][j] / d_k
+// for i, j in k's ancestors -- lane i's multiplier t = a[k] / d_k is nonzero only on the ancestors'
+// lanes (and lane R, whose row update is the forward substitution), so one VALU op per column j
+// updates every row at once.
+//  1. chains, leaves first, the four chains' columns interleaved: each elimination updates only its
+//     own chain's columns on the VALU; its update of the trunk columns -- every lane's a[j], j in the
+//     trunk -- is deferred to one rank-18 product C[j][i] = sum_k a_j[k] t_i[k] on the matrix cores
+//     (the legs' columns pairwise in one v_mfma_f32_32x32x2_f32 per elimination step, the arms' in a
+//     second accumulator), so a chain elimination's VALU work is the chain's own columns only;
+//  2. the trunk, dofs 8 .. 0, on the VALU;
+//  3. lane R's row (z = L'^-1 rhs) through `scratch` to the lanes, x = D^-1 z, then L x = that,
+//     ancestors first: the trunk's 9 columns, then the four chains' columns on four registers (no
+//     false dependency between the chains), each lane keeping its own value at its own step.
+template <int V> using IC = std::integral_constant<int, V>;
+template <class D, class T, bool ADD> INL float tree_factor_solve(const LDSA float* src, LDSA float* scratch,
+                                                                 const LDSA float* rhs, int lane, f32x16 C = {}) {
+  constexpr int NV = D::NV, LD = D::LD, R = NV, TN = T::TN;
+  static_assert(NV == T::NV && NV < 32 && LD > NV && LD % 4 == 0, "tree factor: the humanoid instantiation");
+  static_assert(T::NBR == 4 && T::len(0) == T::len(1) && T::len(2) == T::len(3) && T::len(2) <= T::len(0),
+                "chains paired legs / arms for the deferred trunk update");
+  static_assert(TN <= 12, "trunk rows within the extracted MFMA registers");
+  const int i = lane & 31, kh = lane >> 5;
+  float a[LD];
+  if constexpr (ADD) {
+#pragma unroll
+    for (int v = 0; v < 16; v++) {
+      auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(C[v]), __float_as_uint(C[v]), false, false);
+      const int j0 = (v & 3) + 8 * (v >> 2);
+      if (j0 < LD) a[j0] = __uint_as_float(r[0]);
+      if (j0 + 4 < LD) a[j0 + 4] = __uint_as_float(r[1]);
+    }
+  }
+  {  // row i of S (lanes i < NV), the right-hand side as row R (lanes >= NV; kept by lane R)
+    const LDSA f32x4* rp = (const LDSA f32x4*)((i < NV) ? src + i * LD : rhs);
+#pragma unroll
+    for (int q = 0; q < LD / 4; q++) {
+      const f32x4 v = rp[q];
+#pragma unroll
+      for (int e = 0; e < 4; e++) a[4 * q + e] = ADD ? a[4 * q + e] + v[e] : v[e];
+    }
+  }
+  // the lane's row index for the masks, with row R ordered before every dof (it is updated by
+  // every elimination and never eliminated); opaque: the compares stay at their uses
+  const int io = opaque_int(i == R ? -1 : i);
+  float dinv = 1.f;  // 1 / d of the lane's own dof
+  auto eliminate = [&](auto kc, auto j0c, auto j1c) {  // dof k: update columns [j0, j1) of its ancestors
+    constexpr int k = decltype(kc)::value, j0 = decltype(j0c)::value, j1 = decltype(j1c)::value;
+    const float inv = __builtin_amdgcn_rcpf(rdlane(a[k], k));
+    float s[LD];
+#pragma unroll
+    for (int j = j0; j < j1; j++) s[j] = rdlane(a[j], k);
+    const float t = (io < k) ? a[k] * inv : 0.f;
+#pragma unroll
+    for (int j = j0; j < j1; j++) a[j] = fmaf(-t, s[j], a[j]);
+    dinv = (io == k) ? inv : dinv;
+    return t;
+  };
+  // 1. the chains, leaves first; deferred trunk update C[j][i] = sum_k a_j[k] t_i[k]
+  f32x16 accL, accA;
+#pragma unroll
+  for (int v = 0; v < 16; v++) { accL[v] = 0.f; accA[v] = 0.f; }
+  constexpr int L0 = T::len(0), L2 = T::len(2);
+  static_for<0, L0>([&](auto sc) {
+    constexpr int s = decltype(sc)::value;
+    constexpr int k0 = T::be[0] - 1 - s, k1 = T::be[1] - 1 - s;
+    const float t0 = eliminate(IC<k0>{}, IC<T::bs[0]>{}, IC<k0>{});
+    const float t1 = eliminate(IC<k1>{}, IC<T::bs[1]>{}, IC<k1>{});
+    accL = __builtin_amdgcn_mfma_f32_32x32x2f32(kh ? a[k1] : a[k0], kh ? t1 : t0, accL, 0, 0, 0);
+    if constexpr (s < L2) {
+      constexpr int k2 = T::be[2] - 1 - s, k3 = T::be[3] - 1 - s;
+      const float t2 = eliminate(IC<k2>{}, IC<T::bs[2]>{}, IC<k2>{});
+      const float t3 = eliminate(IC<k3>{}, IC<T::bs[3]>{}, IC<k3>{});
+      accA = __builtin_amdgcn_mfma_f32_32x32x2f32(kh ? a[k3] : a[k2], kh ? t3 : t2, accA, 0, 0, 0);
+    }
+  });
+  {  // a[j] -= C[j][lane] for the trunk columns (C layout: row j of column l & 31 in half (j >> 2) & 1,
+     // register (j & 3) + 4 (j >> 3); one v_permlane32_swap hands each lane both halves)
+    float lo[4], hi[4];
+#pragma unroll
+    for (int v = 0; v < 4 * ((TN + 7) / 8); v++) {
+      const int vv = v;  // registers 0..3 (rows 0-7), 4..7 (rows 8-15)
+      const float c = accL[vv] + accA[vv];
+      auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(c), __float_as_uint(c), false, false);
+      if (vv < 4) { lo[vv] = __uint_as_float(r[0]); hi[vv] = __uint_as_float(r[1]); }
+      else {
+#pragma unroll
+        for (int j = 8; j < TN; j++)
+          if ((j & 3) + 4 == vv) a[j] -= ((j >> 2) & 1) ? __uint_as_float(r[1]) : __uint_as_float(r[0]);
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < (TN < 8 ? TN : 8); j++) a[j] -= ((j >> 2) & 1) ? hi[j & 3] : lo[j & 3];
+  }
+  // 2. the trunk (a chain: every lower dof is an ancestor)
+  static_for<0, TN>([&](auto sc) {
+    constexpr int k = TN - 1 - decltype(sc)::value;
+    (void)eliminate(IC<k>{}, IC<0>{}, IC<k>{});
+  });
+  // 3. z = lane R's row, x = D^-1 z, then L x = that (L[i][j] = a_i[j] / d_i, j an ancestor of i)
+  if (lane == R) {
+    LDSA f32x4* wp = (LDSA f32x4*)scratch;
+#pragma unroll
+    for (int q = 0; q < LD / 4; q++) {
+      f32x4 v;
+      v[0] = a[4 * q]; v[1] = a[4 * q + 1]; v[2] = a[4 * q + 2]; v[3] = a[4 * q + 3];
+      wp[q] = v;
+    }
+  }
+  // (same wave: the LDS store completes before the read)
+  const float z = scratch[i < NV ? i : 0];
+  float x = (i < NV) ? z * dinv : 0.f, xf = x;
+#pragma unroll
+  for (int j = 0; j < NV; j++) a[j] *= dinv;  // rows of L (lanes past a finished dof's step may take
+                                              // junk updates: each lane keeps its value at its own step)
+  static_for<0, TN>([&](auto jc) {
+    constexpr int j = decltype(jc)::value;
+    const float xj = rdlane(x, j);
+    xf = (io == j) ? xj : xf;
+    x = fmaf(-a[j], xj, x);
+  });
+  float xb[T::NBR];
+#pragma unroll
+  for (int b = 0; b < T::NBR; b++) xb[b] = x;
+  static_for<0, L0>([&](auto sc) {
+    constexpr int s = decltype(sc)::value;
+    static_for<0, T::NBR>([&](auto bc) {
+      constexpr int b = decltype(bc)::value;
+      if constexpr (s < T::len(b)) {
+        constexpr int j = T::bs[b] + s;
+        const float xj = rdlane(xb[b], j);
+        xf = (io == j) ? xj : xf;
+        xb[b] = fmaf(-a[j], xj, xb[b]);
+      }
+    });
+  });
+  return xf;
+}
+
+}  // namespace mjl
+
 using namespace mjl;
 using D = DHum;
 constexpr int NV = D::NV, LD = D::LD, NMAT = 97;
