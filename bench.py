@@ -503,9 +503,13 @@ def ppo_leg(tr, iters: int, warmup: int, dist, device, curve=()) -> dict:
         one()
     world = 1 if dist is None else dist.get_world_size()
     env_steps = float(tr.env.num_envs * world * tr.cfg.rollout_length * iters)
+    # RCCL collectives captured in the update's step graph (ppo.DP_CAPTURE) have no events of their own:
+    # their count comes from the updater, their time is inside the update phase
+    captured = dist is not None and not ar and getattr(tr.updater, "collectives_last_run", 0) > 0
+    n_ar = tr.updater.collectives_last_run if captured else len(ar) // max(1, iters)
     return {"env_steps_per_s": env_steps / wall, "ms_per_iter": wall / iters * 1e3, "iters": iters,
             "warmup": warmup, "envs_per_rank": tr.env.num_envs, "ranks": world,
-            "allreduce_ms": ar_ms, "allreduces_per_iter": len(ar) // max(1, iters),
+            "allreduce_ms": None if captured else ar_ms, "allreduces_per_iter": n_ar, "allreduce_captured": captured,
             "train_return_avg": [r["train_return_avg"] for r in res], "return_at_iter": returns,
             "next_iteration": it[0], "phase_ms": phases, "update_rows": getattr(tr, "last_update_rows", 0)}
 
@@ -515,6 +519,7 @@ def c5_fields(res: dict, world: int, backend: str, grad_numel: int) -> dict:
     return {"ppo_c5_env_steps_per_s": res["env_steps_per_s"], "ppo_c5_ms_per_iter": res["ms_per_iter"],
             "ppo_c5_envs_per_rank": res["envs_per_rank"], "ppo_c5_global_envs": res["envs_per_rank"] * world,
             "allreduce_ms_per_minibatch": res["allreduce_ms"], "allreduces_per_iteration": res["allreduces_per_iter"],
+            "allreduce_captured_in_graph": res.get("allreduce_captured", False),
             "allreduce_bytes": 4 * grad_numel, "collective_backend": backend, "collective_ranks": world,
             "rccl_ranks": world if backend == "nccl" else 0,
             "ppo_c5_train_return_avg": res["train_return_avg"], "ppo_c5_phase_ms_per_rank": res["phase_ms"]}
@@ -581,7 +586,8 @@ def policy_roofline(tr, local) -> dict:
     sync(dev)
     n = 100
     g = torch.cuda.CUDAGraph()
-    with torch.cuda.graph(g):
+    from mjx_amd.ppo import graph_capture
+    with graph_capture(g):
         for _ in range(n):
             launch()
     g.replay()
@@ -738,7 +744,8 @@ def apg_c4(args, local) -> dict:
             # launches run back to back as in the trainer's graph (per-launch event pairs around eager
             # launches also timed the gaps between them: 127 against rocprofv3's 101 us in round 3)
             g = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(g):
+            from mjx_amd.ppo import graph_capture
+            with graph_capture(g):
                 sweep()
             g.replay()
             sync(dev)

@@ -2358,9 +2358,11 @@ template <class D> INL void rs_load(MP m, const CSTA KParams* Pk, LDSA WS<D>* W,
 // ---------------------------------------------------------------------------------------------
 // the kernel: one workgroup (= one wavefront) per env
 // ---------------------------------------------------------------------------------------------
-// MW = the waves per SIMD the register budget is sized for: 2 (248 VGPRs, the full-occupancy launches:
-// 2048 envs resident on 256 CUs) or 1 (the whole 512-entry register file: launches of at most one wave
-// per SIMD, e.g. C3's 1024-env rollout, where a second wave's share of the file would sit unused)
+// MW = the waves-per-SIMD bound of the launch: 2 (the full-occupancy launches: 2048 envs resident on
+// 256 CUs) or 1 (launches of at most one wave per SIMD, e.g. C3's 1024-env rollout). The one-wave
+// instantiation does not take the whole 512-entry register file: it compiles to the same 248 VGPRs (+ 32
+// AGPRs) with fewer SGPR spills (69 against 94 in the env step); its gain is the compiler's schedule and
+// spill placement under the looser bound, not registers.
 template <class D, int MODE, int MW = MJL_MINWAVES> __global__ __launch_bounds__(64, MW) void step_kernel(KParams P) {
   __shared__ WS<D> Ws;
   __shared__ float aux_s[MJL_AUX_DIM + 3];

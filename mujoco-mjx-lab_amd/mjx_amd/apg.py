@@ -24,7 +24,7 @@ from typing import Optional
 
 import torch
 
-from .ppo import APGPolicy, RunningMeanStd, _flat_grads, _jsonable, _set_grads
+from .ppo import APGPolicy, RunningMeanStd, _flat_grads, _jsonable, _set_grads, graph_capture
 
 
 def _u8(t: torch.Tensor):
@@ -165,7 +165,7 @@ class APGTrainer:
             graph = torch.cuda.CUDAGraph()
             c0 = env.counter
             self.opt.zero_grad(set_to_none=True)
-            with torch.cuda.graph(graph):
+            with graph_capture(graph):
                 out = self._loss_and_grad(use_norm, False, graph=True)
             # the counters the eager call takes: the host code's during capture, plus the reset's own
             # (passed explicitly, relative to the base, under capture)

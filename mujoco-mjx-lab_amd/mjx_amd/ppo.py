@@ -730,10 +730,23 @@ def _set_grads(params: List[torch.Tensor], flat: torch.Tensor):
 
 
 TWO_STREAM_UPDATE = os.environ.get("MJL_TWO_STREAM", "1") != "0"  # value net on a side stream in ppo_update
+def graph_capture(graph, pool=None):
+    """torch.cuda.graph with capture_error_mode="thread_local": RCCL's watchdog thread queries its
+    collectives' events while this thread captures, and under the default "global" mode such a query
+    invalidates the capture (measured: an eager bucketed update followed by the rollout capture failed
+    with hipErrorStreamCaptureInvalidated). Only this thread's own calls are checked."""
+    return torch.cuda.graph(graph, pool=pool, capture_error_mode="thread_local")
+
+
 # data-parallel twin update: the gradient all-reduce in two buckets, the top layers' (and log_std's) in
-# flight while the lower layers' backward runs (PPOUpdater._allreduce_buckets); MJL_DP_BUCKETS=0: one
-# all-reduce after the whole backward
-DP_BUCKETS = os.environ.get("MJL_DP_BUCKETS", "1") != "0"
+# flight while the lower layers' backward runs (PPOUpdater._allreduce_buckets). MJL_DP_BUCKETS: "auto"
+# (default) = with more than one rank (one rank has no link time to hide, and the second collective
+# costs 0.85 ms per C5 update there, DESIGN.md §5), "1" always, "0" never
+DP_BUCKETS = os.environ.get("MJL_DP_BUCKETS", "auto")
+# data-parallel update over RCCL: the minibatch step's collective(s) captured in its graph, one replay
+# per minibatch step (MJL_DP_CAPTURE=0: eager collectives between the graphs). One-rank RCCL, C5's
+# per-rank update (128 steps of 8,192 rows): 33.1 ms eager -> 30.0 ms captured (profiles/r5/)
+DP_CAPTURE = os.environ.get("MJL_DP_CAPTURE", "1") != "0"
 _SIDE_STREAMS = {}
 
 
@@ -828,7 +841,7 @@ class PPOUpdater:
         self._tw = False  # this run takes the twin path (minibatch shape permitting)
         self.runs = 0
         self._src = self._idx = self._st = None
-        self._ga = self._gb = None
+        self._ga = self._gb = self._gstep = None
 
     def _twin_ok(self, rows: int, act_dim: int) -> bool:
         return (self.twin is not None and rows >= UPDATE_MIN_ROWS and rows % SPLIT_ROWS == 0 and rows % 128 == 0
@@ -893,7 +906,9 @@ class PPOUpdater:
     def _bucketed(self) -> bool:
         """Data-parallel twin runs all-reduce the gradient in two buckets, the first overlapping the
         lower layers' backward (DP_BUCKETS; needs a hidden-hidden layer below the top two)."""
-        return DP_BUCKETS and self.dist is not None and self._tw and self.twin.nl > 2
+        if DP_BUCKETS == "0" or self.dist is None or not self._tw or self.twin.nl <= 2:
+            return False
+        return DP_BUCKETS == "1" or self.world > 1
 
     def _body_a_phases(self, idx, src, st, row: Optional[torch.Tensor] = None):
         """_body_a of the data-parallel twin path in two phases (a generator): the gather, forward, loss
@@ -979,7 +994,7 @@ class PPOUpdater:
         stats = minibatch_adv_stats(adv, index_batches, self.dist) if self.dist is not None else None
         tw = self._twin_ok(int(index_batches.shape[1]), int(acts.shape[1]) if acts.dim() == 2 else -1)
         if tw != self._tw:
-            self._ga = self._gb = None  # the captured bodies belong to the other path
+            self._ga = self._gb = self._gstep = None  # the captured bodies belong to the other path
         self._tw = tw
         use_graph = self.graph_ok and self.runs > 0
         self.runs += 1
@@ -1001,7 +1016,7 @@ class PPOUpdater:
             self._src = tuple(torch.empty_like(x, memory_format=torch.contiguous_format) for x in src)
             self._idx = torch.empty(mb, dtype=index_batches.dtype, device=index_batches.device)
             self._st = torch.zeros(2, device=adv.device)
-            self._ga = self._gb = None
+            self._ga = self._gb = self._gstep = None
         for dst, x in zip(self._src, src):  # the graphs read the static copies
             dst.copy_(x)
         if self._tw:  # the twin graphs read the update's index / statistics tables at a device row
@@ -1013,11 +1028,11 @@ class PPOUpdater:
                 self._st.copy_(stats[i])
             if self._ga is None:
                 self._ga = torch.cuda.CUDAGraph()
-                with torch.cuda.graph(self._ga):
+                with graph_capture(self._ga):
                     self._body_a(self._idx, self._src, None if stats is None else self._st)
                 if self.dist is not None:
                     self._gb = torch.cuda.CUDAGraph()
-                    with torch.cuda.graph(self._gb):
+                    with graph_capture(self._gb):
                         self._body_b()
             self._ga.replay()
             if self.dist is not None:
@@ -1034,31 +1049,34 @@ class PPOUpdater:
             self._idx_all = torch.empty_like(index_batches, memory_format=torch.contiguous_format)
             self._st_all = torch.zeros((nmb, 2), device=index_batches.device)
             self._row = torch.zeros(1, dtype=torch.int32, device=index_batches.device)
-            self._ga = self._gb = None
+            self._ga = self._gb = self._gstep = None
         self._idx_all.copy_(index_batches)
         if stats is not None:
             self._st_all.copy_(stats)
         self._row.zero_()
         st = self._st_all if stats is not None else None
         bucketed = self._bucketed()
+        if self._capture_collectives():
+            self._run_captured_steps(nmb, st, bucketed)
+            return
         for _ in range(nmb):
             if self._ga is None:
                 self._ga = torch.cuda.CUDAGraph()
                 if bucketed:  # graph A in two parts around bucket 1's all-reduce, one memory pool
                     pool = torch.cuda.graph_pool_handle()
-                    with torch.cuda.graph(self._ga, pool=pool):
+                    with graph_capture(self._ga, pool=pool):
                         gen = self._body_a_phases(self._idx_all, self._src, st, row=self._row)
                         next(gen)
                     self._ga2 = torch.cuda.CUDAGraph()
-                    with torch.cuda.graph(self._ga2, pool=pool):
+                    with graph_capture(self._ga2, pool=pool):
                         next(gen, None)
                     self._gen_keep = gen  # phase 1's tensors, read by phase 2's replays
                 else:
-                    with torch.cuda.graph(self._ga):
+                    with graph_capture(self._ga):
                         self._body_a(self._idx_all, self._src, st, row=self._row)
                 if self.dist is not None:
                     self._gb = torch.cuda.CUDAGraph()
-                    with torch.cuda.graph(self._gb):
+                    with graph_capture(self._gb):
                         self._body_b(row=self._row)
             self._ga.replay()
             if bucketed:
@@ -1067,6 +1085,40 @@ class PPOUpdater:
             elif self.dist is not None:
                 self._allreduce(events)
                 self._gb.replay()
+
+
+    def _capture_collectives(self) -> bool:
+        """The data-parallel minibatch step as ONE graph with its RCCL all-reduce(s) captured inside
+        (DP_CAPTURE, RCCL process groups only): no host round trip and no eager cross-stream
+        synchronisation between the backward, the collective and the Adam step."""
+        if not (DP_CAPTURE and self.dist is not None and self._tw):
+            return False
+        try:
+            return self.dist.get_backend() == "nccl"
+        except Exception:  # a stand-in without backends (bench's identity collective)
+            return False
+
+    def _run_captured_steps(self, nmb, st, bucketed):
+        if getattr(self, "_gstep", None) is None:
+            self._gstep = torch.cuda.CUDAGraph()
+            with graph_capture(self._gstep):
+                if bucketed:
+                    gen = self._body_a_phases(self._idx_all, self._src, st, row=self._row)
+                    next(gen)
+                    b1, b2 = self.twin.buckets()
+                    w1 = self.dist.all_reduce(b1, async_op=True)
+                    next(gen, None)
+                    w2 = self.dist.all_reduce(b2, async_op=True)
+                    w1.wait()
+                    w2.wait()
+                    self._gen_keep = gen
+                else:
+                    self._body_a(self._idx_all, self._src, st, row=self._row)
+                    self.dist.all_reduce(self._grad_buffer())
+                self._body_b(row=self._row)
+        for _ in range(nmb):
+            self._gstep.replay()
+        self.collectives_last_run = nmb * (2 if bucketed else 1)
 
 
 def ppo_update(policy, value, opt_p, opt_v, obs, acts, logp, ret, adv, index_batches, cfg, dist=None, world=1,
@@ -1243,7 +1295,7 @@ class PPOTrainer:
         use_graph = self.use_graph and self.device.type == "cuda" and hasattr(env, "ctr_base")
         if use_graph and self._graph is None and self._rollouts > 0:
             self._graph = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(self._graph):
+            with graph_capture(self._graph):
                 self._rollout_body(graph=True)
         if use_graph and self._graph is not None:
             env.ctr_base.fill_(env.counter)

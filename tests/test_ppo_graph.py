@@ -85,6 +85,55 @@ def test_data_parallel_update_graph_bit_identical_to_eager():
         tdist.destroy_process_group()
 
 
+def _one_rank_group(backend):
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    kw = {"device_id": torch.device("cuda", 0)} if backend == "nccl" else {}
+    tdist.init_process_group(backend, init_method=f"tcp://127.0.0.1:{port}", rank=0, world_size=1, **kw)
+
+
+def test_data_parallel_bucketed_update_graph_bit_identical_to_eager(monkeypatch):
+    """The bucketed data-parallel step (the gradient all-reduced in two buckets, the first in flight
+    while the lower layers' backward runs; graph A in two parts around it) equals its eager run bit for
+    bit (gloo, one rank, buckets forced on: by default they are on only with more than one rank)."""
+    monkeypatch.setattr(ppo, "DP_BUCKETS", "1")
+    _one_rank_group("gloo")
+    try:
+        cfg = reference_ppo_config()
+        cfg.minibatch_size, cfg.epochs = 8192, 2
+        _run_pair(cfg, 4 * 8192, tdist)
+    finally:
+        tdist.destroy_process_group()
+
+
+@pytest.mark.parametrize("buckets", ["0", "1"])
+def test_rccl_captured_step_graph_bit_identical_to_eager(monkeypatch, buckets):
+    """Over RCCL the data-parallel minibatch step is ONE graph with its all-reduce(s) captured inside
+    (ppo.DP_CAPTURE): the replays equal the eager update (collectives between eager bodies) bit for bit,
+    one rank on cuda:0, one bucket and two."""
+    monkeypatch.setattr(ppo, "DP_BUCKETS", buckets)
+    _one_rank_group("nccl")
+    try:
+        cfg = reference_ppo_config()
+        cfg.minibatch_size, cfg.epochs = 8192, 2
+        A = _nets_and_data(cfg, 4 * 8192)
+        B = _nets_and_data(cfg, 4 * 8192)
+        ua = ppo.PPOUpdater(*A[:4], cfg, tdist, 1, use_graph=True)
+        ub = ppo.PPOUpdater(*B[:4], cfg, tdist, 1, use_graph=False)
+        for run in range(3):
+            idx = ppo.make_index_batches(4 * 8192, cfg.minibatch_size, cfg.epochs,
+                                         torch.Generator(device="cuda").manual_seed(200 + run), "cuda")
+            ua.run(*A[4], idx)
+            ub.run(*B[4], idx)
+            torch.cuda.synchronize()
+            _compare(_state(*A[:4]), _state(*B[:4]), run)
+        assert ua._gstep is not None and ua.collectives_last_run == idx.shape[0] * (2 if buckets == "1" else 1)
+    finally:
+        tdist.destroy_process_group()
+
+
 def test_native_adam_state_dict_is_torch_layout():
     """NativeAdam checkpoints use torch.optim.Adam's state-dict layout, both ways, and a
     mismatched parameter count is refused."""
