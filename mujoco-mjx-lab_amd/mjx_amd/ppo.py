@@ -1056,9 +1056,17 @@ class PPOUpdater:
         self._row.zero_()
         st = self._st_all if stats is not None else None
         bucketed = self._bucketed()
-        if self._capture_collectives():
-            self._run_captured_steps(nmb, st, bucketed)
-            return
+        if self._capture_collectives() and not getattr(self, "_capture_failed", False):
+            try:
+                self._run_captured_steps(nmb, st, bucketed)
+                return
+            except RuntimeError as e:  # (a capture refused by this RCCL build: eager collectives from here on;
+                # nothing ran — the replays come after a successful capture)
+                import warnings
+                warnings.warn(f"PPOUpdater: RCCL collective capture failed ({e}); eager collectives instead")
+                self._capture_failed = True
+                self._gstep = None
+                torch.cuda.synchronize()
         for _ in range(nmb):
             if self._ga is None:
                 self._ga = torch.cuda.CUDAGraph()
