@@ -756,6 +756,31 @@ def apg_c4(args, local) -> dict:
             sync(dev)
             kms = e0.elapsed_time(e1) / H
             del g
+            # the same H launches on the trainer's own workload: the last update's reward cotangents and
+            # actions, the state cotangents chained step to step (the observation / policy terms the
+            # trainer adds between launches left out), so the envs past termination take the kernel's
+            # all-zero early exit as in training (the rocprofv3 average of the trainer)
+            kms_tr = None
+            if tr.last_reverse_inputs is not None:
+                grew_all, acts = tr.last_reverse_inputs
+
+                def sweep_tr():
+                    q, v, ax = torch.zeros_like(gq), torch.zeros_like(gv), gaux
+                    for t in range(H - 1, -1, -1):
+                        q, v, _, _, ax = aenv.step_vjp_replay(t, acts[t], q, v, None, grew_all[t], ax, nonf)
+                sweep_tr()
+                sync(dev)
+                g = torch.cuda.CUDAGraph()
+                with graph_capture(g):
+                    sweep_tr()
+                g.replay()
+                sync(dev)
+                e0.record()
+                g.replay()
+                e1.record()
+                sync(dev)
+                kms_tr = e0.elapsed_time(e1) / H
+                del g
             # the rollout's solver statistics (the same policy from fresh resets; CG reports no active-row
             # count, so the implicit Hessian is counted over all rows)
             env.data.set_option(0, 1)
@@ -772,6 +797,7 @@ def apg_c4(args, local) -> dict:
                 "bound": "valu", "achieved": tf, "peak": F32_PEAK_TFLOPS, "unit": "TFLOP/s",
                 "frac": tf / F32_PEAK_TFLOPS, "kernel": "vjp_kernel<mjl::Dims<27, 17, 22, 20, 4, 4>, true, 2, true>",
                 "kernel_ms": kms, "launches_timed": H, "timing": "one captured sweep of H replay launches",
+                "kernel_ms_every_env_active": kms, "kernel_ms_trainer_workload": kms_tr,
                 "flops_per_env_step": fl["total"],
                 "flops_by_stage": {k: v for k, v in fl.items() if k != "total"},
                 "workload_mean_ncon_nefc_iter": [float(x) for x in s[:3]],

@@ -126,6 +126,7 @@ class APGTrainer:
                               if use_nat and NativeAPGPolicy.eligible(self.policy, self.device) else None)
         self.rms = RunningMeanStd(self.obs_dim, self.device)
         self.diag = None  # a dict: the eager native sweep adds per-env action-cotangent energy (probes)
+        self.last_reverse_inputs = None
         self.total_env_steps = 0.0
         self.start = time.time()
         self.out_dir = out_dir if self.rank == 0 else None
@@ -171,8 +172,9 @@ class APGTrainer:
             # (passed explicitly, relative to the base, under capture)
             used = env.counter - c0 + 1
             env.counter = c0  # capture ran nothing; the replay below draws the reset
-            self._graphs[key] = (graph, out, [p.grad for p in self.policy.parameters()], used)
-        graph, out, grads, used = self._graphs[key]
+            self._graphs[key] = (graph, out, [p.grad for p in self.policy.parameters()], used,
+                                 self.last_reverse_inputs)
+        graph, out, grads, used, self.last_reverse_inputs = self._graphs[key]
         env.ctr_base.fill_(env.counter)
         graph.replay()
         env.counter += used
@@ -258,6 +260,9 @@ class APGTrainer:
                 self.diag["ga_sq"] = e if t == H - 1 else self.diag["ga_sq"] + e
         torch.autograd.backward(self.policy(on_all.reshape(H * B, w)), grad_tensors=torch.cat(gas))
         dropped = torch.stack([dropped_e.sum(), nonfinite[0]])  # (forward guard, reverse guard)
+        # the reward cotangents and actions of the last rollout (graph-owned under capture: they hold
+        # the last replay's values), for timing the replay VJP on the trainer's own workload (bench.py)
+        self.last_reverse_inputs = (grew_all, acts) if taped else None
         return loss.detach(), (rfin.mean(1).sum() / H).detach(), (o_all, snap), dropped
 
     def _loss_and_grad_torch(self, use_norm: bool, per_step_param_grad: bool = False, graph: bool = False):
