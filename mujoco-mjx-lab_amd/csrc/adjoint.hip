@@ -1884,6 +1884,8 @@ __global__ __launch_bounds__(64, LEAN ? 2 : 1) void vjp_kernel(KParams P, VjpArg
   LDSA float* aux = (LDSA float*)aux_s;
   constexpr int LD = D::LD;
   MP m = (MP)P.m;
+  // env = blockIdx.x: the XCD-aware order of the step kernel (block_env) measured 0.5 % slower here
+  // (101.2 / 101.4 against 100.7 / 100.7 us per replay, 2048 envs) for 3.7 % less traffic
   const int env = blockIdx.x, lane = threadIdx.x;
   if (env >= P.nenv) return;
   const int nq = m->nq, nv = m->nv, nu = m->nu;

@@ -42,24 +42,45 @@ namespace mjl {
 #define INL __device__ __forceinline__
 #define SYNC() __syncthreads()
 
+// XCD-aware env order. The dispatcher deals workgroups round-robin over the 8 XCDs (MI355X_MICROARCH.md,
+// workgroup dispatch: observed, speed only), so with env = blockIdx.x the neighbours of an env -- whose
+// 108-112-B segments of every per-env array (qpos, qvel, qacc_warmstart, ctrl, aux, obs ...) share its
+// 128-B lines -- run on the other seven XCDs, and each line is fetched and written back through up to
+// three L2s. Block b = 8k + x (XCD slot x) runs env (8 (k / C) + x) C + k % C: runs of C = 16 consecutive
+// envs on one XCD, the runs dealt round-robin over the XCDs so each XCD still holds envs from the whole
+// batch (a contiguous eighth per XCD, which puts e.g. the speed test's highest initial velocities on one
+// XCD, measured 0.4-0.6 % slower). Blocks past the last whole round of 8 C keep env = b. Results do not
+// depend on the order. Measured (2048 envs, profiles/r5/env_order_ab.json): HBM bytes per launch pooled env
+// step 5.78 -> 3.93 MB, in place 6.88 -> 5.05 MB, speed test 1.37 -> 1.15 MB; kernel times unchanged.
+INL int block_env() {
+  constexpr int C = 16;
+  const int b = blockIdx.x, n = gridDim.x;
+#ifdef MJL_BLOCK_ORDER  // A/B builds only: env = blockIdx.x
+  return b;
+#endif
+  if (b >= n / (8 * C) * (8 * C)) return b;
+  const int x = b & 7, k = b >> 3;
+  return ((k / C) * 8 + x) * C + (k % C);
+}
+
 #ifdef MJL_TIMING  // diagnostic build only: per-phase s_memtime stamps to a side buffer
 __device__ unsigned long long* g_stamps;
 #define STAMP(slot, lane)                                                                        \
   do {                                                                                           \
     unsigned long long t_ = __builtin_amdgcn_s_memtime();                                        \
-    if ((lane) == 0 && g_stamps) g_stamps[(size_t)blockIdx.x * 48 + (slot)] = t_;               \
+    if ((lane) == 0 && g_stamps) g_stamps[(size_t)block_env() * 48 + (slot)] = t_;               \
   } while (0)
 // accumulate the cycles since `var` into slot (solver sub-phases), restart `var`
 #define TSTART(var) unsigned long long var = __builtin_amdgcn_s_memtime()
 #define TACC(slot, var, lane)                                                                    \
   do {                                                                                           \
     unsigned long long t_ = __builtin_amdgcn_s_memtime();                                        \
-    if ((lane) == 0 && g_stamps) g_stamps[(size_t)blockIdx.x * 48 + (slot)] += t_ - (var);      \
+    if ((lane) == 0 && g_stamps) g_stamps[(size_t)block_env() * 48 + (slot)] += t_ - (var);      \
     (var) = t_;                                                                                  \
   } while (0)
 #define TCOUNT(slot, n, lane)                                                                    \
   do {                                                                                           \
-    if ((lane) == 0 && g_stamps) g_stamps[(size_t)blockIdx.x * 48 + (slot)] += (n);             \
+    if ((lane) == 0 && g_stamps) g_stamps[(size_t)block_env() * 48 + (slot)] += (n);             \
   } while (0)
 #else
 #define STAMP(slot, lane) do { } while (0)
@@ -2370,7 +2391,7 @@ template <class D, int MODE, int MW = MJL_MINWAVES> __global__ __launch_bounds__
   LDSA float* aux = (LDSA float*)aux_s;
   constexpr int LD = D::LD;
   MP m = (MP)P.m;
-  const int env = blockIdx.x;
+  const int env = block_env();
   const int lane = threadIdx.x;
   if (env >= P.nenv) return;
   if ((MODE == MODE_FORWARD || MODE == MODE_ENV_RESET) && P.mask && !(P.mask[env] > 0.5f)) return;
