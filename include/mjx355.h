@@ -376,6 +376,17 @@ int mjl_small_mlp_fwd(const float* x, int B, int k0, int nl, const int* widths, 
                       const float* const* b, float* const* ys, void* stream);
 int mjl_small_mlp_bwd_input(const float* g_out, int B, int k0, int nl, const int* widths, const float* const* w,
                             const float* const* ys, float* g_x, void* stream);
+/* The two fused per-step launches of the APG sweep (bit-identical to the pairs they replace):
+ * mjl_apg_obs_policy_fwd = mjl_apg_obs, then mjl_small_mlp_fwd with x = on and k0 = nq + nv;
+ * mjl_apg_policy_bwd_obs_vjp = mjl_small_mlp_bwd_input (k0 = nq + nv), then mjl_apg_obs_vjp with go = its
+ * g_x (not stored). */
+int mjl_apg_obs_policy_fwd(mjlBatch* batch, const uint8_t* alive, const float* mean, const float* var, int use_norm,
+                           float* o, float* on, uint8_t* alive_snap, int nl, const int* widths, const float* const* w,
+                           const float* const* b, float* const* ys, void* stream);
+int mjl_apg_policy_bwd_obs_vjp(const float* g_out, int nenv, int nq, int nv, int nl, const int* widths,
+                               const float* const* w, const float* const* ys, const float* o, const uint8_t* alive_snap,
+                               const float* mean, const float* var, int use_norm, float* g_qpos, float* g_qvel,
+                               void* stream);
 
 /* PPO update (train_ppo.py:233-252, the bias-gradient column sums of every dense layer's backward
  * in value_and_grad of ppo_loss_fn / value_loss_fn, and the split-K weight-gradient sum):

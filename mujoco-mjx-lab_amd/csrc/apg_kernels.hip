@@ -49,23 +49,35 @@ __global__ void apg_obs_kernel(StateBuf S, int B, int nq, int nv, const uint8_t*
 }
 
 // after env e's step: the non-finite / divergence guard, the discount and the return
-// (apg.py _loss_and_grad, in the same order of float operations)
-__global__ void apg_post_kernel(StateBuf S, int B, int nq, int nv, const float* __restrict__ rew,
-                                const float* __restrict__ term, const float* __restrict__ trunc, float gamma,
-                                float diverge_qvel, uint8_t* __restrict__ alive, float* __restrict__ disc,
-                                float* __restrict__ ret, float* __restrict__ dropped, float* __restrict__ grew,
-                                float* __restrict__ rfin) {
-  const int e = blockIdx.x * blockDim.x + threadIdx.x;
-  if (e >= B) return;
-  const float r = rew[e];
-  bool ok = isfinite(r);
-  for (int j = 0; j < nq; j++) ok = ok && isfinite(S.qpos[(size_t)e * nq + j]);
+// (apg.py _loss_and_grad, in the same order of float operations). One wave per env: lane j loads
+// qpos[j] / qvel[j] (coalesced), the finite test by ballot, max |qvel| by a wave max (fmaxf is
+// order-free: the serial loop's value); lane 0 updates the env's scalars. (A thread per env looped over
+// the env's nq + nv words: 55 strided loads per lane, 9.4 us per 2048-env launch on 8 workgroups.)
+constexpr int kPostEnvs = 4;  // envs (waves) per block
+__global__ __launch_bounds__(64 * kPostEnvs) void apg_post_kernel(StateBuf S, int B, int nq, int nv,
+                                                                  const float* __restrict__ rew,
+                                                                  const float* __restrict__ term,
+                                                                  const float* __restrict__ trunc, float gamma,
+                                                                  float diverge_qvel, uint8_t* __restrict__ alive,
+                                                                  float* __restrict__ disc, float* __restrict__ ret,
+                                                                  float* __restrict__ dropped, float* __restrict__ grew,
+                                                                  float* __restrict__ rfin) {
+  const int lane = threadIdx.x & 63, e = blockIdx.x * kPostEnvs + (threadIdx.x >> 6);
+  if (e >= B) return;  // wave-uniform
+  bool fin = true;
   float vmax = 0.f;
-  for (int j = 0; j < nv; j++) {
+  for (int j = lane; j < nq; j += 64) fin &= isfinite(S.qpos[(size_t)e * nq + j]);
+  for (int j = lane; j < nv; j += 64) {
     const float v = S.qvel[(size_t)e * nv + j];
-    ok = ok && isfinite(v);
+    fin &= isfinite(v);
     vmax = fmaxf(vmax, fabsf(v));
   }
+  const bool allfin = __ballot(!fin) == 0ull;
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) vmax = fmaxf(vmax, __shfl_xor(vmax, o));
+  if (lane != 0) return;
+  const float r = rew[e];
+  bool ok = isfinite(r) && allfin;
   if (diverge_qvel > 0.f) ok = ok && vmax <= diverge_qvel;
   bool al = alive[e] != 0;
   const bool bad = al && !ok;
@@ -107,38 +119,117 @@ __global__ void apg_obs_vjp_kernel(int B, int nq, int nv, const float* __restric
 // mjx_amd APGPolicy) as one launch each, where torch ran three GEMMs and three tanh launches forward
 // and three GEMMs and three tanh-backward launches for the observation cotangent (~4.5 us each at
 // 2048 rows: 12 launches per rollout step). A block takes kSmlThreads / U rows, thread (row, unit
-// < U) one output unit; each layer's weights are staged through LDS (transposed for the forward so
-// the units read consecutive words), activations through LDS, sums in k order from the bias.
+// < U) one output unit; activations go through LDS, sums in k order from the bias. Every layer's
+// weights are loaded at the kernel's start (registers, then LDS: transposed for the forward so the
+// units read consecutive words), all loads in flight together with the input's: one global round
+// trip per launch instead of one per layer; the biases and the backward's stored activations likewise.
 constexpr int kSmlMaxW = 64, kSmlMaxL = 4, kSmlThreads = 256;
+constexpr int kSmlPre = kSmlMaxW * kSmlMaxW / kSmlThreads;  // weight words per thread and layer
 struct SmallMlp {
   int nl, k0, u;            // layers, input width, units per row slot (32 or 64: >= every width)
   int n[kSmlMaxL];          // layer widths; layer l reads k = l ? n[l - 1] : k0
+  int woff[kSmlMaxL + 1];   // layer l's weights at [woff[l], woff[l + 1]) of the dynamic LDS; h after them
   const float* w[kSmlMaxL];  // [n_l, k_l] row-major (torch Linear.weight)
   const float* b[kSmlMaxL];
   float* y[kSmlMaxL];       // [B, n_l] tanh outputs: written by the forward, read by the backward
 };
+// dynamic LDS bytes of a small-MLP launch: the weights, then h[2][rows][kSmlMaxW]
+inline size_t small_mlp_lds(const SmallMlp& P) {
+  return sizeof(float) * ((size_t)P.woff[P.nl] + 2 * (kSmlThreads / P.u) * kSmlMaxW);
+}
 
-__global__ __launch_bounds__(kSmlThreads) void small_mlp_fwd_kernel(const float* __restrict__ x, int B, SmallMlp P) {
-  __shared__ float wt[kSmlMaxW * kSmlMaxW];
-  __shared__ float h[2][kSmlThreads / 32][kSmlMaxW];
-  const int U = P.u, R = kSmlThreads / U, t = threadIdx.x, r = t / U, j = t - r * U;
-  const int row0 = blockIdx.x * R, row = row0 + r;
-  for (int e = t; e < R * P.k0; e += kSmlThreads) {
-    const int rr = e / P.k0, k = e - rr * P.k0;
-    h[0][rr][k] = row0 + rr < B ? x[(size_t)(row0 + rr) * P.k0 + k] : 0.f;
-  }
-  int K = P.k0, cur = 0;
-  for (int l = 0; l < P.nl; l++) {
-    const int N = P.n[l];
+// every layer's weights into registers (issued back to back), k = in width of layer l
+__device__ __forceinline__ void sml_prefetch(const SmallMlp& P, int t, float (&wr)[kSmlMaxL][kSmlPre]) {
+#pragma unroll
+  for (int l = 0; l < kSmlMaxL; l++) {
+    const int NK = l < P.nl ? P.woff[l + 1] - P.woff[l] : 0;
     const float* __restrict__ W = P.w[l];
-    __syncthreads();  // the previous layer's activations written, its weights no longer read
-    for (int e = t; e < N * K; e += kSmlThreads) {
-      const int jj = e / K, k = e - jj * K;
-      wt[k * N + jj] = W[e];
+#pragma unroll
+    for (int c = 0; c < kSmlPre; c++) {
+      const int e = t + c * kSmlThreads;
+      wr[l][c] = e < NK ? W[e] : 0.f;
     }
-    __syncthreads();
+  }
+}
+// ... and into LDS: layer l at sm + woff[l], transposed ([k][n]) for the forward, as stored otherwise
+template <bool TRANSPOSE>
+__device__ __forceinline__ void sml_stage(const SmallMlp& P, int t, const float (&wr)[kSmlMaxL][kSmlPre], float* sm) {
+#pragma unroll
+  for (int l = 0; l < kSmlMaxL; l++) {
+    if (l >= P.nl) break;
+    const int N = P.n[l], K = l ? P.n[l - 1] : P.k0, NK = N * K;
+    float* wl = sm + P.woff[l];
+#pragma unroll
+    for (int c = 0; c < kSmlPre; c++) {
+      const int e = t + c * kSmlThreads;
+      if (e < NK) {
+        if (TRANSPOSE) { const int jj = e / K, k = e - jj * K; wl[k * N + jj] = wr[l][c]; }
+        else wl[e] = wr[l][c];
+      }
+    }
+  }
+}
+
+// the APG observation feeding the policy forward (mjl_apg_obs_policy_fwd): apg_obs_kernel's o / on /
+// alive_snap for the block's rows, written as there, with on staged as the first layer's input
+struct ObsIn {
+  const float *qpos, *qvel;
+  int nq, nv, use_norm;
+  const uint8_t* alive;
+  const float *mean, *var;
+  float *o, *on;
+  uint8_t* snap;
+};
+// the observation's backward fused into the policy's input backward (mjl_apg_policy_bwd_obs_vjp):
+// apg_obs_vjp_kernel on the input cotangent where small_mlp_bwd_input_kernel wrote g_x
+struct ObsVjp {
+  int nq, nv, use_norm;
+  const float* o;
+  const uint8_t* snap;
+  const float *mean, *var;
+  float *g_qpos, *g_qvel;
+};
+
+template <bool OBS>
+__global__ __launch_bounds__(kSmlThreads) void small_mlp_fwd_kernel(const float* __restrict__ x, int B, SmallMlp P,
+                                                                    ObsIn O) {
+  extern __shared__ float sm[];
+  const int U = P.u, R = kSmlThreads / U, t = threadIdx.x, r = t / U, j = t - r * U;
+  float (*h)[kSmlThreads / 32][kSmlMaxW] = (float (*)[kSmlThreads / 32][kSmlMaxW])(sm + P.woff[P.nl]);
+  const int row0 = blockIdx.x * R, row = row0 + r;
+  float wr[kSmlMaxL][kSmlPre], bias[kSmlMaxL];
+  sml_prefetch(P, t, wr);
+#pragma unroll
+  for (int l = 0; l < kSmlMaxL; l++) bias[l] = (l < P.nl && j < P.n[l]) ? P.b[l][j] : 0.f;
+  for (int e = t; e < R * P.k0; e += kSmlThreads) {
+    const int rr = e / P.k0, k = e - rr * P.k0, rw = row0 + rr;
+    if constexpr (OBS) {  // apg_obs_kernel's element (rw, k), the same float operations
+      float in = 0.f;
+      if (rw < B) {
+        const size_t i = (size_t)rw * P.k0 + k;
+        const float v = k < O.nq ? O.qpos[(size_t)rw * O.nq + k] : O.qvel[(size_t)rw * O.nv + (k - O.nq)];
+        const bool al = O.alive[rw] != 0;
+        O.o[i] = v;
+        const float xv = al ? v : 0.f;
+        in = O.use_norm ? clamp_keep_nan(div_rn(xv - O.mean[k], sqrt_rn(O.var[k]) + 1e-8f), 10.f) : xv;
+        O.on[i] = in;
+        if (k == 0) O.snap[rw] = al;
+      }
+      h[0][rr][k] = in;
+    } else {
+      h[0][rr][k] = rw < B ? x[(size_t)rw * P.k0 + k] : 0.f;
+    }
+  }
+  sml_stage<true>(P, t, wr, sm);
+  int K = P.k0, cur = 0;
+#pragma unroll
+  for (int l = 0; l < kSmlMaxL; l++) {
+    if (l >= P.nl) break;
+    const int N = P.n[l];
+    const float* wt = sm + P.woff[l];
+    __syncthreads();  // the weights staged / the previous layer's activations written
     if (j < N) {
-      float s = P.b[l][j];
+      float s = bias[l];
       for (int k = 0; k < K; k++) s = fmaf(wt[k * N + j], h[cur][r][k], s);
       const float y = tanhf(s);
       h[cur ^ 1][r][j] = y;
@@ -151,32 +242,56 @@ __global__ __launch_bounds__(kSmlThreads) void small_mlp_fwd_kernel(const float*
 
 // d loss / d x from d loss / d y_L (ga): g = ga (1 - y_L^2), then per layer from the top
 // g_in = W_l^T g, times (1 - y_{l-1}^2) below the first layer; gx = W_0^T g
+template <bool OBS>
 __global__ __launch_bounds__(kSmlThreads) void small_mlp_bwd_input_kernel(const float* __restrict__ ga, int B,
-                                                                          SmallMlp P, float* __restrict__ gx) {
-  __shared__ float wl[kSmlMaxW * kSmlMaxW];
-  __shared__ float g[2][kSmlThreads / 32][kSmlMaxW];
+                                                                          SmallMlp P, float* __restrict__ gx,
+                                                                          ObsVjp O) {
+  extern __shared__ float sm[];
   const int U = P.u, R = kSmlThreads / U, t = threadIdx.x, r = t / U, u = t - r * U;
+  float (*g)[kSmlThreads / 32][kSmlMaxW] = (float (*)[kSmlThreads / 32][kSmlMaxW])(sm + P.woff[P.nl]);
   const int row = blockIdx.x * R + r;
   const int L = P.nl, NL = P.n[L - 1];
+  float wr[kSmlMaxL][kSmlPre], yin[kSmlMaxL];  // yin[l]: layer l's input activation at (row, u), l >= 1
+  sml_prefetch(P, t, wr);
+#pragma unroll
+  for (int l = 1; l < kSmlMaxL; l++) {
+    const int K = l < L ? P.n[l - 1] : 0;
+    yin[l] = (row < B && u < K) ? P.y[l - 1][(size_t)row * K + u] : 0.f;
+  }
   if (u < NL) {
     const float y = row < B ? P.y[L - 1][(size_t)row * NL + u] : 0.f;
     g[0][r][u] = row < B ? ga[(size_t)row * NL + u] * (1.f - y * y) : 0.f;
   }
+  sml_stage<false>(P, t, wr, sm);
   int cur = 0;
-  for (int l = L - 1; l >= 0; l--) {
+#pragma unroll
+  for (int l = kSmlMaxL - 1; l >= 0; l--) {
+    if (l >= L) continue;
     const int N = P.n[l], K = l ? P.n[l - 1] : P.k0;
-    const float* __restrict__ W = P.w[l];
-    __syncthreads();
-    for (int e = t; e < N * K; e += kSmlThreads) wl[e] = W[e];
+    const float* wl = sm + P.woff[l];
     __syncthreads();
     if (u < K) {
       float s = 0.f;
       for (int jj = 0; jj < N; jj++) s = fmaf(wl[jj * K + u], g[cur][r][jj], s);
       if (l) {
-        const float y = row < B ? P.y[l - 1][(size_t)row * K + u] : 0.f;
+        const float y = yin[l];
         g[cur ^ 1][r][u] = s * (1.f - y * y);
       } else if (row < B) {
-        gx[(size_t)row * K + u] = s;
+        if constexpr (OBS) {  // apg_obs_vjp_kernel's element (row, u) with go = s
+          float gg = 0.f;
+          if (O.snap[row]) {
+            gg = s;
+            if (O.use_norm) {
+              const float den = sqrt_rn(O.var[u]) + 1e-8f;
+              const float y = div_rn(O.o[(size_t)row * K + u] - O.mean[u], den);
+              gg = (y >= -10.f && y <= 10.f) ? div_rn(gg, den) : 0.f;
+            }
+          }
+          if (u < O.nq) O.g_qpos[(size_t)row * O.nq + u] = O.g_qpos[(size_t)row * O.nq + u] + gg;
+          else O.g_qvel[(size_t)row * O.nv + (u - O.nq)] = O.g_qvel[(size_t)row * O.nv + (u - O.nq)] + gg;
+        } else {
+          gx[(size_t)row * K + u] = s;
+        }
       }
     }
     cur ^= 1;

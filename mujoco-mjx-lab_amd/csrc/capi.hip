@@ -1186,6 +1186,7 @@ static int small_mlp_setup(int B, int k0, int nl, const int* widths, const float
     if (widths[l] < 1 || widths[l] > kSmlMaxW || !w[l] || !b[l] || !ys[l])
       return fail(MJL_ERR_ARG, "small MLP: layer %d: width 1..%d and non-null pointers expected", l, kSmlMaxW);
     P.n[l] = widths[l]; P.w[l] = w[l]; P.b[l] = b[l]; P.y[l] = ys[l];
+    P.woff[l + 1] = P.woff[l] + widths[l] * (l ? widths[l - 1] : k0);
     wmax = widths[l] > wmax ? widths[l] : wmax;
   }
   P.u = wmax <= 32 ? 32 : 64;
@@ -1200,8 +1201,8 @@ extern "C" int mjl_small_mlp_fwd(const float* x, int B, int k0, int nl, const in
   if (!x && B > 0) return fail(MJL_ERR_ARG, "bad argument");
   if (B == 0) return MJL_OK;
   const int R = kSmlThreads / P.u;
-  hipLaunchKernelGGL(small_mlp_fwd_kernel, dim3((unsigned)((B + R - 1) / R)), dim3(kSmlThreads), 0, (hipStream_t)stream,
-                     x, B, P);
+  hipLaunchKernelGGL(small_mlp_fwd_kernel<false>, dim3((unsigned)((B + R - 1) / R)), dim3(kSmlThreads), small_mlp_lds(P),
+                     (hipStream_t)stream, x, B, P, ObsIn{});
   HIPCHK(hipGetLastError());
   return MJL_OK;
 }
@@ -1216,8 +1217,8 @@ extern "C" int mjl_small_mlp_bwd_input(const float* g_out, int B, int k0, int nl
   if ((!g_out || !g_x) && B > 0) return fail(MJL_ERR_ARG, "bad argument");
   if (B == 0) return MJL_OK;
   const int R = kSmlThreads / P.u;
-  hipLaunchKernelGGL(small_mlp_bwd_input_kernel, dim3((unsigned)((B + R - 1) / R)), dim3(kSmlThreads), 0,
-                     (hipStream_t)stream, g_out, B, P, g_x);
+  hipLaunchKernelGGL(small_mlp_bwd_input_kernel<false>, dim3((unsigned)((B + R - 1) / R)), dim3(kSmlThreads), small_mlp_lds(P),
+                     (hipStream_t)stream, g_out, B, P, g_x, ObsVjp{});
   HIPCHK(hipGetLastError());
   return MJL_OK;
 }
@@ -1240,7 +1241,7 @@ extern "C" int mjl_apg_post(mjlBatch* B, const float* rew, const float* term, co
   if (!B || !rew || !term || !trunc || !alive || !disc || !ret || !dropped || !grew || !rfin)
     return fail(MJL_ERR_ARG, "bad argument");
   HIPCHK(hipSetDevice(B->device));
-  hipLaunchKernelGGL(apg_post_kernel, dim3((B->nenv + 255) / 256), dim3(256), 0, (hipStream_t)stream, B->s, B->nenv,
+  hipLaunchKernelGGL(apg_post_kernel, dim3((B->nenv + kPostEnvs - 1) / kPostEnvs), dim3(64 * kPostEnvs), 0, (hipStream_t)stream, B->s, B->nenv,
                      B->model->desc.nq, B->model->desc.nv, rew, term, trunc, gamma, diverge_qvel, alive, disc, ret,
                      dropped, grew, rfin);
   HIPCHK(hipGetLastError());
@@ -1256,6 +1257,47 @@ extern "C" int mjl_apg_obs_vjp(int B, int nq, int nv, const float* o, const uint
   if (n == 0) return MJL_OK;
   hipLaunchKernelGGL(apg_obs_vjp_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, (hipStream_t)stream, B, nq,
                      nv, o, alive_snap, mean, var, use_norm, go, g_qpos, g_qvel);
+  HIPCHK(hipGetLastError());
+  return MJL_OK;
+}
+
+// mjl_apg_obs then mjl_small_mlp_fwd on its `on`, in one launch (k0 = nq + nv)
+extern "C" int mjl_apg_obs_policy_fwd(mjlBatch* B, const uint8_t* alive, const float* mean, const float* var,
+                                      int use_norm, float* o, float* on, uint8_t* alive_snap, int nl, const int* widths,
+                                      const float* const* w, const float* const* b, float* const* ys, void* stream) {
+  if (!B || !alive || !o || !on || !alive_snap || (use_norm && (!mean || !var))) return fail(MJL_ERR_ARG, "bad argument");
+  const int nq = B->model->desc.nq, nv = B->model->desc.nv;
+  SmallMlp P;
+  int rc = small_mlp_setup(B->nenv, nq + nv, nl, widths, w, b, ys, P);
+  if (rc != MJL_OK) return rc;
+  HIPCHK(hipSetDevice(B->device));
+  if (B->nenv == 0) return MJL_OK;
+  const ObsIn O{B->s.qpos, B->s.qvel, nq, nv, use_norm, alive, mean, var, o, on, alive_snap};
+  const int R = kSmlThreads / P.u;
+  hipLaunchKernelGGL(small_mlp_fwd_kernel<true>, dim3((unsigned)((B->nenv + R - 1) / R)), dim3(kSmlThreads), small_mlp_lds(P),
+                     (hipStream_t)stream, nullptr, B->nenv, P, O);
+  HIPCHK(hipGetLastError());
+  return MJL_OK;
+}
+
+// mjl_small_mlp_bwd_input then mjl_apg_obs_vjp on its g_x, in one launch (k0 = nq + nv; g_x not stored)
+extern "C" int mjl_apg_policy_bwd_obs_vjp(const float* g_out, int nenv, int nq, int nv, int nl, const int* widths,
+                                          const float* const* w, const float* const* ys, const float* o,
+                                          const uint8_t* alive_snap, const float* mean, const float* var, int use_norm,
+                                          float* g_qpos, float* g_qvel, void* stream) {
+  if (!w || !w[0]) return fail(MJL_ERR_ARG, "bad argument");
+  if (nenv < 0 || nq < 0 || nv < 0 || ((!g_out || !o || !alive_snap || !g_qpos || !g_qvel) && nenv > 0) ||
+      (use_norm && (!mean || !var)))
+    return fail(MJL_ERR_ARG, "bad argument");
+  SmallMlp P;
+  const float* nob[kSmlMaxL] = {w[0], w[0], w[0], w[0]};  // biases unused by the backward
+  int rc = small_mlp_setup(nenv, nq + nv, nl, widths, w, nob, (float* const*)ys, P);
+  if (rc != MJL_OK) return rc;
+  if (nenv == 0) return MJL_OK;
+  const ObsVjp O{nq, nv, use_norm, o, alive_snap, mean, var, g_qpos, g_qvel};
+  const int R = kSmlThreads / P.u;
+  hipLaunchKernelGGL(small_mlp_bwd_input_kernel<true>, dim3((unsigned)((nenv + R - 1) / R)), dim3(kSmlThreads), small_mlp_lds(P),
+                     (hipStream_t)stream, g_out, nenv, P, nullptr, O);
   HIPCHK(hipGetLastError());
   return MJL_OK;
 }

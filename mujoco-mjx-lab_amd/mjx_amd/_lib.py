@@ -24,7 +24,7 @@ EXPORTS = [
     "mjl_step_vjp", "mjl_env_step_vjp", "mjl_gae", "mjl_batch_set_counter_base",
     "mjl_env_set_reset_keys", "mjl_prng_split", "mjl_env_step_vjp_guarded", "mjl_state_size", "mjl_get_state",
     "mjl_set_state", "mjl_obs_normalize", "mjl_policy_head", "mjl_colsum_scratch", "mjl_colsum", "mjl_tanh_bwd_colsum", "mjl_slice_sum", "mjl_tanh_inplace", "mjl_small_mlp_fwd",
-    "mjl_small_mlp_bwd_input",
+    "mjl_small_mlp_bwd_input", "mjl_apg_obs_policy_fwd", "mjl_apg_policy_bwd_obs_vjp",
     "mjl_policy_param_floats", "mjl_policy_fwd",
     "mjl_step_vjp_full", "mjl_env_step_vjp_full", "mjl_env_fill_reset_pool",
     "mjl_apg_obs", "mjl_apg_post", "mjl_apg_obs_vjp", "mjl_env_step_record", "mjl_env_step_vjp_replay",
@@ -142,6 +142,8 @@ def lib() -> C.CDLL:
     L.mjl_tanh_bwd_colsum_partials.argtypes = [vp, vp, i32, i32, i32, i32, vp, vp, vp]
     L.mjl_small_mlp_fwd.argtypes = [vp, i32, i32, i32, vp, vp, vp, vp, vp]
     L.mjl_small_mlp_bwd_input.argtypes = [vp, i32, i32, i32, vp, vp, vp, vp, vp]
+    L.mjl_apg_obs_policy_fwd.argtypes = [vp, vp, vp, vp, i32, vp, vp, vp, i32, vp, vp, vp, vp, vp]
+    L.mjl_apg_policy_bwd_obs_vjp.argtypes = [vp, i32, i32, i32, i32, vp, vp, vp, vp, vp, vp, vp, i32, vp, vp, vp]
     L.mjl_step_vjp.argtypes = [vp, f32p, f32p, f32p, f32p, f32p, vp]
     L.mjl_env_step_vjp.argtypes = [vp, f32p, f32p, f32p, f32p, f32p, f32p, f32p, f32p, f32p, vp]
     L.mjl_step_vjp_full.argtypes = [vp] + [f32p] * 7 + [vp]

@@ -80,6 +80,27 @@ class NativeAPGPolicy:
                                       self._ptrs(ys), torch.cuda.current_stream(x.device).cuda_stream))
         return ys[-1]
 
+    def forward_obs(self, env, alive, rms, use_norm, o, on, snap, ys) -> torch.Tensor:
+        """HumanoidAPGEnv.apg_obs, then forward(on, ys), as one launch (mjl_apg_obs_policy_fwd)."""
+        from ._lib import check, lib
+        from .mjx import _ptr, _stream
+        check(lib().mjl_apg_obs_policy_fwd(env.env.data.handle, _u8(alive), _ptr(rms.mean), _ptr(rms.var),
+                                           int(use_norm), _ptr(o), _ptr(on), _u8(snap), len(self.widths),
+                                           self._widths, self._ptrs([w for w, _ in self.params]),
+                                           self._ptrs([b for _, b in self.params]), self._ptrs(ys), _stream()))
+        return ys[-1]
+
+    def backward_obs_vjp(self, env, g_out, ys, o, snap, rms, use_norm, gq, gv):
+        """backward_input(g_out, ys), then HumanoidAPGEnv.apg_obs_vjp on its result, as one launch
+        (mjl_apg_policy_bwd_obs_vjp): gq / gv accumulate the observation's cotangent."""
+        from ._lib import check, lib
+        from .mjx import _ptr, _stream
+        g_out = g_out.contiguous()
+        check(lib().mjl_apg_policy_bwd_obs_vjp(_ptr(g_out), env.num_envs, env.nq, env.nv, len(self.widths),
+                                               self._widths, self._ptrs([w for w, _ in self.params]),
+                                               self._ptrs(ys), _ptr(o), _u8(snap), _ptr(rms.mean), _ptr(rms.var),
+                                               int(use_norm), _ptr(gq), _ptr(gv), _stream()))
+
     def backward_input(self, g_out: torch.Tensor, ys) -> torch.Tensor:
         from ._lib import check, lib
         g_out = g_out.contiguous()
@@ -213,13 +234,19 @@ class APGTrainer:
         tape, acts, leaves = [], [], []
         nat = self.native_policy
         ys_all = [torch.empty((H, B, n), device=dev) for n in nat.widths] if nat is not None else None
+        # the observation and the policy forward as one launch (and their backward as one), when the env
+        # is the native one (HumanoidAPGEnv); MJL_APG_FUSED_OBS=0 keeps the separate launches
+        fused = nat is not None and isinstance(env, HumanoidAPGEnv) and os.environ.get("MJL_APG_FUSED_OBS", "1") != "0"
         for t in range(H):
             if not taped:
                 tape.append(env.get_state())
-            env.apg_obs(alive, self.rms, use_norm, o_all[t], on_all[t], snap[t])
-            if nat is not None:  # one launch; the layers' outputs kept for the reverse
+            if fused:
+                a = nat.forward_obs(env, alive, self.rms, use_norm, o_all[t], on_all[t], snap[t], [y[t] for y in ys_all])
+            elif nat is not None:  # one launch; the layers' outputs kept for the reverse
+                env.apg_obs(alive, self.rms, use_norm, o_all[t], on_all[t], snap[t])
                 a = nat.forward(on_all[t], [y[t] for y in ys_all])
             else:
+                env.apg_obs(alive, self.rms, use_norm, o_all[t], on_all[t], snap[t])
                 on = on_all[t].detach().requires_grad_(True)
                 a = self.policy(on)
                 leaves.append(on)
@@ -249,11 +276,14 @@ class APGTrainer:
                                                               nonfinite)
                 else:
                     gq, gv, ga, gaux = env.step_vjp(acts[t].detach(), gq, gv, grew_all[t], gaux, nonfinite)
-            if nat is not None:
-                og = nat.backward_input(ga, [y[t] for y in ys_all])
+            if fused:
+                nat.backward_obs_vjp(env, ga, [y[t] for y in ys_all], o_all[t], snap[t], self.rms, use_norm, gq, gv)
             else:
-                og, = torch.autograd.grad(acts[t], leaves[t], grad_outputs=ga)
-            env.apg_obs_vjp(o_all[t], snap[t], self.rms, use_norm, og, gq, gv)
+                if nat is not None:
+                    og = nat.backward_input(ga, [y[t] for y in ys_all])
+                else:
+                    og, = torch.autograd.grad(acts[t], leaves[t], grad_outputs=ga)
+                env.apg_obs_vjp(o_all[t], snap[t], self.rms, use_norm, og, gq, gv)
             gas[t] = ga
             if self.diag is not None and not graph:  # sum over steps of |d loss / d a_t|^2 per env
                 e = (ga.double() ** 2).sum(1)

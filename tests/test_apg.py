@@ -413,6 +413,35 @@ def test_apg_native_sweep_matches_pure_torch_restatement():
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("graph", [False, True])
+def test_apg_fused_obs_policy_launches_bit_identical(monkeypatch, graph):
+    """The fused per-step launches (mjl_apg_obs_policy_fwd, mjl_apg_policy_bwd_obs_vjp) against the pairs
+    they replace (MJL_APG_FUSED_OBS=0): loss, gradient, returns and parameters bit for bit over 4 updates
+    on the taped sweep (the first without observation normalisation, the rest with it), eager and under
+    the update's hipGraph."""
+    import mjx_amd
+    from mjx_amd import mjx
+    from mjx_amd.config import reference_ppo_config
+    from mjx_amd.envs import HumanoidEnv, resolve_ids
+    m = mjx_amd.load_model("humanoid_mjx")
+    ecfg = resolve_ids(m, reference_ppo_config().env_config)
+    cfg = _cfg(batch_size=100, horizon=8, hidden_size=32)
+    envs = [apg.HumanoidAPGEnv(HumanoidEnv(mjx.put_model(m), ecfg, cfg.batch_size, seed=5), "implicit")
+            for _ in range(2)]
+    trs = [apg.APGTrainer(cfg, e, device="cuda", use_graph=graph) for e in envs]
+    assert all(tr.native_policy is not None for tr in trs)
+    for step in range(4):
+        ms = []
+        for tr, fused in zip(trs, ("1", "0")):
+            monkeypatch.setenv("MJL_APG_FUSED_OBS", fused)
+            ms.append(tr.update(step))
+        for k in ("loss", "grad_norm", "mean_reward", "return", "nonfinite_envs"):
+            assert ms[0][k] == ms[1][k], f"update {step}: {k}"
+        for p, q in zip(trs[0].policy.parameters(), trs[1].policy.parameters()):
+            assert torch.equal(p, q), f"update {step}"
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("k0,hidden,depth,act_dim,B", [(55, 32, 2, 21, 2048), (55, 64, 3, 21, 1000), (7, 16, 1, 3, 5)])
 def test_native_apg_policy_matches_torch(k0, hidden, depth, act_dim, B):
     """mjl_small_mlp_fwd / mjl_small_mlp_bwd_input against the APGPolicy's torch forward and the
