@@ -119,56 +119,18 @@ __global__ void apg_obs_vjp_kernel(int B, int nq, int nv, const float* __restric
 // mjx_amd APGPolicy) as one launch each, where torch ran three GEMMs and three tanh launches forward
 // and three GEMMs and three tanh-backward launches for the observation cotangent (~4.5 us each at
 // 2048 rows: 12 launches per rollout step). A block takes kSmlThreads / U rows, thread (row, unit
-// < U) one output unit; activations go through LDS, sums in k order from the bias. Every layer's
-// weights are loaded at the kernel's start (registers, then LDS: transposed for the forward so the
-// units read consecutive words), all loads in flight together with the input's: one global round
-// trip per launch instead of one per layer; the biases and the backward's stored activations likewise.
+// < U) one output unit; each layer's weights are staged through LDS (transposed for the forward so
+// the units read consecutive words), activations through LDS, sums in k order from the bias.
+// (Loading every layer's weights, the biases and the stored activations at the kernel's start, one
+// global round trip per launch, measured slower: 10.0 -> 11.0 us forward, 8.1 -> 8.9 us backward.)
 constexpr int kSmlMaxW = 64, kSmlMaxL = 4, kSmlThreads = 256;
-constexpr int kSmlPre = kSmlMaxW * kSmlMaxW / kSmlThreads;  // weight words per thread and layer
 struct SmallMlp {
   int nl, k0, u;            // layers, input width, units per row slot (32 or 64: >= every width)
   int n[kSmlMaxL];          // layer widths; layer l reads k = l ? n[l - 1] : k0
-  int woff[kSmlMaxL + 1];   // layer l's weights at [woff[l], woff[l + 1]) of the dynamic LDS; h after them
   const float* w[kSmlMaxL];  // [n_l, k_l] row-major (torch Linear.weight)
   const float* b[kSmlMaxL];
   float* y[kSmlMaxL];       // [B, n_l] tanh outputs: written by the forward, read by the backward
 };
-// dynamic LDS bytes of a small-MLP launch: the weights, then h[2][rows][kSmlMaxW]
-inline size_t small_mlp_lds(const SmallMlp& P) {
-  return sizeof(float) * ((size_t)P.woff[P.nl] + 2 * (kSmlThreads / P.u) * kSmlMaxW);
-}
-
-// every layer's weights into registers (issued back to back), k = in width of layer l
-__device__ __forceinline__ void sml_prefetch(const SmallMlp& P, int t, float (&wr)[kSmlMaxL][kSmlPre]) {
-#pragma unroll
-  for (int l = 0; l < kSmlMaxL; l++) {
-    const int NK = l < P.nl ? P.woff[l + 1] - P.woff[l] : 0;
-    const float* __restrict__ W = P.w[l];
-#pragma unroll
-    for (int c = 0; c < kSmlPre; c++) {
-      const int e = t + c * kSmlThreads;
-      wr[l][c] = e < NK ? W[e] : 0.f;
-    }
-  }
-}
-// ... and into LDS: layer l at sm + woff[l], transposed ([k][n]) for the forward, as stored otherwise
-template <bool TRANSPOSE>
-__device__ __forceinline__ void sml_stage(const SmallMlp& P, int t, const float (&wr)[kSmlMaxL][kSmlPre], float* sm) {
-#pragma unroll
-  for (int l = 0; l < kSmlMaxL; l++) {
-    if (l >= P.nl) break;
-    const int N = P.n[l], K = l ? P.n[l - 1] : P.k0, NK = N * K;
-    float* wl = sm + P.woff[l];
-#pragma unroll
-    for (int c = 0; c < kSmlPre; c++) {
-      const int e = t + c * kSmlThreads;
-      if (e < NK) {
-        if (TRANSPOSE) { const int jj = e / K, k = e - jj * K; wl[k * N + jj] = wr[l][c]; }
-        else wl[e] = wr[l][c];
-      }
-    }
-  }
-}
 
 // the APG observation feeding the policy forward (mjl_apg_obs_policy_fwd): apg_obs_kernel's o / on /
 // alive_snap for the block's rows, written as there, with on staged as the first layer's input
@@ -193,14 +155,10 @@ struct ObsVjp {
 template <bool OBS>
 __global__ __launch_bounds__(kSmlThreads) void small_mlp_fwd_kernel(const float* __restrict__ x, int B, SmallMlp P,
                                                                     ObsIn O) {
-  extern __shared__ float sm[];
+  __shared__ float wt[kSmlMaxW * kSmlMaxW];
+  __shared__ float h[2][kSmlThreads / 32][kSmlMaxW];
   const int U = P.u, R = kSmlThreads / U, t = threadIdx.x, r = t / U, j = t - r * U;
-  float (*h)[kSmlThreads / 32][kSmlMaxW] = (float (*)[kSmlThreads / 32][kSmlMaxW])(sm + P.woff[P.nl]);
   const int row0 = blockIdx.x * R, row = row0 + r;
-  float wr[kSmlMaxL][kSmlPre], bias[kSmlMaxL];
-  sml_prefetch(P, t, wr);
-#pragma unroll
-  for (int l = 0; l < kSmlMaxL; l++) bias[l] = (l < P.nl && j < P.n[l]) ? P.b[l][j] : 0.f;
   for (int e = t; e < R * P.k0; e += kSmlThreads) {
     const int rr = e / P.k0, k = e - rr * P.k0, rw = row0 + rr;
     if constexpr (OBS) {  // apg_obs_kernel's element (rw, k), the same float operations
@@ -220,16 +178,18 @@ __global__ __launch_bounds__(kSmlThreads) void small_mlp_fwd_kernel(const float*
       h[0][rr][k] = rw < B ? x[(size_t)rw * P.k0 + k] : 0.f;
     }
   }
-  sml_stage<true>(P, t, wr, sm);
   int K = P.k0, cur = 0;
-#pragma unroll
-  for (int l = 0; l < kSmlMaxL; l++) {
-    if (l >= P.nl) break;
+  for (int l = 0; l < P.nl; l++) {
     const int N = P.n[l];
-    const float* wt = sm + P.woff[l];
-    __syncthreads();  // the weights staged / the previous layer's activations written
+    const float* __restrict__ W = P.w[l];
+    __syncthreads();  // the previous layer's activations written, its weights no longer read
+    for (int e = t; e < N * K; e += kSmlThreads) {
+      const int jj = e / K, k = e - jj * K;
+      wt[k * N + jj] = W[e];
+    }
+    __syncthreads();
     if (j < N) {
-      float s = bias[l];
+      float s = P.b[l][j];
       for (int k = 0; k < K; k++) s = fmaf(wt[k * N + j], h[cur][r][k], s);
       const float y = tanhf(s);
       h[cur ^ 1][r][j] = y;
@@ -246,35 +206,27 @@ template <bool OBS>
 __global__ __launch_bounds__(kSmlThreads) void small_mlp_bwd_input_kernel(const float* __restrict__ ga, int B,
                                                                           SmallMlp P, float* __restrict__ gx,
                                                                           ObsVjp O) {
-  extern __shared__ float sm[];
+  __shared__ float wl[kSmlMaxW * kSmlMaxW];
+  __shared__ float g[2][kSmlThreads / 32][kSmlMaxW];
   const int U = P.u, R = kSmlThreads / U, t = threadIdx.x, r = t / U, u = t - r * U;
-  float (*g)[kSmlThreads / 32][kSmlMaxW] = (float (*)[kSmlThreads / 32][kSmlMaxW])(sm + P.woff[P.nl]);
   const int row = blockIdx.x * R + r;
   const int L = P.nl, NL = P.n[L - 1];
-  float wr[kSmlMaxL][kSmlPre], yin[kSmlMaxL];  // yin[l]: layer l's input activation at (row, u), l >= 1
-  sml_prefetch(P, t, wr);
-#pragma unroll
-  for (int l = 1; l < kSmlMaxL; l++) {
-    const int K = l < L ? P.n[l - 1] : 0;
-    yin[l] = (row < B && u < K) ? P.y[l - 1][(size_t)row * K + u] : 0.f;
-  }
   if (u < NL) {
     const float y = row < B ? P.y[L - 1][(size_t)row * NL + u] : 0.f;
     g[0][r][u] = row < B ? ga[(size_t)row * NL + u] * (1.f - y * y) : 0.f;
   }
-  sml_stage<false>(P, t, wr, sm);
   int cur = 0;
-#pragma unroll
-  for (int l = kSmlMaxL - 1; l >= 0; l--) {
-    if (l >= L) continue;
+  for (int l = L - 1; l >= 0; l--) {
     const int N = P.n[l], K = l ? P.n[l - 1] : P.k0;
-    const float* wl = sm + P.woff[l];
+    const float* __restrict__ W = P.w[l];
+    __syncthreads();
+    for (int e = t; e < N * K; e += kSmlThreads) wl[e] = W[e];
     __syncthreads();
     if (u < K) {
       float s = 0.f;
       for (int jj = 0; jj < N; jj++) s = fmaf(wl[jj * K + u], g[cur][r][jj], s);
       if (l) {
-        const float y = yin[l];
+        const float y = row < B ? P.y[l - 1][(size_t)row * K + u] : 0.f;
         g[cur ^ 1][r][u] = s * (1.f - y * y);
       } else if (row < B) {
         if constexpr (OBS) {  // apg_obs_vjp_kernel's element (row, u) with go = s

@@ -1175,18 +1175,20 @@ extern "C" int mjl_prng_split(const uint32_t* keys, int n, int num, int mode, ui
 }
 
 // ---------------------------------------------------------------- APG rollout bookkeeping
+// U (units per row slot) covers every layer width, and k0 for the backward, whose last layer writes k0
+// input cotangents per row (the forward stages its k0 inputs by a loop: 32-unit slots, 8 rows per block,
+// for the APG policy's 32-wide layers)
 static int small_mlp_setup(int B, int k0, int nl, const int* widths, const float* const* w, const float* const* b,
-                           float* const* ys, SmallMlp& P) {
+                           float* const* ys, SmallMlp& P, bool fwd = false) {
   if (B < 0 || nl < 1 || nl > kSmlMaxL || k0 < 1 || k0 > kSmlMaxW || !widths || !w || !b || !ys)
     return fail(MJL_ERR_ARG, "small MLP: 1..%d layers of width 1..%d expected", kSmlMaxL, kSmlMaxW);
   std::memset(&P, 0, sizeof(P));
   P.nl = nl; P.k0 = k0;
-  int wmax = k0;
+  int wmax = fwd ? 1 : k0;
   for (int l = 0; l < nl; l++) {
     if (widths[l] < 1 || widths[l] > kSmlMaxW || !w[l] || !b[l] || !ys[l])
       return fail(MJL_ERR_ARG, "small MLP: layer %d: width 1..%d and non-null pointers expected", l, kSmlMaxW);
     P.n[l] = widths[l]; P.w[l] = w[l]; P.b[l] = b[l]; P.y[l] = ys[l];
-    P.woff[l + 1] = P.woff[l] + widths[l] * (l ? widths[l - 1] : k0);
     wmax = widths[l] > wmax ? widths[l] : wmax;
   }
   P.u = wmax <= 32 ? 32 : 64;
@@ -1196,12 +1198,12 @@ static int small_mlp_setup(int B, int k0, int nl, const int* widths, const float
 extern "C" int mjl_small_mlp_fwd(const float* x, int B, int k0, int nl, const int* widths, const float* const* w,
                                  const float* const* b, float* const* ys, void* stream) {
   SmallMlp P;
-  int rc = small_mlp_setup(B, k0, nl, widths, w, b, ys, P);
+  int rc = small_mlp_setup(B, k0, nl, widths, w, b, ys, P, true);
   if (rc != MJL_OK) return rc;
   if (!x && B > 0) return fail(MJL_ERR_ARG, "bad argument");
   if (B == 0) return MJL_OK;
   const int R = kSmlThreads / P.u;
-  hipLaunchKernelGGL(small_mlp_fwd_kernel<false>, dim3((unsigned)((B + R - 1) / R)), dim3(kSmlThreads), small_mlp_lds(P),
+  hipLaunchKernelGGL(small_mlp_fwd_kernel<false>, dim3((unsigned)((B + R - 1) / R)), dim3(kSmlThreads), 0,
                      (hipStream_t)stream, x, B, P, ObsIn{});
   HIPCHK(hipGetLastError());
   return MJL_OK;
@@ -1217,7 +1219,7 @@ extern "C" int mjl_small_mlp_bwd_input(const float* g_out, int B, int k0, int nl
   if ((!g_out || !g_x) && B > 0) return fail(MJL_ERR_ARG, "bad argument");
   if (B == 0) return MJL_OK;
   const int R = kSmlThreads / P.u;
-  hipLaunchKernelGGL(small_mlp_bwd_input_kernel<false>, dim3((unsigned)((B + R - 1) / R)), dim3(kSmlThreads), small_mlp_lds(P),
+  hipLaunchKernelGGL(small_mlp_bwd_input_kernel<false>, dim3((unsigned)((B + R - 1) / R)), dim3(kSmlThreads), 0,
                      (hipStream_t)stream, g_out, B, P, g_x, ObsVjp{});
   HIPCHK(hipGetLastError());
   return MJL_OK;
@@ -1268,13 +1270,13 @@ extern "C" int mjl_apg_obs_policy_fwd(mjlBatch* B, const uint8_t* alive, const f
   if (!B || !alive || !o || !on || !alive_snap || (use_norm && (!mean || !var))) return fail(MJL_ERR_ARG, "bad argument");
   const int nq = B->model->desc.nq, nv = B->model->desc.nv;
   SmallMlp P;
-  int rc = small_mlp_setup(B->nenv, nq + nv, nl, widths, w, b, ys, P);
+  int rc = small_mlp_setup(B->nenv, nq + nv, nl, widths, w, b, ys, P, true);
   if (rc != MJL_OK) return rc;
   HIPCHK(hipSetDevice(B->device));
   if (B->nenv == 0) return MJL_OK;
   const ObsIn O{B->s.qpos, B->s.qvel, nq, nv, use_norm, alive, mean, var, o, on, alive_snap};
   const int R = kSmlThreads / P.u;
-  hipLaunchKernelGGL(small_mlp_fwd_kernel<true>, dim3((unsigned)((B->nenv + R - 1) / R)), dim3(kSmlThreads), small_mlp_lds(P),
+  hipLaunchKernelGGL(small_mlp_fwd_kernel<true>, dim3((unsigned)((B->nenv + R - 1) / R)), dim3(kSmlThreads), 0,
                      (hipStream_t)stream, nullptr, B->nenv, P, O);
   HIPCHK(hipGetLastError());
   return MJL_OK;
@@ -1296,7 +1298,7 @@ extern "C" int mjl_apg_policy_bwd_obs_vjp(const float* g_out, int nenv, int nq, 
   if (nenv == 0) return MJL_OK;
   const ObsVjp O{nq, nv, use_norm, o, alive_snap, mean, var, g_qpos, g_qvel};
   const int R = kSmlThreads / P.u;
-  hipLaunchKernelGGL(small_mlp_bwd_input_kernel<true>, dim3((unsigned)((nenv + R - 1) / R)), dim3(kSmlThreads), small_mlp_lds(P),
+  hipLaunchKernelGGL(small_mlp_bwd_input_kernel<true>, dim3((unsigned)((nenv + R - 1) / R)), dim3(kSmlThreads), 0,
                      (hipStream_t)stream, g_out, nenv, P, nullptr, O);
   HIPCHK(hipGetLastError());
   return MJL_OK;

@@ -96,6 +96,9 @@ __global__ __launch_bounds__(256) void policy_head_kernel(const float* __restric
 // lane's A values (X row lane & 15) and B values are 16-B contiguous: the weights come packed as
 // WP[k / 4][n][k % 4] (zero-padded to K, N multiples of 16: mjl_policy_pack's layout), b after
 // each layer's WP. Output C[4 g + r][n] of a block sits in lane (g, n) register r.
+// (A vector-ALU variant, 8 envs per 256-thread workgroup and thread n owning column n, packed weights
+// read as b128 per 4 k: twice the workgroups, measured 33.2 against 20.5 us at 1024 envs and 34.1-35.0
+// against 21.2 us at 2048; not kept.)
 constexpr int kPolMaxLayers = 6;
 constexpr int kPolLdx = 260;  // LDS row stride (floats): rows 4 banks apart, conflict-free b128
 #ifndef MJL_POL_WAVES
@@ -217,6 +220,7 @@ __global__ __launch_bounds__(64 * MJL_POL_WAVES) void policy_rollout_kernel(cons
     }
   }
 }
+
 #pragma clang fp contract(on)
 
 // Column sums of a row-major [n, d] matrix (the PPO update's bias gradients dY.sum(0) over a

@@ -4,6 +4,7 @@
   envstep_pool  the same with the trainer's reset pool (16 slots, refilled every 64 steps)
   envstep_nr    the same steps without auto-reset (the physics + env post only)
   vjp           mjl_env_step_vjp_replay over every slot of a 2048 x 128 CG 4/4 implicit APG tape
+  policy        mjl_policy_fwd, the PPO rollout policy (obs 54 -> 256 x 3 -> 21) on B envs
 python tools/prof_target.py MODE [B] [n]"""
 import os
 import sys
@@ -64,5 +65,17 @@ elif mode == "vjp":
     for _ in range(max(1, n // cfg.horizon)):
         for t in range(cfg.horizon - 1, -1, -1):
             aenv.step_vjp_replay(t, act, gq, gv, None, grew, None, nonf)
+elif mode == "policy":
+    from mjx_amd import ppo
+    g = torch.Generator().manual_seed(0)
+    pol = ppo.GaussianPolicy(54, 21, [(256, "tanh")] * 3, 0.0, g).cuda()
+    gd = torch.Generator(device="cuda").manual_seed(0)
+    x = torch.randn((B, 54), generator=gd, device="cuda")
+    rms = ppo.RunningMeanStd(54, "cuda")
+    eps = torch.randn((B, 21), generator=gd, device="cuda")
+    dims, params = ppo.policy_fused_dims(pol), ppo.pack_policy_params(pol)
+    act, lp = torch.empty((B, 21), device="cuda"), torch.empty(B, device="cuda")
+    for _ in range(n):
+        ppo.policy_fwd_native(x, rms.mean, rms.var, 10.0, params, dims, pol.log_std, eps, act, lp)
 torch.cuda.synchronize()
 print("done", mode, B, n)
