@@ -5,7 +5,7 @@
 # timeout (status other than 0).
 set -o pipefail
 export TMPDIR=/tmp
-O=gpurun_out/prof5
+O=gpurun_out/${PROF_OUT:-prof5}
 mkdir -p $O
 step() {  # name, limit, command...
   local name=$1 lim=$2; shift 2
