@@ -121,8 +121,10 @@ __global__ void apg_obs_vjp_kernel(int B, int nq, int nv, const float* __restric
 // 2048 rows: 12 launches per rollout step). A block takes kSmlThreads / U rows, thread (row, unit
 // < U) one output unit; each layer's weights are staged through LDS (transposed for the forward so
 // the units read consecutive words), activations through LDS, sums in k order from the bias.
-// (Loading every layer's weights, the biases and the stored activations at the kernel's start, one
-// global round trip per launch, measured slower: 10.0 -> 11.0 us forward, 8.1 -> 8.9 us backward.)
+// (Measured slower and not kept: every layer's weights, biases and stored activations loaded at the
+// kernel's start, 10.0 -> 11.0 us forward and 8.1 -> 8.9 us backward (fused forms); each layer's
+// weights loaded into registers with all loads issued together and the next layer's loaded during
+// this one, 8.2 -> 11.4 us forward and 7.2 -> 8.9 us backward (plain forms, tools/prof_target.py apgmlp).)
 constexpr int kSmlMaxW = 64, kSmlMaxL = 4, kSmlThreads = 256;
 struct SmallMlp {
   int nl, k0, u;            // layers, input width, units per row slot (32 or 64: >= every width)

@@ -5,6 +5,7 @@
   envstep_nr    the same steps without auto-reset (the physics + env post only)
   vjp           mjl_env_step_vjp_replay over every slot of a 2048 x 128 CG 4/4 implicit APG tape
   policy        mjl_policy_fwd, the PPO rollout policy (obs 54 -> 256 x 3 -> 21) on B envs
+  apgmlp        mjl_small_mlp_fwd + mjl_small_mlp_bwd_input, the APG policy (55 -> 32 x 2 -> 21) on B rows
 python tools/prof_target.py MODE [B] [n]"""
 import os
 import sys
@@ -77,5 +78,16 @@ elif mode == "policy":
     act, lp = torch.empty((B, 21), device="cuda"), torch.empty(B, device="cuda")
     for _ in range(n):
         ppo.policy_fwd_native(x, rms.mean, rms.var, 10.0, params, dims, pol.log_std, eps, act, lp)
+elif mode == "apgmlp":
+    from mjx_amd import apg, ppo
+    pol = ppo.APGPolicy(55, 21, 32, 2, None, torch.Generator().manual_seed(0)).cuda()
+    nat = apg.NativeAPGPolicy(pol)
+    gd = torch.Generator(device="cuda").manual_seed(0)
+    x = torch.randn((B, 55), generator=gd, device="cuda")
+    ga = torch.randn((B, 21), generator=gd, device="cuda")
+    ys = [torch.empty((B, w), device="cuda") for w in nat.widths]
+    for _ in range(n):
+        nat.forward(x, ys)
+        nat.backward_input(ga, ys)
 torch.cuda.synchronize()
 print("done", mode, B, n)
