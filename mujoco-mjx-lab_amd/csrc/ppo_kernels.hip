@@ -106,6 +106,10 @@ constexpr int kPolLdx = 260;  // LDS row stride (floats): rows 4 banks apart, co
 #endif
 constexpr int kPolWaves = MJL_POL_WAVES;        // waves per 16-env workgroup
 constexpr int kPolBpw = 16 / kPolWaves;         // 16-column blocks per wave per pass (256 columns)
+#ifndef MJL_POL_PD
+#define MJL_POL_PD 4
+#endif
+constexpr int kPolPD = MJL_POL_PD;  // K chunks (16 k each) of weights and activations in flight per wave
 struct PolicyDims {
   int nlayer, obs_dim, act_dim;
   int K[kPolMaxLayers], N[kPolMaxLayers];  // padded (multiples of 16), K[0] >= obs_dim
@@ -169,14 +173,23 @@ __global__ __launch_bounds__(64 * MJL_POL_WAVES) void policy_rollout_kernel(cons
             if (nbs[q] < nblk) acc[q] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[t], b[q][t], acc[q], 0, 0, 0);
         }
       };
-      f4 a0, a1, b0[kPolBpw], b1[kPolBpw];
-      load(0, a0, b0);
-      for (int c = 0; c < K; c += 32) {
-        if (c + 16 < K) load(c + 16, a1, b1);
-        mac(a0, b0);
-        if (c + 16 < K) {
-          if (c + 32 < K) load(c + 32, a0, b0);
-          mac(a1, b1);
+      // a ring of kPolPD chunks in flight: chunk c + kPolPD - 1's loads issue before chunk c's MFMAs
+      // (one chunk ahead: 21.6 us per 1024-env launch, 22.0 at 2048; three ahead 20.7 / 21.2; five the
+      // same as three: tools/r5/gpu_polpd.sh). The MFMA sequence, and so every bit, is unchanged.
+      f4 ra[kPolPD], rb[kPolPD][kPolBpw];
+      const int nc = K >> 4;
+#pragma unroll
+      for (int p = 0; p < kPolPD - 1; p++)
+        if (p < nc) load(16 * p, ra[p], rb[p]);
+      for (int c0 = 0; c0 < nc; c0 += kPolPD) {
+#pragma unroll
+        for (int p = 0; p < kPolPD; p++) {
+          const int c = c0 + p;
+          if (c < nc) {
+            const int pn = (p + kPolPD - 1) % kPolPD;
+            if (c + kPolPD - 1 < nc) load(16 * (c + kPolPD - 1), ra[pn], rb[pn]);
+            mac(ra[p], rb[p]);
+          }
         }
       }
 #pragma unroll
