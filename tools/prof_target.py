@@ -6,6 +6,8 @@
   vjp           mjl_env_step_vjp_replay over every slot of a 2048 x 128 CG 4/4 implicit APG tape
   policy        mjl_policy_fwd, the PPO rollout policy (obs 54 -> 256 x 3 -> 21) on B envs
   apgmlp        mjl_small_mlp_fwd + mjl_small_mlp_bwd_input, the APG policy (55 -> 32 x 2 -> 21) on B rows
+  apgstep       the APG rollout's physics (CG 4/4 model) through mjl_env_step without reset, random
+                actions, against the record kernel of the `vjp` mode (rows in LDS vs in global memory)
 python tools/prof_target.py MODE [B] [n]"""
 import os
 import sys
@@ -78,6 +80,21 @@ elif mode == "policy":
     act, lp = torch.empty((B, 21), device="cuda"), torch.empty(B, device="cuda")
     for _ in range(n):
         ppo.policy_fwd_native(x, rms.mean, rms.var, 10.0, params, dims, pol.log_std, eps, act, lp)
+elif mode == "apgstep":
+    from mjx_amd.config import APGConfig, EnvConfig
+    from mjx_amd.envs import HumanoidEnv, resolve_ids
+    sys.path.insert(0, os.path.join(ROOT, "mujoco-mjx-lab_amd"))
+    from train_apg import apg_model
+    cfg = APGConfig()
+    ma = apg_model(cfg, solver="cg")
+    env = HumanoidEnv(mjx.put_model(ma), resolve_ids(ma, EnvConfig()), B, seed=cfg.seed)
+    env.reset()
+    g = torch.Generator(device="cuda").manual_seed(0)
+    for i in range(n):
+        if i % 128 == 0:
+            env.reset()
+        act = (torch.rand((B, ma.nu), generator=g, device="cuda") * 2 - 1) * 0.3
+        env.step(act, auto_reset=False)
 elif mode == "apgmlp":
     from mjx_amd import apg, ppo
     pol = ppo.APGPolicy(55, 21, 32, 2, None, torch.Generator().manual_seed(0)).cuda()
