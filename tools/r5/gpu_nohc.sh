@@ -1,7 +1,6 @@
 #!/bin/bash
 # round 5 diagnostic: the APG record kernel with and without the implicit VJP's Hc factor (a temporary build with the
 # record path's `solver_hessian` + `chol_factor_solve` block compiled out, not kept in the sources; its gradients are wrong, only the record's time is read), 2048 envs
-# build; its gradients are wrong, only the record's time is read), 2048 envs
 set -o pipefail
 export TMPDIR=/tmp
 O=gpurun_out/r5h2
