@@ -139,12 +139,14 @@ def test_cg_solver_parity():
     assert np.median(errs) <= 1e-4, f"median step {np.median(errs):.2e}"
 
 
-@pytest.mark.parametrize("name,B", [("humanoid_mjx", 64), ("humanoid_mjx", 1024), ("humanoid_mjx", 2048),
-                                    ("humanoid", 2048)])
+@pytest.mark.parametrize("name,B", [("humanoid_mjx", 64), ("humanoid_mjx", 1000), ("humanoid_mjx", 1024),
+                                    ("humanoid_mjx", 2048), ("humanoid", 2048)])
 def test_speedtest_parity(name, B):
     """The speed-test step (mjx_humanoid_speed_test.py:48-57) against the oracle at the bench's own
     size (B = 2048, BASELINE configs[1]): every env's qpos[0] to 1e-6. B <= 1024 (one wave per SIMD)
-    runs the one-wave kernel instantiation, B = 2048 the two-wave one."""
+    runs the one-wave kernel instantiation, B = 2048 the two-wave one. The sizes cover the XCD-aware
+    env order's cases (step_kernels.hip block_env): B < 128 (block order), multiples of 128 (runs of
+    16 envs per XCD) and B = 1000 (both: the last 104 blocks keep block order)."""
     m = mjx_amd.load_model(name)
     sys_ = mjx.put_model(m)
     vel = torch.linspace(0, 1, B, device="cuda")
