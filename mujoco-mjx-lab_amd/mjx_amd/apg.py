@@ -292,7 +292,7 @@ class APGTrainer:
         dropped = torch.stack([dropped_e.sum(), nonfinite[0]])  # (forward guard, reverse guard)
         # the reward cotangents and actions of the last rollout (graph-owned under capture: they hold
         # the last replay's values), for timing the replay VJP on the trainer's own workload (bench.py)
-        self.last_reverse_inputs = (grew_all, acts) if taped else None
+        self.last_reverse_inputs = (grew_all, [a.detach() for a in acts]) if taped else None
         return loss.detach(), (rfin.mean(1).sum() / H).detach(), (o_all, snap), dropped
 
     def _loss_and_grad_torch(self, use_norm: bool, per_step_param_grad: bool = False, graph: bool = False):
