@@ -171,6 +171,23 @@ def pmc_traffic(B: int, key: str = "bytes_per_launch"):
     return t.get(key)
 
 
+def gather_over_ranks(x, dist, device="cuda") -> list:
+    """[x of rank 0, x of rank 1, ...] (one value per rank), or [x] single-process."""
+    if dist is None:
+        return [x]
+    t = torch.tensor([x], dtype=torch.float64, device=torch.device(device))
+    out = [torch.zeros_like(t) for _ in range(dist.get_world_size())]
+    dist.all_gather(out, t)
+    return [float(o.item()) for o in out]
+
+
+def build_info() -> dict:
+    """The native library this run loaded and the source hash it was built from (equal to the tree's:
+    _lib.lib() refuses a stale library unless MJX355_LIB overrides it)."""
+    from mjx_amd import _lib
+    return _lib.build_info()
+
+
 def free_gpu():
     gc.collect()
     if torch.cuda.is_available():
@@ -332,6 +349,7 @@ def speedtest(args, dist, world, local):
         "config": {"workload": f"{args.model}.xml speed-test step (fresh state per step), {B} envs per GPU",
                    "envs_per_gpu": B, "parallelism": f"env-sharded x{world}, no collective in the speed test",
                    "baseline_note": "vs_baseline divides by the README HUMANOID_MJX row (72,618 steps/s, batch 4096)"},
+        "build": build_info(),
         "roofline": {"bound": "valu", "achieved": achieved_tflops, "peak": F32_PEAK_TFLOPS, "unit": "TFLOP/s",
                      "frac": achieved_tflops / F32_PEAK_TFLOPS, "traffic": pmc_traffic(B),
                      "kernel": SPEEDTEST_KERNEL, "kernel_ms": kern_ms,
@@ -492,12 +510,14 @@ def ppo_leg(tr, iters: int, warmup: int, dist, device, curve=()) -> dict:
     tr.allreduce_events = None
     ar_ms = max_over_ranks(sum(ar) / len(ar) if ar else 0.0, dist, device)
     # phase split of the timed iterations (events on the trainer's stream), median, max over ranks
-    phases = {}
+    phases, update_per_rank = {}, []
     if tr.phase_events:
         import statistics
         for name, (a, b) in (("rollout", (0, 1)), ("between", (1, 2)), ("update", (2, 3))):
-            phases[name] = max_over_ranks(statistics.median(e[a].elapsed_time(e[b]) for e in tr.phase_events), dist,
-                                          device)
+            med = statistics.median(e[a].elapsed_time(e[b]) for e in tr.phase_events)
+            phases[name] = max_over_ranks(med, dist, device)
+            if name == "update":
+                update_per_rank = gather_over_ranks(med, dist, device)
     tr.phase_events = None
     while curve and it[0] <= max(curve):
         one()
@@ -505,13 +525,16 @@ def ppo_leg(tr, iters: int, warmup: int, dist, device, curve=()) -> dict:
     env_steps = float(tr.env.num_envs * world * tr.cfg.rollout_length * iters)
     # RCCL collectives captured in the update's step graph (ppo.DP_CAPTURE) have no events of their own:
     # their count comes from the updater, their time is inside the update phase
-    captured = dist is not None and not ar and getattr(tr.updater, "collectives_last_run", 0) > 0
-    n_ar = tr.updater.collectives_last_run if captured else len(ar) // max(1, iters)
+    up = tr.updater
+    captured = dist is not None and bool(getattr(up, "captured_last_run", False))
+    n_ar = up.collectives_last_run if captured else len(ar) // max(1, iters)
     return {"env_steps_per_s": env_steps / wall, "ms_per_iter": wall / iters * 1e3, "iters": iters,
             "warmup": warmup, "envs_per_rank": tr.env.num_envs, "ranks": world,
             "allreduce_ms": None if captured else ar_ms, "allreduces_per_iter": n_ar, "allreduce_captured": captured,
             "train_return_avg": [r["train_return_avg"] for r in res], "return_at_iter": returns,
-            "next_iteration": it[0], "phase_ms": phases, "update_rows": getattr(tr, "last_update_rows", 0)}
+            "next_iteration": it[0], "phase_ms": phases, "update_rows": getattr(tr, "last_update_rows", 0),
+            "update_ms_per_rank": update_per_rank, "dp_buckets": getattr(up, "dp_buckets", 0),
+            "capture_fallback_reason": getattr(up, "capture_fallback_reason", None)}
 
 
 def c5_fields(res: dict, world: int, backend: str, grad_numel: int) -> dict:
@@ -522,7 +545,12 @@ def c5_fields(res: dict, world: int, backend: str, grad_numel: int) -> dict:
             "allreduce_captured_in_graph": res.get("allreduce_captured", False),
             "allreduce_bytes": 4 * grad_numel, "collective_backend": backend, "collective_ranks": world,
             "rccl_ranks": world if backend == "nccl" else 0,
-            "ppo_c5_train_return_avg": res["train_return_avg"], "ppo_c5_phase_ms_per_rank": res["phase_ms"]}
+            "ppo_c5_train_return_avg": res["train_return_avg"], "ppo_c5_phase_ms_per_rank": res["phase_ms"],
+            # which data-parallel path ran (a SCALE record then says it): gradient buckets per minibatch
+            # step, why the in-graph collective capture was given up (null: it ran captured, or was not
+            # attempted on this backend), and every rank's update-phase median
+            "dp_buckets": res.get("dp_buckets", 0), "dp_capture_fallback_reason": res.get("capture_fallback_reason"),
+            "ppo_c5_update_ms_per_rank": res.get("update_ms_per_rank", [])}
 
 
 def ppo_trainer(args, envs, dist, rank, local, eval_envs=0):
@@ -831,7 +859,7 @@ def main():
                 "config": {"workload": f"PPO src/config.json: {args.envs} envs per GPU x 256 rollout x 4 epochs, "
                                        f"global minibatch 65536", "envs_per_gpu": args.envs},
                 "step": "one PPO iteration (rollout + GAE + updates), synced", "roofline": None, "cpu_baseline": None,
-                "rehearsal": os.environ.get("MJL_BENCH_REHEARSAL") == "1"}
+                "rehearsal": os.environ.get("MJL_BENCH_REHEARSAL") == "1", "build": build_info()}
         if dist is not None:
             line.update(c5_fields(res, world, backend, grad_numel(tr)))
         if rank == 0:

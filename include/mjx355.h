@@ -149,7 +149,8 @@ typedef struct mjlBatch mjlBatch;
 
 /* Message of the last failing call on this thread. */
 const char* mjl_last_error(void);
-/* Library version string. */
+/* Library version string, "mjx355 <version> (gfx950) src=<hash>": <hash> is the sha256 prefix of the
+   sources the library was built from (mjx_amd/_srchash.py); loaders compare it with their tree. */
 const char* mjl_version(void);
 
 /* Replaces mjx.put_model(MjModel) (src/training_utils.py:105): validate + upload constants.

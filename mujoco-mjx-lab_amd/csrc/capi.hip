@@ -81,7 +81,12 @@ struct mjlBatch {
 extern "C" {
 
 const char* mjl_last_error(void) { return g_err.c_str(); }
-const char* mjl_version(void) { return "mjx355 0.1 (gfx950)"; }
+#ifndef MJL_SRC_HASH
+#define MJL_SRC_HASH "unstamped"
+#endif
+// "mjx355 <ver> (gfx950) src=<hash>": the hash of the sources this library was built from
+// (mjx_amd/_srchash.py, stamped by the Makefile); the loader refuses a stale library
+const char* mjl_version(void) { return "mjx355 0.2 (gfx950) src=" MJL_SRC_HASH; }
 
 #ifdef MJL_TIMING
 // diagnostic build only: install a device buffer [nenv, 16] of per-phase s_memtime stamps

@@ -158,9 +158,7 @@ __global__ __launch_bounds__(RB) void ppo_surrogate_kernel(
   __syncthreads();
   const float* dr = sd + (in ? t : 0) * A;
   float qs = 0.f;
-  // the row waves only: the staging-only waves (w >= NW) would read row 0's sd while thread 0 writes it
-  if (w < NW)
-    for (int j = 0; j < A; j++) qs += dr[j] * dr[j] * ivs[j];
+  for (int j = 0; j < A; j++) qs += dr[j] * dr[j] * ivs[j];
   float surr = 0.f, dlogp = 0.f;
   if (in) {
     const float logp = -0.5f * (qs + lss);
@@ -313,7 +311,8 @@ __global__ __launch_bounds__(2 * RB) void twin_loss_head_kernel(
   float* dr = sd + (in ? t : 0) * A;
   const float* mr = sm + (in ? t : 0) * A;
   float qs = 0.f;
-  // the row waves only: the staging-only waves (w >= NW) would read row 0's sd while thread 0 writes it
+  // the row waves only: a staging-only wave (w >= NW) is never `in`, so its qs would be discarded; the
+  // guard only skips that benign read of row 0's sd (thread 0 may be writing it)
   if (w < NW)
     for (int j = 0; j < A; j++) qs += dr[j] * dr[j] * ivs[j];
   float surr = 0.f, dlogp = 0.f;

@@ -2180,9 +2180,15 @@ INL float jax_uniform(int mode, uint32_t k0, uint32_t k1, int i, int n) {
 // runs after the whole step, and a field read in the kernel prologue would hold an SGPR across it).
 // Kernel bodies only: in a called function the intrinsic is not the kernel's segment (it lowers to a
 // null pointer), so a callee takes the pointer as an argument.
+// Guarded two ways: the debug build (make debug, -DMJL_DEBUG) traps on a null pointer, and
+// tests/test_kernarg_guard.py scans the shipped code object for a non-kernel function that loads
+// through a zeroed SGPR pair (the round-5 fault: `s_mov_b64 s[4:5], 0` feeding the loads).
 INL const CSTA KParams* kparams_late() {
   const CSTA KParams* p = (const CSTA KParams*)__builtin_amdgcn_kernarg_segment_ptr();
   asm volatile("" : "+s"(p));
+#ifdef MJL_DEBUG
+  if (p == nullptr) __builtin_trap();
+#endif
   return p;
 }
 

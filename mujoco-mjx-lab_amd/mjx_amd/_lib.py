@@ -10,7 +10,7 @@ import ctypes as C
 import os
 import subprocess
 
-from . import abi
+from . import _srchash, abi
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("MJX355_LIB", os.path.join(_HERE, "libmjx355.so"))  # override: A/B builds
@@ -43,16 +43,14 @@ class MjlError(RuntimeError):
 
 
 def source_hash() -> str:
-    """sha256 over the native sources (kernel + C ABI), to tie recorded profiles to a kernel build."""
-    import hashlib
-    h = hashlib.sha256()
-    inc = os.path.join(os.path.dirname(os.path.dirname(_HERE)), "include", "mjx355.h")
-    for p in sorted(os.listdir(CSRC)) + [inc]:
-        fp = p if os.path.isabs(p) else os.path.join(CSRC, p)
-        if fp.endswith((".hip", ".h")):
-            with open(fp, "rb") as f:
-                h.update(os.path.basename(fp).encode() + b"\0" + f.read())
-    return h.hexdigest()[:16]
+    """sha256 prefix over the native sources (kernel + C ABI) of this tree (_srchash.py): the stamp a
+    library built from them carries, and the key of recorded profiles."""
+    return _srchash.source_hash(CSRC)
+
+
+def stamped_hash(version: str) -> str:
+    """The source hash a library stamped into its mjl_version() string ("... src=<hash>"), or ""."""
+    return version.rsplit("src=", 1)[1].strip() if "src=" in version else ""
 
 
 def build(force: bool = False):
@@ -62,6 +60,15 @@ def build(force: bool = False):
     subprocess.run(args, check=True)
 
 
+def build_info() -> dict:
+    """Which library this process runs and what it was built from (bench line, smoke)."""
+    L = lib()
+    v = L.mjl_version().decode()
+    return {"lib": os.path.relpath(LIB_PATH, os.path.dirname(os.path.dirname(_HERE))), "version": v,
+            "lib_src_hash": stamped_hash(v), "tree_src_hash": source_hash(),
+            "override": "MJX355_LIB" in os.environ}
+
+
 def lib() -> C.CDLL:
     global _lib
     if _lib is not None:
@@ -69,6 +76,14 @@ def lib() -> C.CDLL:
     if not os.path.exists(LIB_PATH):
         raise MjlError(f"native library missing: {LIB_PATH} (run `make -C {CSRC}` or __graft_entry__.build())")
     L = C.CDLL(LIB_PATH)
+    L.mjl_version.restype = C.c_char_p
+    # provenance: the product library must have been built from this tree's sources. An explicit
+    # MJX355_LIB (A/B and diagnostic builds) opts out of the check.
+    if "MJX355_LIB" not in os.environ:
+        built, tree = stamped_hash(L.mjl_version().decode()), source_hash()
+        if built != tree:
+            raise MjlError(f"stale native library {LIB_PATH}: built from sources {built or '(unstamped)'}, "
+                           f"the tree's sources are {tree} (rebuild: make -C {CSRC})")
     P, vp, f32p, i32 = C.POINTER, C.c_void_p, C.c_void_p, C.c_int
     u64 = C.c_uint64
     L.mjl_last_error.restype = C.c_char_p

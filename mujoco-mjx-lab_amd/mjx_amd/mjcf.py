@@ -438,9 +438,12 @@ def compile_xml_string(text: str, name_hint: str = "", sha: str = "") -> Compile
                     if o in a:
                         raise MJCFError(f"geom orientation '{o}' not supported")
                 # an explicit mass sets the density (mjCGeom::SetInertia: density = mass / volume)
+                # (worldbody geoms and planes carry no mass: MuJoCo ignores the attribute there)
                 dens = float(a["density"])
-                if "mass" in a:
+                if "mass" in a and bid != 0 and gtype != GEOM_PLANE:
                     vol, _ = _geom_inertia(gtype, size, 1.0)
+                    if not vol > 0.0:
+                        raise MJCFError(f"geom with mass {a['mass']} has zero volume (size {size})")
                     dens = float(a["mass"]) / vol
                 frv = _floats(a["friction"])  # missing trailing values keep MuJoCo's defaults
                 fr = (frv + [1.0, 0.005, 0.0001][len(frv):])[:3]

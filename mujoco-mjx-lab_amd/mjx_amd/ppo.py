@@ -842,6 +842,12 @@ class PPOUpdater:
         self.runs = 0
         self._src = self._idx = self._st = None
         self._ga = self._gb = self._gstep = None
+        # data-parallel observability (bench line): gradient buckets per minibatch step (0 single
+        # process), whether the last run replayed the step graph with its collectives captured, and why
+        # the capture was given up (None: not attempted or succeeded)
+        self.dp_buckets = 0
+        self.captured_last_run = False
+        self.capture_fallback_reason: Optional[str] = None
 
     def _twin_ok(self, rows: int, act_dim: int) -> bool:
         return (self.twin is not None and rows >= UPDATE_MIN_ROWS and rows % SPLIT_ROWS == 0 and rows % 128 == 0
@@ -996,6 +1002,8 @@ class PPOUpdater:
         if tw != self._tw:
             self._ga = self._gb = self._gstep = None  # the captured bodies belong to the other path
         self._tw = tw
+        self.dp_buckets = (2 if self._bucketed() else 1) if self.dist is not None else 0
+        self.captured_last_run = False
         use_graph = self.graph_ok and self.runs > 0
         self.runs += 1
         if not use_graph:
@@ -1056,17 +1064,15 @@ class PPOUpdater:
         self._row.zero_()
         st = self._st_all if stats is not None else None
         bucketed = self._bucketed()
-        if self._capture_collectives() and not getattr(self, "_capture_failed", False):
-            try:
-                self._run_captured_steps(nmb, st, bucketed)
+        if self._capture_collectives() and self.capture_fallback_reason is None:
+            if self._gstep is None:
+                self._capture_step(st, bucketed)
+            if self.capture_fallback_reason is None:
+                for _ in range(nmb):  # replay errors propagate (no eager re-run of applied steps)
+                    self._gstep.replay()
+                self.collectives_last_run = nmb * self.dp_buckets
+                self.captured_last_run = True
                 return
-            except RuntimeError as e:  # (a capture refused by this RCCL build: eager collectives from here on;
-                # nothing ran — the replays come after a successful capture)
-                import warnings
-                warnings.warn(f"PPOUpdater: RCCL collective capture failed ({e}); eager collectives instead")
-                self._capture_failed = True
-                self._gstep = None
-                torch.cuda.synchronize()
         for _ in range(nmb):
             if self._ga is None:
                 self._ga = torch.cuda.CUDAGraph()
@@ -1106,10 +1112,16 @@ class PPOUpdater:
         except Exception:  # a stand-in without backends (bench's identity collective)
             return False
 
-    def _run_captured_steps(self, nmb, st, bucketed):
-        if getattr(self, "_gstep", None) is None:
-            self._gstep = torch.cuda.CUDAGraph()
-            with graph_capture(self._gstep):
+    def _capture_step(self, st, bucketed):
+        """Capture the minibatch step with its collective(s) inside. Only the capture is guarded: a
+        capture refused on any rank (this RCCL build, a collective the capture does not take) sends
+        EVERY rank to the eager collectives — the ranks agree through one eager all-reduce of a
+        failure flag, so no rank replays captured collectives that another rank issues eagerly.
+        Nothing captured has run: the replays come only after the agreement."""
+        reason = None
+        g = torch.cuda.CUDAGraph()
+        try:
+            with graph_capture(g):
                 if bucketed:
                     gen = self._body_a_phases(self._idx_all, self._src, st, row=self._row)
                     next(gen)
@@ -1124,9 +1136,22 @@ class PPOUpdater:
                     self._body_a(self._idx_all, self._src, st, row=self._row)
                     self.dist.all_reduce(self._grad_buffer())
                 self._body_b(row=self._row)
-        for _ in range(nmb):
-            self._gstep.replay()
-        self.collectives_last_run = nmb * (2 if bucketed else 1)
+        except RuntimeError as e:
+            reason = f"{type(e).__name__}: {e}"[:300]
+            g = None
+            torch.cuda.synchronize()
+        flag = torch.tensor([0.0 if reason is None else 1.0], device=self._row.device)
+        self.dist.all_reduce(flag)  # eager, outside any capture: how many ranks failed
+        nfail = int(flag.item())
+        if nfail:
+            import warnings
+            self.capture_fallback_reason = reason or f"capture refused on {nfail} other rank(s)"
+            warnings.warn(f"PPOUpdater: RCCL collective capture failed ({self.capture_fallback_reason}); "
+                          "eager collectives between the captured bodies instead")
+            self._gstep = None
+            self._ga = self._gb = None
+        else:
+            self._gstep = g
 
 
 def ppo_update(policy, value, opt_p, opt_v, obs, acts, logp, ret, adv, index_batches, cfg, dist=None, world=1,

@@ -30,6 +30,7 @@ single ones, so results agree to rounding, not bit for bit (tests/test_twin.py).
 from __future__ import annotations
 
 import os
+import weakref
 from typing import List, Optional
 
 import torch
@@ -276,14 +277,20 @@ class TwinNets:
 
 def twin_for(policy, value) -> Optional[TwinNets]:
     """A TwinNets over (policy, value) when MJL_TWIN_UPDATE is on and the pair is eligible. The pair's
-    TwinNets is kept on the policy module and reused while it still owns both modules' storage: a
+    TwinNets is cached per policy module (a weak-keyed table: no attribute on the module, nothing
+    pulled along when it is pickled or copied) and reused while it still owns both modules' storage: a
     second TwinNets over the same modules would re-point their parameters and leave the first one's
-    holder (a trainer's updater) on stale storage."""
+    holder (a trainer's updater) on stale storage. Every updater built over the same pair therefore
+    SHARES one TwinNets, including its scratch and kept-alive buffers: such updaters must not run
+    concurrently (on different streams or threads)."""
     if not (TWIN_UPDATE and TwinNets.eligible(policy, value)):
         return None
-    tw = getattr(policy, "_twin_nets", None)
+    tw = _TWINS.get(policy)
     if tw is not None and tw.value is value and tw.owns_storage():
         return tw
     tw = TwinNets(policy, value)
-    object.__setattr__(policy, "_twin_nets", tw)  # a plain attribute (not a registered submodule)
+    _TWINS[policy] = tw
     return tw
+
+
+_TWINS: "weakref.WeakKeyDictionary" = weakref.WeakKeyDictionary()  # policy module -> its TwinNets

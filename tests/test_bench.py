@@ -98,3 +98,8 @@ def test_c5_line_over_gloo_world_size_2(tmp_path):
     assert line["allreduces_per_iteration"] == 2 * (8 * 8 // 16)
     assert line["ppo_c5_env_steps_per_s"] > 0 and line["allreduce_ms_per_minibatch"] > 0
     assert line["ppo_c5_global_envs"] == 16
+    # which data-parallel path ran: one bucket (eager, the CPU stand-in nets take the
+    # per-net path), no capture over gloo, so no fallback reason; the per-rank update list is filled
+    # from the update-phase events on the GPU (none on the CPU)
+    assert line["dp_buckets"] == 1 and line["dp_capture_fallback_reason"] is None
+    assert line["allreduce_captured_in_graph"] is False and isinstance(line["ppo_c5_update_ms_per_rank"], list)

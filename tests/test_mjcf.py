@@ -176,3 +176,16 @@ def test_explicit_geom_mass_sets_density():
                                 "</body></worldbody></mujoco>")
     assert m.body_mass[1] == pytest.approx(1.0, rel=1e-12)
     assert m.body_inertia[1][:3] == pytest.approx([0.4 * 0.15 ** 2] * 3, rel=1e-12)
+
+
+def test_geom_mass_on_worldbody_plane_is_ignored():
+    """a worldbody plane with a mass attribute (legal MJCF, MuJoCo ignores it) compiles; a
+    zero-volume geom with an explicit mass is a clear compile error, not a ZeroDivisionError."""
+    from mjx_amd import mjcf
+    m = mjcf.compile_xml_string("<mujoco><worldbody><geom type='plane' size='5 5 .1' mass='3'/>"
+                                "<body><freejoint/><geom size='.15' mass='1' type='sphere'/></body></worldbody>"
+                                "</mujoco>")
+    assert m.body_mass[1] == pytest.approx(1.0, rel=1e-12)
+    with pytest.raises(mjcf.MJCFError, match="zero volume"):
+        mjcf.compile_xml_string("<mujoco><worldbody><body><freejoint/><geom size='0' mass='1' type='sphere'/>"
+                                "</body></worldbody></mujoco>")

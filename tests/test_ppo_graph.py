@@ -134,6 +134,81 @@ def test_rccl_captured_step_graph_bit_identical_to_eager(monkeypatch, buckets):
         tdist.destroy_process_group()
 
 
+def _refuse_capture(monkeypatch):
+    """all_reduce raises while the current stream captures (a capture this RCCL build refuses);
+    eager calls go through."""
+    orig = tdist.all_reduce
+
+    def refusing(t, *a, **k):
+        if torch.cuda.is_current_stream_capturing():
+            raise RuntimeError("collective capture refused (test)")
+        return orig(t, *a, **k)
+    monkeypatch.setattr(tdist, "all_reduce", refusing)
+
+
+@pytest.mark.parametrize("buckets", ["0", "1"])
+def test_rccl_capture_refused_falls_back_to_eager_bit_identical(monkeypatch, buckets):
+    """VERDICT r5 item 5 / ADVICE r5: when the in-graph collective capture is refused, the updater
+    agrees on it across ranks (one eager all-reduce of a failure flag), replays nothing captured, and
+    runs the eager collectives between captured bodies — equal to the eager update bit for bit."""
+    monkeypatch.setattr(ppo, "DP_BUCKETS", buckets)
+    _one_rank_group("nccl")
+    _refuse_capture(monkeypatch)
+    try:
+        cfg = reference_ppo_config()
+        cfg.minibatch_size, cfg.epochs = 8192, 2
+        A = _nets_and_data(cfg, 4 * 8192)
+        B = _nets_and_data(cfg, 4 * 8192)
+        ua = ppo.PPOUpdater(*A[:4], cfg, tdist, 1, use_graph=True)
+        ub = ppo.PPOUpdater(*B[:4], cfg, tdist, 1, use_graph=False)
+        with pytest.warns(UserWarning, match="capture failed"):
+            for run in range(3):
+                idx = ppo.make_index_batches(4 * 8192, cfg.minibatch_size, cfg.epochs,
+                                             torch.Generator(device="cuda").manual_seed(300 + run), "cuda")
+                ua.run(*A[4], idx)
+                ub.run(*B[4], idx)
+                torch.cuda.synchronize()
+                _compare(_state(*A[:4]), _state(*B[:4]), run)
+        assert ua._gstep is None and not ua.captured_last_run
+        assert "refused" in ua.capture_fallback_reason and ua._ga is not None  # the eager-collective graphs ran
+        assert ua.dp_buckets == (2 if buckets == "1" else 1)
+    finally:
+        tdist.destroy_process_group()
+
+
+def test_c5_line_reports_the_capture_fallback(monkeypatch):
+    """The bench's C5 keys say which path ran: with the capture refused, allreduce_captured_in_graph
+    is false, dp_capture_fallback_reason names the refusal and the eager all-reduces are timed; a
+    one-rank RCCL PPOTrainer over a 64-env humanoid shard, 8,192 rows per update."""
+    import importlib.util
+    import os
+    import mjx_amd
+    from mjx_amd import mjx
+    from mjx_amd.envs import HumanoidEnv, resolve_ids
+    spec = importlib.util.spec_from_file_location(
+        "bench_mod", os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "bench.py"))
+    bench = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(bench)
+    _one_rank_group("nccl")
+    _refuse_capture(monkeypatch)
+    try:
+        cfg = reference_ppo_config()
+        cfg.num_envs, cfg.rollout_length, cfg.minibatch_size, cfg.epochs = 64, 128, 4096, 2
+        cfg.eval_interval, cfg.checkpoint_every, cfg.log_interval = 10 ** 9, 10 ** 9, 1
+        m = mjx_amd.load_model("humanoid_mjx")
+        env = HumanoidEnv(mjx.put_model(m), resolve_ids(m, cfg.env_config), 64, device=0, seed=3)
+        tr = ppo.PPOTrainer(cfg, env, None, device="cuda:0", dist=tdist)
+        with pytest.warns(UserWarning, match="capture failed"):
+            res = bench.ppo_leg(tr, 1, 2, tdist, "cuda:0")
+        line = bench.c5_fields(res, 1, tdist.get_backend(), bench.grad_numel(tr))
+        assert line["allreduce_captured_in_graph"] is False and line["rccl_ranks"] == 1
+        assert "refused" in line["dp_capture_fallback_reason"] and line["dp_buckets"] == 1
+        assert line["allreduces_per_iteration"] == 4 and line["allreduce_ms_per_minibatch"] > 0
+        assert len(line["ppo_c5_update_ms_per_rank"]) == 1 and line["ppo_c5_update_ms_per_rank"][0] > 0
+    finally:
+        tdist.destroy_process_group()
+
+
 def test_native_adam_state_dict_is_torch_layout():
     """NativeAdam checkpoints use torch.optim.Adam's state-dict layout, both ways, and a
     mismatched parameter count is refused."""
