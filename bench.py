@@ -648,6 +648,10 @@ class _IdentityComm:
     def get_world_size():
         return 1
 
+    @staticmethod
+    def get_backend():  # the updater captures its collectives for this stand-in as for RCCL
+        return "identity"
+
 
 def c5_rank_update(local, reps: int = 3) -> dict:
     """One rank's PPO update at BASELINE C5's per-rank shape on 8 GPUs (1024 envs x 256 steps, 4 epochs

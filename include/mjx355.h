@@ -444,6 +444,26 @@ int mjl_slice_sum_multi(int nseg, const float* const* x, float* const* out, cons
  * biases — mean = tanh(z[0] + bias[0]), v = z[1][:, 0] + bias[1][0]. scratch: mjl_ppo_loss_scratch(n, A)
  * floats. A <= 32. */
 long long mjl_twin_loss_head_blocks(int n);
+
+/* The twin PPO update's thin ends as single launches (train_ppo.py:233-252 run_ppo_updates over the
+   src/networks.py:82-131 MLPs; both nets stacked as in mjl_twin_loss_head). Bit 0 of
+   mjl_twin_fused_shapes: mjl_twin_gather_in is instantiated for (k0, N); bit 1: mjl_twin_head_bwd for
+   (A, N). Other shapes take the library GEMM path. */
+int mjl_twin_fused_shapes(int k0, int A, int N);
+/* The minibatch gather (make_index_batches' rows, train_ppo.py:222-231; idx [n], or row *idx_row of an
+   [n_minibatches, n] table) fused with both nets' input layer: o2 [2, n, k0] (the observations twice),
+   a [n, A], ol / r / ad [n] gathered from obs / act / logp / ret / adv (an out-of-range index gives NaN);
+   h [2, n, N] = tanh(o W[net]^T + b[net]) with W [2, N, k0], b [2, N]. */
+int mjl_twin_gather_in(const long long* idx, const int* idx_row, int n, long long nsrc, int k0, int A, int N,
+                       const float* obs, const float* act, const float* logp, const float* ret, const float* adv,
+                       float* o2, float* a, float* ol, float* r, float* ad, const float* W, const float* b,
+                       float* h, void* stream);
+/* The output layers' backward fused with the last hidden layer's tanh backward: dzh [2, n, N] =
+   (dz W) (1 - y^2) for dz [2, n, A], W [2, A, N], y [2, n, N]; per chunk c of 128 rows the column sums of
+   dzh into cs [2, n/128, N] and the output weight gradient's partial dz^T y into gw [2, n/128, A, N]
+   (summed by mjl_slice_sum_multi). n % 128 == 0, 16-byte aligned buffers. */
+int mjl_twin_head_bwd(const float* dz, const float* W, const float* y, int n, int A, int N, float* dzh, float* cs,
+                      float* gw, void* stream);
 int mjl_twin_loss_head(const float* z, const float* log_std, const float* act, const float* old_logp, const float* adv,
                        const float* ret, const float* adv_stats, const int* stats_row, int n, int A, float clip_eps,
                        float ent_coef, float log_std_lo, float log_std_hi, const float* bias, float* scratch,

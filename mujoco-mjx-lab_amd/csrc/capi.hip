@@ -15,6 +15,7 @@
 #include "ppo_kernels.hip"
 #include "apg_kernels.hip"
 #include "ppo_loss_kernels.hip"
+#include "twin_kernels.hip"
 
 using namespace mjl;
 
@@ -1365,6 +1366,44 @@ extern "C" int mjl_twin_loss_head(const float* z, const float* log_std, const fl
   hipLaunchKernelGGL(twin_loss_head_kernel<kSurrRows>, dim3(nb), dim3(2 * kSurrRows), 0, s, z, log_std, act, old_logp, adv,
                      ret, n, A, clip_eps, ent_coef, scratch, nb_adv, adv_stats, stats_row, log_std_lo, log_std_hi, bias,
                      dz, lossp, glsp, biasp);
+  HIPCHK(hipGetLastError());
+  return MJL_OK;
+}
+
+// The twin update's fused thin ends (twin_kernels.hip). Shapes: bit 0 set when the gather + input
+// layer launch has an instantiation for (k0, N), bit 1 when the output backward has one for (A, N).
+extern "C" int mjl_twin_fused_shapes(int k0, int A, int N) {
+  return (k0 == kTinK0 && N == kTinN ? 1 : 0) | (A == kHbA && N > 0 && N % kHbCols == 0 ? 2 : 0);
+}
+
+extern "C" int mjl_twin_gather_in(const long long* idx, const int* idx_row, int n, long long nsrc, int k0, int A,
+                                  int N, const float* obs, const float* act, const float* logp, const float* ret,
+                                  const float* adv, float* o2, float* a, float* ol, float* r, float* ad,
+                                  const float* W, const float* b, float* h, void* stream) {
+  if (!idx || !obs || !act || !logp || !ret || !adv || !o2 || !a || !ol || !r || !ad || !W || !b || !h || n <= 0 ||
+      nsrc < 0 || A <= 0)
+    return fail(MJL_ERR_ARG, "bad argument");
+  if (!(mjl_twin_fused_shapes(k0, A, N) & 1))
+    return fail(MJL_ERR_UNSUPPORTED, "twin_gather_in: input width %d / hidden width %d not instantiated", k0, N);
+  if ((uintptr_t)h % 8) return fail(MJL_ERR_ARG, "twin_gather_in: 8-byte aligned output expected");
+  TwinInArgs p{idx, idx_row, n, A, nsrc, obs, act, logp, ret, adv, o2, a, ol, r, ad, W, b, h};
+  hipLaunchKernelGGL((twin_gather_in_kernel<kTinK0, kTinN>), dim3((unsigned)((n + kTinRows - 1) / kTinRows)),
+                     dim3(kTinN), 0, (hipStream_t)stream, p);
+  HIPCHK(hipGetLastError());
+  return MJL_OK;
+}
+
+extern "C" int mjl_twin_head_bwd(const float* dz, const float* W, const float* y, int n, int A, int N, float* dzh,
+                                 float* cs, float* gw, void* stream) {
+  if (!dz || !W || !y || !dzh || !cs || !gw || n <= 0 || A <= 0 || N <= 0) return fail(MJL_ERR_ARG, "bad argument");
+  if (!(mjl_twin_fused_shapes(0, A, N) & 2))
+    return fail(MJL_ERR_UNSUPPORTED, "twin_head_bwd: %d outputs / hidden width %d not instantiated", A, N);
+  if (n % kHbRows) return fail(MJL_ERR_ARG, "twin_head_bwd: rows must be a multiple of %d", kHbRows);
+  if (((uintptr_t)W | (uintptr_t)y | (uintptr_t)dzh | (uintptr_t)cs | (uintptr_t)gw) % 16)
+    return fail(MJL_ERR_ARG, "twin_head_bwd: 16-byte aligned buffers expected");
+  TwinHeadBwdArgs p{dz, W, y, dzh, cs, gw, n, N};
+  hipLaunchKernelGGL(twin_head_bwd_kernel<kHbA>, dim3((unsigned)(n / kHbRows), (unsigned)(N / kHbCols), 2), dim3(256),
+                     0, (hipStream_t)stream, p);
   HIPCHK(hipGetLastError());
   return MJL_OK;
 }

@@ -747,6 +747,11 @@ DP_BUCKETS = os.environ.get("MJL_DP_BUCKETS", "auto")
 # per minibatch step (MJL_DP_CAPTURE=0: eager collectives between the graphs). One-rank RCCL, C5's
 # per-rank update (128 steps of 8,192 rows): 33.1 ms eager -> 30.0 ms captured (profiles/r5/)
 DP_CAPTURE = os.environ.get("MJL_DP_CAPTURE", "1") != "0"
+# the twin update's minibatch steps captured as ONE graph per update (single process, and
+# data-parallel with the collectives captured): one replay per update instead of one per minibatch
+# step — a graph boundary idled the GPU ~8.7 us per replay (rocprofv3, C5's 8,192-row steps);
+# MJL_WHOLE_UPDATE_GRAPH=0: one graph per minibatch step, replayed per step
+WHOLE_UPDATE_GRAPH = os.environ.get("MJL_WHOLE_UPDATE_GRAPH", "1") != "0"
 _SIDE_STREAMS = {}
 
 
@@ -848,6 +853,7 @@ class PPOUpdater:
         self.dp_buckets = 0
         self.captured_last_run = False
         self.capture_fallback_reason: Optional[str] = None
+        self._gstep_n = 0
 
     def _twin_ok(self, rows: int, act_dim: int) -> bool:
         return (self.twin is not None and rows >= UPDATE_MIN_ROWS and rows % SPLIT_ROWS == 0 and rows % 128 == 0
@@ -870,7 +876,7 @@ class PPOUpdater:
         graphs), idx and st are the whole update's [n_minibatches, ...] tables, read at row *row, which
         the Adam launch advances: the replays need no per-minibatch host copies."""
         cfg, opt_p, opt_v = self.cfg, self.opt_p, self.opt_v
-        o, a, ol, r, ad = _gather_minibatch(idx, *src, row=row, twice_first=self._tw and row is not None)
+        o, a, ol, r, ad, h1 = self._gather(idx, src, row)
         dp = self.dist is not None
         if self._tw:
             tw = self.twin
@@ -878,7 +884,7 @@ class PPOUpdater:
             # and the row, Adam takes them as they are
             ctrs = (opt_p.step_t, opt_v.step_t, row) if row is not None else None
             tw.forward_backward(o, a, ol, r, ad, st, cfg.clip_eps, cfg.ent_coef, min(64, o.shape[-2] // SPLIT_ROWS),
-                                stats_row=row, counters=ctrs)
+                                stats_row=row, counters=ctrs, h1=h1)
             if not dp:  # both nets' Adam steps in one launch
                 adam_steps([(opt_p, tw.grads_p), (opt_v, tw.grads_v)], advanced=ctrs is not None)
             return
@@ -909,6 +915,13 @@ class PPOUpdater:
             opt_p.step()
             opt_v.step()
 
+    def _gather(self, idx, src, row=None):
+        """The minibatch's rows (+ h1, the first hidden layer of both nets, when the twin path's fused
+        gather + input layer launch applies — eager and captured alike, so replays equal eager runs)."""
+        if self._tw and self.twin.fused_input_ok(src):
+            return self.twin.gather_input(idx, src, row)
+        return _gather_minibatch(idx, *src, row=row, twice_first=self._tw and row is not None) + (None,)
+
     def _bucketed(self) -> bool:
         """Data-parallel twin runs all-reduce the gradient in two buckets, the first overlapping the
         lower layers' backward (DP_BUCKETS; needs a hidden-hidden layer below the top two)."""
@@ -921,14 +934,15 @@ class PPOUpdater:
         head and the top two layers' backward, after which bucket 1 of the gradient is final (yield);
         then the layers below, finishing bucket 2 (and advancing the captured counters)."""
         cfg, opt_p, opt_v = self.cfg, self.opt_p, self.opt_v
-        o, a, ol, r, ad = _gather_minibatch(idx, *src, row=row, twice_first=row is not None)
+        o, a, ol, r, ad, h1 = self._gather(idx, src, row)
         ctrs = (opt_p.step_t, opt_v.step_t, row) if row is not None else None
         gen = self.twin.forward_backward_phases(o, a, ol, r, ad, st, cfg.clip_eps, cfg.ent_coef,
-                                                min(64, o.shape[-2] // SPLIT_ROWS), stats_row=row, counters=ctrs)
+                                                min(64, o.shape[-2] // SPLIT_ROWS), stats_row=row, counters=ctrs,
+                                                h1=h1)
         next(gen)
         yield
         next(gen)
-        self._keep_phase = (o, a, ol, r, ad, gen)
+        self._keep_phase = (o, a, ol, r, ad, h1, gen)
 
     def _allreduce_buckets(self, run_phase2, events):
         """Bucket 1's all-reduce in flight while run_phase2() enqueues the lower layers' backward, then
@@ -1064,14 +1078,19 @@ class PPOUpdater:
         self._row.zero_()
         st = self._st_all if stats is not None else None
         bucketed = self._bucketed()
-        if self._capture_collectives() and self.capture_fallback_reason is None:
-            if self._gstep is None:
-                self._capture_step(st, bucketed)
+        whole = self.dist is None or self._capture_collectives()
+        if whole and self.capture_fallback_reason is None:
+            k = nmb if WHOLE_UPDATE_GRAPH else 1  # minibatch steps per captured graph
+            if nmb % k:
+                k = 1
+            if self._gstep is None or self._gstep_n != k:
+                self._capture_steps(st, bucketed, k)
             if self.capture_fallback_reason is None:
-                for _ in range(nmb):  # replay errors propagate (no eager re-run of applied steps)
+                for _ in range(nmb // k):  # replay errors propagate (no eager re-run of applied steps)
                     self._gstep.replay()
-                self.collectives_last_run = nmb * self.dp_buckets
-                self.captured_last_run = True
+                if self.dist is not None:
+                    self.collectives_last_run = nmb * self.dp_buckets
+                    self.captured_last_run = True
                 return
         for _ in range(nmb):
             if self._ga is None:
@@ -1107,35 +1126,54 @@ class PPOUpdater:
         synchronisation between the backward, the collective and the Adam step."""
         if not (DP_CAPTURE and self.dist is not None and self._tw):
             return False
-        try:
-            return self.dist.get_backend() == "nccl"
-        except Exception:  # a stand-in without backends (bench's identity collective)
+        try:  # RCCL, or bench's one-rank identity stand-in (the same captured structure, no link)
+            return self.dist.get_backend() in ("nccl", "identity")
+        except Exception:  # a stand-in without backends
             return False
 
-    def _capture_step(self, st, bucketed):
-        """Capture the minibatch step with its collective(s) inside. Only the capture is guarded: a
+    def _step_body(self, st, bucketed):
+        """One minibatch step as captured: single process, graph A's body (both Adam steps inside);
+        data-parallel, the body with its collective(s) and the Adam launch."""
+        if self.dist is None:
+            self._body_a(self._idx_all, self._src, st, row=self._row)
+            return
+        if bucketed:
+            gen = self._body_a_phases(self._idx_all, self._src, st, row=self._row)
+            next(gen)
+            b1, b2 = self.twin.buckets()
+            w1 = self.dist.all_reduce(b1, async_op=True)
+            next(gen, None)
+            w2 = self.dist.all_reduce(b2, async_op=True)
+            for w in (w1, w2):
+                if w is not None:
+                    w.wait()
+            self._gen_keep = gen
+        else:
+            self._body_a(self._idx_all, self._src, st, row=self._row)
+            self.dist.all_reduce(self._grad_buffer())
+        self._body_b(row=self._row)
+
+    def _capture_steps(self, st, bucketed, k):
+        """Capture k consecutive minibatch steps as ONE graph (WHOLE_UPDATE_GRAPH: k = the update's
+        minibatch count, so an update is one replay; the steps read the device row counter, so they
+        differ only in the row they gather). Data-parallel, only the capture is guarded: a
         capture refused on any rank (this RCCL build, a collective the capture does not take) sends
         EVERY rank to the eager collectives — the ranks agree through one eager all-reduce of a
         failure flag, so no rank replays captured collectives that another rank issues eagerly.
         Nothing captured has run: the replays come only after the agreement."""
-        reason = None
+        self._gstep = None
         g = torch.cuda.CUDAGraph()
+        if self.dist is None:
+            with graph_capture(g):
+                for _ in range(k):
+                    self._step_body(st, bucketed)
+            self._gstep, self._gstep_n = g, k
+            return
+        reason = None
         try:
             with graph_capture(g):
-                if bucketed:
-                    gen = self._body_a_phases(self._idx_all, self._src, st, row=self._row)
-                    next(gen)
-                    b1, b2 = self.twin.buckets()
-                    w1 = self.dist.all_reduce(b1, async_op=True)
-                    next(gen, None)
-                    w2 = self.dist.all_reduce(b2, async_op=True)
-                    w1.wait()
-                    w2.wait()
-                    self._gen_keep = gen
-                else:
-                    self._body_a(self._idx_all, self._src, st, row=self._row)
-                    self.dist.all_reduce(self._grad_buffer())
-                self._body_b(row=self._row)
+                for _ in range(k):
+                    self._step_body(st, bucketed)
         except RuntimeError as e:
             reason = f"{type(e).__name__}: {e}"[:300]
             g = None
@@ -1151,7 +1189,7 @@ class PPOUpdater:
             self._gstep = None
             self._ga = self._gb = None
         else:
-            self._gstep = g
+            self._gstep, self._gstep_n = g, k
 
 
 def ppo_update(policy, value, opt_p, opt_v, obs, acts, logp, ret, adv, index_batches, cfg, dist=None, world=1,

@@ -47,6 +47,11 @@ HIDDEN_SPLITS = None
 THIN_SPLITS = None
 # rows per column-sum partial (the bias gradients' first stage); 32 and 64 measured no faster
 COLSUM_CHUNK = int(os.environ.get("MJL_TWIN_COLSUM_CHUNK", "128"))
+# the thin ends as single native launches where instantiated (csrc/twin_kernels.hip): the gather fused
+# with both input layers (mjl_twin_gather_in), the output layers' backward fused with the last hidden
+# layer's tanh backward (mjl_twin_head_bwd). MJL_TWIN_FUSED_ENDS=0: the library GEMM path for both
+FUSED_ENDS = os.environ.get("MJL_TWIN_FUSED_ENDS", "1") != "0"
+HEAD_BWD_ROWS = 128  # the fused output backward's row chunk (kHbRows)
 
 
 # launch caps of the twin step's fused launches (csrc/ppo_loss_kernels.hip): mjl_adam_multi takes at most
@@ -128,6 +133,40 @@ class TwinNets:
         self.grads_p: List[torch.Tensor] = [gview[id(p)] for p in policy.parameters()]
         self.grads_v: List[torch.Tensor] = [gview[id(p)] for p in value.parameters()]
         self._scr = {}
+        self.N0 = shapes[0][0]            # the first hidden width
+        self.NH = shapes[-1][1]           # the last hidden width (the output layers' input)
+        self._fused = int(lib().mjl_twin_fused_shapes(self.K0, self.A, self.N0)) & 1
+        self._fused |= int(lib().mjl_twin_fused_shapes(self.K0, self.A, self.NH)) & 2
+
+    def fused_input_ok(self, src) -> bool:
+        """The gather + input layer launch applies: instantiated shape, the rollout arrays as the
+        update passes them (f32, contiguous, the policy's widths)."""
+        obs, acts = src[0], src[1]
+        return (FUSED_ENDS and bool(self._fused & 1) and all(x.is_cuda and x.dtype == torch.float32 and x.is_contiguous()
+                                                            for x in src)
+                and obs.dim() == 2 and obs.shape[1] == self.K0 and acts.dim() == 2 and acts.shape[1] == self.A)
+
+    def gather_input(self, idx, src, row: Optional[torch.Tensor] = None):
+        """make_index_batches' rows of the rollout arrays (train_ppo.py:222-231) and both nets' first
+        hidden layer in ONE launch (mjl_twin_gather_in): (o2 [2, M, K0] — the observations once per
+        net —, acts [M, A], old_logp, ret, adv [M], h1 [2, M, N0] = tanh(o W0^T + b0)). With `row`
+        (device int32) idx is the update's [n_minibatches, M] table, read at row *row when the launch
+        runs (a captured minibatch step)."""
+        obs, acts, logp, ret, adv = src
+        idx = idx.contiguous()
+        M = idx.shape[-1]
+        dev = obs.device
+        o2 = torch.empty((2, M, self.K0), device=dev)
+        a = torch.empty((M, self.A), device=dev)
+        ol, r, ad = (torch.empty(M, device=dev) for _ in range(3))
+        h1 = torch.empty((2, M, self.N0), device=dev)
+        nsrc = min(int(x.shape[0]) for x in src)
+        check(lib().mjl_twin_gather_in(idx.data_ptr(), None if row is None else row.data_ptr(), M, nsrc, self.K0,
+                                       self.A, self.N0, obs.data_ptr(), acts.data_ptr(), logp.data_ptr(),
+                                       ret.data_ptr(), adv.data_ptr(), o2.data_ptr(), a.data_ptr(), ol.data_ptr(),
+                                       r.data_ptr(), ad.data_ptr(), self.W[0].data_ptr(), self.b[0].data_ptr(),
+                                       h1.data_ptr(), torch.cuda.current_stream(dev).cuda_stream))
+        return o2, a, ol, r, ad, h1
 
     def owns_storage(self) -> bool:
         """Whether every parameter of both modules still is its view of the stacked storage (a
@@ -160,7 +199,7 @@ class TwinNets:
         return self.grad[o:], self.grad[:o]
 
     def forward_backward(self, o, acts, old_logp, ret, adv, adv_stats, clip_eps: float, ent_coef: float, splits: int,
-                         want_value_loss: bool = False, stats_row=None, counters=None):
+                         want_value_loss: bool = False, stats_row=None, counters=None, h1=None):
         """Both nets' losses and gradients for one minibatch (o [M, K0] — or [2, M, K0], the same rows
         twice, as the update's gather writes them —, acts [M, A], old_logp / ret / adv [M]); the
         gradients into self.grad. Returns (policy loss, value loss) device scalars (the value loss only
@@ -169,18 +208,19 @@ class TwinNets:
         device counters that the final reduction launch advances (the captured update; Adam then runs
         with advanced=True)."""
         for out in self.forward_backward_phases(o, acts, old_logp, ret, adv, adv_stats, clip_eps, ent_coef, splits,
-                                                want_value_loss, stats_row, counters, split=False):
+                                                want_value_loss, stats_row, counters, split=False, h1=h1):
             pass
         return out
 
     def forward_backward_phases(self, o, acts, old_logp, ret, adv, adv_stats, clip_eps: float, ent_coef: float,
                                 splits: int, want_value_loss: bool = False, stats_row=None, counters=None,
-                                split: bool = True):
+                                split: bool = True, h1=None):
         """forward_backward as a generator. split: it yields None once bucket 1 of buckets() is final
         (the top two layers' weight-gradient slices and column-sum partials, the loss head's partials,
         summed in one launch), so the caller can start that bucket's all-reduce while the lower layers'
         backward runs (the data-parallel update's overlap); its last item is (policy loss, value
-        loss) once bucket 2 -- and, with counters, the captured update's counters -- are final."""
+        loss) once bucket 2 -- and, with counters, the captured update's counters -- are final.
+        h1: the first hidden layer's outputs from gather_input (o then is its [2, M, K0] copy)."""
         L = lib()
         dev = o.device
         st = torch.cuda.current_stream(dev).cuda_stream
@@ -190,10 +230,10 @@ class TwinNets:
         # Both nets read the same observations: a batch-stride-0 view, or the gathered copy per net
         # (which the first layer's weight-gradient slices can then read without an expand copy)
         x = o if o.dim() == 3 else o.unsqueeze(0).expand(2, M, self.K0)
-        hs = [x]
+        hs = [x] if h1 is None else [x, h1]
         # (the output layer's bias and tanh go into the loss launch unless the value loss is wanted)
         fold = FOLD_HEAD and not want_value_loss
-        for l in range(nl):
+        for l in range(len(hs) - 1, nl):
             h = torch.bmm(hs[-1], self.W[l].transpose(1, 2))
             mask = 3 if l < nl - 1 else 1  # the output layer: tanh for the policy's mean, linear value
             if l < nl - 1 or not fold:
@@ -233,13 +273,28 @@ class TwinNets:
         ch = ch if M % ch == 0 else M
         R = M // ch  # column-sum partial rows per matrix
         g = dz
+        # the output layers' backward and the last hidden layer's tanh backward as one launch
+        head_fused = FUSED_ENDS and bool(self._fused & 2) and nl >= 2 and M % HEAD_BWD_ROWS == 0
         for l in range(nl - 1, -1, -1):
             N, K = self.W[l].shape[1], self.W[l].shape[2]
             xin = hs[l]  # the layer's input: H_{l-1}, or the observations for l = 0
+            if head_fused and l == nl - 1:  # dZ_{l-1}, its column-sum partials, this layer's dW partials
+                R2 = M // HEAD_BWD_ROWS
+                dzh = torch.empty((2, M, K), device=dev)
+                csh = self._scratch("hb_cs", 2 * R2 * K)
+                gwh = self._scratch("hb_gw", 2 * R2 * N * K)
+                check(L.mjl_twin_head_bwd(g.data_ptr(), self.W[l].data_ptr(), xin.data_ptr(), M, N, K, dzh.data_ptr(),
+                                          csh.data_ptr(), gwh.data_ptr(), st))
+                segs.append((gwh, self.gW[l], 2, R2, N * K))
+                segs.append((csh, self.gb[l - 1], 2, R2, K))
+                g = dzh
+                continue
             # split-K slices of the weight gradient: the thin layers (the 21 / 1-unit outputs, the 54-wide
             # input) are a few output tiles per slice, so they take more, shorter slices
             s = (HIDDEN_SPLITS or splits) if (N >= 64 and K >= 64) else max(splits, THIN_SPLITS or min(64, M // 256))
-            if l < nl - 1:  # tanh layer: dZ = dH (1 - H^2) and the bias gradient's partials in one pass
+            if head_fused and l == nl - 2:  # (its dZ and bias partials came from the fused launch)
+                dzl = g
+            elif l < nl - 1:  # tanh layer: dZ = dH (1 - H^2) and the bias gradient's partials in one pass
                 dzl = torch.empty_like(g)
                 cs = self._scratch(f"cs{l}", 2 * R * N)
                 check(L.mjl_tanh_bwd_colsum_partials(g.data_ptr(), hs[l + 1].data_ptr(), 2, M, N, ch, dzl.data_ptr(),

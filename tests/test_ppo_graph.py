@@ -61,11 +61,14 @@ def _run_pair(cfg, n, dist=None):
         ub.run(*B[4], idx)
         torch.cuda.synchronize()
         _compare(_state(*A[:4]), _state(*B[:4]), run)
-    assert ua._ga is not None  # the graphs were captured and replayed
+    assert ua._ga is not None or ua._gstep is not None  # the graphs were captured and replayed
     assert float(A[2].step_t) == 4 * idx.shape[0]
 
 
-def test_update_graph_replay_bit_identical_to_eager():
+@pytest.mark.parametrize("whole", [True, False])
+def test_update_graph_replay_bit_identical_to_eager(monkeypatch, whole):
+    """One graph per update (ppo.WHOLE_UPDATE_GRAPH) and one per minibatch step, both against eager."""
+    monkeypatch.setattr(ppo, "WHOLE_UPDATE_GRAPH", whole)
     cfg = reference_ppo_config()
     cfg.epochs = 2
     _run_pair(cfg, 2 * cfg.minibatch_size)  # 2 epochs x 2 minibatches of 65,536 rows
@@ -108,12 +111,14 @@ def test_data_parallel_bucketed_update_graph_bit_identical_to_eager(monkeypatch)
         tdist.destroy_process_group()
 
 
-@pytest.mark.parametrize("buckets", ["0", "1"])
-def test_rccl_captured_step_graph_bit_identical_to_eager(monkeypatch, buckets):
+@pytest.mark.parametrize("buckets,whole", [("0", True), ("1", True), ("0", False), ("1", False)])
+def test_rccl_captured_step_graph_bit_identical_to_eager(monkeypatch, buckets, whole):
     """Over RCCL the data-parallel minibatch step is ONE graph with its all-reduce(s) captured inside
-    (ppo.DP_CAPTURE): the replays equal the eager update (collectives between eager bodies) bit for bit,
-    one rank on cuda:0, one bucket and two."""
+    (ppo.DP_CAPTURE) — and, with ppo.WHOLE_UPDATE_GRAPH, every minibatch step of the update in one
+    graph: the replays equal the eager update (collectives between eager bodies) bit for bit, one rank
+    on cuda:0, one bucket and two."""
     monkeypatch.setattr(ppo, "DP_BUCKETS", buckets)
+    monkeypatch.setattr(ppo, "WHOLE_UPDATE_GRAPH", whole)
     _one_rank_group("nccl")
     try:
         cfg = reference_ppo_config()
@@ -130,6 +135,7 @@ def test_rccl_captured_step_graph_bit_identical_to_eager(monkeypatch, buckets):
             torch.cuda.synchronize()
             _compare(_state(*A[:4]), _state(*B[:4]), run)
         assert ua._gstep is not None and ua.collectives_last_run == idx.shape[0] * (2 if buckets == "1" else 1)
+        assert ua._gstep_n == (idx.shape[0] if whole else 1)
     finally:
         tdist.destroy_process_group()
 

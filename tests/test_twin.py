@@ -31,11 +31,15 @@ def _data(n, seed=1):
             torch.randn(n, generator=gd, device="cuda"), torch.randn(n, generator=gd, device="cuda"))
 
 
+@pytest.mark.parametrize("fused", [True, False])
 @pytest.mark.parametrize("dup", [False, True])
 @pytest.mark.parametrize("n", [8192, 65536])
-def test_twin_gradients_match_float64_autograd(n, dup):
+def test_twin_gradients_match_float64_autograd(monkeypatch, n, dup, fused):
     """dup: the observations handed over as the [2, M, K0] block the graphed update's gather writes
-    (one copy per net) instead of one [M, K0] matrix read through a batch-stride-0 view."""
+    (one copy per net) instead of one [M, K0] matrix read through a batch-stride-0 view. fused: the
+    output layers' backward + the last tanh backward as one launch (mjl_twin_head_bwd), or the library
+    GEMM path (twin.FUSED_ENDS off)."""
+    monkeypatch.setattr(twin, "FUSED_ENDS", fused)
     cfg = reference_ppo_config()
     pol, val = _nets(cfg)
     ref_p = ppo.GaussianPolicy(54, 21, cfg.policy_hidden_layer_specs).cuda().double()
@@ -74,6 +78,56 @@ def test_twin_gradients_match_float64_autograd(n, dup):
     # the modules' parameters are views of the stacked storage, the value's padded output rows stay 0
     assert tw.owns_storage()
     assert float(tw.W[-1][1, 1:].abs().max()) == 0.0 and float(tw.gW[-1][1, 1:].abs().max()) == 0.0
+
+
+@pytest.mark.parametrize("n", [8192, 1000])
+def test_fused_gather_input_layer_matches_float64(n):
+    """mjl_twin_gather_in: the minibatch rows (a permutation with one out-of-range index, which gathers
+    NaN as mjl_gather_rows does) and both nets' first hidden layer tanh(o W0^T + b0) against float64;
+    n = 1000 leaves a ragged last block of 8 rows."""
+    cfg = reference_ppo_config()
+    pol, val = _nets(cfg)
+    tw = twin.TwinNets(pol, val)
+    src = _data(4096)
+    assert tw.fused_input_ok(src)
+    g = torch.Generator(device="cuda").manual_seed(5)
+    idx = torch.randint(0, 4096, (n,), generator=g, device="cuda")
+    idx[7] = 4096  # out of range
+    o2, a, ol, r, ad, h1 = tw.gather_input(idx, src)
+    torch.cuda.synchronize()
+    ok = idx < 4096
+    for got, x in ((a, src[1]), (ol, src[2]), (r, src[3]), (ad, src[4])):
+        assert torch.equal(got[ok], x[idx[ok]]) and bool(torch.isnan(got[~ok]).all())
+    for k in range(2):
+        assert torch.equal(o2[k][ok], src[0][idx[ok]]) and bool(torch.isnan(o2[k][~ok]).all())
+    x = src[0][idx[ok]].double()
+    for k, net in enumerate((pol, val)):
+        lin = net.mlp.layers[0]
+        want = torch.tanh(x @ lin.weight.double().T + lin.bias.double())
+        err = float((h1[k][ok].double() - want).abs().max())
+        assert err <= 2e-6, f"net {k}: max error {err:.3e}"
+
+
+def test_fused_ends_update_matches_library_path(monkeypatch):
+    """The whole twin forward + backward with the fused thin ends (gather + input layer, output backward
+    + last tanh backward) against the same minibatch through the library GEMM path: every gradient of
+    both nets to 1e-5 of its scale."""
+    cfg = reference_ppo_config()
+    pol, val = _nets(cfg)
+    tw = twin.TwinNets(pol, val)
+    src = _data(16384)
+    idx = torch.randperm(16384, generator=torch.Generator(device="cuda").manual_seed(3), device="cuda")[:8192]
+    splits = 8192 // ppo.SPLIT_ROWS
+    o2, a, ol, r, ad, h1 = tw.gather_input(idx, src)
+    tw.forward_backward(o2, a, ol, r, ad, None, cfg.clip_eps, cfg.ent_coef, splits, h1=h1)
+    got = [g.clone() for g in tw.grads_p + tw.grads_v]
+    monkeypatch.setattr(twin, "FUSED_ENDS", False)
+    o, a, ol, r, ad = (x[idx] for x in src)
+    tw.forward_backward(o, a, ol, r, ad, None, cfg.clip_eps, cfg.ent_coef, splits)
+    torch.cuda.synchronize()
+    for g1, g0 in zip(got, tw.grads_p + tw.grads_v):
+        scale = float(g0.abs().max()) + 1e-12
+        assert float((g1 - g0).abs().max()) <= 1e-5 * scale
 
 
 def test_twin_update_matches_per_net_update():
