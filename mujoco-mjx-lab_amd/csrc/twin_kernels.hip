@@ -41,94 +41,124 @@ struct TwinInArgs {
   float* h;                                    // out: [2, n, N] = tanh(o W^T + b) per net
 };
 
-// block: kTinRows rows; thread t: net t / (N/2), output columns 2 (t mod N/2) and +1 of that net.
-// Both nets' weights staged transposed in LDS (ws[k][net N + c]: a thread's two columns are one 8-byte
-// read per k), the gathered observations transposed too (xs[k][row]: 4 rows per 16-byte broadcast
-// read); two rows per packed FMA, 32 rows x 2 columns of accumulators per thread. (Weights held in
-// registers instead spilled: the unrolled k loop's hoisted LDS reads took every VGPR.)
+// block: kTinRows rows, N threads = N / 64 waves. Wave w takes rows 8w .. 8w + 7 (their observations
+// are wave-uniform: 16-byte LDS broadcasts), lane l the 8 columns l + 64 c of the two nets' 2N outputs
+// (c < N / 64: the policy's, the rest the value's), so a k step reads 8 conflict-free words of the
+// transposed weights and 2 broadcasts, for 32 packed FMAs — LDS and VALU time balanced (one lane per
+// column pair and 32 rows was LDS-bound). Every global load of the gather and of the weight staging
+// is issued before the first wait (one wave per SIMD: nothing else hides their latency).
 template <int K0, int N>
 __global__ __launch_bounds__(N) void twin_gather_in_kernel(TwinInArgs p) {
-  constexpr int XS = kTinRows + 4;  // padded row stride (16-byte aligned: 144 B)
-  constexpr int TH = N / 2;
-  static_assert(K0 % 2 == 0, "pairs of weights per load");
-  __shared__ __attribute__((aligned(16))) float ws[K0 * 2 * N];
+  constexpr int XS = kTinRows + 4;  // xs row stride (16-byte aligned: 144 B)
+  constexpr int WS = 2 * N + 1;     // ws row stride (odd: the transposing writes spread over banks)
+  constexpr int NC = 2 * N / 64;    // columns per lane
+  constexpr int RPW = 8;            // rows per wave
+  static_assert(K0 % 2 == 0 && N % 64 == 0 && (N / 64) * RPW == kTinRows, "tile shape");
+  constexpr int WF2 = K0;           // float2 of the [2N, K0] weights per thread: 2N K0 / 2 / N
+  constexpr int OBS_IT = (kTinRows * K0 + N - 1) / N;
+  constexpr int ACT_IT = (kTinRows * 32 + N - 1) / N;  // A <= 32
+  __shared__ float ws[K0 * WS];
   __shared__ __attribute__((aligned(16))) float xs[K0 * XS];
   __shared__ long long sidx[kTinRows];
-  const int t = threadIdx.x, n = p.n, r0 = blockIdx.x * kTinRows;
+  const int t = threadIdx.x, n = p.n, r0 = blockIdx.x * kTinRows, A = p.A;
   const int rows = min(kTinRows, n - r0);
   const long long* idx = p.idx + (p.idx_row ? (size_t)*p.idx_row * n : 0);
-  if (t < kTinRows) sidx[t] = t < rows ? idx[r0 + t] : -1;
-  const int net = t / TH, c0 = 2 * (t - net * TH), wc = net * N + c0;
-  {
-    const float* wr = p.W + (size_t)wc * K0;  // rows wc and wc + 1 of W viewed as [2 N, K0]
-#pragma unroll 9
-    for (int k = 0; k < K0; k += 2) {
-      const float2 u = *reinterpret_cast<const float2*>(wr + k), v = *reinterpret_cast<const float2*>(wr + K0 + k);
-      *reinterpret_cast<float2*>(&ws[k * 2 * N + wc]) = make_float2(u.x, v.x);
-      *reinterpret_cast<float2*>(&ws[(k + 1) * 2 * N + wc]) = make_float2(u.y, v.y);
-    }
-  }
+  long long my_idx = -1;
+  if (t < rows) my_idx = idx[r0 + t];
+  float2 wv[WF2];  // the weights, coalesced: float2 f = t + i N of W viewed as [2N, K0]
+  const float2* W2 = reinterpret_cast<const float2*>(p.W);
+#pragma unroll
+  for (int i = 0; i < WF2; i++) wv[i] = W2[t + i * N];
+  if (t < kTinRows) sidx[t] = my_idx;
   __syncthreads();
   const long long nsrc = p.nsrc;
   const float nan = __builtin_nanf("");
-  for (int e = t; e < kTinRows * K0; e += N) {  // observations: coalesced row reads and writes
-    const int r = e / K0, k = e - r * K0;
-    const long long s = sidx[r];
-    const float v = (s >= 0 && s < nsrc) ? p.obs[(size_t)s * K0 + k] : nan;
-    xs[k * XS + r] = v;
-    if (r < rows) {
-      p.o2[(size_t)(r0 + r) * K0 + k] = v;
-      p.o2[((size_t)n + r0 + r) * K0 + k] = v;
+  float ov[OBS_IT], av[ACT_IT];
+#pragma unroll
+  for (int i = 0; i < OBS_IT; i++) {
+    const int e = t + i * N, r = e / K0, k = e - r * K0;
+    const long long s = e < kTinRows * K0 ? sidx[r] : -1;
+    ov[i] = (s >= 0 && s < nsrc) ? p.obs[(size_t)s * K0 + k] : nan;
+  }
+#pragma unroll
+  for (int i = 0; i < ACT_IT; i++) {
+    const int e = t + i * N, r = e / A, k = e - r * A;
+    const long long s = e < rows * A ? sidx[r] : -1;
+    av[i] = (s >= 0 && s < nsrc) ? p.act[(size_t)s * A + k] : nan;
+  }
+  float olv = nan, rv = nan, adv = nan;
+  const bool own = t < rows && my_idx >= 0 && my_idx < nsrc;
+  if (own) {
+    olv = p.logp[my_idx];
+    rv = p.ret[my_idx];
+    adv = p.adv[my_idx];
+  }
+#pragma unroll
+  for (int i = 0; i < WF2; i++) {
+    const int f = t + i * N, row = f / (K0 / 2), k = 2 * (f - row * (K0 / 2));
+    ws[k * WS + row] = wv[i].x;
+    ws[(k + 1) * WS + row] = wv[i].y;
+  }
+#pragma unroll
+  for (int i = 0; i < OBS_IT; i++) {
+    const int e = t + i * N, r = e / K0, k = e - r * K0;
+    if (e < kTinRows * K0) {
+      xs[k * XS + r] = ov[i];
+      if (r < rows) {
+        p.o2[(size_t)(r0 + r) * K0 + k] = ov[i];
+        p.o2[((size_t)n + r0 + r) * K0 + k] = ov[i];
+      }
     }
   }
-  const int A = p.A;
-  for (int e = t; e < rows * A; e += N) {
-    const int r = e / A, k = e - r * A;
-    const long long s = sidx[r];
-    p.a[(size_t)(r0 + r) * A + k] = (s >= 0 && s < nsrc) ? p.act[(size_t)s * A + k] : nan;
+#pragma unroll
+  for (int i = 0; i < ACT_IT; i++) {
+    const int e = t + i * N;
+    if (e < rows * A) p.a[(size_t)r0 * A + e] = av[i];
   }
   if (t < rows) {
-    const long long s = sidx[t];
-    const bool ok = s >= 0 && s < nsrc;
-    p.ol[r0 + t] = ok ? p.logp[s] : nan;
-    p.r[r0 + t] = ok ? p.ret[s] : nan;
-    p.ad[r0 + t] = ok ? p.adv[s] : nan;
+    p.ol[r0 + t] = olv;
+    p.r[r0 + t] = rv;
+    p.ad[r0 + t] = adv;
   }
   __syncthreads();
-  tw_f2 acc0[kTinRows / 2], acc1[kTinRows / 2];
+  const int lane = t & 63, rg = t >> 6;
+  tw_f2 acc[NC][RPW / 2];
 #pragma unroll
-  for (int i = 0; i < kTinRows / 2; i++) acc0[i] = acc1[i] = tw_f2{0.f, 0.f};
+  for (int c = 0; c < NC; c++)
+#pragma unroll
+    for (int i = 0; i < RPW / 2; i++) acc[c][i] = tw_f2{0.f, 0.f};
 #pragma unroll 2
   for (int k = 0; k < K0; k++) {
-    const float2 w = *reinterpret_cast<const float2*>(&ws[k * 2 * N + wc]);
+    const float4 x0 = *reinterpret_cast<const float4*>(&xs[k * XS + RPW * rg]);
+    const float4 x1 = *reinterpret_cast<const float4*>(&xs[k * XS + RPW * rg + 4]);
+    const tw_f2 xp[4] = {{x0.x, x0.y}, {x0.z, x0.w}, {x1.x, x1.y}, {x1.z, x1.w}};
 #pragma unroll
-    for (int q = 0; q < kTinRows / 4; q++) {
-      const float4 xv = *reinterpret_cast<const float4*>(&xs[k * XS + 4 * q]);
-      const tw_f2 lo{xv.x, xv.y}, hi{xv.z, xv.w};
-      acc0[2 * q] = tw_fma(lo, w.x, acc0[2 * q]);
-      acc0[2 * q + 1] = tw_fma(hi, w.x, acc0[2 * q + 1]);
-      acc1[2 * q] = tw_fma(lo, w.y, acc1[2 * q]);
-      acc1[2 * q + 1] = tw_fma(hi, w.y, acc1[2 * q + 1]);
+    for (int c = 0; c < NC; c++) {
+      const float w = ws[k * WS + lane + 64 * c];
+#pragma unroll
+      for (int i = 0; i < RPW / 2; i++) acc[c][i] = tw_fma(xp[i], w, acc[c][i]);
     }
   }
-  const float b0 = p.b[wc], b1 = p.b[wc + 1];
-  float* hr = p.h + ((size_t)net * n + r0) * N + c0;
 #pragma unroll
-  for (int i = 0; i < kTinRows / 2; i++) {
-    if (2 * i < rows)
-      *reinterpret_cast<float2*>(hr + (size_t)(2 * i) * N) = make_float2(tanhf(acc0[i].x + b0), tanhf(acc1[i].x + b1));
-    if (2 * i + 1 < rows)
-      *reinterpret_cast<float2*>(hr + (size_t)(2 * i + 1) * N) =
-          make_float2(tanhf(acc0[i].y + b0), tanhf(acc1[i].y + b1));
+  for (int c = 0; c < NC; c++) {
+    const int col = lane + 64 * c, net = col / N, cn = col - net * N;
+    const float b = p.b[col];
+    float* hr = p.h + ((size_t)net * n + r0 + RPW * rg) * N + cn;
+#pragma unroll
+    for (int i = 0; i < RPW / 2; i++) {
+      if (RPW * rg + 2 * i < rows) hr[(size_t)(2 * i) * N] = tanhf(acc[c][i].x + b);
+      if (RPW * rg + 2 * i + 1 < rows) hr[(size_t)(2 * i + 1) * N] = tanhf(acc[c][i].y + b);
+    }
   }
 }
 
 // ------------------------------------------------------------------ output layers' backward
-constexpr int kHbRows = 128;   // rows per block (= the weight-gradient / column-sum partial chunk)
-constexpr int kHbCols = 128;   // columns per block: 32 quads
-constexpr int kHbGroups = 8;   // row groups: thread t = quad t % 32, group t / 32
-constexpr int kHbA = 21;       // instantiated output width (the humanoid's 21 actions)
+constexpr int kHbRows = 128;     // rows per block (= the weight-gradient / column-sum partial chunk)
+constexpr int kHbCols = 64;      // columns per block: 16 quads
+constexpr int kHbGroups = 16;    // row groups: thread t = quad t % 16, group t / 16 (8 rows each)
+constexpr int kHbA = 21;         // instantiated output width (the humanoid's 21 actions)
 constexpr int kHbDzStride = 24;  // LDS row stride of the staged dz rows (16-byte aligned)
+constexpr int kHbPass = 7;       // output rows of the weight-gradient reduction per LDS pass
 
 struct TwinHeadBwdArgs {
   const float* dz;  // [2, n, A]: the output layers' dZ (mjl_twin_loss_head)
@@ -140,19 +170,24 @@ struct TwinHeadBwdArgs {
   int n, N;
 };
 
+// block: 128 rows x 64 columns of one net, 256 threads (quad q = 4 columns, 8 rows of group g);
+// every y row the thread reads is issued before the first FMA (two blocks per CU: 16 quad-rows in
+// flight per lane pair); the group partials reduce through LDS in a fixed order, the weight gradient's
+// in passes of kHbPass output rows.
 template <int A>
-__global__ __launch_bounds__(256) void twin_head_bwd_kernel(TwinHeadBwdArgs p) {
+__global__ __launch_bounds__(256, 2) void twin_head_bwd_kernel(TwinHeadBwdArgs p) {
+  constexpr int RPT = kHbRows / kHbGroups;  // rows per thread
+  static_assert(A % kHbPass == 0, "reduction passes");
   __shared__ __attribute__((aligned(16))) float sdz[kHbRows * kHbDzStride];
-  __shared__ float4 red[kHbGroups * A * 32];
-  const int t = threadIdx.x, q = t & 31, g = t >> 5;
+  __shared__ float4 red[kHbGroups * kHbPass * 16];
+  const int t = threadIdx.x, q = t & 15, g = t >> 4;
   const int chunk = blockIdx.x, net = blockIdx.z, n = p.n, N = p.N;
   const int col = blockIdx.y * kHbCols + 4 * q;
   const int r0 = chunk * kHbRows;
-  const float* dzb = p.dz + ((size_t)net * n + r0) * A;
-  for (int e = t; e < kHbRows * A; e += 256) {
-    const int r = e / A, a = e - r * A;
-    sdz[r * kHbDzStride + a] = dzb[e];
-  }
+  const float* yb = p.y + ((size_t)net * n + r0) * N + col;
+  float4 yv[RPT];
+#pragma unroll
+  for (int u = 0; u < RPT; u++) yv[u] = *reinterpret_cast<const float4*>(yb + (size_t)(g + u * kHbGroups) * N);
   tw_f2 wl[A], wh[A];  // this thread's 4 columns of W_out
 #pragma unroll
   for (int a = 0; a < A; a++) {
@@ -160,62 +195,65 @@ __global__ __launch_bounds__(256) void twin_head_bwd_kernel(TwinHeadBwdArgs p) {
     wl[a] = tw_f2{w.x, w.y};
     wh[a] = tw_f2{w.z, w.w};
   }
+  const float* dzb = p.dz + ((size_t)net * n + r0) * A;
+  for (int e = t; e < kHbRows * A; e += 256) {
+    const int r = e / A, a = e - r * A;
+    sdz[r * kHbDzStride + a] = dzb[e];
+  }
   __syncthreads();
   tw_f2 gl[A], gh[A];
 #pragma unroll
   for (int a = 0; a < A; a++) gl[a] = gh[a] = tw_f2{0.f, 0.f};
   tw_f2 csl{0.f, 0.f}, csh{0.f, 0.f};
-  const float* yb = p.y + ((size_t)net * n + r0) * N + col;
   float* zb = p.dzh + ((size_t)net * n + r0) * N + col;
-  constexpr int U = 4;  // rows in flight per trip
-  for (int r = g; r < kHbRows; r += U * kHbGroups) {
-    float4 yv[U];
 #pragma unroll
-    for (int u = 0; u < U; u++) yv[u] = *reinterpret_cast<const float4*>(yb + (size_t)(r + u * kHbGroups) * N);
+  for (int u = 0; u < RPT; u++) {
+    const int r = g + u * kHbGroups;
+    const float* d = &sdz[r * kHbDzStride];
+    const tw_f2 yl{yv[u].x, yv[u].y}, yh{yv[u].z, yv[u].w};
+    tw_f2 hl{0.f, 0.f}, hh{0.f, 0.f};
 #pragma unroll
-    for (int u = 0; u < U; u++) {
-      const float* d = &sdz[(r + u * kHbGroups) * kHbDzStride];
-      const tw_f2 yl{yv[u].x, yv[u].y}, yh{yv[u].z, yv[u].w};
-      tw_f2 hl{0.f, 0.f}, hh{0.f, 0.f};
-#pragma unroll
-      for (int a = 0; a < A; a++) {
-        const float da = d[a];
-        hl = tw_fma(wl[a], da, hl);
-        hh = tw_fma(wh[a], da, hh);
-        gl[a] = tw_fma(yl, da, gl[a]);
-        gh[a] = tw_fma(yh, da, gh[a]);
-      }
-      const tw_f2 zl = hl * (tw_f2{1.f, 1.f} - yl * yl), zh = hh * (tw_f2{1.f, 1.f} - yh * yh);
-      *reinterpret_cast<float4*>(zb + (size_t)(r + u * kHbGroups) * N) = make_float4(zl.x, zl.y, zh.x, zh.y);
-      csl += zl;
-      csh += zh;
+    for (int a = 0; a < A; a++) {
+      const float da = d[a];
+      hl = tw_fma(wl[a], da, hl);
+      hh = tw_fma(wh[a], da, hh);
+      gl[a] = tw_fma(yl, da, gl[a]);
+      gh[a] = tw_fma(yh, da, gh[a]);
     }
+    const tw_f2 zl = hl * (tw_f2{1.f, 1.f} - yl * yl), zh = hh * (tw_f2{1.f, 1.f} - yh * yh);
+    *reinterpret_cast<float4*>(zb + (size_t)r * N) = make_float4(zl.x, zl.y, zh.x, zh.y);
+    csl += zl;
+    csh += zh;
   }
-  // the 8 row groups' partials, summed in group order (fixed: deterministic)
-  red[g * 32 + q] = make_float4(csl.x, csl.y, csh.x, csh.y);
+  // the 16 row groups' partials, summed in group order (fixed: deterministic)
+  red[g * 16 + q] = make_float4(csl.x, csl.y, csh.x, csh.y);
   __syncthreads();
-  if (t < 32) {
+  if (t < 16) {
     float4 s = red[t];
     for (int k = 1; k < kHbGroups; k++) {
-      const float4 v = red[k * 32 + t];
+      const float4 v = red[k * 16 + t];
       s.x += v.x; s.y += v.y; s.z += v.z; s.w += v.w;
     }
     const int R = n / kHbRows;
     *reinterpret_cast<float4*>(p.cs + ((size_t)net * R + chunk) * N + blockIdx.y * kHbCols + 4 * t) = s;
   }
-  __syncthreads();
-#pragma unroll
-  for (int a = 0; a < A; a++) red[(g * A + a) * 32 + q] = make_float4(gl[a].x, gl[a].y, gh[a].x, gh[a].y);
-  __syncthreads();
   const int S = n / kHbRows;
-  for (int e = t; e < A * 32; e += 256) {
-    const int a = e >> 5, qq = e & 31;
-    float4 s = red[a * 32 + qq];
-    for (int k = 1; k < kHbGroups; k++) {
-      const float4 v = red[(k * A + a) * 32 + qq];
-      s.x += v.x; s.y += v.y; s.z += v.z; s.w += v.w;
+#pragma unroll
+  for (int a0 = 0; a0 < A; a0 += kHbPass) {
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < kHbPass; j++)
+      red[(g * kHbPass + j) * 16 + q] = make_float4(gl[a0 + j].x, gl[a0 + j].y, gh[a0 + j].x, gh[a0 + j].y);
+    __syncthreads();
+    if (t < kHbPass * 16) {
+      const int j = t >> 4, qq = t & 15;
+      float4 s = red[j * 16 + qq];
+      for (int k = 1; k < kHbGroups; k++) {
+        const float4 v = red[(k * kHbPass + j) * 16 + qq];
+        s.x += v.x; s.y += v.y; s.z += v.z; s.w += v.w;
+      }
+      *reinterpret_cast<float4*>(p.gw + (((size_t)net * S + chunk) * A + a0 + j) * N + blockIdx.y * kHbCols + 4 * qq) = s;
     }
-    *reinterpret_cast<float4*>(p.gw + (((size_t)net * S + chunk) * A + a) * N + blockIdx.y * kHbCols + 4 * qq) = s;
   }
 }
 
