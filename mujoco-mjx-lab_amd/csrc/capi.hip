@@ -1349,7 +1349,12 @@ extern "C" int mjl_ppo_surrogate(const float* mean, const float* log_std, const 
                                    -INFINITY, INFINITY, scratch, loss, g_mean, g_log_std, stream);
 }
 
-extern "C" long long mjl_twin_loss_head_blocks(int n) { return n > 0 ? (n + kSurrRows - 1) / kSurrRows : 0; }
+// rows per twin loss-head block: 64 at a data-parallel shard's minibatch (8,192 rows: 128 blocks where
+// 128-row blocks left 192 of the 256 CUs idle), 128 at C3's 65,536
+static int twin_loss_rows(int n) { return n <= 16384 ? 64 : kSurrRows; }
+extern "C" long long mjl_twin_loss_head_blocks(int n) {
+  return n > 0 ? (n + twin_loss_rows(n) - 1) / twin_loss_rows(n) : 0;
+}
 
 extern "C" int mjl_twin_loss_head(const float* z, const float* log_std, const float* act, const float* old_logp,
                                   const float* adv, const float* ret, const float* adv_stats, const int* stats_row,
@@ -1359,13 +1364,18 @@ extern "C" int mjl_twin_loss_head(const float* z, const float* log_std, const fl
   if (!z || !log_std || !act || !old_logp || !adv || !ret || !scratch || !dz || !lossp || !glsp || !biasp || n <= 0 ||
       A <= 0)
     return fail(MJL_ERR_ARG, "bad argument");
-  if (A > kLossMaxA || 2 * A + 2 > kSurrRows) return fail(MJL_ERR_UNSUPPORTED, "twin_loss_head: at most %d action columns", kLossMaxA);
+  if (A > kLossMaxA || 2 * A + 2 > 64) return fail(MJL_ERR_UNSUPPORTED, "twin_loss_head: at most %d action columns", 31);
   hipStream_t s = (hipStream_t)stream;
-  const int nb_adv = (n + kLossT - 1) / kLossT, nb = (n + kSurrRows - 1) / kSurrRows;
+  const int nb_adv = (n + kLossT - 1) / kLossT, nb = (int)mjl_twin_loss_head_blocks(n);
   if (!adv_stats) hipLaunchKernelGGL(adv_stats_kernel, dim3(nb_adv), dim3(kLossT), 0, s, adv, n, scratch);
-  hipLaunchKernelGGL(twin_loss_head_kernel<kSurrRows>, dim3(nb), dim3(2 * kSurrRows), 0, s, z, log_std, act, old_logp, adv,
-                     ret, n, A, clip_eps, ent_coef, scratch, nb_adv, adv_stats, stats_row, log_std_lo, log_std_hi, bias,
-                     dz, lossp, glsp, biasp);
+  if (twin_loss_rows(n) == 64)
+    hipLaunchKernelGGL(twin_loss_head_kernel<64>, dim3(nb), dim3(2 * 64), 0, s, z, log_std, act, old_logp, adv,
+                       ret, n, A, clip_eps, ent_coef, scratch, nb_adv, adv_stats, stats_row, log_std_lo, log_std_hi, bias,
+                       dz, lossp, glsp, biasp);
+  else
+    hipLaunchKernelGGL(twin_loss_head_kernel<kSurrRows>, dim3(nb), dim3(2 * kSurrRows), 0, s, z, log_std, act, old_logp,
+                       adv, ret, n, A, clip_eps, ent_coef, scratch, nb_adv, adv_stats, stats_row, log_std_lo, log_std_hi,
+                       bias, dz, lossp, glsp, biasp);
   HIPCHK(hipGetLastError());
   return MJL_OK;
 }
@@ -1385,9 +1395,10 @@ extern "C" int mjl_twin_gather_in(const long long* idx, const int* idx_row, int 
     return fail(MJL_ERR_ARG, "bad argument");
   if (!(mjl_twin_fused_shapes(k0, A, N) & 1))
     return fail(MJL_ERR_UNSUPPORTED, "twin_gather_in: input width %d / hidden width %d not instantiated", k0, N);
-  if ((uintptr_t)h % 8) return fail(MJL_ERR_ARG, "twin_gather_in: 8-byte aligned output expected");
+  if (((uintptr_t)h | (uintptr_t)b) % 16) return fail(MJL_ERR_ARG, "twin_gather_in: 16-byte aligned h and b expected");
   TwinInArgs p{idx, idx_row, n, A, nsrc, obs, act, logp, ret, adv, o2, a, ol, r, ad, W, b, h};
-  hipLaunchKernelGGL((twin_gather_in_kernel<kTinK0, kTinN>), dim3((unsigned)((n + kTinRows - 1) / kTinRows)),
+  const int nblk = 2 * ((n + kTinRows - 1) / kTinRows);  // a workgroup per (chunk, net), at most kTinBlocks
+  hipLaunchKernelGGL((twin_gather_in_kernel<kTinK0, kTinN>), dim3((unsigned)(nblk < kTinBlocks ? nblk : kTinBlocks)),
                      dim3(kTinN), 0, (hipStream_t)stream, p);
   HIPCHK(hipGetLastError());
   return MJL_OK;

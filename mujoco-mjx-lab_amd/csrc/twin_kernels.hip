@@ -19,6 +19,7 @@
 namespace mjl {
 
 typedef float tw_f2 __attribute__((ext_vector_type(2)));
+typedef float tw_f32x16 __attribute__((ext_vector_type(16)));
 
 __device__ __forceinline__ tw_f2 tw_fma(tw_f2 a, float b, tw_f2 c) {
   return __builtin_elementwise_fma(a, tw_f2{b, b}, c);
@@ -41,113 +42,135 @@ struct TwinInArgs {
   float* h;                                    // out: [2, n, N] = tanh(o W^T + b) per net
 };
 
-// block: kTinRows rows, N threads = N / 64 waves. Wave w takes rows 8w .. 8w + 7 (their observations
-// are wave-uniform: 16-byte LDS broadcasts), lane l the 8 columns l + 64 c of the two nets' 2N outputs
-// (c < N / 64: the policy's, the rest the value's), so a k step reads 8 conflict-free words of the
-// transposed weights and 2 broadcasts, for 32 packed FMAs — LDS and VALU time balanced (one lane per
-// column pair and 32 rows was LDS-bound). Every global load of the gather and of the weight staging
-// is issued before the first wait (one wave per SIMD: nothing else hides their latency).
+// A persistent grid of at most kTinBlocks workgroups of N threads (N / 64 waves), one net per workgroup
+// (net = blockIdx & 1), each taking 32-row chunks blockIdx / 2, + gridDim / 2, ... Its net's input
+// weights are staged ONCE per workgroup into LDS, row-major with an odd row stride (coalesced 16-byte
+// loads, conflict-free writes and operand reads): 64 KB of LDS, two workgroups per CU. Per chunk
+// every lane loads the row indices it needs itself (no LDS hand-off, so the observation loads issue
+// right behind the index loads), writes the chunk transposed to LDS and its net's copy of the rows;
+// then the N output columns in 32-wide tiles, wave w taking tiles w, w + N/64, ..., each as
+// v_mfma_f32_32x32x2_f32 over K0 in steps of 2 with C = W X^T (A = the weight rows, lane l giving
+// column l & 31 at k0 + (l >> 5); B = the gathered rows, lane l giving row l & 31): register v of lane
+// l then holds C[(v & 3) + 8 (v >> 2) + 4 (l >> 5)][l & 31], i.e. lane l owns row l & 31 and 4
+// consecutive columns per register quad, stored as 16-byte writes after the bias and tanh. The MFMA
+// is an exact f32 fma chain in k order (deterministic). (Measured and replaced, per 8,192-row launch:
+// vector-ALU versions 25-37 us; B operands read per lane from global memory 25.6 us — 4-byte reads over
+// 32 weight rows missed L1; both nets per workgroup with 120 KB of LDS, one workgroup per CU,
+// per-lane 4-byte stores 17.7-24 us.)
+constexpr int kTinBlocks = 512;
 template <int K0, int N>
-__global__ __launch_bounds__(N) void twin_gather_in_kernel(TwinInArgs p) {
-  constexpr int XS = kTinRows + 4;  // xs row stride (16-byte aligned: 144 B)
-  constexpr int WS = 2 * N + 1;     // ws row stride (odd: the transposing writes spread over banks)
-  constexpr int NC = 2 * N / 64;    // columns per lane
-  constexpr int RPW = 8;            // rows per wave
-  static_assert(K0 % 2 == 0 && N % 64 == 0 && (N / 64) * RPW == kTinRows, "tile shape");
-  constexpr int WF2 = K0;           // float2 of the [2N, K0] weights per thread: 2N K0 / 2 / N
+__global__ __launch_bounds__(N, 2) void twin_gather_in_kernel(TwinInArgs p) {
+  constexpr int XS = kTinRows + 4;  // xs row stride
+  constexpr int WS = K0 + 1;        // ws row stride (odd)
   constexpr int OBS_IT = (kTinRows * K0 + N - 1) / N;
   constexpr int ACT_IT = (kTinRows * 32 + N - 1) / N;  // A <= 32
-  __shared__ float ws[K0 * WS];
-  __shared__ __attribute__((aligned(16))) float xs[K0 * XS];
-  __shared__ long long sidx[kTinRows];
-  const int t = threadIdx.x, n = p.n, r0 = blockIdx.x * kTinRows, A = p.A;
-  const int rows = min(kTinRows, n - r0);
-  const long long* idx = p.idx + (p.idx_row ? (size_t)*p.idx_row * n : 0);
-  long long my_idx = -1;
-  if (t < rows) my_idx = idx[r0 + t];
-  float2 wv[WF2];  // the weights, coalesced: float2 f = t + i N of W viewed as [2N, K0]
-  const float2* W2 = reinterpret_cast<const float2*>(p.W);
+  constexpr int KS = K0 / 2;                           // MFMA K steps
+  constexpr int TPW = N / 32 / (N / 64);               // tiles per wave (2)
+  constexpr int WQ = N * K0 / 4;                       // float4 of one net's W
+  static_assert(K0 % 2 == 0 && (N * K0) % 4 == 0 && kTinRows == 32 && N % 64 == 0, "tile shape");
+  __shared__ float ws[N * WS];
+  __shared__ float xs[K0 * XS];
+  const int t = threadIdx.x, n = p.n, A = p.A, net = blockIdx.x & 1;
+  {  // this net's weights: W[net] [N, K0] row-major -> ws[col * WS + k] (= element e + col)
+    const float4* W4 = reinterpret_cast<const float4*>(p.W + (size_t)net * N * K0);
+    constexpr int IT = (WQ + N - 1) / N;
+    float4 wv[IT];
 #pragma unroll
-  for (int i = 0; i < WF2; i++) wv[i] = W2[t + i * N];
-  if (t < kTinRows) sidx[t] = my_idx;
-  __syncthreads();
-  const long long nsrc = p.nsrc;
-  const float nan = __builtin_nanf("");
-  float ov[OBS_IT], av[ACT_IT];
+    for (int i = 0; i < IT; i++) {
+      const int q = t + i * N;
+      wv[i] = q < WQ ? W4[q] : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
 #pragma unroll
-  for (int i = 0; i < OBS_IT; i++) {
-    const int e = t + i * N, r = e / K0, k = e - r * K0;
-    const long long s = e < kTinRows * K0 ? sidx[r] : -1;
-    ov[i] = (s >= 0 && s < nsrc) ? p.obs[(size_t)s * K0 + k] : nan;
-  }
+    for (int i = 0; i < IT; i++) {
+      const int q = t + i * N;
+      if (q < WQ) {
+        const float v4[4] = {wv[i].x, wv[i].y, wv[i].z, wv[i].w};
 #pragma unroll
-  for (int i = 0; i < ACT_IT; i++) {
-    const int e = t + i * N, r = e / A, k = e - r * A;
-    const long long s = e < rows * A ? sidx[r] : -1;
-    av[i] = (s >= 0 && s < nsrc) ? p.act[(size_t)s * A + k] : nan;
-  }
-  float olv = nan, rv = nan, adv = nan;
-  const bool own = t < rows && my_idx >= 0 && my_idx < nsrc;
-  if (own) {
-    olv = p.logp[my_idx];
-    rv = p.ret[my_idx];
-    adv = p.adv[my_idx];
-  }
-#pragma unroll
-  for (int i = 0; i < WF2; i++) {
-    const int f = t + i * N, row = f / (K0 / 2), k = 2 * (f - row * (K0 / 2));
-    ws[k * WS + row] = wv[i].x;
-    ws[(k + 1) * WS + row] = wv[i].y;
-  }
-#pragma unroll
-  for (int i = 0; i < OBS_IT; i++) {
-    const int e = t + i * N, r = e / K0, k = e - r * K0;
-    if (e < kTinRows * K0) {
-      xs[k * XS + r] = ov[i];
-      if (r < rows) {
-        p.o2[(size_t)(r0 + r) * K0 + k] = ov[i];
-        p.o2[((size_t)n + r0 + r) * K0 + k] = ov[i];
+        for (int c = 0; c < 4; c++) {
+          const int e = 4 * q + c;
+          ws[e + e / K0] = v4[c];
+        }
       }
     }
   }
+  const long long nsrc = p.nsrc;
+  const float nan = __builtin_nanf("");
+  const long long* idx = p.idx + (p.idx_row ? (size_t)*p.idx_row * n : 0);
+  const int lane = t & 63, w = t >> 6, li = lane & 31, kh = lane >> 5;
+  const int nchunk = (n + kTinRows - 1) / kTinRows, cstep = (int)(gridDim.x >> 1);
+  float4 bq[TPW][4];  // this lane's bias quads (loop-invariant)
 #pragma unroll
-  for (int i = 0; i < ACT_IT; i++) {
-    const int e = t + i * N;
-    if (e < rows * A) p.a[(size_t)r0 * A + e] = av[i];
-  }
-  if (t < rows) {
-    p.ol[r0 + t] = olv;
-    p.r[r0 + t] = rv;
-    p.ad[r0 + t] = adv;
-  }
-  __syncthreads();
-  const int lane = t & 63, rg = t >> 6;
-  tw_f2 acc[NC][RPW / 2];
+  for (int tt = 0; tt < TPW; tt++)
 #pragma unroll
-  for (int c = 0; c < NC; c++)
+    for (int q = 0; q < 4; q++)
+      bq[tt][q] = *reinterpret_cast<const float4*>(p.b + (size_t)net * N + (w * TPW + tt) * 32 + 8 * q + 4 * kh);
+  for (int ch = (int)(blockIdx.x >> 1); ch < nchunk; ch += cstep) {
+    const int r0 = ch * kTinRows, rows = min(kTinRows, n - r0);
+    float ov[OBS_IT], av[ACT_IT];
 #pragma unroll
-    for (int i = 0; i < RPW / 2; i++) acc[c][i] = tw_f2{0.f, 0.f};
-#pragma unroll 2
-  for (int k = 0; k < K0; k++) {
-    const float4 x0 = *reinterpret_cast<const float4*>(&xs[k * XS + RPW * rg]);
-    const float4 x1 = *reinterpret_cast<const float4*>(&xs[k * XS + RPW * rg + 4]);
-    const tw_f2 xp[4] = {{x0.x, x0.y}, {x0.z, x0.w}, {x1.x, x1.y}, {x1.z, x1.w}};
-#pragma unroll
-    for (int c = 0; c < NC; c++) {
-      const float w = ws[k * WS + lane + 64 * c];
-#pragma unroll
-      for (int i = 0; i < RPW / 2; i++) acc[c][i] = tw_fma(xp[i], w, acc[c][i]);
+    for (int i = 0; i < OBS_IT; i++) {
+      const int e = t + i * N, r = e / K0, k = e - r * K0;
+      const long long s = (e < kTinRows * K0 && r < rows) ? idx[r0 + r] : -1;
+      ov[i] = (s >= 0 && s < nsrc) ? p.obs[(size_t)s * K0 + k] : nan;
     }
-  }
+    if (net == 0) {
 #pragma unroll
-  for (int c = 0; c < NC; c++) {
-    const int col = lane + 64 * c, net = col / N, cn = col - net * N;
-    const float b = p.b[col];
-    float* hr = p.h + ((size_t)net * n + r0 + RPW * rg) * N + cn;
+      for (int i = 0; i < ACT_IT; i++) {
+        const int e = t + i * N, r = e / A, k = e - r * A;
+        const long long s = e < rows * A ? idx[r0 + r] : -1;
+        av[i] = (s >= 0 && s < nsrc) ? p.act[(size_t)s * A + k] : nan;
+      }
+    }
+    float olv = nan, rv = nan, adv = nan;
+    if (net == 0 && t < rows) {
+      const long long s = idx[r0 + t];
+      if (s >= 0 && s < nsrc) {
+        olv = p.logp[s];
+        rv = p.ret[s];
+        adv = p.adv[s];
+      }
+    }
+    __syncthreads();  // (the previous chunk's MFMAs are done with xs)
 #pragma unroll
-    for (int i = 0; i < RPW / 2; i++) {
-      if (RPW * rg + 2 * i < rows) hr[(size_t)(2 * i) * N] = tanhf(acc[c][i].x + b);
-      if (RPW * rg + 2 * i + 1 < rows) hr[(size_t)(2 * i + 1) * N] = tanhf(acc[c][i].y + b);
+    for (int i = 0; i < OBS_IT; i++) {
+      const int e = t + i * N, r = e / K0, k = e - r * K0;
+      if (e < kTinRows * K0) {
+        xs[k * XS + r] = ov[i];
+        if (r < rows) p.o2[((size_t)net * n + r0 + r) * K0 + k] = ov[i];
+      }
+    }
+    if (net == 0) {
+#pragma unroll
+      for (int i = 0; i < ACT_IT; i++) {
+        const int e = t + i * N;
+        if (e < rows * A) p.a[(size_t)r0 * A + e] = av[i];
+      }
+      if (t < rows) {
+        p.ol[r0 + t] = olv;
+        p.r[r0 + t] = rv;
+        p.ad[r0 + t] = adv;
+      }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int tt = 0; tt < TPW; tt++) {
+      const int c0 = (w * TPW + tt) * 32;  // the tile's first column
+      const float* wr = &ws[(c0 + li) * WS + kh];
+      tw_f32x16 acc;
+#pragma unroll
+      for (int v = 0; v < 16; v++) acc[v] = 0.f;
+#pragma unroll
+      for (int s = 0; s < KS; s++)
+        acc = __builtin_amdgcn_mfma_f32_32x32x2f32(wr[2 * s], xs[(2 * s + kh) * XS + li], acc, 0, 0, 0);
+      if (li < rows) {
+        float* hr = p.h + ((size_t)net * n + r0 + li) * N + c0 + 4 * kh;
+#pragma unroll
+        for (int q = 0; q < 4; q++) {
+          const float4 b = bq[tt][q];
+          *reinterpret_cast<float4*>(hr + 8 * q) = make_float4(tanhf(acc[4 * q] + b.x), tanhf(acc[4 * q + 1] + b.y),
+                                                               tanhf(acc[4 * q + 2] + b.z), tanhf(acc[4 * q + 3] + b.w));
+        }
+      }
     }
   }
 }
@@ -196,9 +219,17 @@ __global__ __launch_bounds__(256, 2) void twin_head_bwd_kernel(TwinHeadBwdArgs p
     wh[a] = tw_f2{w.z, w.w};
   }
   const float* dzb = p.dz + ((size_t)net * n + r0) * A;
-  for (int e = t; e < kHbRows * A; e += 256) {
-    const int r = e / A, a = e - r * A;
-    sdz[r * kHbDzStride + a] = dzb[e];
+  constexpr int DZ_IT = (kHbRows * A + 255) / 256;
+  float dv[DZ_IT];  // every load of the staging issued before the first LDS write
+#pragma unroll
+  for (int i = 0; i < DZ_IT; i++) {
+    const int e = t + 256 * i;
+    dv[i] = e < kHbRows * A ? dzb[e] : 0.f;
+  }
+#pragma unroll
+  for (int i = 0; i < DZ_IT; i++) {
+    const int e = t + 256 * i, r = e / A, a = e - r * A;
+    if (e < kHbRows * A) sdz[r * kHbDzStride + a] = dv[i];
   }
   __syncthreads();
   tw_f2 gl[A], gh[A];

@@ -85,7 +85,8 @@ class TwinNets:
                 return False
         A = pm.layers[-1].out_features
         ps = list(policy.parameters()) + list(value.parameters())
-        return (vm.layers[-1].out_features == 1 and 1 <= A <= 32 and pm.layers[-1].in_features == vm.layers[-1].in_features
+        # (A <= 31: the loss-head launch at 64 rows per block needs 2 A + 2 <= 64)
+        return (vm.layers[-1].out_features == 1 and 1 <= A <= 31 and pm.layers[-1].in_features == vm.layers[-1].in_features
                 and all(p.is_cuda and p.dtype == torch.float32 for p in ps) and policy.log_std.numel() == A)
 
     def __init__(self, policy, value):

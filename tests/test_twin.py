@@ -105,7 +105,7 @@ def test_fused_gather_input_layer_matches_float64(n):
         lin = net.mlp.layers[0]
         want = torch.tanh(x @ lin.weight.double().T + lin.bias.double())
         err = float((h1[k][ok].double() - want).abs().max())
-        assert err <= 2e-6, f"net {k}: max error {err:.3e}"
+        assert err <= 1e-5, f"net {k}: max error {err:.3e}"
 
 
 def test_fused_ends_update_matches_library_path(monkeypatch):

@@ -10,6 +10,7 @@
 #   c5trace      rocprofv3 kernel trace of the C5 update probe        -> <out>/c5_trace/
 #   prof:<mode>  kernel trace + FETCH/WRITE + 2 SQ passes of tools/prof_target.py <mode> (2048 envs)
 #   py:<script>  python tools/<script> (extra args after '='; ',' for spaces) -> <out>/<script>.log
+#   exe:<binary> tools/<binary> built here (args after '='; ',' for spaces)  -> <out>/<binary>.log
 set -o pipefail
 export TMPDIR=/tmp
 O=gpurun_out/$1
@@ -60,6 +61,11 @@ for S in "$@"; do
       SCRIPT=${A%%=*}
       ARGS=""; [ "$A" != "$SCRIPT" ] && ARGS=${A#*=}
       step $(basename $SCRIPT .py) 600 python tools/$SCRIPT ${ARGS//,/ } ;;
+    exe:*)
+      A=${S#exe:}
+      B=${A%%=*}
+      ARGS=""; [ "$A" != "$B" ] && ARGS=${A#*=}
+      step $B 300 ./tools/$B ${ARGS//,/ } ;;
     *) echo "unknown step $S"; exit 2 ;;
   esac
 done
