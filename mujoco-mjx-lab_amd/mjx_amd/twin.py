@@ -52,6 +52,18 @@ COLSUM_CHUNK = int(os.environ.get("MJL_TWIN_COLSUM_CHUNK", "128"))
 # layer's tanh backward (mjl_twin_head_bwd). MJL_TWIN_FUSED_ENDS=0: the library GEMM path for both
 FUSED_ENDS = os.environ.get("MJL_TWIN_FUSED_ENDS", "1") != "0"
 HEAD_BWD_ROWS = 128  # the fused output backward's row chunk (kHbRows)
+# the weight-gradient GEMMs on a second stream (fork / join inside the captured step): each layer's
+# split-K dW = dZ^T X (matrix-core bound) runs beside the main stream's dH = dZ W and the next tanh
+# backward (memory bound). MJL_TWIN_SIDE=0: one stream
+SIDE_STREAM = os.environ.get("MJL_TWIN_SIDE", "1") != "0"
+_SIDE = {}
+
+
+def _side(dev):
+    s = _SIDE.get(dev)
+    if s is None:
+        s = _SIDE[dev] = torch.cuda.Stream(dev)
+    return s
 
 
 # launch caps of the twin step's fused launches (csrc/ppo_loss_kernels.hip): mjl_adam_multi takes at most
@@ -274,6 +286,9 @@ class TwinNets:
         ch = ch if M % ch == 0 else M
         R = M // ch  # column-sum partial rows per matrix
         g = dz
+        main = torch.cuda.current_stream(dev)
+        side = _side(dev) if SIDE_STREAM else None
+        keep = []  # main-stream tensors the side stream reads: alive until the next step
         # the output layers' backward and the last hidden layer's tanh backward as one launch
         head_fused = FUSED_ENDS and bool(self._fused & 2) and nl >= 2 and M % HEAD_BWD_ROWS == 0
         for l in range(nl - 1, -1, -1):
@@ -307,16 +322,27 @@ class TwinNets:
                 xs = o.view(1, s, M // s, K).expand(2, s, M // s, K).reshape(2 * s, M // s, K)
             else:
                 xs = xin.view(2 * s, M // s, K)
-            part = torch.bmm(dzl.view(2 * s, M // s, N).transpose(1, 2), xs)  # [2s, N, K]
+            if side is not None:  # dW beside the main stream's dH and the next tanh backward
+                side.wait_stream(main)
+                with torch.cuda.stream(side):
+                    part = torch.bmm(dzl.view(2 * s, M // s, N).transpose(1, 2), xs)  # [2s, N, K]
+                keep.append((dzl, xs))
+            else:
+                part = torch.bmm(dzl.view(2 * s, M // s, N).transpose(1, 2), xs)  # [2s, N, K]
             segs.append((part, self.gW[l], 2, s, N * K))
             if l > 0:
                 g = torch.bmm(dzl, self.W[l])  # [2, M, K]
             if split and l == nl - 2:  # bucket 1 complete: its second stages now, then the caller's turn
+                if side is not None:
+                    main.wait_stream(side)
                 self._slice_sum(segs, None, st)
                 self._keep1 = (segs, hs, g)  # read by the launches in flight (and, captured, by the replays)
                 segs = []
                 yield None
+        if side is not None:
+            main.wait_stream(side)
         self._slice_sum(segs, counters, st)
+        self._keep_side = keep
         yield loss_p, loss_v
 
     def _slice_sum(self, segs, counters, st):
