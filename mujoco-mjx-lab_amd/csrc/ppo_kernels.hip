@@ -98,7 +98,10 @@ __global__ __launch_bounds__(256) void policy_head_kernel(const float* __restric
 // each layer's WP. Output C[4 g + r][n] of a block sits in lane (g, n) register r.
 // (A vector-ALU variant, 8 envs per 256-thread workgroup and thread n owning column n, packed weights
 // read as b128 per 4 k: twice the workgroups, measured 33.2 against 20.5 us at 1024 envs and 34.1-35.0
-// against 21.2 us at 2048; not kept.)
+// against 21.2 us at 2048; not kept. Split-K of the 21-wide output layer over the 14 waves its two
+// column blocks leave idle — each wave 2 of the 16 K chunks, the partials summed through LDS in part
+// order — measured 21.2 against 20.3 us at 1024 envs (round 6): the output layer's
+// 64-MFMA chain was not on the critical path once the other waves' barriers are counted; not kept.)
 constexpr int kPolMaxLayers = 6;
 constexpr int kPolLdx = 260;  // LDS row stride (floats): rows 4 banks apart, conflict-free b128
 #ifndef MJL_POL_WAVES
@@ -123,7 +126,6 @@ __global__ __launch_bounds__(64 * MJL_POL_WAVES) void policy_rollout_kernel(cons
                                                              const float* __restrict__ eps, int B,
                                                              float* __restrict__ act, float* __restrict__ logp) {
   __shared__ __attribute__((aligned(16))) float X[2][16 * kPolLdx];
-  __shared__ float Psum[16 * 256];  // split-K partials of a thin layer: [part][16 rows][N], P N <= 256
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int row0 = blockIdx.x * 16;
   {  // normalised, clipped observations (obs_normalize_kernel's arithmetic), zero-padded to K[0]
@@ -148,35 +150,6 @@ __global__ __launch_bounds__(64 * MJL_POL_WAVES) void policy_rollout_kernel(cons
     const float* bias = WP + (size_t)K * N;
     const bool last = l == pd.nlayer - 1;
     const int nblk = N >> 4;
-    if (2 * nblk <= kPolWaves) {
-      // a thin layer (the 21-wide head: 2 column blocks for 16 waves): split-K over the idle waves,
-      // wave w taking block w % nblk and the P-th share of the K chunks; the partials summed in part
-      // order (fixed: deterministic) with the bias (and tanh) by all threads
-      const int P = kPolWaves / nblk, nb = wave % nblk, pp = wave / nblk, nc = K >> 4;
-      if (pp < P) {
-        f4 acc = (f4){0.f, 0.f, 0.f, 0.f};
-        const int c_lo = pp * nc / P, c_hi = (pp + 1) * nc / P;
-        for (int c = c_lo; c < c_hi; c++) {
-          const f4 a = *(const f4*)&X[cur][c16 * kPolLdx + 16 * c + 4 * g];
-          const f4 b = *(const f4*)&WP[((size_t)(4 * c + g) * N + nb * 16 + c16) * 4];
-#pragma unroll
-          for (int t = 0; t < 4; t++) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a[t], b[t], acc, 0, 0, 0);
-        }
-#pragma unroll
-        for (int r = 0; r < 4; r++) Psum[(pp * 16 + 4 * g + r) * N + nb * 16 + c16] = acc[r];
-      }
-      __syncthreads();
-      for (int e = tid; e < 16 * N; e += 64 * kPolWaves) {
-        const int r = e / N, n = e - r * N;
-        float y = 0.f;
-        for (int q = 0; q < P; q++) y += Psum[(q * 16 + r) * N + n];
-        y += bias[n];
-        X[cur ^ 1][r * kPolLdx + n] = last ? y : tanhf(y);
-      }
-      __syncthreads();
-      cur ^= 1;
-      continue;
-    }
     for (int nb0 = wave; nb0 < nblk; nb0 += kPolWaves * kPolBpw) {  // kPolBpw blocks per wave per pass
       f4 acc[kPolBpw];
       int nbs[kPolBpw];
