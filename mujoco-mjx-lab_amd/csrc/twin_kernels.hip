@@ -56,7 +56,9 @@ struct TwinInArgs {
 // is an exact f32 fma chain in k order (deterministic). (Measured and replaced, per 8,192-row launch:
 // vector-ALU versions 25-37 us; B operands read per lane from global memory 25.6 us — 4-byte reads over
 // 32 weight rows missed L1; both nets per workgroup with 120 KB of LDS, one workgroup per CU,
-// per-lane 4-byte stores 17.7-24 us.)
+// per-lane 4-byte stores 17.7-24 us. Where this one's 16.3-16.9 us go, by knocking parts out
+// (tools/twin_micro.hip, profiles/r6/twin_micro.txt): ~6 us launch + weight staging + gather, ~4 us
+// the MFMAs, ~6 us the 16.8 MB of H stores; a branch-free tanh in the epilogue changed nothing.)
 constexpr int kTinBlocks = 512;
 template <int K0, int N>
 __global__ __launch_bounds__(N, 2) void twin_gather_in_kernel(TwinInArgs p) {

@@ -13,6 +13,7 @@
 using namespace mjl;
 
 
+
 static float* dev_rand(size_t n, unsigned seed, float scale) {
   std::vector<float> h(n);
   unsigned s = seed * 2654435761u + 1u;
