@@ -656,7 +656,8 @@ class _IdentityComm:
 def c5_rank_update(local, reps: int = 3) -> dict:
     """One rank's PPO update at BASELINE C5's per-rank shape on 8 GPUs (1024 envs x 256 steps, 4 epochs
     of 8,192-row minibatches = 128 minibatch steps) through PPOUpdater's data-parallel graphs with the
-    all-reduce replaced by the identity: the update's compute per rank (synthetic rollout data,
+    all-reduce replaced by the identity (captured inside the update's graph, as the RCCL path captures
+    it): the update's compute per rank (synthetic rollout data,
     random-init reference-size nets). The collective itself is measured at --gpus N > 1."""
     from mjx_amd import ppo
     from mjx_amd.config import reference_ppo_config
@@ -686,8 +687,10 @@ def c5_rank_update(local, reps: int = 3) -> dict:
     out = {"ppo_c5_rank_update_ms": 1e3 * sorted(ts)[len(ts) // 2], "ppo_c5_rank_update_steps": steps,
            "ppo_c5_rank_update_twin": up.twin is not None,
            "ppo_c5_rank_update_note": "one rank of C5 on 8 GPUs: 1024 envs x 256 steps, 4 epochs x 32 minibatches "
-                                      "of 8,192 rows, the data-parallel update graphs with an identity collective; "
-                                      "median of 3 synced runs after 2 (capture)"}
+                                      "of 8,192 rows, the data-parallel update as at N > 1 over RCCL (one graph per "
+                                      "update, the collective captured inside) with an identity collective; "
+                                      "median of 3 synced runs after 2 (capture)",
+           "ppo_c5_rank_update_captured": bool(up.captured_last_run)}
     del up, pol, val, op, ov
     return out
 
