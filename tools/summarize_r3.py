@@ -69,7 +69,7 @@ def mean(v):
 
 def main():
     out = os.path.join(ROOT, "profiles")
-    pre = os.path.join(out, ROUND, "") if ROUND in ("r4", "r5") else os.path.join(out, ROUND + "_")
+    pre = os.path.join(out, ROUND, "") if ROUND in ("r4", "r5", "r6") else os.path.join(out, ROUND + "_")
     os.makedirs(os.path.dirname(pre), exist_ok=True)
     rec = {"round": ROUND, "src_hash": _lib.source_hash(), "envs": 2048,
            "units": {"kernel_us": "rocprofv3 --stats AverageNs / 1e3",
