@@ -5,6 +5,7 @@
 // Build: hipcc -O2 -std=c++17 --offload-arch=gfx950 -fapprox-func -fno-slp-vectorize \
 //          -o tools/twin_micro tools/twin_micro.hip
 #include "../mujoco-mjx-lab_amd/csrc/twin_kernels.hip"
+#include "../mujoco-mjx-lab_amd/csrc/ppo_loss_kernels.hip"
 
 #include <cstdio>
 #include <cstdlib>
@@ -81,6 +82,26 @@ int main(int argc, char** argv) {
     const float t_hb = time_ms([&] {
       hipLaunchKernelGGL(twin_head_bwd_kernel<A>, dim3(M / kHbRows, N / kHbCols, 2), dim3(256), 0, 0, ph);
     }, reps);
+    {  // the twin loss head (mjl_twin_loss_head's kernel) at 64 and 128 rows per block
+      float *z = dev_rand(2ull * M * A, 11, 0.5f), *lstd = dev_rand(A, 12, 0.3f), *st = dev_rand(2, 13, 1.f);
+      float *lp2, *glsp, *biasp, *dzl;
+      int* row;
+      (void)hipMalloc(&lp2, 4 * (M / 64 + 1));
+      (void)hipMalloc(&glsp, 4ull * (M / 64 + 1) * A);
+      (void)hipMalloc(&biasp, 8ull * (M / 64 + 1) * A);
+      (void)hipMalloc(&dzl, 8ull * M * A);
+      (void)hipMalloc(&row, 4);
+      (void)hipMemset(row, 0, 4);
+      const float t64 = time_ms([&] {
+        hipLaunchKernelGGL(twin_loss_head_kernel<64>, dim3(M / 64), dim3(128), 0, 0, z, lstd, act, lp, av, rt, M, A, 0.2f,
+                           0.01f, nullptr, 0, st, row, -20.f, 2.f, b0, dzl, lp2, glsp, biasp);
+      }, reps);
+      const float t128 = time_ms([&] {
+        hipLaunchKernelGGL(twin_loss_head_kernel<128>, dim3(M / 128), dim3(256), 0, 0, z, lstd, act, lp, av, rt, M, A,
+                           0.2f, 0.01f, nullptr, 0, st, row, -20.f, 2.f, b0, dzl, lp2, glsp, biasp);
+      }, reps);
+      printf("M %6d  twin_loss_head  RB 64: %7.2f us   RB 128: %7.2f us\n", M, t64 * 1e3, t128 * 1e3);
+    }
     const double in_bytes = 2.0 * M * N * 4 + 3.0 * M * K0 * 4, hb_bytes = 4.0 * M * N * 4;
     printf("M %6d  gather_in %7.2f us (%5.1f TFLOP/s, %5.2f TB/s)   head_bwd %7.2f us (%5.2f TB/s)\n", M, t_in * 1e3,
            2.0 * M * K0 * 2 * N / (t_in * 1e-3) / 1e12, in_bytes / (t_in * 1e-3) / 1e12, t_hb * 1e3,
