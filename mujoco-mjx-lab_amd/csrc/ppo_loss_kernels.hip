@@ -245,7 +245,7 @@ __global__ __launch_bounds__(2 * RB) void twin_loss_head_kernel(
   __shared__ float sd[RB * kLossMaxA];  // a - mean of the block's rows (row-major), then dz[0]
   __shared__ float sm[RB * kLossMaxA];  // the mean
   __shared__ float sgv[RB];             // dz[1][:, 0]
-  __shared__ float wred[NW][2 * kLossMaxA + 2];
+  __shared__ float ssurr[RB];
   __shared__ float ivs[kLossMaxA], lsd[kLossMaxA], lss;
   __shared__ float mu_s, sd_s;
   const int t = threadIdx.x, lane = t & 63, w = t >> 6, r0 = blockIdx.x * RB, i = r0 + t;
@@ -287,10 +287,14 @@ __global__ __launch_bounds__(2 * RB) void twin_loss_head_kernel(
     }
   }
   if (t < RB) sgv[t] = gv;
-  if (t < A) {
-    const float ls = fminf(fmaxf(log_std[t], ls_lo), ls_hi);  // networks.py:103's clip
-    lsd[t] = ls;
-    ivs[t] = expf(-2.f * ls);
+  if (w == 0) {  // (A <= 32: lanes of wave 0) the clipped log_std, networks.py:103, and sum_j (2 s_j + log 2 pi)
+    const float ls = t < A ? fminf(fmaxf(log_std[t], ls_lo), ls_hi) : 0.f;
+    if (t < A) {
+      lsd[t] = ls;
+      ivs[t] = expf(-2.f * ls);
+    }
+    const float tot = wave_sum_dpp(t < A ? 2.f * ls + kLog2Pi : 0.f);
+    if (t == 0) lss = tot;
   }
   if (w == (NW > 1 ? 1 : 0)) {  // the advantage statistics
     float mu, sdv;
@@ -302,14 +306,7 @@ __global__ __launch_bounds__(2 * RB) void twin_loss_head_kernel(
     if (lane == 0) { mu_s = mu; sd_s = sdv; }
   }
   __syncthreads();
-  if (t == 0) {
-    float s = 0.f;
-    for (int j = 0; j < A; j++) s += 2.f * lsd[j] + kLog2Pi;
-    lss = s;
-  }
-  __syncthreads();
   float* dr = sd + (in ? t : 0) * A;
-  const float* mr = sm + (in ? t : 0) * A;
   float qs = 0.f;
   // the row waves only: a staging-only wave (w >= NW) is never `in`, so its qs would be discarded; the
   // guard only skips that benign read of row 0's sd (thread 0 may be writing it)
@@ -329,20 +326,18 @@ __global__ __launch_bounds__(2 * RB) void twin_loss_head_kernel(
     const float dratio = (-1.f / (float)n) * (w1 * an + ((ratio >= lo && ratio <= hi) ? w2 * an : 0.f));
     dlogp = dratio * ratio;
   }
-  if (w < NW) {  // the row waves
-  const float ssum = wave_sum_dpp(surr);
-  if (lane == 0) wred[w][0] = ssum;
-  for (int j = 0; j < A; j++) {
-    const float d = dr[j], m = mr[j];
-    const float c = wave_sum_dpp(in ? dlogp * (d * d * ivs[j] - 1.f) : 0.f);  // d logp / d s_j = q_j - 1
-    const float g = in ? dlogp * d * ivs[j] * (1.f - m * m) : 0.f;          // d loss / d z_j
-    const float cz = wave_sum_dpp(g);
-    if (in) dr[j] = g;  // (row t's a - mean is read by thread t only)
-    if (lane == 0) { wred[w][1 + j] = c; wred[w][1 + A + j] = cz; }
+  // per row, the column terms in place: c_j = d logp / d s_j = dlogp (q_j - 1) over the mean (sm), the
+  // loss gradient g_j = d loss / d z_j over a - mean (sd); row t's entries are read by thread t only.
+  // (Summed per column by 42 wave butterflies in a row, the chain was 11.6K of a block's 24.8K cycles.)
+  if (in) {
+    float* mw = sm + (size_t)t * A;
+    for (int j = 0; j < A; j++) {
+      const float d = dr[j], m = mw[j], iv = ivs[j];
+      mw[j] = dlogp * (d * d * iv - 1.f);
+      dr[j] = dlogp * d * iv * (1.f - m * m);
+    }
   }
-  const float gsum = wave_sum_dpp(gv);
-  if (lane == 0) wred[w][1 + 2 * A] = gsum;
-  }
+  if (t < RB) ssurr[t] = surr;
   __syncthreads();
   float* dz0 = dz + base;
   float* dz1 = dz + (size_t)n * A + base;
@@ -359,9 +354,17 @@ __global__ __launch_bounds__(2 * RB) void twin_loss_head_kernel(
   }
   const int nb = gridDim.x, b = blockIdx.x;
   if (t <= 2 * A + 1) {
-    float acc = wred[0][t];
-#pragma unroll
-    for (int k = 1; k < NW; k++) acc += wred[k][t];
+    // column t of [surr | c_0 .. c_{A-1} | g_0 .. g_{A-1} | gv] summed over the block's rows in row
+    // order, four interleaved partials (fixed order: deterministic)
+    const float* col = t == 0 ? ssurr : t <= A ? sm + (t - 1) : t <= 2 * A ? sd + (t - 1 - A) : sgv;
+    const int cs = (t == 0 || t == 2 * A + 1) ? 1 : A;
+    float p0 = 0.f, p1 = 0.f, p2 = 0.f, p3 = 0.f;
+    int r = 0;
+    for (; r + 3 < rows; r += 4) {
+      p0 += col[r * cs]; p1 += col[(r + 1) * cs]; p2 += col[(r + 2) * cs]; p3 += col[(r + 3) * cs];
+    }
+    for (; r < rows; r++) p0 += col[r * cs];
+    const float acc = (p0 + p1) + (p2 + p3);
     if (t == 0) {
       float val = -acc / (float)n;
       if (b == 0) val -= ent_coef * (0.5f * ((float)A + lss) / (float)A);  // entropy, train_ppo.py:215
