@@ -464,6 +464,22 @@ int mjl_twin_gather_in(const long long* idx, const int* idx_row, int n, long lon
    (summed by mjl_slice_sum_multi). n % 128 == 0, 16-byte aligned buffers. */
 int mjl_twin_head_bwd(const float* dz, const float* W, const float* y, int n, int A, int N, float* dzh, float* cs,
                       float* gw, void* stream);
+/* The twin update's whole head in one launch (bit 2 of mjl_twin_fused_shapes; train_ppo.py:204-220 on
+   both nets' output layers): H = tanh(zh + bh) for the last hidden layer's bias-less GEMM output zh
+   [2, n, K] and bias bh [2, K]; z = H W^T + bo (W [2, A, K], bo [2, A]); the policy's clipped
+   surrogate + entropy and the value's MSE gradient exactly as mjl_twin_loss_head (advantages
+   normalised by row *stats_row of adv_stats, or, adv_stats NULL, by this minibatch's own statistics
+   through scratch of mjl_ppo_loss_scratch(n, A) floats); then dzh [2, n, K] = (dz W)(1 - H^2). Per
+   workgroup b < S = mjl_twin_head_blocks(n) of each net k, partials summed in order by
+   mjl_slice_sum_multi: lossp[b] (policy loss, b = 0 adds the entropy term), glsp[b][A] (log_std),
+   biasp[k][b][A] (output biases), cs[k][b][K] (the last hidden bias), gw[k][b][A][K] (output weights).
+   n % 64 == 0. */
+long long mjl_twin_head_blocks(int n);
+int mjl_twin_head(const float* zh, const float* bh, const float* W, const float* bo, const float* log_std,
+                  const float* act, const float* old_logp, const float* adv, const float* ret, const float* adv_stats,
+                  const int* stats_row, int n, int A, int K, float clip_eps, float ent_coef, float log_std_lo,
+                  float log_std_hi, float* scratch, float* dzh, float* cs, float* gw, float* lossp, float* glsp,
+                  float* biasp, void* stream);
 int mjl_twin_loss_head(const float* z, const float* log_std, const float* act, const float* old_logp, const float* adv,
                        const float* ret, const float* adv_stats, const int* stats_row, int n, int A, float clip_eps,
                        float ent_coef, float log_std_lo, float log_std_hi, const float* bias, float* scratch,

@@ -1381,9 +1381,41 @@ extern "C" int mjl_twin_loss_head(const float* z, const float* log_std, const fl
 }
 
 // The twin update's fused thin ends (twin_kernels.hip). Shapes: bit 0 set when the gather + input
-// layer launch has an instantiation for (k0, N), bit 1 when the output backward has one for (A, N).
+// layer launch has an instantiation for (k0, N), bit 1 when the output backward has one for (A, N),
+// bit 2 when the fused head (forward + losses + backward) has one for (A, N = the last hidden width).
 extern "C" int mjl_twin_fused_shapes(int k0, int A, int N) {
-  return (k0 == kTinK0 && N == kTinN ? 1 : 0) | (A == kHbA && N > 0 && N % kHbCols == 0 ? 2 : 0);
+  return (k0 == kTinK0 && N == kTinN ? 1 : 0) | (A == kHbA && N > 0 && N % kHbCols == 0 ? 2 : 0) |
+         (A == kThA && N == kThK ? 4 : 0);
+}
+
+// workgroups per net of the fused head launch (the partial rows of its reductions)
+extern "C" long long mjl_twin_head_blocks(int n) {
+  if (n <= 0) return 0;
+  const int nchunk = (n + kThRows - 1) / kThRows;
+  return nchunk < kThBlocks / 2 ? nchunk : kThBlocks / 2;
+}
+
+extern "C" int mjl_twin_head(const float* zh, const float* bh, const float* W, const float* bo, const float* log_std,
+                             const float* act, const float* old_logp, const float* adv, const float* ret,
+                             const float* adv_stats, const int* stats_row, int n, int A, int K, float clip_eps,
+                             float ent_coef, float log_std_lo, float log_std_hi, float* scratch, float* dzh, float* cs,
+                             float* gw, float* lossp, float* glsp, float* biasp, void* stream) {
+  if (!zh || !bh || !W || !bo || !log_std || !act || !old_logp || !adv || !ret || !dzh || !cs || !gw || !lossp ||
+      !glsp || !biasp || n <= 0 || A <= 0 || K <= 0 || (!adv_stats && !scratch))
+    return fail(MJL_ERR_ARG, "bad argument");
+  if (!(mjl_twin_fused_shapes(0, A, K) & 4))
+    return fail(MJL_ERR_UNSUPPORTED, "twin_head: %d outputs / hidden width %d not instantiated", A, K);
+  if (n % kThRows) return fail(MJL_ERR_ARG, "twin_head: rows must be a multiple of %d", kThRows);
+  if (((uintptr_t)zh | (uintptr_t)bh | (uintptr_t)W | (uintptr_t)dzh) % 16)
+    return fail(MJL_ERR_ARG, "twin_head: 16-byte aligned zh, bh, W, dzh expected");
+  hipStream_t s = (hipStream_t)stream;
+  const int nb_adv = (n + kLossT - 1) / kLossT;
+  if (!adv_stats) hipLaunchKernelGGL(adv_stats_kernel, dim3(nb_adv), dim3(kLossT), 0, s, adv, n, scratch);
+  TwinHeadArgs p{zh, bh, W, bo, log_std, act, old_logp, adv, ret, adv_stats, stats_row, scratch, nb_adv, n, clip_eps,
+                 ent_coef, log_std_lo, log_std_hi, dzh, cs, gw, lossp, glsp, biasp};
+  hipLaunchKernelGGL((twin_head_kernel<kThA, kThK>), dim3((unsigned)(2 * mjl_twin_head_blocks(n))), dim3(256), 0, s, p);
+  HIPCHK(hipGetLastError());
+  return MJL_OK;
 }
 
 extern "C" int mjl_twin_gather_in(const long long* idx, const int* idx_row, int n, long long nsrc, int k0, int A,

@@ -16,6 +16,8 @@
 #pragma once
 #include <hip/hip_runtime.h>
 
+#include "ppo_loss_kernels.hip"  // wave_sum_dpp, kLog2Pi
+
 namespace mjl {
 
 typedef float tw_f2 __attribute__((ext_vector_type(2)));
@@ -287,6 +289,302 @@ __global__ __launch_bounds__(256, 2) void twin_head_bwd_kernel(TwinHeadBwdArgs p
       }
       *reinterpret_cast<float4*>(p.gw + (((size_t)net * S + chunk) * A + a0 + j) * N + blockIdx.y * kHbCols + 4 * qq) = s;
     }
+  }
+}
+
+
+// ------------------------------------------------------------------ fused head (forward + losses + backward)
+// The twin update's head in ONE launch (train_ppo.py:204-220 for both nets' output layers, the last
+// hidden layer's bias + tanh and its tanh backward): replaces the last hidden layer's bias + tanh pass,
+// the output layers' batched GEMM, the loss launch (mjl_twin_loss_head) and the output backward
+// (mjl_twin_head_bwd). A persistent grid of at most kThBlocks workgroups, one net each (net =
+// blockIdx & 1), taking 64-row chunks blockIdx / 2, + gridDim / 2, ... Per chunk:
+//   H = tanh(zh + bh) of the chunk into LDS (zh: the last hidden layer's bias-less GEMM output);
+//   z = H W^T + bo on v_mfma_f32_32x32x2_f32 (the 4 waves split the 2 row tiles x 2 K halves, summed
+//     in K order through LDS);
+//   per row (wave 0): the policy's clipped surrogate exactly as twin_loss_head_kernel (mean = tanh z,
+//     the Gaussian log-prob with log_std clipped, ratio, torch.minimum's tie gradient, dz = d loss /
+//     d z), or the value's dz = 2 (v - ret) / n in column 0;
+//   the chunk's column sums (the loss, d loss / d log_std, the output bias gradient) added to the
+//     workgroup's accumulators in chunk order;
+//   dH = dz W on MFMA, dZ = dH (1 - H^2) stored and column-summed (the hidden bias gradient);
+//   the output weight gradient dz^T H on MFMA, accumulated across the workgroup's chunks in registers.
+// Per workgroup one partial of every reduction (block b of net k): lossp[b], glsp[b][A] (policy),
+// biasp[k][b][A], cs[k][b][K], gw[k][b][A][K], summed over the workgroups in order by
+// mjl_slice_sum_multi. Deterministic (fixed orders throughout).
+constexpr int kThRows = 64;       // rows per chunk
+constexpr int kThK = 256;         // instantiated last hidden width
+constexpr int kThA = 21;          // instantiated output width
+constexpr int kThBlocks = 256;    // at most this many workgroups (one per CU)
+constexpr int kThHS = kThK + 4;   // hs / ws row stride (16-byte rows, 4 banks apart)
+constexpr int kThZS = 33;         // sz row stride (32 output columns + 1)
+
+struct TwinHeadArgs {
+  const float* zh;  // [2, n, K]: the last hidden layer's bias-less pre-activation
+  const float* bh;  // [2, K]: its bias
+  const float* W;   // [2, A, K]: the output layers' weights
+  const float* bo;  // [2, A]: their biases
+  const float *log_std, *act, *old_logp, *adv, *ret;  // [A], [n, A], [n] x 3
+  const float* adv_stats;                             // [n_minibatches, 2] (mean, std), read at *stats_row;
+  const int* stats_row;                               // or NULL: merged from adv_part (adv_stats_kernel)
+  const float* adv_part;
+  int nb_adv;
+  int n;
+  float clip_eps, ent_coef, ls_lo, ls_hi;
+  float* dzh;    // out [2, n, K]: dZ of the last hidden layer
+  float* cs;     // out [2, S, K]: its column sums per workgroup
+  float* gw;     // out [2, S, A, K]: the output weight gradient per workgroup
+  float* lossp;  // out [S]: policy loss partials (workgroup 0 adds the entropy term)
+  float* glsp;   // out [S, A]: d loss / d log_std partials
+  float* biasp;  // out [2, S, A]: the output bias gradients
+};
+
+template <int A, int K>
+__global__ __launch_bounds__(256) void twin_head_kernel(TwinHeadArgs p) {
+  static_assert(A <= 31 && K % 64 == 0 && K == 4 * 64, "tile shape: 4 waves x 2 column tiles of 32");
+  constexpr int R = kThRows, HS = kThHS, ZS = kThZS;
+  __shared__ __attribute__((aligned(16))) float hs[R * HS];  // H of the chunk
+  __shared__ __attribute__((aligned(16))) float ws[32 * HS];  // W_out rows, rows A..31 zero
+  __shared__ float red[4 * 16 * 64];                          // z partials of the 4 waves
+  __shared__ float sz[R * ZS];                                // z, then d, then dz (cols A..31 zero)
+  __shared__ float sx[R * 32];                                // act, then the mean, then c_j
+  __shared__ float srow[4][R];                                // old_logp, adv, ret, surr
+  __shared__ float ivs[32];
+  __shared__ float lss_s, mu_s, sd_s;
+  __shared__ float acc_col[2 * 32 + 1];                       // c_j, dz column sums, loss: chunk order
+  __shared__ float csh[2][K];
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6, li = lane & 31, kh = lane >> 5;
+  const int net = blockIdx.x & 1, S = (int)(gridDim.x >> 1), blk = (int)(blockIdx.x >> 1), n = p.n;
+  const int nchunk = (n + R - 1) / R;
+  // ---- once per workgroup: W_out of this net, the log_std terms, the advantage statistics
+  {
+    constexpr int Q = 32 * K / 4 / 256;  // float4 per thread
+#pragma unroll
+    for (int i = 0; i < Q; i++) {
+      const int q = t + 256 * i, a = q / (K / 4), c4 = q - a * (K / 4);
+      const float4 v = a < A ? *reinterpret_cast<const float4*>(p.W + ((size_t)net * A + a) * K + 4 * c4)
+                             : make_float4(0.f, 0.f, 0.f, 0.f);
+      *reinterpret_cast<float4*>(&ws[a * HS + 4 * c4]) = v;
+    }
+  }
+  if (w == 0) {
+    const float ls = lane < A ? fminf(fmaxf(p.log_std[lane], p.ls_lo), p.ls_hi) : 0.f;  // networks.py:103
+    if (lane < 32) ivs[lane] = lane < A ? expf(-2.f * ls) : 0.f;
+    const float tot = wave_sum_dpp(lane < A ? 2.f * ls + kLog2Pi : 0.f);
+    float mu, sdv;
+    if (p.adv_stats) {
+      const float* st = p.adv_stats + (p.stats_row ? 2 * (size_t)*p.stats_row : 0);
+      mu = st[0];
+      sdv = st[1];
+    } else {
+      adv_merge_wave(p.adv_part, p.nb_adv, lane, mu, sdv);
+    }
+    if (lane == 0) {
+      lss_s = tot;
+      mu_s = mu;
+      sd_s = sdv;
+    }
+  }
+  if (t < 2 * 32 + 1) acc_col[t] = 0.f;
+  tw_f32x16 gwacc[2];
+  float csacc[2] = {0.f, 0.f};
+#pragma unroll
+  for (int c = 0; c < 2; c++)
+#pragma unroll
+    for (int v = 0; v < 16; v++) gwacc[c][v] = 0.f;
+  const float4 bq = *reinterpret_cast<const float4*>(p.bh + (size_t)net * K + 4 * (t & (K / 4 - 1)));
+  const float nf = (float)n;
+  for (int ch = blk; ch < nchunk; ch += S) {
+    const int r0 = ch * R, rows = min(R, n - r0);
+    // ---- loads: the chunk's pre-activations, actions and per-row scalars, all issued together
+    constexpr int QZ = R * K / 4 / 256;  // float4 of zh per thread (16)
+    float4 zv[QZ];
+#pragma unroll
+    for (int i = 0; i < QZ; i++) {
+      const int q = t + 256 * i, r = q / (K / 4), c4 = q - r * (K / 4);
+      zv[i] = r < rows ? *reinterpret_cast<const float4*>(p.zh + ((size_t)net * n + r0 + r) * K + 4 * c4)
+                       : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+    constexpr int QA = (R * 32 + 255) / 256;
+    float av[QA];
+    if (net == 0) {
+#pragma unroll
+      for (int i = 0; i < QA; i++) {
+        const int e = t + 256 * i;
+        av[i] = e < rows * A ? p.act[(size_t)r0 * A + e] : 0.f;
+      }
+    }
+    float rv0 = 0.f, rv1 = 0.f, rv2 = 0.f;
+    if (t < rows) {
+      rv0 = p.old_logp[r0 + t];
+      rv1 = p.adv[r0 + t];
+      rv2 = p.ret[r0 + t];
+    }
+    __syncthreads();  // (the previous chunk's reads of hs / sz / sx are done)
+#pragma unroll
+    for (int i = 0; i < QZ; i++) {
+      const int q = t + 256 * i, r = q / (K / 4), c4 = q - r * (K / 4);
+      float4 h = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (r < rows)
+        h = make_float4(tanhf(zv[i].x + bq.x), tanhf(zv[i].y + bq.y), tanhf(zv[i].z + bq.z), tanhf(zv[i].w + bq.w));
+      *reinterpret_cast<float4*>(&hs[r * HS + 4 * c4]) = h;
+    }
+    if (net == 0) {
+#pragma unroll
+      for (int i = 0; i < QA; i++) {
+        const int e = t + 256 * i;
+        if (e < rows * A) sx[(e / A) * 32 + e % A] = av[i];
+      }
+    }
+    if (t < R) {
+      srow[0][t] = rv0;
+      srow[1][t] = rv1;
+      srow[2][t] = rv2;
+    }
+    __syncthreads();
+    // ---- z = H W^T: wave w takes row tile w & 1 and K half w >> 1
+    {
+      const int rt = w & 1, k0 = (w >> 1) * (K / 2);
+      tw_f32x16 acc;
+#pragma unroll
+      for (int v = 0; v < 16; v++) acc[v] = 0.f;
+      const float* ha = &hs[(32 * rt + li) * HS + k0 + kh];
+      const float* wb = &ws[li * HS + k0 + kh];
+#pragma unroll 8
+      for (int s = 0; s < K / 4; s++) acc = __builtin_amdgcn_mfma_f32_32x32x2f32(ha[2 * s], wb[2 * s], acc, 0, 0, 0);
+#pragma unroll
+      for (int v = 0; v < 16; v++) red[(w * 16 + v) * 64 + lane] = acc[v];
+    }
+    __syncthreads();
+    // z[row][a] = lower K half + upper K half + bo (C[i][j] in register (i & 3) + 4 (i >> 3) of lane
+    // j + 32 ((i >> 2) & 1))
+    for (int e = t; e < R * 32; e += 256) {
+      const int row = e >> 5, a = e & 31, rt = row >> 5, i = row & 31;
+      const int v = (i & 3) + 4 * (i >> 3), L = a + 32 * ((i >> 2) & 1);
+      const float zz = red[(rt * 16 + v) * 64 + L] + red[((2 + rt) * 16 + v) * 64 + L];
+      sz[row * ZS + a] = a < A ? zz + p.bo[net * A + a] : 0.f;
+    }
+    __syncthreads();
+    // ---- per row: the losses and dz (wave 0, lane = row)
+    if (w == 0) {
+      const int r = lane;
+      float surr = 0.f;
+      if (r < rows) {
+        float* zr = &sz[r * ZS];
+        if (net == 0) {
+          float* xr = &sx[r * 32];
+          float qs = 0.f;
+          for (int j = 0; j < A; j++) {
+            const float m = tanhf(zr[j]), d = xr[j] - m;
+            zr[j] = d;
+            xr[j] = m;
+            qs += d * d * ivs[j];
+          }
+          const float logp = -0.5f * (qs + lss_s);
+          const float ratio = expf(logp - srow[0][r]);
+          const float an = (srow[1][r] - mu_s) / (sd_s + 1e-8f);
+          const float lo = 1.f - p.clip_eps, hi = 1.f + p.clip_eps;
+          const float rc = fminf(fmaxf(ratio, lo), hi);
+          const float t1 = ratio * an, t2 = rc * an;
+          surr = fminf(t1, t2);
+          const float w1 = t1 < t2 ? 1.f : (t1 == t2 ? 0.5f : 0.f);
+          const float w2 = t2 < t1 ? 1.f : (t1 == t2 ? 0.5f : 0.f);
+          const float dratio = (-1.f / nf) * (w1 * an + ((ratio >= lo && ratio <= hi) ? w2 * an : 0.f));
+          const float dlogp = dratio * ratio;
+          for (int j = 0; j < A; j++) {
+            const float d = zr[j], m = xr[j], iv = ivs[j];
+            xr[j] = dlogp * (d * d * iv - 1.f);    // d logp / d s_j = q_j - 1
+            zr[j] = dlogp * d * iv * (1.f - m * m);  // d loss / d z_j
+          }
+        } else {
+          zr[0] = 2.f * (zr[0] - srow[2][r]) / nf;  // value: d loss / d v (train_ppo.py:218-220)
+          for (int j = 1; j < A; j++) zr[j] = 0.f;
+        }
+      } else {
+        for (int j = 0; j < 32; j++) {
+          sz[r * ZS + j] = 0.f;
+          sx[r * 32 + j] = 0.f;
+        }
+      }
+      srow[3][r] = surr;
+    }
+    __syncthreads();
+    // ---- the chunk's column sums into the workgroup's accumulators (rows in order, chunks in order)
+    if (t < 2 * 32 + 1) {
+      const bool pol = net == 0;
+      const float* col = t == 2 * 32 ? srow[3] : t < 32 ? &sx[t] : &sz[t - 32];
+      const int cstr = t == 2 * 32 ? 1 : (t < 32 ? 32 : ZS);
+      const bool on = t == 2 * 32 ? pol : (t < 32 ? (pol && t < A) : (t - 32 < A));
+      if (on) {
+        float p0 = 0.f, p1 = 0.f, p2 = 0.f, p3 = 0.f;
+        for (int r = 0; r < R; r += 4) {
+          p0 += col[r * cstr]; p1 += col[(r + 1) * cstr]; p2 += col[(r + 2) * cstr]; p3 += col[(r + 3) * cstr];
+        }
+        acc_col[t] += (p0 + p1) + (p2 + p3);
+      }
+    }
+    // ---- dH = dz W, dZ = dH (1 - H^2): wave w takes column tiles 2w, 2w + 1 over both row tiles
+#pragma unroll
+    for (int c = 0; c < 2; c++) {
+      const int ct = 2 * w + c, col = 32 * ct + li;
+#pragma unroll
+      for (int rt = 0; rt < 2; rt++) {
+        tw_f32x16 acc;
+#pragma unroll
+        for (int v = 0; v < 16; v++) acc[v] = 0.f;
+#pragma unroll
+        for (int s = 0; s < (A + 1) / 2; s++)
+          acc = __builtin_amdgcn_mfma_f32_32x32x2f32(sz[(32 * rt + li) * ZS + 2 * s + kh], ws[(2 * s + kh) * HS + col],
+                                                     acc, 0, 0, 0);
+        float* out = p.dzh + ((size_t)net * n + r0) * K + col;
+#pragma unroll
+        for (int v = 0; v < 16; v++) {
+          const int row = 32 * rt + (v & 3) + 8 * (v >> 2) + 4 * kh;
+          const float y = hs[row * HS + col];
+          const float dzv = acc[v] * (1.f - y * y);
+          if (row < rows) out[(size_t)row * K] = dzv;
+          csacc[c] += dzv;
+        }
+      }
+    }
+    // ---- the output weight gradient dz^T H, accumulated over the chunks: column tiles 2w, 2w + 1
+#pragma unroll
+    for (int c = 0; c < 2; c++) {
+      const int col = 32 * (2 * w + c) + li;
+#pragma unroll 8
+      for (int s = 0; s < R / 2; s++)
+        gwacc[c] = __builtin_amdgcn_mfma_f32_32x32x2f32(sz[(2 * s + kh) * ZS + li], hs[(2 * s + kh) * HS + col],
+                                                        gwacc[c], 0, 0, 0);
+    }
+  }
+  // ---- the workgroup's partials
+  const int nb = S;
+#pragma unroll
+  for (int c = 0; c < 2; c++) {
+    const int col = 32 * (2 * w + c) + li;
+#pragma unroll
+    for (int v = 0; v < 16; v++) {
+      const int a = (v & 3) + 8 * (v >> 2) + 4 * kh;
+      if (a < A) p.gw[(((size_t)net * nb + blk) * A + a) * K + col] = gwacc[c][v];
+    }
+    csh[kh][col] = csacc[c];
+  }
+  __syncthreads();
+  if (t < K) p.cs[((size_t)net * nb + blk) * K + t] = csh[0][t] + csh[1][t];
+  if (net == 0) {
+    if (t == 0) {
+      float val = -acc_col[2 * 32] / nf;
+      if (blk == 0) val -= p.ent_coef * (0.5f * ((float)A + lss_s) / (float)A);  // entropy, train_ppo.py:215
+      p.lossp[blk] = val;
+    }
+    if (t < A) {
+      const float ls = p.log_std[t];
+      const float val = blk == 0 ? acc_col[t] - p.ent_coef / (float)A : acc_col[t];
+      p.glsp[(size_t)blk * A + t] = (ls >= p.ls_lo && ls <= p.ls_hi) ? val : 0.f;
+      p.biasp[(size_t)blk * A + t] = acc_col[32 + t];
+    }
+  } else if (t < A) {
+    p.biasp[((size_t)nb + blk) * A + t] = t == 0 ? acc_col[32] : 0.f;
   }
 }
 

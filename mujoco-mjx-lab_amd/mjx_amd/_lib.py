@@ -33,7 +33,7 @@ EXPORTS = [
     "mjl_colsum_batched_scratch", "mjl_colsum_batched", "mjl_tanh_bwd_colsum_batched", "mjl_slice_sum_batched",
     "mjl_mse_strided", "mjl_ppo_surrogate_clipped", "mjl_bias_act", "mjl_adam_multi",
     "mjl_gather_rows_indexed", "mjl_slice_sum_multi", "mjl_tanh_bwd_colsum_partials", "mjl_twin_loss_head_blocks", "mjl_twin_loss_head",
-    "mjl_twin_fused_shapes", "mjl_twin_gather_in", "mjl_twin_head_bwd",
+    "mjl_twin_fused_shapes", "mjl_twin_gather_in", "mjl_twin_head_bwd", "mjl_twin_head_blocks", "mjl_twin_head",
 ]
 
 _lib = None
@@ -158,6 +158,9 @@ def lib() -> C.CDLL:
     L.mjl_twin_fused_shapes.argtypes = [i32, i32, i32]
     L.mjl_twin_gather_in.argtypes = [vp, vp, i32, C.c_longlong, i32, i32, i32] + [vp] * 13 + [vp]
     L.mjl_twin_head_bwd.argtypes = [vp, vp, vp, i32, i32, i32, vp, vp, vp, vp]
+    L.mjl_twin_head_blocks.argtypes = [i32]
+    L.mjl_twin_head_blocks.restype = C.c_longlong
+    L.mjl_twin_head.argtypes = ([vp] * 11 + [i32, i32, i32] + [C.c_float] * 4 + [vp] * 7 + [vp])
     L.mjl_tanh_bwd_colsum_partials.argtypes = [vp, vp, i32, i32, i32, i32, vp, vp, vp]
     L.mjl_small_mlp_fwd.argtypes = [vp, i32, i32, i32, vp, vp, vp, vp, vp]
     L.mjl_small_mlp_bwd_input.argtypes = [vp, i32, i32, i32, vp, vp, vp, vp, vp]

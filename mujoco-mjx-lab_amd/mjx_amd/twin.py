@@ -52,6 +52,7 @@ COLSUM_CHUNK = int(os.environ.get("MJL_TWIN_COLSUM_CHUNK", "128"))
 # layer's tanh backward (mjl_twin_head_bwd). MJL_TWIN_FUSED_ENDS=0: the library GEMM path for both
 FUSED_ENDS = os.environ.get("MJL_TWIN_FUSED_ENDS", "1") != "0"
 HEAD_BWD_ROWS = 128  # the fused output backward's row chunk (kHbRows)
+HEAD_ROWS = 64  # the fused head's row chunk (kThRows)
 # MJL_TWIN_SIDE=1: the weight-gradient GEMMs on a second stream (fork / join inside the captured step),
 # each layer's split-K dW = dZ^T X beside the main stream's dH = dZ W and the next tanh backward.
 # Measured slower and off by default: C5's per-rank update 27.8 -> 33.5 ms (the fork / join events
@@ -150,7 +151,7 @@ class TwinNets:
         self.N0 = shapes[0][0]            # the first hidden width
         self.NH = shapes[-1][1]           # the last hidden width (the output layers' input)
         self._fused = int(lib().mjl_twin_fused_shapes(self.K0, self.A, self.N0)) & 1
-        self._fused |= int(lib().mjl_twin_fused_shapes(self.K0, self.A, self.NH)) & 2
+        self._fused |= int(lib().mjl_twin_fused_shapes(self.K0, self.A, self.NH)) & 6
 
     def fused_input_ok(self, src) -> bool:
         """The gather + input layer launch applies: instantiated shape, the rollout arrays as the
@@ -247,14 +248,22 @@ class TwinNets:
         hs = [x] if h1 is None else [x, h1]
         # (the output layer's bias and tanh go into the loss launch unless the value loss is wanted)
         fold = FOLD_HEAD and not want_value_loss
+        # the whole head as one launch (mjl_twin_head): the last hidden layer's bias + tanh, both output
+        # layers, the losses and the head's backward down to that hidden layer's dZ
+        whole_head = (FUSED_ENDS and fold and bool(self._fused & 4) and nl >= 2 and M % HEAD_ROWS == 0
+                      and len(hs) <= nl - 1)
+        zh = None
         for l in range(len(hs) - 1, nl):
             h = torch.bmm(hs[-1], self.W[l].transpose(1, 2))
+            if whole_head and l == nl - 2:  # its bias and tanh inside the head launch; H never stored
+                zh = h
+                break
             mask = 3 if l < nl - 1 else 1  # the output layer: tanh for the policy's mean, linear value
             if l < nl - 1 or not fold:
                 check(L.mjl_bias_act(h.data_ptr(), self.b[l].data_ptr(), 2, M, h.shape[2], mask, st))
             hs.append(h)
-        z = hs.pop()  # [2, M, A]: the policy's mean and the value in column 0 of z[1] (fold: before the
-        # output bias and the mean's tanh)
+        z = None if whole_head else hs.pop()  # [2, M, A]: the policy's mean and the value in column 0 of
+        # z[1] (fold: before the output bias and the mean's tanh)
         # ---- losses and the output layers' dZ in one launch (networks.py:103 clips log_std to [-20, 2]:
         # in the kernel, with its gradient mask); the value loss itself only for reporting.
         # Every reduction's first stage comes here (block partials of the loss, d loss / d log_std and
@@ -269,30 +278,49 @@ class TwinNets:
             check(L.mjl_mse_strided(z[1].data_ptr(), A, ret.data_ptr(), M, scr_v.data_ptr(), loss_v.data_ptr(),
                                     gv.data_ptr(), st))
         segs = []  # (x, out, nb, ns, m)
-        dz = torch.empty((2, M, A), device=dev)
-        nbk = int(L.mjl_twin_loss_head_blocks(M))
         scr = self._scratch("loss", int(L.mjl_ppo_loss_scratch(M, A)))
-        part = self._scratch("lossparts", nbk * (1 + 3 * A))
-        lossp, glsp, biasp = part[:nbk], part[nbk:nbk * (1 + A)], part[nbk * (1 + A):nbk * (1 + 3 * A)]
-        check(L.mjl_twin_loss_head(z.data_ptr(), log_std.data_ptr(), acts.data_ptr(), old_logp.data_ptr(),
-                                   adv.data_ptr(), ret.data_ptr(), None if adv_stats is None else adv_stats.data_ptr(),
-                                   None if stats_row is None else stats_row.data_ptr(), M, A, float(clip_eps),
-                                   float(ent_coef), -20.0, 2.0, self.b[nl - 1].data_ptr() if fold else None,
-                                   scr.data_ptr(), dz.data_ptr(), lossp.data_ptr(),
-                                   glsp.data_ptr(), biasp.data_ptr(), st))
-        segs += [(lossp, loss_p, 1, nbk, 1), (glsp, self.g_log_std, 1, nbk, A), (biasp, self.gb[nl - 1], 2, nbk, A)]
+        if whole_head:
+            K = self.W[nl - 1].shape[2]
+            S = int(L.mjl_twin_head_blocks(M))
+            dzh = torch.empty((2, M, K), device=dev)
+            lossp, glsp = self._scratch("h_loss", S), self._scratch("h_gls", S * A)
+            biasp, csp = self._scratch("h_bias", 2 * S * A), self._scratch("h_cs", 2 * S * K)
+            gwp = self._scratch("h_gw", 2 * S * A * K)
+            check(L.mjl_twin_head(zh.data_ptr(), self.b[nl - 2].data_ptr(), self.W[nl - 1].data_ptr(),
+                                  self.b[nl - 1].data_ptr(), log_std.data_ptr(), acts.data_ptr(), old_logp.data_ptr(),
+                                  adv.data_ptr(), ret.data_ptr(), None if adv_stats is None else adv_stats.data_ptr(),
+                                  None if stats_row is None else stats_row.data_ptr(), M, A, K, float(clip_eps),
+                                  float(ent_coef), -20.0, 2.0, scr.data_ptr(), dzh.data_ptr(), csp.data_ptr(),
+                                  gwp.data_ptr(), lossp.data_ptr(), glsp.data_ptr(), biasp.data_ptr(), st))
+            segs += [(lossp, loss_p, 1, S, 1), (glsp, self.g_log_std, 1, S, A), (biasp, self.gb[nl - 1], 2, S, A),
+                     (gwp, self.gW[nl - 1], 2, S, A * K), (csp, self.gb[nl - 2], 2, S, K)]
+            self._keep_head = (zh, dzh)
+        else:
+            dz = torch.empty((2, M, A), device=dev)
+            nbk = int(L.mjl_twin_loss_head_blocks(M))
+            part = self._scratch("lossparts", nbk * (1 + 3 * A))
+            lossp, glsp, biasp = part[:nbk], part[nbk:nbk * (1 + A)], part[nbk * (1 + A):nbk * (1 + 3 * A)]
+            check(L.mjl_twin_loss_head(z.data_ptr(), log_std.data_ptr(), acts.data_ptr(), old_logp.data_ptr(),
+                                       adv.data_ptr(), ret.data_ptr(),
+                                       None if adv_stats is None else adv_stats.data_ptr(),
+                                       None if stats_row is None else stats_row.data_ptr(), M, A, float(clip_eps),
+                                       float(ent_coef), -20.0, 2.0, self.b[nl - 1].data_ptr() if fold else None,
+                                       scr.data_ptr(), dz.data_ptr(), lossp.data_ptr(),
+                                       glsp.data_ptr(), biasp.data_ptr(), st))
+            segs += [(lossp, loss_p, 1, nbk, 1), (glsp, self.g_log_std, 1, nbk, A),
+                     (biasp, self.gb[nl - 1], 2, nbk, A)]
         # (32-row chunks — 4x the blocks — where the minibatch is small: 8.4 against 9.0 us per pass
         # at 8,192 rows; at 65,536 the 4x partials cost more than they gain)
         ch = COLSUM_CHUNK if M > 16384 else 32
         ch = ch if M % ch == 0 else M
         R = M // ch  # column-sum partial rows per matrix
-        g = dz
+        g = dzh if whole_head else dz
         main = torch.cuda.current_stream(dev)
         side = _side(dev) if SIDE_STREAM else None
         keep = []  # main-stream tensors the side stream reads: alive until the next step
         # the output layers' backward and the last hidden layer's tanh backward as one launch
         head_fused = FUSED_ENDS and bool(self._fused & 2) and nl >= 2 and M % HEAD_BWD_ROWS == 0
-        for l in range(nl - 1, -1, -1):
+        for l in range(nl - 2 if whole_head else nl - 1, -1, -1):
             N, K = self.W[l].shape[1], self.W[l].shape[2]
             xin = hs[l]  # the layer's input: H_{l-1}, or the observations for l = 0
             if head_fused and l == nl - 1:  # dZ_{l-1}, its column-sum partials, this layer's dW partials
@@ -309,7 +337,7 @@ class TwinNets:
             # split-K slices of the weight gradient: the thin layers (the 21 / 1-unit outputs, the 54-wide
             # input) are a few output tiles per slice, so they take more, shorter slices
             s = (HIDDEN_SPLITS or splits) if (N >= 64 and K >= 64) else max(splits, THIN_SPLITS or min(64, M // 256))
-            if head_fused and l == nl - 2:  # (its dZ and bias partials came from the fused launch)
+            if (head_fused or whole_head) and l == nl - 2:  # (its dZ and bias partials came from a fused launch)
                 dzl = g
             elif l < nl - 1:  # tanh layer: dZ = dH (1 - H^2) and the bias gradient's partials in one pass
                 dzl = torch.empty_like(g)

@@ -103,6 +103,26 @@ int main(int argc, char** argv) {
       }, reps);
       printf("M %6d  twin_loss_head  RB 64: %7.2f us   RB 128: %7.2f us\n", M, t64 * 1e3, t128 * 1e3);
     }
+    {  // the fused head (mjl_twin_head's kernel), statistics from a table row
+      float *zh = dev_rand(2ull * M * N, 14, 1.f), *lstd = dev_rand(A, 12, 0.3f), *st = dev_rand(2, 13, 1.f);
+      float *dzh2, *cs2, *gw2, *lossp2, *glsp2, *biasp2;
+      int* row;
+      const int S = (M / kThRows) < kThBlocks / 2 ? (M / kThRows) : kThBlocks / 2;
+      (void)hipMalloc(&dzh2, 8ull * M * N);
+      (void)hipMalloc(&cs2, 8ull * S * N);
+      (void)hipMalloc(&gw2, 8ull * S * A * N);
+      (void)hipMalloc(&lossp2, 4ull * S);
+      (void)hipMalloc(&glsp2, 4ull * S * A);
+      (void)hipMalloc(&biasp2, 8ull * S * A);
+      (void)hipMalloc(&row, 4);
+      (void)hipMemset(row, 0, 4);
+      TwinHeadArgs ha{zh, b0, Wo, b0, lstd, act, lp, av, rt, st, row, nullptr, 0, M, 0.2f, 0.01f, -20.f, 2.f,
+                      dzh2, cs2, gw2, lossp2, glsp2, biasp2};
+      const float th = time_ms([&] {
+        hipLaunchKernelGGL((twin_head_kernel<kThA, kThK>), dim3(2 * S), dim3(256), 0, 0, ha);
+      }, reps);
+      printf("M %6d  twin_head (fused forward + losses + backward)  %7.2f us\n", M, th * 1e3);
+    }
     const double in_bytes = 2.0 * M * N * 4 + 3.0 * M * K0 * 4, hb_bytes = 4.0 * M * N * 4;
     printf("M %6d  gather_in %7.2f us (%5.1f TFLOP/s, %5.2f TB/s)   head_bwd %7.2f us (%5.2f TB/s)\n", M, t_in * 1e3,
            2.0 * M * K0 * 2 * N / (t_in * 1e-3) / 1e12, in_bytes / (t_in * 1e-3) / 1e12, t_hb * 1e3,
