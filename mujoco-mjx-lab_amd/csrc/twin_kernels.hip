@@ -27,6 +27,22 @@ __device__ __forceinline__ tw_f2 tw_fma(tw_f2 a, float b, tw_f2 c) {
   return __builtin_elementwise_fma(a, tw_f2{b, b}, c);
 }
 
+// tanh without branches, for tiles on a launch's critical path: the device library's odd polynomial
+// below |x| = 0.625, 1 - 2 / (e^{2|x|} + 1) above it (v_exp_f32, v_rcp_f32), both evaluated and one
+// selected; within 3.6 ulp of tanhf over [-12, 12] (tools/twin_micro.hip). The library's tanhf
+// branches per lane on |x|, so a wave holding both kinds of values runs both paths and their
+// exec-mask bookkeeping (~35 instructions per value against ~15).
+__device__ __forceinline__ float tw_tanh(float x) {
+  const float ax = fabsf(x), x2 = x * x;
+  float q = fmaf(__uint_as_float(0xbbbac73du), x2, __uint_as_float(0x3ca908c9u));
+  q = fmaf(x2, q, __uint_as_float(0xbd5c1c4eu));
+  q = fmaf(x2, q, __uint_as_float(0x3e088382u));
+  q = fmaf(x2, q, __uint_as_float(0xbeaaaa99u));
+  const float small = fmaf(x2, ax * q, ax);
+  const float big = fmaf(-2.f, __builtin_amdgcn_rcpf(__expf(2.f * ax) + 1.f), 1.f);
+  return copysignf(ax < 0.625f ? small : big, x);
+}
+
 // ------------------------------------------------------------------ gather + input layer
 constexpr int kTinRows = 32;  // minibatch rows per block
 constexpr int kTinK0 = 54;    // instantiated input width (the humanoid observation)
@@ -426,7 +442,8 @@ __global__ __launch_bounds__(256) void twin_head_kernel(TwinHeadArgs p) {
       const int q = t + 256 * i, r = q / (K / 4), c4 = q - r * (K / 4);
       float4 h = make_float4(0.f, 0.f, 0.f, 0.f);
       if (r < rows)
-        h = make_float4(tanhf(zv[i].x + bq.x), tanhf(zv[i].y + bq.y), tanhf(zv[i].z + bq.z), tanhf(zv[i].w + bq.w));
+        h = make_float4(tw_tanh(zv[i].x + bq.x), tw_tanh(zv[i].y + bq.y), tw_tanh(zv[i].z + bq.z),
+                        tw_tanh(zv[i].w + bq.w));
       *reinterpret_cast<float4*>(&hs[r * HS + 4 * c4]) = h;
     }
     if (net == 0) {
@@ -465,21 +482,24 @@ __global__ __launch_bounds__(256) void twin_head_kernel(TwinHeadArgs p) {
       sz[row * ZS + a] = a < A ? zz + p.bo[net * A + a] : 0.f;
     }
     __syncthreads();
-    // ---- per row: the losses and dz (wave 0, lane = row)
-    if (w == 0) {
-      const int r = lane;
+    // ---- per row: the losses and dz, four lanes per row (lane quarter q takes columns q, q + 4, ...;
+    // the row's log-density sum over the quad by DPP, the same total in all four lanes)
+    {
+      const int r = t >> 2, q = t & 3;
+      float* zr = &sz[r * ZS];
+      float* xr = &sx[r * 32];
       float surr = 0.f;
       if (r < rows) {
-        float* zr = &sz[r * ZS];
         if (net == 0) {
-          float* xr = &sx[r * 32];
           float qs = 0.f;
-          for (int j = 0; j < A; j++) {
+          for (int j = q; j < A; j += 4) {
             const float m = tanhf(zr[j]), d = xr[j] - m;
             zr[j] = d;
             xr[j] = m;
             qs += d * d * ivs[j];
           }
+          qs += dpp_f<0xb1>(qs);  // quad_perm [1, 0, 3, 2]
+          qs += dpp_f<0x4e>(qs);  // quad_perm [2, 3, 0, 1]
           const float logp = -0.5f * (qs + lss_s);
           const float ratio = expf(logp - srow[0][r]);
           const float an = (srow[1][r] - mu_s) / (sd_s + 1e-8f);
@@ -491,22 +511,22 @@ __global__ __launch_bounds__(256) void twin_head_kernel(TwinHeadArgs p) {
           const float w2 = t2 < t1 ? 1.f : (t1 == t2 ? 0.5f : 0.f);
           const float dratio = (-1.f / nf) * (w1 * an + ((ratio >= lo && ratio <= hi) ? w2 * an : 0.f));
           const float dlogp = dratio * ratio;
-          for (int j = 0; j < A; j++) {
+          for (int j = q; j < A; j += 4) {
             const float d = zr[j], m = xr[j], iv = ivs[j];
             xr[j] = dlogp * (d * d * iv - 1.f);    // d logp / d s_j = q_j - 1
             zr[j] = dlogp * d * iv * (1.f - m * m);  // d loss / d z_j
           }
         } else {
-          zr[0] = 2.f * (zr[0] - srow[2][r]) / nf;  // value: d loss / d v (train_ppo.py:218-220)
-          for (int j = 1; j < A; j++) zr[j] = 0.f;
+          if (q == 0) zr[0] = 2.f * (zr[0] - srow[2][r]) / nf;  // value: d loss / d v (train_ppo.py:218-220)
+          for (int j = (q == 0 ? 4 : q); j < A; j += 4) zr[j] = 0.f;
         }
       } else {
-        for (int j = 0; j < 32; j++) {
-          sz[r * ZS + j] = 0.f;
-          sx[r * 32 + j] = 0.f;
+        for (int j = q; j < 32; j += 4) {
+          zr[j] = 0.f;
+          xr[j] = 0.f;
         }
       }
-      srow[3][r] = surr;
+      if (q == 0) srow[3][r] = surr;
     }
     __syncthreads();
     // ---- the chunk's column sums into the workgroup's accumulators (rows in order, chunks in order)

@@ -13,6 +13,274 @@
 
 using namespace mjl;
 
+namespace mjl {
+// the fused head with s_memtime stamps (workgroup 6, thread 0), cycles accumulated per phase
+template <int A, int K>
+__global__ __launch_bounds__(256) void th_stamped(TwinHeadArgs p, unsigned long long* stamps) {
+  unsigned long long tq = __builtin_amdgcn_s_memtime();
+  auto STMP = [&](int i) { if (threadIdx.x == 0 && blockIdx.x == 6) { const unsigned long long x = __builtin_amdgcn_s_memtime(); stamps[i] += x - tq; tq = x; } };
+  static_assert(A <= 31 && K % 64 == 0 && K == 4 * 64, "tile shape: 4 waves x 2 column tiles of 32");
+  constexpr int R = kThRows, HS = kThHS, ZS = kThZS;
+  __shared__ __attribute__((aligned(16))) float hs[R * HS];  // H of the chunk
+  __shared__ __attribute__((aligned(16))) float ws[32 * HS];  // W_out rows, rows A..31 zero
+  __shared__ float red[4 * 16 * 64];                          // z partials of the 4 waves
+  __shared__ float sz[R * ZS];                                // z, then d, then dz (cols A..31 zero)
+  __shared__ float sx[R * 32];                                // act, then the mean, then c_j
+  __shared__ float srow[4][R];                                // old_logp, adv, ret, surr
+  __shared__ float ivs[32];
+  __shared__ float lss_s, mu_s, sd_s;
+  __shared__ float acc_col[2 * 32 + 1];                       // c_j, dz column sums, loss: chunk order
+  __shared__ float csh[2][K];
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6, li = lane & 31, kh = lane >> 5;
+  const int net = blockIdx.x & 1, S = (int)(gridDim.x >> 1), blk = (int)(blockIdx.x >> 1), n = p.n;
+  const int nchunk = (n + R - 1) / R;
+  // ---- once per workgroup: W_out of this net, the log_std terms, the advantage statistics
+  {
+    constexpr int Q = 32 * K / 4 / 256;  // float4 per thread
+#pragma unroll
+    for (int i = 0; i < Q; i++) {
+      const int q = t + 256 * i, a = q / (K / 4), c4 = q - a * (K / 4);
+      const float4 v = a < A ? *reinterpret_cast<const float4*>(p.W + ((size_t)net * A + a) * K + 4 * c4)
+                             : make_float4(0.f, 0.f, 0.f, 0.f);
+      *reinterpret_cast<float4*>(&ws[a * HS + 4 * c4]) = v;
+    }
+  }
+  if (w == 0) {
+    const float ls = lane < A ? fminf(fmaxf(p.log_std[lane], p.ls_lo), p.ls_hi) : 0.f;  // networks.py:103
+    if (lane < 32) ivs[lane] = lane < A ? expf(-2.f * ls) : 0.f;
+    const float tot = wave_sum_dpp(lane < A ? 2.f * ls + kLog2Pi : 0.f);
+    float mu, sdv;
+    if (p.adv_stats) {
+      const float* st = p.adv_stats + (p.stats_row ? 2 * (size_t)*p.stats_row : 0);
+      mu = st[0];
+      sdv = st[1];
+    } else {
+      adv_merge_wave(p.adv_part, p.nb_adv, lane, mu, sdv);
+    }
+    if (lane == 0) {
+      lss_s = tot;
+      mu_s = mu;
+      sd_s = sdv;
+    }
+  }
+  if (t < 2 * 32 + 1) acc_col[t] = 0.f;
+  tw_f32x16 gwacc[2];
+  float csacc[2] = {0.f, 0.f};
+#pragma unroll
+  for (int c = 0; c < 2; c++)
+#pragma unroll
+    for (int v = 0; v < 16; v++) gwacc[c][v] = 0.f;
+  const float4 bq = *reinterpret_cast<const float4*>(p.bh + (size_t)net * K + 4 * (t & (K / 4 - 1)));
+  const float nf = (float)n;
+  STMP(0);
+  for (int ch = blk; ch < nchunk; ch += S) {
+    const int r0 = ch * R, rows = min(R, n - r0);
+    // ---- loads: the chunk's pre-activations, actions and per-row scalars, all issued together
+    constexpr int QZ = R * K / 4 / 256;  // float4 of zh per thread (16)
+    float4 zv[QZ];
+#pragma unroll
+    for (int i = 0; i < QZ; i++) {
+      const int q = t + 256 * i, r = q / (K / 4), c4 = q - r * (K / 4);
+      zv[i] = r < rows ? *reinterpret_cast<const float4*>(p.zh + ((size_t)net * n + r0 + r) * K + 4 * c4)
+                       : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+    constexpr int QA = (R * 32 + 255) / 256;
+    float av[QA];
+    if (net == 0) {
+#pragma unroll
+      for (int i = 0; i < QA; i++) {
+        const int e = t + 256 * i;
+        av[i] = e < rows * A ? p.act[(size_t)r0 * A + e] : 0.f;
+      }
+    }
+    float rv0 = 0.f, rv1 = 0.f, rv2 = 0.f;
+    if (t < rows) {
+      rv0 = p.old_logp[r0 + t];
+      rv1 = p.adv[r0 + t];
+      rv2 = p.ret[r0 + t];
+    }
+    __syncthreads();  // (the previous chunk's reads of hs / sz / sx are done)
+#pragma unroll
+    for (int i = 0; i < QZ; i++) {
+      const int q = t + 256 * i, r = q / (K / 4), c4 = q - r * (K / 4);
+      float4 h = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (r < rows)
+        h = make_float4(tw_tanh(zv[i].x + bq.x), tw_tanh(zv[i].y + bq.y), tw_tanh(zv[i].z + bq.z),
+                        tw_tanh(zv[i].w + bq.w));
+      *reinterpret_cast<float4*>(&hs[r * HS + 4 * c4]) = h;
+    }
+    if (net == 0) {
+#pragma unroll
+      for (int i = 0; i < QA; i++) {
+        const int e = t + 256 * i;
+        if (e < rows * A) sx[(e / A) * 32 + e % A] = av[i];
+      }
+    }
+    if (t < R) {
+      srow[0][t] = rv0;
+      srow[1][t] = rv1;
+      srow[2][t] = rv2;
+    }
+    __syncthreads();
+  STMP(1);
+    // ---- z = H W^T: wave w takes row tile w & 1 and K half w >> 1
+    {
+      const int rt = w & 1, k0 = (w >> 1) * (K / 2);
+      tw_f32x16 acc;
+#pragma unroll
+      for (int v = 0; v < 16; v++) acc[v] = 0.f;
+      const float* ha = &hs[(32 * rt + li) * HS + k0 + kh];
+      const float* wb = &ws[li * HS + k0 + kh];
+#pragma unroll 8
+      for (int s = 0; s < K / 4; s++) acc = __builtin_amdgcn_mfma_f32_32x32x2f32(ha[2 * s], wb[2 * s], acc, 0, 0, 0);
+#pragma unroll
+      for (int v = 0; v < 16; v++) red[(w * 16 + v) * 64 + lane] = acc[v];
+    }
+    __syncthreads();
+  STMP(2);
+    // z[row][a] = lower K half + upper K half + bo (C[i][j] in register (i & 3) + 4 (i >> 3) of lane
+    // j + 32 ((i >> 2) & 1))
+    for (int e = t; e < R * 32; e += 256) {
+      const int row = e >> 5, a = e & 31, rt = row >> 5, i = row & 31;
+      const int v = (i & 3) + 4 * (i >> 3), L = a + 32 * ((i >> 2) & 1);
+      const float zz = red[(rt * 16 + v) * 64 + L] + red[((2 + rt) * 16 + v) * 64 + L];
+      sz[row * ZS + a] = a < A ? zz + p.bo[net * A + a] : 0.f;
+    }
+    __syncthreads();
+  STMP(3);
+    // ---- per row: the losses and dz, four lanes per row (lane quarter q takes columns q, q + 4, ...;
+    // the row's log-density sum over the quad by DPP, the same total in all four lanes)
+    {
+      const int r = t >> 2, q = t & 3;
+      float* zr = &sz[r * ZS];
+      float* xr = &sx[r * 32];
+      float surr = 0.f;
+      if (r < rows) {
+        if (net == 0) {
+          float qs = 0.f;
+          for (int j = q; j < A; j += 4) {
+            const float m = tanhf(zr[j]), d = xr[j] - m;
+            zr[j] = d;
+            xr[j] = m;
+            qs += d * d * ivs[j];
+          }
+          qs += dpp_f<0xb1>(qs);  // quad_perm [1, 0, 3, 2]
+          qs += dpp_f<0x4e>(qs);  // quad_perm [2, 3, 0, 1]
+          const float logp = -0.5f * (qs + lss_s);
+          const float ratio = expf(logp - srow[0][r]);
+          const float an = (srow[1][r] - mu_s) / (sd_s + 1e-8f);
+          const float lo = 1.f - p.clip_eps, hi = 1.f + p.clip_eps;
+          const float rc = fminf(fmaxf(ratio, lo), hi);
+          const float t1 = ratio * an, t2 = rc * an;
+          surr = fminf(t1, t2);
+          const float w1 = t1 < t2 ? 1.f : (t1 == t2 ? 0.5f : 0.f);
+          const float w2 = t2 < t1 ? 1.f : (t1 == t2 ? 0.5f : 0.f);
+          const float dratio = (-1.f / nf) * (w1 * an + ((ratio >= lo && ratio <= hi) ? w2 * an : 0.f));
+          const float dlogp = dratio * ratio;
+          for (int j = q; j < A; j += 4) {
+            const float d = zr[j], m = xr[j], iv = ivs[j];
+            xr[j] = dlogp * (d * d * iv - 1.f);    // d logp / d s_j = q_j - 1
+            zr[j] = dlogp * d * iv * (1.f - m * m);  // d loss / d z_j
+          }
+        } else {
+          if (q == 0) zr[0] = 2.f * (zr[0] - srow[2][r]) / nf;  // value: d loss / d v (train_ppo.py:218-220)
+          for (int j = (q == 0 ? 4 : q); j < A; j += 4) zr[j] = 0.f;
+        }
+      } else {
+        for (int j = q; j < 32; j += 4) {
+          zr[j] = 0.f;
+          xr[j] = 0.f;
+        }
+      }
+      if (q == 0) srow[3][r] = surr;
+    }
+    __syncthreads();
+  STMP(4);
+    // ---- the chunk's column sums into the workgroup's accumulators (rows in order, chunks in order)
+    if (t < 2 * 32 + 1) {
+      const bool pol = net == 0;
+      const float* col = t == 2 * 32 ? srow[3] : t < 32 ? &sx[t] : &sz[t - 32];
+      const int cstr = t == 2 * 32 ? 1 : (t < 32 ? 32 : ZS);
+      const bool on = t == 2 * 32 ? pol : (t < 32 ? (pol && t < A) : (t - 32 < A));
+      if (on) {
+        float p0 = 0.f, p1 = 0.f, p2 = 0.f, p3 = 0.f;
+        for (int r = 0; r < R; r += 4) {
+          p0 += col[r * cstr]; p1 += col[(r + 1) * cstr]; p2 += col[(r + 2) * cstr]; p3 += col[(r + 3) * cstr];
+        }
+        acc_col[t] += (p0 + p1) + (p2 + p3);
+      }
+    }
+  STMP(5);
+    // ---- dH = dz W, dZ = dH (1 - H^2): wave w takes column tiles 2w, 2w + 1 over both row tiles
+#pragma unroll
+    for (int c = 0; c < 2; c++) {
+      const int ct = 2 * w + c, col = 32 * ct + li;
+#pragma unroll
+      for (int rt = 0; rt < 2; rt++) {
+        tw_f32x16 acc;
+#pragma unroll
+        for (int v = 0; v < 16; v++) acc[v] = 0.f;
+#pragma unroll
+        for (int s = 0; s < (A + 1) / 2; s++)
+          acc = __builtin_amdgcn_mfma_f32_32x32x2f32(sz[(32 * rt + li) * ZS + 2 * s + kh], ws[(2 * s + kh) * HS + col],
+                                                     acc, 0, 0, 0);
+        float* out = p.dzh + ((size_t)net * n + r0) * K + col;
+#pragma unroll
+        for (int v = 0; v < 16; v++) {
+          const int row = 32 * rt + (v & 3) + 8 * (v >> 2) + 4 * kh;
+          const float y = hs[row * HS + col];
+          const float dzv = acc[v] * (1.f - y * y);
+          if (row < rows) out[(size_t)row * K] = dzv;
+          csacc[c] += dzv;
+        }
+      }
+    }
+  STMP(6);
+    // ---- the output weight gradient dz^T H, accumulated over the chunks: column tiles 2w, 2w + 1
+#pragma unroll
+    for (int c = 0; c < 2; c++) {
+      const int col = 32 * (2 * w + c) + li;
+#pragma unroll 8
+      for (int s = 0; s < R / 2; s++)
+        gwacc[c] = __builtin_amdgcn_mfma_f32_32x32x2f32(sz[(2 * s + kh) * ZS + li], hs[(2 * s + kh) * HS + col],
+                                                        gwacc[c], 0, 0, 0);
+    }
+  STMP(7);
+  }
+  // ---- the workgroup's partials
+  const int nb = S;
+#pragma unroll
+  for (int c = 0; c < 2; c++) {
+    const int col = 32 * (2 * w + c) + li;
+#pragma unroll
+    for (int v = 0; v < 16; v++) {
+      const int a = (v & 3) + 8 * (v >> 2) + 4 * kh;
+      if (a < A) p.gw[(((size_t)net * nb + blk) * A + a) * K + col] = gwacc[c][v];
+    }
+    csh[kh][col] = csacc[c];
+  }
+  __syncthreads();
+  if (t < K) p.cs[((size_t)net * nb + blk) * K + t] = csh[0][t] + csh[1][t];
+  STMP(8);
+  if (net == 0) {
+    if (t == 0) {
+      float val = -acc_col[2 * 32] / nf;
+      if (blk == 0) val -= p.ent_coef * (0.5f * ((float)A + lss_s) / (float)A);  // entropy, train_ppo.py:215
+      p.lossp[blk] = val;
+    }
+    if (t < A) {
+      const float ls = p.log_std[t];
+      const float val = blk == 0 ? acc_col[t] - p.ent_coef / (float)A : acc_col[t];
+      p.glsp[(size_t)blk * A + t] = (ls >= p.ls_lo && ls <= p.ls_hi) ? val : 0.f;
+      p.biasp[(size_t)blk * A + t] = acc_col[32 + t];
+    }
+  } else if (t < A) {
+    p.biasp[((size_t)nb + blk) * A + t] = t == 0 ? acc_col[32] : 0.f;
+  }
+}
+
+}  // namespace mjl
+
 
 
 
@@ -122,6 +390,14 @@ int main(int argc, char** argv) {
         hipLaunchKernelGGL((twin_head_kernel<kThA, kThK>), dim3(2 * S), dim3(256), 0, 0, ha);
       }, reps);
       printf("M %6d  twin_head (fused forward + losses + backward)  %7.2f us\n", M, th * 1e3);
+      unsigned long long* stp;
+      (void)hipMalloc(&stp, 16 * 8);
+      (void)hipMemset(stp, 0, 16 * 8);
+      hipLaunchKernelGGL((th_stamped<kThA, kThK>), dim3(2 * S), dim3(256), 0, 0, ha, stp);
+      unsigned long long hs[16];
+      (void)hipMemcpy(hs, stp, 16 * 8, hipMemcpyDeviceToHost);
+      printf("   head workgroup 6 cycles: setup %llu | loads+H %llu | z MFMA %llu | z sum %llu | losses %llu | col sums %llu | dH %llu | dW %llu | partials %llu\n",
+             hs[0], hs[1], hs[2], hs[3], hs[4], hs[5], hs[6], hs[7], hs[8]);
     }
     const double in_bytes = 2.0 * M * N * 4 + 3.0 * M * K0 * 4, hb_bytes = 4.0 * M * N * 4;
     printf("M %6d  gather_in %7.2f us (%5.1f TFLOP/s, %5.2f TB/s)   head_bwd %7.2f us (%5.2f TB/s)\n", M, t_in * 1e3,
