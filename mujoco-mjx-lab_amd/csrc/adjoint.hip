@@ -2124,4 +2124,146 @@ __global__ __launch_bounds__(64, LEAN ? 2 : 1) void vjp_kernel(KParams P, VjpArg
   }
 }
 
+// Record (implicit VJP) with the constraint rows in LDS, as mjl_env_step keeps them: rows in the
+// global slab cost the record ~6 us per 2048-env launch (the same env step measured 62.1 -> 68.1 us
+// with its rows forced into global memory, tools/prof_target.py apgstep). DL: the LDS workspace (the
+// env step's 48 rows); DI: the dims of the tape image the replay reads (DHumV, whose union holds only
+// the smooth-dynamics scratch). The slot it leaves is vjp_kernel<DI, true, 1>'s, field for field:
+//  - the smooth-dynamics scratch (the image's union) goes to the slot before the rows overwrite it;
+//  - the rows go to the slot's global row layout once the solve and the sensors are done;
+//  - the A part has no LDS copy: qpos0 / qvel0 / aux go to the slot from registers at the start,
+//    and a', the factor of Hc and its inverse diagonal are formed in the freed row area,
+// so the kernel's LDS is the env step's (8 waves per CU). Rows beyond the LDS capacity take the
+// global slab in the slot (record_rows_global), as vjp_kernel does for every env.
+template <class DL, int MW> NOINL void record_rows_global(MP m, LDSA WS<DL>* W, float* rows, int gmax_efc, int gmax_con,
+                                                          int lane) {
+  Rows<true> R = global_rows<DL>(rows, gmax_efc, gmax_con);
+  build_rows<DL, true>(m, W, R, lane);
+  solver<DL, true>(m, W, R, lane);
+  sensors<DL, true>(m, W, R, lane);
+  solver_hessian<DL, true>(m, W, R, lane);  // Hc at the converged active set, into H
+}
+
+template <class DL, class DI> __global__ __launch_bounds__(64, 2) void vjp_record_kernel(KParams P, VjpArgs V) {
+  constexpr int LD = DL::LD, NV = DL::NV;
+  static_assert(LD == DI::LD && NV == DI::NV, "the tape image's dims are the workspace's, rows aside");
+  static_assert(offsetof(WS<DL>, cinert) == offsetof(WS<DI>, cinert) && offsetof(WS<DI>, cinert) % 16 == 0,
+                "the image shares the workspace's layout up to the row / smooth-scratch union");
+  static_assert(sizeof(WS<DI>) - offsetof(WS<DI>, cinert) <= sizeof(WS<DL>) - offsetof(WS<DL>, cinert),
+                "the image's union is a prefix of the workspace's");
+  static_assert(2 * LD + NV * LD <= DL::CAP * LD, "a', 1/diag and the Hc factor fit in the row area");
+  static_assert(MJL_MAXQ <= 64 && LD <= 64 && MJL_AUX_DIM <= 12, "one lane per pre-step entry");
+  static_assert(sizeof(WS<DL>) + 4 * (MJL_AUX_DIM + 3) <= kLdsBudget, "record workspace exceeds the 8-waves-per-CU LDS budget");
+  __shared__ WS<DL> Ws;
+  __shared__ float aux_s[MJL_AUX_DIM + 3];  // (as the env step kernel's: env_post's scratch past the aux)
+  LDSA WS<DL>* W = (LDSA WS<DL>*)&Ws;
+  LDSA float* aux = (LDSA float*)aux_s;
+  MP m = (MP)P.m;
+  const int env = blockIdx.x, lane = threadIdx.x;
+  if (env >= P.nenv) return;
+  const int nq = m->nq, nv = m->nv, nu = m->nu;
+  const StateBuf& S = P.s;
+  GLBA float* slot = (GLBA float*)(V.slot + (size_t)env * (size_t)V.slot_stride);
+  GLBA float* sa = slot + V.s_a;
+  constexpr int O1 = MJL_MAXQ, O2 = O1 + LD, O3 = O2 + 12;  // A part: qpos0, qvel0, aux, then a', 1/diag, Lc
+  constexpr int U0 = (int)(offsetof(WS<DI>, cinert) / 16), NI = (int)(sizeof(WS<DI>) / 16);
+  for (int i = lane; i < LD; i += 64) {  // the LD-wide vectors vjp_kernel zeroes
+    W->qvel[i] = 0.f; W->qacc_ws[i] = 0.f;
+    W->frc_bias[i] = W->frc_passive[i] = W->frc_act[i] = W->frc_smooth[i] = W->qacc_smooth[i] = 0.f;
+    W->qacc[i] = W->frc_con[i] = W->grad[i] = W->Mgrad[i] = W->search[i] = W->Ma[i] = W->Mv[i] = 0.f;
+    W->gradold[i] = W->Mgradold[i] = 0.f;
+  }
+  SYNC();
+  // state loads as vjp_kernel's (clamped lane indices, every load before the first wait)
+  const int iq = lane < nq ? lane : max(nq - 1, 0), iv = lane < nv ? lane : max(nv - 1, 0);
+  const int iu = lane < nu ? lane : max(nu - 1, 0), ia = lane < MJL_AUX_DIM ? lane : MJL_AUX_DIM - 1;
+  const float q = nq > 0 ? S.qpos[(size_t)env * nq + iq] : 0.f;
+  const float v = nv > 0 ? S.qvel[(size_t)env * nv + iv] : 0.f;
+  const float w = nv > 0 ? S.qacc_warmstart[(size_t)env * nv + iv] : 0.f;
+  float c = nu > 0 ? V.act[(size_t)env * nu + iu] : 0.f;
+  const float t = S.time[env];
+  const float ax = S.aux[(size_t)env * MJL_AUX_DIM + ia];
+  const int perm = nu > 0 ? P.env->act_perm[iu] : 0;
+  const float sgn = nu > 0 ? P.env->act_sign[iu] : 1.f;
+  if (lane < nq) W->qpos[lane] = q;
+  if (lane < nv) { W->qvel[lane] = v; W->qacc_ws[lane] = w; }
+  if (lane == 0) W->sc[SC_TIME] = t;
+  if (lane < MJL_AUX_DIM) aux[lane] = ax;
+  // the A part's pre-step state, straight from the registers (zero past nq / nv, as the zeroed A was)
+  if (lane < MJL_MAXQ) sa[lane] = lane < nq ? q : 0.f;
+  if (lane < LD) sa[O1 + lane] = lane < nv ? v : 0.f;
+  if (lane < MJL_AUX_DIM) sa[O2 + lane] = ax;
+  {  // flip + clip the action (envs.py:335-344): act[perm[j]] from lane perm[j]
+    const bool flip = rdlane(ax, 0) > 0.5f;
+    const float ap = __shfl(c, perm);
+    c = fminf(fmaxf(flip ? ap * sgn : c, -1.f), 1.f);
+    if (lane == 0) W->sc[SC_FLIP] = ax;
+  }
+  if (lane < nu) W->ctrl[lane] = c;
+  SYNC();
+  STAMP(0, lane);
+  {
+    const KinPre kp = kin_prefetch(m, lane);
+    kinematics<DL>(m, W, lane, kp);
+    com_pos_crb<DL>(m, W, lane, kp);
+    velocity_stage<DL>(m, W, lane, kp);
+  }
+  {
+    const float x = chol_factor_solve<DL>(W->M, W->H, W->invd, nv, W->frc_smooth, lane);
+    if (lane < LD) W->qacc_smooth[lane] = (lane < nv) ? x : 0.f;
+    SYNC();
+  }
+  GLBA f32x4* img = (GLBA f32x4*)(slot + V.s_w);
+  {  // the image's union: the smooth-dynamics scratch, before the rows take its place
+    const LDSA f32x4* src = (const LDSA f32x4*)W;
+    for (int i = U0 + lane; i < NI; i += 64) img[i] = src[i];
+  }
+  float* rows = (float*)(slot + V.s_r);
+  if (build_rows<DL, false>(m, W, lds_rows<DL>(W), lane)) {
+    const Rows<false> R = lds_rows<DL>(W);
+    solver<DL, false>(m, W, R, lane);
+    sensors<DL, false>(m, W, R, lane);
+    {  // the rows into the slot's global layout (what vjp_kernel's record leaves there)
+      const Rows<true> G = global_rows<DL>(rows, P.gmax_efc, P.gmax_con);
+      const int nefc = W->nefc, ncon = W->ncon;
+      for (int i = lane; i < nefc * LD / 4; i += 64) ((GLBA f32x4*)G.J)[i] = ((const LDSA f32x4*)R.J)[i];
+      for (int i = lane; i < nefc; i += 64) {
+        G.D[i] = R.D[i]; G.aref[i] = R.aref[i]; G.jar[i] = R.jar[i]; G.force[i] = R.force[i];
+        G.Jv[i] = R.Jv[i]; G.epos[i] = R.epos[i]; G.einvw[i] = R.einvw[i]; G.emeta[i] = R.emeta[i];
+      }
+      for (int i = lane; i < ncon * CONW; i += 64) G.con[i] = R.con[i];
+      for (int i = lane; i < ncon; i += 64) { G.con_pair[i] = R.con_pair[i]; G.con_efc[i] = R.con_efc[i]; }
+    }
+    solver_hessian<DL, false>(m, W, R, lane);  // Hc at the converged active set, into H
+  } else {
+    record_rows_global<DL, 2>(m, W, rows, P.gmax_efc, P.gmax_con, lane);
+  }
+  // a', 1/diag and the factor of Hc in the row area (free now), zeroed as vjp_kernel's A part is
+  LDSA float* ab = (LDSA float*)W->J;
+  for (int i = lane; i < 2 * LD + NV * LD; i += 64) ab[i] = 0.f;
+  SYNC();
+  chol_factor_solve<DL>(W->H, ab + 2 * LD, ab + LD, nv, W->frc_smooth, lane);
+  SYNC();
+  integrate<DL>(m, W, lane, ab);
+  STAMP(1, lane);
+  SYNC();
+  for (int i = lane; i < 2 * LD + NV * LD; i += 64) sa[O3 + i] = ab[i];
+  {  // the rest of the image: the workspace up to the union
+    const LDSA f32x4* src = (const LDSA f32x4*)W;
+    for (int i = lane; i < U0; i += 64) img[i] = src[i];
+  }
+  float* obs = P.obs + (size_t)env * P.env->obs_dim;
+  env_post<DL>(m, W, P.env, aux, obs, lane, false);
+  if (lane == 0) { P.rew[env] = W->sc[SC_REW]; P.term[env] = W->sc[SC_TERM]; P.trunc[env] = W->sc[SC_TRUNC]; }
+  SYNC();
+  if (lane < nq) S.qpos[(size_t)env * nq + lane] = W->qpos[lane];
+  if (lane < nv) {
+    S.qvel[(size_t)env * nv + lane] = W->qvel[lane];
+    S.qacc_warmstart[(size_t)env * nv + lane] = W->qacc_ws[lane];
+  }
+  if (lane < nu) S.ctrl[(size_t)env * nu + lane] = W->ctrl[lane];
+  if (lane == 0) S.time[env] = W->sc[SC_TIME];
+  if (lane < MJL_AUX_DIM) S.aux[(size_t)env * MJL_AUX_DIM + lane] = aux[lane];
+}
+
 }  // namespace mjl

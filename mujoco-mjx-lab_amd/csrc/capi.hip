@@ -824,6 +824,15 @@ template <bool ENV, int TM = 0> static int launch_vjp(mjlBatch* B, const VjpArgs
       return MJL_OK;
     }
   }
+  // the implicit record on the humanoid dims keeps its rows in LDS (vjp_record_kernel, the same slot as
+  // vjp_kernel's record); MJL_OPT_FORCE_GLOBAL_ROWS keeps the global-row record (A/B, parity tests)
+  if constexpr (TM == 1 && ENV) {
+    if (B->model->nvc == 0 && !B->vjp_unrolled && !B->force_global_rows) {
+      hipLaunchKernelGGL((vjp_record_kernel<DHum, DHumV>), grid, block, 0, (hipStream_t)stream, P, V);
+      HIPCHK(hipGetLastError());
+      return MJL_OK;
+    }
+  }
   if (B->model->nvc == 0)
     hipLaunchKernelGGL((vjp_kernel<DHumV, ENV, TM>), grid, block, 0, (hipStream_t)stream, P, V);
   else

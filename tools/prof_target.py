@@ -7,7 +7,8 @@
   policy        mjl_policy_fwd, the PPO rollout policy (obs 54 -> 256 x 3 -> 21) on B envs
   apgmlp        mjl_small_mlp_fwd + mjl_small_mlp_bwd_input, the APG policy (55 -> 32 x 2 -> 21) on B rows
   apgstep       the APG rollout's physics (CG 4/4 model) through mjl_env_step without reset, random
-                actions, against the record kernel of the `vjp` mode (rows in LDS vs in global memory)
+                actions, against the record kernel of the `vjp` mode (rows in LDS vs in global memory;
+                PROF_FORCE_GLOBAL=1 keeps them in global memory as the record does)
 python tools/prof_target.py MODE [B] [n]"""
 import os
 import sys
@@ -88,6 +89,9 @@ elif mode == "apgstep":
     cfg = APGConfig()
     ma = apg_model(cfg, solver="cg")
     env = HumanoidEnv(mjx.put_model(ma), resolve_ids(ma, EnvConfig()), B, seed=cfg.seed)
+    if os.environ.get("PROF_FORCE_GLOBAL") == "1":  # rows in the global slab, as the record kernel keeps them
+        from mjx_amd import abi
+        env.data.set_option(abi.OPT_FORCE_GLOBAL_ROWS, 1)
     env.reset()
     g = torch.Generator(device="cuda").manual_seed(0)
     for i in range(n):
