@@ -9,6 +9,7 @@
   apgstep       the APG rollout's physics (CG 4/4 model) through mjl_env_step without reset, random
                 actions, against the record kernel of the `vjp` mode (rows in LDS vs in global memory;
                 PROF_FORCE_GLOBAL=1 keeps them in global memory as the record does)
+  recab         the APG record and the env step without reset on the same states and actions
 python tools/prof_target.py MODE [B] [n]"""
 import os
 import sys
@@ -99,6 +100,25 @@ elif mode == "apgstep":
             env.reset()
         act = (torch.rand((B, ma.nu), generator=g, device="cuda") * 2 - 1) * 0.3
         env.step(act, auto_reset=False)
+elif mode == "recab":  # the record and the env step (no reset) on the same states and actions, alternating
+    from mjx_amd.apg import HumanoidAPGEnv
+    from mjx_amd.config import APGConfig, EnvConfig
+    from mjx_amd.envs import HumanoidEnv, resolve_ids
+    sys.path.insert(0, os.path.join(ROOT, "mujoco-mjx-lab_amd"))
+    from train_apg import apg_model
+    cfg = APGConfig()
+    ma = apg_model(cfg, solver="cg")
+    env = HumanoidEnv(mjx.put_model(ma), resolve_ids(ma, EnvConfig()), B, seed=cfg.seed)
+    aenv = HumanoidAPGEnv(env, "implicit")
+    aenv.enable_vjp_tape(128)
+    env.reset()
+    g = torch.Generator(device="cuda").manual_seed(0)
+    for i in range(n):
+        act = (torch.rand((B, ma.nu), generator=g, device="cuda") * 2 - 1) * 0.3
+        st = env.get_state()
+        env.step(act, auto_reset=False)
+        env.set_state(st)
+        aenv.step_record(i % 128, act)
 elif mode == "apgmlp":
     from mjx_amd import apg, ppo
     pol = ppo.APGPolicy(55, 21, 32, 2, None, torch.Generator().manual_seed(0)).cuda()
