@@ -101,7 +101,11 @@ __global__ __launch_bounds__(256) void policy_head_kernel(const float* __restric
 // against 21.2 us at 2048; not kept. Split-K of the 21-wide output layer over the 14 waves its two
 // column blocks leave idle — each wave 2 of the 16 K chunks, the partials summed through LDS in part
 // order — measured 21.2 against 20.3 us at 1024 envs (round 6): the output layer's
-// 64-MFMA chain was not on the critical path once the other waves' barriers are counted; not kept.)
+// 64-MFMA chain was not on the critical path once the other waves' barriers are counted; not kept.
+// Four envs per workgroup on v_mfma_f32_4x4x1_16b_f32, so that 1024 envs fill all 256 CUs, bit-identical
+// to this kernel: 18.3-19.0 against 20.3 us at 1024 envs, 22.1-22.4 against 20.3 at 2048 -- the 4x4x1
+// form issues at ~40 cycles for a quarter of 16x16x4's MACs, so the CUs gained are spent on issue
+// (tools/pol4_kernel.inc, tools/pol_micro.hip, profiles/r6/pol_micro.txt); not kept.)
 constexpr int kPolMaxLayers = 6;
 constexpr int kPolLdx = 260;  // LDS row stride (floats): rows 4 banks apart, conflict-free b128
 #ifndef MJL_POL_WAVES

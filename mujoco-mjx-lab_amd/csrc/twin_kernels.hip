@@ -313,12 +313,13 @@ __global__ __launch_bounds__(256, 2) void twin_head_bwd_kernel(TwinHeadBwdArgs p
 // The twin update's head in ONE launch (train_ppo.py:204-220 for both nets' output layers, the last
 // hidden layer's bias + tanh and its tanh backward): replaces the last hidden layer's bias + tanh pass,
 // the output layers' batched GEMM, the loss launch (mjl_twin_loss_head) and the output backward
-// (mjl_twin_head_bwd). A persistent grid of at most kThBlocks workgroups, one net each (net =
-// blockIdx & 1), taking 64-row chunks blockIdx / 2, + gridDim / 2, ... Per chunk:
+// (mjl_twin_head_bwd). A persistent grid of workgroups, one net each (net = blockIdx & 1), taking
+// R-row chunks blockIdx / 2, + gridDim / 2, ...: the launch takes R = 32 with two workgroups per CU
+// (75 KB of LDS each, at most kThBlocks); R = 64 (one per CU) measured slower at every size. Per chunk:
 //   H = tanh(zh + bh) of the chunk into LDS (zh: the last hidden layer's bias-less GEMM output);
-//   z = H W^T + bo on v_mfma_f32_32x32x2_f32 (the 4 waves split the 2 row tiles x 2 K halves, summed
-//     in K order through LDS);
-//   per row (wave 0): the policy's clipped surrogate exactly as twin_loss_head_kernel (mean = tanh z,
+//   z = H W^T + bo on v_mfma_f32_32x32x2_f32 (2 K halves per 32-row tile, one wave each, summed in K
+//     order through LDS);
+//   per row (256 / R lanes, DPP sums): the policy's clipped surrogate as twin_loss_head_kernel (mean = tanh z,
 //     the Gaussian log-prob with log_std clipped, ratio, torch.minimum's tie gradient, dz = d loss /
 //     d z), or the value's dz = 2 (v - ret) / n in column 0;
 //   the chunk's column sums (the loss, d loss / d log_std, the output bias gradient) added to the
@@ -328,10 +329,10 @@ __global__ __launch_bounds__(256, 2) void twin_head_bwd_kernel(TwinHeadBwdArgs p
 // Per workgroup one partial of every reduction (block b of net k): lossp[b], glsp[b][A] (policy),
 // biasp[k][b][A], cs[k][b][K], gw[k][b][A][K], summed over the workgroups in order by
 // mjl_slice_sum_multi. Deterministic (fixed orders throughout).
-constexpr int kThRows = 64;       // rows per chunk
+constexpr int kThRows = 32;       // rows per chunk of the launch (two workgroups per CU)
 constexpr int kThK = 256;         // instantiated last hidden width
 constexpr int kThA = 21;          // instantiated output width
-constexpr int kThBlocks = 256;    // at most this many workgroups (one per CU)
+constexpr int kThBlocks = 512;    // at most this many workgroups
 constexpr int kThHS = kThK + 4;   // hs / ws row stride (16-byte rows, 4 banks apart)
 constexpr int kThZS = 33;         // sz row stride (32 output columns + 1)
 
@@ -355,13 +356,14 @@ struct TwinHeadArgs {
   float* biasp;  // out [2, S, A]: the output bias gradients
 };
 
-template <int A, int K>
-__global__ __launch_bounds__(256) void twin_head_kernel(TwinHeadArgs p) {
+template <int A, int K, int R>
+__global__ __launch_bounds__(256, 64 / R) void twin_head_kernel(TwinHeadArgs p) {
   static_assert(A <= 31 && K % 64 == 0 && K == 4 * 64, "tile shape: 4 waves x 2 column tiles of 32");
-  constexpr int R = kThRows, HS = kThHS, ZS = kThZS;
+  static_assert(R == 32 || R == 64, "32 or 64 rows per chunk");
+  constexpr int HS = kThHS, ZS = kThZS, NRT = R / 32, LPR = 256 / R;  // row tiles; lanes per loss row
   __shared__ __attribute__((aligned(16))) float hs[R * HS];  // H of the chunk
-  __shared__ __attribute__((aligned(16))) float ws[32 * HS];  // W_out rows, rows A..31 zero
-  __shared__ float red[4 * 16 * 64];                          // z partials of the 4 waves
+  __shared__ __attribute__((aligned(16))) float ws[A * HS];   // W_out rows (rows A..31 read as zero)
+  __shared__ float red[2 * NRT * 16 * 64];                    // z partials: (K half, row tile) per wave
   __shared__ float sz[R * ZS];                                // z, then d, then dz (cols A..31 zero)
   __shared__ float sx[R * 32];                                // act, then the mean, then c_j
   __shared__ float srow[4][R];                                // old_logp, adv, ret, surr
@@ -378,9 +380,9 @@ __global__ __launch_bounds__(256) void twin_head_kernel(TwinHeadArgs p) {
 #pragma unroll
     for (int i = 0; i < Q; i++) {
       const int q = t + 256 * i, a = q / (K / 4), c4 = q - a * (K / 4);
-      const float4 v = a < A ? *reinterpret_cast<const float4*>(p.W + ((size_t)net * A + a) * K + 4 * c4)
-                             : make_float4(0.f, 0.f, 0.f, 0.f);
-      *reinterpret_cast<float4*>(&ws[a * HS + 4 * c4]) = v;
+      if (a < A)
+        *reinterpret_cast<float4*>(&ws[a * HS + 4 * c4]) =
+            *reinterpret_cast<const float4*>(p.W + ((size_t)net * A + a) * K + 4 * c4);
     }
   }
   if (w == 0) {
@@ -459,16 +461,18 @@ __global__ __launch_bounds__(256) void twin_head_kernel(TwinHeadArgs p) {
       srow[2][t] = rv2;
     }
     __syncthreads();
-    // ---- z = H W^T: wave w takes row tile w & 1 and K half w >> 1
-    {
-      const int rt = w & 1, k0 = (w >> 1) * (K / 2);
+    // ---- z = H W^T: wave w < 2 NRT takes row tile w % NRT and K half w / NRT
+    if (w < 2 * NRT) {
+      const int rt = w % NRT, k0 = (w / NRT) * (K / 2);
       tw_f32x16 acc;
 #pragma unroll
       for (int v = 0; v < 16; v++) acc[v] = 0.f;
       const float* ha = &hs[(32 * rt + li) * HS + k0 + kh];
-      const float* wb = &ws[li * HS + k0 + kh];
+      const float* wb = &ws[(li < A ? li : 0) * HS + k0 + kh];
+      const bool wr = li < A;  // W_out rows A..31: zero
 #pragma unroll 8
-      for (int s = 0; s < K / 4; s++) acc = __builtin_amdgcn_mfma_f32_32x32x2f32(ha[2 * s], wb[2 * s], acc, 0, 0, 0);
+      for (int s = 0; s < K / 4; s++)
+        acc = __builtin_amdgcn_mfma_f32_32x32x2f32(ha[2 * s], wr ? wb[2 * s] : 0.f, acc, 0, 0, 0);
 #pragma unroll
       for (int v = 0; v < 16; v++) red[(w * 16 + v) * 64 + lane] = acc[v];
     }
@@ -478,28 +482,29 @@ __global__ __launch_bounds__(256) void twin_head_kernel(TwinHeadArgs p) {
     for (int e = t; e < R * 32; e += 256) {
       const int row = e >> 5, a = e & 31, rt = row >> 5, i = row & 31;
       const int v = (i & 3) + 4 * (i >> 3), L = a + 32 * ((i >> 2) & 1);
-      const float zz = red[(rt * 16 + v) * 64 + L] + red[((2 + rt) * 16 + v) * 64 + L];
+      const float zz = red[(rt * 16 + v) * 64 + L] + red[((NRT + rt) * 16 + v) * 64 + L];
       sz[row * ZS + a] = a < A ? zz + p.bo[net * A + a] : 0.f;
     }
     __syncthreads();
-    // ---- per row: the losses and dz, four lanes per row (lane quarter q takes columns q, q + 4, ...;
-    // the row's log-density sum over the quad by DPP, the same total in all four lanes)
+    // ---- per row: the losses and dz, LPR lanes per row (lane q of the row's group takes columns q,
+    // q + LPR, ...; the row's log-density sum over the group by DPP, the same total in all its lanes)
     {
-      const int r = t >> 2, q = t & 3;
+      const int r = t / LPR, q = t % LPR;
       float* zr = &sz[r * ZS];
       float* xr = &sx[r * 32];
       float surr = 0.f;
       if (r < rows) {
         if (net == 0) {
           float qs = 0.f;
-          for (int j = q; j < A; j += 4) {
+          for (int j = q; j < A; j += LPR) {
             const float m = tanhf(zr[j]), d = xr[j] - m;
             zr[j] = d;
             xr[j] = m;
             qs += d * d * ivs[j];
           }
-          qs += dpp_f<0xb1>(qs);  // quad_perm [1, 0, 3, 2]
-          qs += dpp_f<0x4e>(qs);  // quad_perm [2, 3, 0, 1]
+          qs += dpp_f<0xb1>(qs);                // quad_perm [1, 0, 3, 2]
+          qs += dpp_f<0x4e>(qs);                // quad_perm [2, 3, 0, 1]
+          if constexpr (LPR == 8) qs += dpp_f<0x141>(qs);  // row_half_mirror: the other quad of the 8
           const float logp = -0.5f * (qs + lss_s);
           const float ratio = expf(logp - srow[0][r]);
           const float an = (srow[1][r] - mu_s) / (sd_s + 1e-8f);
@@ -511,17 +516,17 @@ __global__ __launch_bounds__(256) void twin_head_kernel(TwinHeadArgs p) {
           const float w2 = t2 < t1 ? 1.f : (t1 == t2 ? 0.5f : 0.f);
           const float dratio = (-1.f / nf) * (w1 * an + ((ratio >= lo && ratio <= hi) ? w2 * an : 0.f));
           const float dlogp = dratio * ratio;
-          for (int j = q; j < A; j += 4) {
+          for (int j = q; j < A; j += LPR) {
             const float d = zr[j], m = xr[j], iv = ivs[j];
             xr[j] = dlogp * (d * d * iv - 1.f);    // d logp / d s_j = q_j - 1
             zr[j] = dlogp * d * iv * (1.f - m * m);  // d loss / d z_j
           }
         } else {
           if (q == 0) zr[0] = 2.f * (zr[0] - srow[2][r]) / nf;  // value: d loss / d v (train_ppo.py:218-220)
-          for (int j = (q == 0 ? 4 : q); j < A; j += 4) zr[j] = 0.f;
+          for (int j = (q == 0 ? LPR : q); j < A; j += LPR) zr[j] = 0.f;
         }
       } else {
-        for (int j = q; j < 32; j += 4) {
+        for (int j = q; j < 32; j += LPR) {
           zr[j] = 0.f;
           xr[j] = 0.f;
         }
@@ -548,14 +553,16 @@ __global__ __launch_bounds__(256) void twin_head_kernel(TwinHeadArgs p) {
     for (int c = 0; c < 2; c++) {
       const int ct = 2 * w + c, col = 32 * ct + li;
 #pragma unroll
-      for (int rt = 0; rt < 2; rt++) {
+      for (int rt = 0; rt < NRT; rt++) {
         tw_f32x16 acc;
 #pragma unroll
         for (int v = 0; v < 16; v++) acc[v] = 0.f;
 #pragma unroll
-        for (int s = 0; s < (A + 1) / 2; s++)
-          acc = __builtin_amdgcn_mfma_f32_32x32x2f32(sz[(32 * rt + li) * ZS + 2 * s + kh], ws[(2 * s + kh) * HS + col],
+        for (int s = 0; s < (A + 1) / 2; s++) {
+          const int a = 2 * s + kh;  // W_out row a < A (row A of an odd A: zero)
+          acc = __builtin_amdgcn_mfma_f32_32x32x2f32(sz[(32 * rt + li) * ZS + a], a < A ? ws[a * HS + col] : 0.f,
                                                      acc, 0, 0, 0);
+        }
         float* out = p.dzh + ((size_t)net * n + r0) * K + col;
 #pragma unroll
         for (int v = 0; v < 16; v++) {

@@ -52,7 +52,7 @@ COLSUM_CHUNK = int(os.environ.get("MJL_TWIN_COLSUM_CHUNK", "128"))
 # layer's tanh backward (mjl_twin_head_bwd). MJL_TWIN_FUSED_ENDS=0: the library GEMM path for both
 FUSED_ENDS = os.environ.get("MJL_TWIN_FUSED_ENDS", "1") != "0"
 HEAD_BWD_ROWS = 128  # the fused output backward's row chunk (kHbRows)
-HEAD_ROWS = 64  # the fused head's row chunk (kThRows)
+HEAD_ROWS = 64  # the fused head takes row counts in multiples of this (its 32-row chunks, kThRows, divide it)
 # MJL_TWIN_SIDE=1: the weight-gradient GEMMs on a second stream (fork / join inside the captured step),
 # each layer's split-K dW = dZ^T X beside the main stream's dH = dZ W and the next tanh backward.
 # Measured slower and off by default: C5's per-rank update 27.8 -> 33.5 ms (the fork / join events

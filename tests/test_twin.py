@@ -37,8 +37,8 @@ def _data(n, seed=1):
 def test_twin_gradients_match_float64_autograd(monkeypatch, n, dup, fused):
     """dup: the observations handed over as the [2, M, K0] block the graphed update's gather writes
     (one copy per net) instead of one [M, K0] matrix read through a batch-stride-0 view. fused: the
-    output layers' backward + the last tanh backward as one launch (mjl_twin_head_bwd), or the library
-    GEMM path (twin.FUSED_ENDS off)."""
+    update's thin ends as single launches (at these shapes the whole head as mjl_twin_head, 32-row
+    chunks: one per workgroup at 8,192 rows, eight at 65,536), or the library GEMM path (twin.FUSED_ENDS off)."""
     monkeypatch.setattr(twin, "FUSED_ENDS", fused)
     cfg = reference_ppo_config()
     pol, val = _nets(cfg)
@@ -78,6 +78,13 @@ def test_twin_gradients_match_float64_autograd(monkeypatch, n, dup, fused):
     # the modules' parameters are views of the stacked storage, the value's padded output rows stay 0
     assert tw.owns_storage()
     assert float(tw.W[-1][1, 1:].abs().max()) == 0.0 and float(tw.gW[-1][1, 1:].abs().max()) == 0.0
+
+
+@pytest.mark.parametrize("n", [12800, 16448])
+def test_fused_head_uneven_chunks_match_float64_autograd(monkeypatch, n):
+    """The fused head where workgroups take different chunk counts: 12,800 rows = 400 chunks of 32 over
+    256 workgroups per net (one or two each), 16,448 rows = 514 chunks (two or three)."""
+    test_twin_gradients_match_float64_autograd(monkeypatch, n, False, True)
 
 
 @pytest.mark.parametrize("n", [8192, 1000])

@@ -6,11 +6,13 @@
 //          -fno-slp-vectorize -o tools/pol_micro tools/pol_micro.hip
 #include "../mujoco-mjx-lab_amd/csrc/ppo_kernels.hip"
 
+#include <cmath>
 #include <cstdio>
 #include <cstdlib>
 #include <vector>
 
 namespace mjl {
+#include "pol4_kernel.inc"
 #pragma clang fp contract(off)
 #include "pol_stamped.inc"
 #pragma clang fp contract(on)
@@ -66,6 +68,43 @@ int main(int argc, char** argv) {
     float ms;
     (void)hipEventElapsedTime(&ms, e0, e1);
     printf("B %5d  policy_rollout_kernel %8.2f us\n", B, 1000.f * ms / reps);
+    {  // the 4-env layout: same bits, time
+      std::vector<float> a16((size_t)B * 21), l16(B), a4((size_t)B * 21), l4(B);
+      (void)hipMemcpy(a16.data(), act, a16.size() * 4, hipMemcpyDeviceToHost);
+      (void)hipMemcpy(l16.data(), lp, l16.size() * 4, hipMemcpyDeviceToHost);
+      (void)hipMemset(act, 0, a16.size() * 4);
+      const dim3 g4((B + 3) / 4), b4(64 * kPol4Waves);
+      for (int i = 0; i < 10; i++)
+        hipLaunchKernelGGL(policy_rollout4_kernel, g4, b4, 0, 0, obs, mean, var, 10.f, params, pd, log_std, eps, B, act, lp);
+      (void)hipEventRecord(e0, 0);
+      for (int i = 0; i < reps; i++)
+        hipLaunchKernelGGL(policy_rollout4_kernel, g4, b4, 0, 0, obs, mean, var, 10.f, params, pd, log_std, eps, B, act, lp);
+      (void)hipEventRecord(e1, 0);
+      (void)hipEventSynchronize(e1);
+      float ms4;
+      (void)hipEventElapsedTime(&ms4, e0, e1);
+      (void)hipMemcpy(a4.data(), act, a4.size() * 4, hipMemcpyDeviceToHost);
+      (void)hipMemcpy(l4.data(), lp, l4.size() * 4, hipMemcpyDeviceToHost);
+      size_t diff = 0;
+      double md = 0;
+      for (size_t i = 0; i < a4.size(); i++) { diff += a4[i] != a16[i]; md = fmax(md, fabs(a4[i] - a16[i])); }
+      for (int i = 0; i < B; i++) { diff += l4[i] != l16[i]; md = fmax(md, fabs(l4[i] - l16[i])); }
+      printf("B %5d  policy_rollout4_kernel %8.2f us  (outputs differing from the 16-env kernel: %zu, max |diff| %.3g)\n",
+             B, 1000.f * ms4 / reps, diff, md);
+      (void)hipMemset(st, 0, 64 * 8);
+      for (int i = 0; i < reps; i++)
+        hipLaunchKernelGGL(pol4_stamped, g4, b4, 0, 0, st, obs, mean, var, 10.f, params, pd, log_std, eps, B, act, lp);
+      (void)hipDeviceSynchronize();
+      unsigned long long h4[64];
+      (void)hipMemcpy(h4, st, 64 * 8, hipMemcpyDeviceToHost);
+      const char* nm4[13] = {"prologue", "L0 mfma", "L0 bar", "L1 mfma", "L1 bar", "L2 mfma", "L2 bar", "L3 mfma", "L3 bar", "-", "-", "-", "head"};
+      for (int w = 0; w < 2; w++) {
+        printf("   4-env wave %d cycles:", w ? 3 : 0);
+        for (int i = 0; i < 13; i++)
+          if (nm4[i][0] != '-') printf(" %s %llu |", nm4[i], h4[16 * w + i] / reps);
+        printf("\n");
+      }
+    }
     (void)hipMemset(st, 0, 64 * 8);
     for (int i = 0; i < reps; i++)
       hipLaunchKernelGGL(pol_stamped, grid, block, 0, 0, st, obs, mean, var, 10.f, params, pd, log_std, eps, B, act, lp);

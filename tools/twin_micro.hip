@@ -15,15 +15,16 @@ using namespace mjl;
 
 namespace mjl {
 // the fused head with s_memtime stamps (workgroup 6, thread 0), cycles accumulated per phase
-template <int A, int K>
-__global__ __launch_bounds__(256) void th_stamped(TwinHeadArgs p, unsigned long long* stamps) {
+template <int A, int K, int R>
+__global__ __launch_bounds__(256, 64 / R) void th_stamped(TwinHeadArgs p, unsigned long long* stamps) {
   unsigned long long tq = __builtin_amdgcn_s_memtime();
   auto STMP = [&](int i) { if (threadIdx.x == 0 && blockIdx.x == 6) { const unsigned long long x = __builtin_amdgcn_s_memtime(); stamps[i] += x - tq; tq = x; } };
   static_assert(A <= 31 && K % 64 == 0 && K == 4 * 64, "tile shape: 4 waves x 2 column tiles of 32");
-  constexpr int R = kThRows, HS = kThHS, ZS = kThZS;
+  static_assert(R == 32 || R == 64, "32 or 64 rows per chunk");
+  constexpr int HS = kThHS, ZS = kThZS, NRT = R / 32, LPR = 256 / R;  // row tiles; lanes per loss row
   __shared__ __attribute__((aligned(16))) float hs[R * HS];  // H of the chunk
-  __shared__ __attribute__((aligned(16))) float ws[32 * HS];  // W_out rows, rows A..31 zero
-  __shared__ float red[4 * 16 * 64];                          // z partials of the 4 waves
+  __shared__ __attribute__((aligned(16))) float ws[A * HS];   // W_out rows (rows A..31 read as zero)
+  __shared__ float red[2 * NRT * 16 * 64];                    // z partials: (K half, row tile) per wave
   __shared__ float sz[R * ZS];                                // z, then d, then dz (cols A..31 zero)
   __shared__ float sx[R * 32];                                // act, then the mean, then c_j
   __shared__ float srow[4][R];                                // old_logp, adv, ret, surr
@@ -40,9 +41,9 @@ __global__ __launch_bounds__(256) void th_stamped(TwinHeadArgs p, unsigned long 
 #pragma unroll
     for (int i = 0; i < Q; i++) {
       const int q = t + 256 * i, a = q / (K / 4), c4 = q - a * (K / 4);
-      const float4 v = a < A ? *reinterpret_cast<const float4*>(p.W + ((size_t)net * A + a) * K + 4 * c4)
-                             : make_float4(0.f, 0.f, 0.f, 0.f);
-      *reinterpret_cast<float4*>(&ws[a * HS + 4 * c4]) = v;
+      if (a < A)
+        *reinterpret_cast<float4*>(&ws[a * HS + 4 * c4]) =
+            *reinterpret_cast<const float4*>(p.W + ((size_t)net * A + a) * K + 4 * c4);
     }
   }
   if (w == 0) {
@@ -123,16 +124,18 @@ __global__ __launch_bounds__(256) void th_stamped(TwinHeadArgs p, unsigned long 
     }
     __syncthreads();
   STMP(1);
-    // ---- z = H W^T: wave w takes row tile w & 1 and K half w >> 1
-    {
-      const int rt = w & 1, k0 = (w >> 1) * (K / 2);
+    // ---- z = H W^T: wave w < 2 NRT takes row tile w % NRT and K half w / NRT
+    if (w < 2 * NRT) {
+      const int rt = w % NRT, k0 = (w / NRT) * (K / 2);
       tw_f32x16 acc;
 #pragma unroll
       for (int v = 0; v < 16; v++) acc[v] = 0.f;
       const float* ha = &hs[(32 * rt + li) * HS + k0 + kh];
-      const float* wb = &ws[li * HS + k0 + kh];
+      const float* wb = &ws[(li < A ? li : 0) * HS + k0 + kh];
+      const bool wr = li < A;  // W_out rows A..31: zero
 #pragma unroll 8
-      for (int s = 0; s < K / 4; s++) acc = __builtin_amdgcn_mfma_f32_32x32x2f32(ha[2 * s], wb[2 * s], acc, 0, 0, 0);
+      for (int s = 0; s < K / 4; s++)
+        acc = __builtin_amdgcn_mfma_f32_32x32x2f32(ha[2 * s], wr ? wb[2 * s] : 0.f, acc, 0, 0, 0);
 #pragma unroll
       for (int v = 0; v < 16; v++) red[(w * 16 + v) * 64 + lane] = acc[v];
     }
@@ -143,29 +146,30 @@ __global__ __launch_bounds__(256) void th_stamped(TwinHeadArgs p, unsigned long 
     for (int e = t; e < R * 32; e += 256) {
       const int row = e >> 5, a = e & 31, rt = row >> 5, i = row & 31;
       const int v = (i & 3) + 4 * (i >> 3), L = a + 32 * ((i >> 2) & 1);
-      const float zz = red[(rt * 16 + v) * 64 + L] + red[((2 + rt) * 16 + v) * 64 + L];
+      const float zz = red[(rt * 16 + v) * 64 + L] + red[((NRT + rt) * 16 + v) * 64 + L];
       sz[row * ZS + a] = a < A ? zz + p.bo[net * A + a] : 0.f;
     }
     __syncthreads();
   STMP(3);
-    // ---- per row: the losses and dz, four lanes per row (lane quarter q takes columns q, q + 4, ...;
-    // the row's log-density sum over the quad by DPP, the same total in all four lanes)
+    // ---- per row: the losses and dz, LPR lanes per row (lane q of the row's group takes columns q,
+    // q + LPR, ...; the row's log-density sum over the group by DPP, the same total in all its lanes)
     {
-      const int r = t >> 2, q = t & 3;
+      const int r = t / LPR, q = t % LPR;
       float* zr = &sz[r * ZS];
       float* xr = &sx[r * 32];
       float surr = 0.f;
       if (r < rows) {
         if (net == 0) {
           float qs = 0.f;
-          for (int j = q; j < A; j += 4) {
+          for (int j = q; j < A; j += LPR) {
             const float m = tanhf(zr[j]), d = xr[j] - m;
             zr[j] = d;
             xr[j] = m;
             qs += d * d * ivs[j];
           }
-          qs += dpp_f<0xb1>(qs);  // quad_perm [1, 0, 3, 2]
-          qs += dpp_f<0x4e>(qs);  // quad_perm [2, 3, 0, 1]
+          qs += dpp_f<0xb1>(qs);                // quad_perm [1, 0, 3, 2]
+          qs += dpp_f<0x4e>(qs);                // quad_perm [2, 3, 0, 1]
+          if constexpr (LPR == 8) qs += dpp_f<0x141>(qs);  // row_half_mirror: the other quad of the 8
           const float logp = -0.5f * (qs + lss_s);
           const float ratio = expf(logp - srow[0][r]);
           const float an = (srow[1][r] - mu_s) / (sd_s + 1e-8f);
@@ -177,17 +181,17 @@ __global__ __launch_bounds__(256) void th_stamped(TwinHeadArgs p, unsigned long 
           const float w2 = t2 < t1 ? 1.f : (t1 == t2 ? 0.5f : 0.f);
           const float dratio = (-1.f / nf) * (w1 * an + ((ratio >= lo && ratio <= hi) ? w2 * an : 0.f));
           const float dlogp = dratio * ratio;
-          for (int j = q; j < A; j += 4) {
+          for (int j = q; j < A; j += LPR) {
             const float d = zr[j], m = xr[j], iv = ivs[j];
             xr[j] = dlogp * (d * d * iv - 1.f);    // d logp / d s_j = q_j - 1
             zr[j] = dlogp * d * iv * (1.f - m * m);  // d loss / d z_j
           }
         } else {
           if (q == 0) zr[0] = 2.f * (zr[0] - srow[2][r]) / nf;  // value: d loss / d v (train_ppo.py:218-220)
-          for (int j = (q == 0 ? 4 : q); j < A; j += 4) zr[j] = 0.f;
+          for (int j = (q == 0 ? LPR : q); j < A; j += LPR) zr[j] = 0.f;
         }
       } else {
-        for (int j = q; j < 32; j += 4) {
+        for (int j = q; j < 32; j += LPR) {
           zr[j] = 0.f;
           xr[j] = 0.f;
         }
@@ -216,14 +220,16 @@ __global__ __launch_bounds__(256) void th_stamped(TwinHeadArgs p, unsigned long 
     for (int c = 0; c < 2; c++) {
       const int ct = 2 * w + c, col = 32 * ct + li;
 #pragma unroll
-      for (int rt = 0; rt < 2; rt++) {
+      for (int rt = 0; rt < NRT; rt++) {
         tw_f32x16 acc;
 #pragma unroll
         for (int v = 0; v < 16; v++) acc[v] = 0.f;
 #pragma unroll
-        for (int s = 0; s < (A + 1) / 2; s++)
-          acc = __builtin_amdgcn_mfma_f32_32x32x2f32(sz[(32 * rt + li) * ZS + 2 * s + kh], ws[(2 * s + kh) * HS + col],
+        for (int s = 0; s < (A + 1) / 2; s++) {
+          const int a = 2 * s + kh;  // W_out row a < A (row A of an odd A: zero)
+          acc = __builtin_amdgcn_mfma_f32_32x32x2f32(sz[(32 * rt + li) * ZS + a], a < A ? ws[a * HS + col] : 0.f,
                                                      acc, 0, 0, 0);
+        }
         float* out = p.dzh + ((size_t)net * n + r0) * K + col;
 #pragma unroll
         for (int v = 0; v < 16; v++) {
@@ -371,11 +377,12 @@ int main(int argc, char** argv) {
       }, reps);
       printf("M %6d  twin_loss_head  RB 64: %7.2f us   RB 128: %7.2f us\n", M, t64 * 1e3, t128 * 1e3);
     }
-    {  // the fused head (mjl_twin_head's kernel), statistics from a table row
+    for (int R : {32, 64}) {  // the fused head (mjl_twin_head's kernel), statistics from a table row
       float *zh = dev_rand(2ull * M * N, 14, 1.f), *lstd = dev_rand(A, 12, 0.3f), *st = dev_rand(2, 13, 1.f);
       float *dzh2, *cs2, *gw2, *lossp2, *glsp2, *biasp2;
       int* row;
-      const int S = (M / kThRows) < kThBlocks / 2 ? (M / kThRows) : kThBlocks / 2;
+      const int cap = (R == 32 ? 512 : 256) / 2;
+      const int S = (M / R) < cap ? (M / R) : cap;
       (void)hipMalloc(&dzh2, 8ull * M * N);
       (void)hipMalloc(&cs2, 8ull * S * N);
       (void)hipMalloc(&gw2, 8ull * S * A * N);
@@ -387,13 +394,15 @@ int main(int argc, char** argv) {
       TwinHeadArgs ha{zh, b0, Wo, b0, lstd, act, lp, av, rt, st, row, nullptr, 0, M, 0.2f, 0.01f, -20.f, 2.f,
                       dzh2, cs2, gw2, lossp2, glsp2, biasp2};
       const float th = time_ms([&] {
-        hipLaunchKernelGGL((twin_head_kernel<kThA, kThK>), dim3(2 * S), dim3(256), 0, 0, ha);
+        if (R == 32) hipLaunchKernelGGL((twin_head_kernel<kThA, kThK, 32>), dim3(2 * S), dim3(256), 0, 0, ha);
+        else hipLaunchKernelGGL((twin_head_kernel<kThA, kThK, 64>), dim3(2 * S), dim3(256), 0, 0, ha);
       }, reps);
-      printf("M %6d  twin_head (fused forward + losses + backward)  %7.2f us\n", M, th * 1e3);
+      printf("M %6d  twin_head R %d (fused forward + losses + backward)  %7.2f us\n", M, R, th * 1e3);
       unsigned long long* stp;
       (void)hipMalloc(&stp, 16 * 8);
       (void)hipMemset(stp, 0, 16 * 8);
-      hipLaunchKernelGGL((th_stamped<kThA, kThK>), dim3(2 * S), dim3(256), 0, 0, ha, stp);
+      if (R == 32) hipLaunchKernelGGL((th_stamped<kThA, kThK, 32>), dim3(2 * S), dim3(256), 0, 0, ha, stp);
+      else hipLaunchKernelGGL((th_stamped<kThA, kThK, 64>), dim3(2 * S), dim3(256), 0, 0, ha, stp);
       unsigned long long hs[16];
       (void)hipMemcpy(hs, stp, 16 * 8, hipMemcpyDeviceToHost);
       printf("   head workgroup 6 cycles: setup %llu | loads+H %llu | z MFMA %llu | z sum %llu | losses %llu | col sums %llu | dH %llu | dW %llu | partials %llu\n",

@@ -278,20 +278,23 @@ template <int V> __global__ __launch_bounds__(64, 2) void kern(unsigned long lon
   }
 }
 
-template <int V> void run(int B, int reps, const char* name, std::vector<float>* ref) {
+// lds_per_env > 0: pad each workgroup's LDS to lds_per_env bytes per env (the step kernel's 20 KB
+// workspace: 2 envs per SIMD in either layout) -- the residency the real kernel would have
+template <int V> void run(int B, int reps, const char* name, std::vector<float>* ref, int lds_per_env = 0) {
   constexpr int EPW = (V == 0 || V == 63) ? 1 : 2;
   const int waves = B / EPW;
+  const size_t pad = lds_per_env > 0 ? (size_t)EPW * (lds_per_env - (int)sizeof(EnvWS)) : 0;
   unsigned long long* t;
   float* o;
   hipMalloc(&t, waves * 8);
   hipMalloc(&o, B * 32 * 4);
-  kern<V><<<waves, 64>>>(t, o, 2);  // warm-up
+  kern<V><<<waves, 64, pad>>>(t, o, 2);  // warm-up
   hipDeviceSynchronize();
   hipEvent_t e0, e1;
   hipEventCreate(&e0);
   hipEventCreate(&e1);
   hipEventRecord(e0);
-  kern<V><<<waves, 64>>>(t, o, reps);
+  kern<V><<<waves, 64, pad>>>(t, o, reps);
   hipEventRecord(e1);
   hipEventSynchronize(e1);
   float ms = 0.f;
@@ -312,7 +315,7 @@ template <int V> void run(int B, int reps, const char* name, std::vector<float>*
     *ref = oh;
   }
   printf("B %5d  %-52s waves/SIMD %.2f  %7.0f cycles/call/wave  %7.2f ns per env-factor  max rel dev %.2e\n", B,
-         name, waves / 1024.0, m, ms * 1e6 / ((double)reps * B), dev);
+         name, pad ? fmin(waves / 1024.0, 2.0 / EPW) : waves / 1024.0, m, ms * 1e6 / ((double)reps * B), dev);
   hipFree(t);
   hipFree(o);
 }
@@ -327,6 +330,14 @@ int main(int argc, char** argv) {
     run<62>(B, reps, "two envs per wave: readlane + permlane32_swap", &ref);
     run<63>(B, reps, "one env per wave: LDS column broadcasts", &ref);
     run<0>(B, reps, "product again", &ref);
+  }
+  // at the step kernel's residency: 20,480 bytes of LDS per env in both layouts (8 one-env or 4 two-env
+  // waves per CU: two envs per SIMD either way; 4096 envs take two rounds in both)
+  for (int B : {2048, 4096}) {
+    std::vector<float> ref;
+    run<0>(B, reps, "20 KB/env: product, one env per wave", &ref, 20480);
+    run<61>(B, reps, "20 KB/env: two envs per wave, LDS broadcasts", &ref, 20480);
+    run<0>(B, reps, "20 KB/env: product again", &ref, 20480);
   }
   return 0;
 }
