@@ -80,9 +80,9 @@ def test_twin_gradients_match_float64_autograd(monkeypatch, n, dup, fused):
     assert float(tw.W[-1][1, 1:].abs().max()) == 0.0 and float(tw.gW[-1][1, 1:].abs().max()) == 0.0
 
 
-@pytest.mark.parametrize("n", [12800, 16448])
+@pytest.mark.parametrize("n", [10240, 16448])
 def test_fused_head_uneven_chunks_match_float64_autograd(monkeypatch, n):
-    """The fused head where workgroups take different chunk counts: 12,800 rows = 400 chunks of 32 over
+    """The fused head where workgroups take different chunk counts: 10,240 rows = 320 chunks of 32 over
     256 workgroups per net (one or two each), 16,448 rows = 514 chunks (two or three)."""
     test_twin_gradients_match_float64_autograd(monkeypatch, n, False, True)
 
