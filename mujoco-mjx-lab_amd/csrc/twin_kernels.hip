@@ -315,7 +315,10 @@ __global__ __launch_bounds__(256, 2) void twin_head_bwd_kernel(TwinHeadBwdArgs p
 // the output layers' batched GEMM, the loss launch (mjl_twin_loss_head) and the output backward
 // (mjl_twin_head_bwd). A persistent grid of workgroups, one net each (net = blockIdx & 1), taking
 // R-row chunks blockIdx / 2, + gridDim / 2, ...: the launch takes R = 32 with two workgroups per CU
-// (75 KB of LDS each, at most kThBlocks); R = 64 (one per CU) measured slower at every size. Per chunk:
+// (75 KB of LDS each, at most kThBlocks); R = 64 (one per CU) measured slower at every size, and so
+// did (R = 32) the first chunk's loads hoisted above the setup, the next chunk's issued during the
+// current one and z on two accumulator chains (24.2-27.3 against 22.8 us at 8,192 rows: the live
+// registers spill; profiles/r6/twin_micro.txt). Per chunk:
 //   H = tanh(zh + bh) of the chunk into LDS (zh: the last hidden layer's bias-less GEMM output);
 //   z = H W^T + bo on v_mfma_f32_32x32x2_f32 (2 K halves per 32-row tile, one wave each, summed in K
 //     order through LDS);

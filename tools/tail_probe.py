@@ -50,3 +50,10 @@ it = st[:, 2]
 print("  cycles by solver iterations:", {int(k): (int((it == k).sum()), round(float(tot[it == k].mean()))) for k in np.unique(it)})
 order = np.argsort(-tot)[:12]
 print("  slowest envs (index, cycles, iterations, nefc, ncon):", [(int(i), int(tot[i]), int(st[i, 2]), int(st[i, 1]), int(st[i, 0])) for i in order])
+ph = np.diff(s[:, :9], axis=1)
+names = ["kin", "crb+M", "vel", "factM", "rows", "solver", "sensors", "integ"]
+sub = {9: "warm", 10: "ls", 11: "update", 12: "hess", 13: "chol", 14: "ls iters", 15: "line searches"}
+for lab, idx in (("slowest", np.argsort(-tot)[:8]), ("median", np.argsort(np.abs(tot - np.median(tot)))[:8]),
+                 ("fastest", np.argsort(tot)[:8])):
+    print(f"  {lab} envs: phases " + " ".join(f"{n} {ph[idx, i].mean():.0f}" for i, n in enumerate(names)))
+    print("      solver sub: " + " ".join(f"{n} {s[idx, k].mean():.1f}" for k, n in sub.items()))
