@@ -55,6 +55,8 @@ def parse(argv=None):
                         "ppo: the PPO leg alone as the headline (C3 / C5)")
     p.add_argument("--steps", type=int, default=None, help="timed steps (speedtest launches: 50; ppo iterations: 3)")
     p.add_argument("--warmup", type=int, default=None, help="untimed steps (speedtest: 5; ppo: 2, graph capture)")
+    p.add_argument("--speedtest-launch", choices=["graph", "eager"], default="graph",
+                   help="the headline's K timed steps as one hipGraph replay (default) or K eager launches")
     p.add_argument("--envs", type=int, default=None, help="envs per GPU (speedtest: 2048; ppo: 1024)")
     p.add_argument("--model", default="humanoid_mjx")
     p.add_argument("--ppo-envs", type=int, default=1024, help="PPO leg: envs per GPU (C3 / C5: 1024)")
@@ -140,6 +142,41 @@ def timed_launches(fn, steps, warmup, dist):
     e0.record(stream)
     for _ in range(steps):
         fn()
+    e1.record(stream)
+    torch.cuda.synchronize()
+    barrier(dist)
+    torch.cuda.synchronize()
+    wall = time.perf_counter() - t0
+    return wall, e0.elapsed_time(e1) / steps
+
+
+def timed_graph(fn, steps, warmup, dist):
+    """As timed_launches, with the K launches captured as one hipGraph and replayed once (the launch-bound
+    loop on the GPU's own queue: no per-launch host dispatch between the steps). W eager warmup launches
+    and one untimed replay first. Returns (wall seconds, mean ms per step from HIP events around the
+    replay), or None if the capture is refused."""
+    from mjx_amd.ppo import graph_capture
+    for _ in range(warmup):
+        fn()
+    torch.cuda.synchronize()
+    g = torch.cuda.CUDAGraph()
+    try:
+        with graph_capture(g):
+            for _ in range(steps):
+                fn()
+    except RuntimeError:
+        torch.cuda.synchronize()
+        return None
+    g.replay()
+    torch.cuda.synchronize()
+    barrier(dist)
+    torch.cuda.synchronize()
+    stream = torch.cuda.current_stream()
+    e0 = torch.cuda.Event(enable_timing=True)
+    e1 = torch.cuda.Event(enable_timing=True)
+    t0 = time.perf_counter()
+    e0.record(stream)
+    g.replay()
     e1.record(stream)
     torch.cuda.synchronize()
     barrier(dist)
@@ -317,8 +354,14 @@ def speedtest(args, dist, world, local):
     d = mjx.make_data(sys_, B, device=local)
     vel = torch.linspace(0.0, 1.0, B, device=f"cuda:{local}")
     out = torch.empty_like(vel)
-    wall, kern_ms = timed_launches(lambda: mjx.speedtest_step(sys_, d, vel, out), args.steps, args.warmup, dist)
+    step = lambda: mjx.speedtest_step(sys_, d, vel, out)  # noqa: E731
+    # the timed K steps as one graph replay (eager launches timed beside it, reported as such)
+    ew, ek = timed_launches(step, args.steps, args.warmup, dist)
+    gr = timed_graph(step, args.steps, args.warmup, dist) if args.speedtest_launch == "graph" else None
+    launch = "graph" if gr is not None else "eager"
+    wall, kern_ms = gr if gr is not None else (ew, ek)
     wall = max_over_ranks(wall, dist)
+    ew = max_over_ranks(ew, dist)
     value = B * args.steps * world / wall
     # solver statistics of exactly these states (a forward pass from the same fresh state), for the
     # algorithmic FLOP count of one env-step (mjx_amd/flops.py, DESIGN.md "Roofline")
@@ -350,6 +393,9 @@ def speedtest(args, dist, world, local):
                    "envs_per_gpu": B, "parallelism": f"env-sharded x{world}, no collective in the speed test",
                    "baseline_note": "vs_baseline divides by the README HUMANOID_MJX row (72,618 steps/s, batch 4096)"},
         "build": build_info(),
+        "speedtest_launch": launch,
+        "speedtest_eager_ms_per_step": ew / args.steps * 1e3,
+        "speedtest_eager_kernel_ms": ek,
         "roofline": {"bound": "valu", "achieved": achieved_tflops, "peak": F32_PEAK_TFLOPS, "unit": "TFLOP/s",
                      "frac": achieved_tflops / F32_PEAK_TFLOPS, "traffic": pmc_traffic(B),
                      "kernel": SPEEDTEST_KERNEL, "kernel_ms": kern_ms,
