@@ -185,6 +185,16 @@ def timed_graph(fn, steps, warmup, dist):
     return wall, e0.elapsed_time(e1) / steps
 
 
+def timed_steps(fn, args, dist):
+    """The speed-test legs' timing: one graph replay of K steps (args.speedtest_launch == "graph"), else or
+    if the capture is refused K eager launches."""
+    if getattr(args, "speedtest_launch", "graph") == "graph":
+        r = timed_graph(fn, args.steps, args.warmup, dist)
+        if r is not None:
+            return r
+    return timed_launches(fn, args.steps, args.warmup, dist)
+
+
 def max_over_ranks(x, dist, device="cuda"):
     if dist is None:
         return x
@@ -357,7 +367,7 @@ def speedtest(args, dist, world, local):
     step = lambda: mjx.speedtest_step(sys_, d, vel, out)  # noqa: E731
     # the timed K steps as one graph replay (eager launches timed beside it, reported as such)
     ew, ek = timed_launches(step, args.steps, args.warmup, dist)
-    gr = timed_graph(step, args.steps, args.warmup, dist) if args.speedtest_launch == "graph" else None
+    gr = timed_graph(step, args.steps, args.warmup, dist) if getattr(args, "speedtest_launch", "graph") == "graph" else None
     launch = "graph" if gr is not None else "eager"
     wall, kern_ms = gr if gr is not None else (ew, ek)
     wall = max_over_ranks(wall, dist)
@@ -486,7 +496,7 @@ def speedtest_extras(args, model, sys_, local):
     dh.set_option(0, 0)
     vh = torch.linspace(0.0, 1.0, B, device=dev)
     oh = torch.empty_like(vh)
-    hw, hk = timed_launches(lambda: mjx.speedtest_step(sh, dh, vh, oh), args.steps, args.warmup, None)
+    hw, hk = timed_steps(lambda: mjx.speedtest_step(sh, dh, vh, oh), args, None)
     ex["speedtest_humanoid_xml_steps_per_s"] = B * args.steps / hw
     ex["speedtest_humanoid_xml_kernel_ms"] = hk
     ex["speedtest_humanoid_xml_vs_readme"] = ex["speedtest_humanoid_xml_steps_per_s"] / REF_HUMANOID_XML_STEPS_PER_S
@@ -496,7 +506,7 @@ def speedtest_extras(args, model, sys_, local):
     dh.set_option(0, 0)
     vh = torch.linspace(0.0, 1.0, 4096, device=dev)
     oh = torch.empty_like(vh)
-    hw, hk = timed_launches(lambda: mjx.speedtest_step(sh, dh, vh, oh), args.steps, args.warmup, None)
+    hw, hk = timed_steps(lambda: mjx.speedtest_step(sh, dh, vh, oh), args, None)
     ex["speedtest_humanoid_xml_b4096_steps_per_s"] = 4096 * args.steps / hw
     ex["speedtest_humanoid_xml_b4096_kernel_ms"] = hk
     ex["speedtest_humanoid_xml_b4096_vs_readme"] = 4096 * args.steps / hw / REF_HUMANOID_XML_STEPS_PER_S
@@ -510,7 +520,7 @@ def speedtest_extras(args, model, sys_, local):
     dsp.set_option(0, 0)
     vs = torch.linspace(0.0, 1.0, 4096, device=dev)
     osp = torch.empty_like(vs)
-    sw, sk = timed_launches(lambda: mjx.speedtest_step(ss, dsp, vs, osp), args.steps, args.warmup, None)
+    sw, sk = timed_steps(lambda: mjx.speedtest_step(ss, dsp, vs, osp), args, None)
     ex["speedtest_sphere_b4096_steps_per_s"] = 4096 * args.steps / sw
     ex["speedtest_sphere_b4096_kernel_ms"] = sk
     ex["speedtest_sphere_b4096_vs_readme"] = 4096 * args.steps / sw / REF_SPHERE_STEPS_PER_S
@@ -519,7 +529,7 @@ def speedtest_extras(args, model, sys_, local):
     d4 = mjx.make_data(sys_, 4096, device=local)
     v4 = torch.linspace(0.0, 1.0, 4096, device=dev)
     o4 = torch.empty_like(v4)
-    w4, _ = timed_launches(lambda: mjx.speedtest_step(sys_, d4, v4, o4), args.steps, args.warmup, None)
+    w4, _ = timed_steps(lambda: mjx.speedtest_step(sys_, d4, v4, o4), args, None)
     ex["speedtest_b4096_steps_per_s"] = 4096 * args.steps / w4
     ex["speedtest_b4096_vs_readme"] = ex["speedtest_b4096_steps_per_s"] / REF_DEVICE_STEPS_PER_S
     return ex
