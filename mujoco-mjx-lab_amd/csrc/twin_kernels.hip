@@ -366,14 +366,14 @@ __global__ __launch_bounds__(256, 64 / R) void twin_head_kernel(TwinHeadArgs p) 
   constexpr int HS = kThHS, ZS = kThZS, NRT = R / 32, LPR = 256 / R;  // row tiles; lanes per loss row
   __shared__ __attribute__((aligned(16))) float hs[R * HS];  // H of the chunk
   __shared__ __attribute__((aligned(16))) float ws[A * HS];   // W_out rows (rows A..31 read as zero)
-  __shared__ float red[2 * NRT * 16 * 64];                    // z partials: (K half, row tile) per wave
+  constexpr int KP = 4 / NRT;                                 // K parts of z: every wave takes one (part, row tile)
+  __shared__ float red[4 * 16 * 64];                          // z partials per wave; at the end, the csh sums
   __shared__ float sz[R * ZS];                                // z, then d, then dz (cols A..31 zero)
   __shared__ float sx[R * 32];                                // act, then the mean, then c_j
   __shared__ float srow[4][R];                                // old_logp, adv, ret, surr
   __shared__ float ivs[32];
   __shared__ float lss_s, mu_s, sd_s;
   __shared__ float acc_col[2 * 32 + 1];                       // c_j, dz column sums, loss: chunk order
-  __shared__ float csh[2][K];
   const int t = threadIdx.x, lane = t & 63, w = t >> 6, li = lane & 31, kh = lane >> 5;
   const int net = blockIdx.x & 1, S = (int)(gridDim.x >> 1), blk = (int)(blockIdx.x >> 1), n = p.n;
   const int nchunk = (n + R - 1) / R;
@@ -464,9 +464,9 @@ __global__ __launch_bounds__(256, 64 / R) void twin_head_kernel(TwinHeadArgs p) 
       srow[2][t] = rv2;
     }
     __syncthreads();
-    // ---- z = H W^T: wave w < 2 NRT takes row tile w % NRT and K half w / NRT
-    if (w < 2 * NRT) {
-      const int rt = w % NRT, k0 = (w / NRT) * (K / 2);
+    // ---- z = H W^T: wave w takes row tile w % NRT and K part w / NRT (of KP)
+    {
+      const int rt = w % NRT, k0 = (w / NRT) * (K / KP);
       tw_f32x16 acc;
 #pragma unroll
       for (int v = 0; v < 16; v++) acc[v] = 0.f;
@@ -474,18 +474,19 @@ __global__ __launch_bounds__(256, 64 / R) void twin_head_kernel(TwinHeadArgs p) 
       const float* wb = &ws[(li < A ? li : 0) * HS + k0 + kh];
       const bool wr = li < A;  // W_out rows A..31: zero
 #pragma unroll 8
-      for (int s = 0; s < K / 4; s++)
+      for (int s = 0; s < K / (2 * KP); s++)
         acc = __builtin_amdgcn_mfma_f32_32x32x2f32(ha[2 * s], wr ? wb[2 * s] : 0.f, acc, 0, 0, 0);
 #pragma unroll
       for (int v = 0; v < 16; v++) red[(w * 16 + v) * 64 + lane] = acc[v];
     }
     __syncthreads();
-    // z[row][a] = lower K half + upper K half + bo (C[i][j] in register (i & 3) + 4 (i >> 3) of lane
-    // j + 32 ((i >> 2) & 1))
+    // z[row][a] = the K parts in order (pairwise for 4) + bo (C[i][j] in register (i & 3) + 4 (i >> 3) of
+    // lane j + 32 ((i >> 2) & 1))
     for (int e = t; e < R * 32; e += 256) {
       const int row = e >> 5, a = e & 31, rt = row >> 5, i = row & 31;
       const int v = (i & 3) + 4 * (i >> 3), L = a + 32 * ((i >> 2) & 1);
-      const float zz = red[(rt * 16 + v) * 64 + L] + red[((NRT + rt) * 16 + v) * 64 + L];
+      auto part = [&](int k) { return red[((k * NRT + rt) * 16 + v) * 64 + L]; };
+      const float zz = KP == 2 ? part(0) + part(1) : (part(0) + part(1)) + (part(2) + part(3));
       sz[row * ZS + a] = a < A ? zz + p.bo[net * A + a] : 0.f;
     }
     __syncthreads();
@@ -587,6 +588,7 @@ __global__ __launch_bounds__(256, 64 / R) void twin_head_kernel(TwinHeadArgs p) 
                                                         gwacc[c], 0, 0, 0);
     }
   }
+  float (*csh)[K] = reinterpret_cast<float (*)[K]>(red);  // red is free after the last chunk's z sums
   // ---- the workgroup's partials
   const int nb = S;
 #pragma unroll
