@@ -1439,7 +1439,8 @@ extern "C" int mjl_twin_gather_in(const long long* idx, const int* idx_row, int 
     return fail(MJL_ERR_ARG, "bad argument");
   if (!(mjl_twin_fused_shapes(k0, A, N) & 1))
     return fail(MJL_ERR_UNSUPPORTED, "twin_gather_in: input width %d / hidden width %d not instantiated", k0, N);
-  if (((uintptr_t)h | (uintptr_t)b) % 16) return fail(MJL_ERR_ARG, "twin_gather_in: 16-byte aligned h and b expected");
+  if (((uintptr_t)h | (uintptr_t)b | (uintptr_t)W) % 16)
+    return fail(MJL_ERR_ARG, "twin_gather_in: 16-byte aligned h, b and W expected");
   TwinInArgs p{idx, idx_row, n, A, nsrc, obs, act, logp, ret, adv, o2, a, ol, r, ad, W, b, h};
   const int nblk = 2 * ((n + kTinRows - 1) / kTinRows);  // a workgroup per (chunk, net), at most kTinBlocks
   hipLaunchKernelGGL((twin_gather_in_kernel<kTinK0, kTinN>), dim3((unsigned)(nblk < kTinBlocks ? nblk : kTinBlocks)),

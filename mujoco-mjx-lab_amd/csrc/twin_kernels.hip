@@ -81,37 +81,22 @@ constexpr int kTinBlocks = 512;
 template <int K0, int N>
 __global__ __launch_bounds__(N, 2) void twin_gather_in_kernel(TwinInArgs p) {
   constexpr int XS = kTinRows + 4;  // xs row stride
-  constexpr int WS = K0 + 1;        // ws row stride (odd)
+  constexpr int WS = K0;            // ws row stride (K0 = 54: 54 col mod 64 banks are distinct over 32 lanes)
   constexpr int OBS_IT = (kTinRows * K0 + N - 1) / N;
   constexpr int ACT_IT = (kTinRows * 32 + N - 1) / N;  // A <= 32
   constexpr int KS = K0 / 2;                           // MFMA K steps
   constexpr int TPW = N / 32 / (N / 64);               // tiles per wave (2)
-  constexpr int WQ = N * K0 / 4;                       // float4 of one net's W
-  static_assert(K0 % 2 == 0 && (N * K0) % 4 == 0 && kTinRows == 32 && N % 64 == 0, "tile shape");
-  __shared__ float ws[N * WS];
+  static_assert(K0 % 2 == 0 && (N * K0) % 256 == 0 && kTinRows == 32 && N % 64 == 0, "tile shape");
+  __shared__ __attribute__((aligned(16))) float ws[N * WS];
   __shared__ float xs[K0 * XS];
   const int t = threadIdx.x, n = p.n, A = p.A, net = blockIdx.x & 1;
-  {  // this net's weights: W[net] [N, K0] row-major -> ws[col * WS + k] (= element e + col)
-    const float4* W4 = reinterpret_cast<const float4*>(p.W + (size_t)net * N * K0);
-    constexpr int IT = (WQ + N - 1) / N;
-    float4 wv[IT];
-#pragma unroll
-    for (int i = 0; i < IT; i++) {
-      const int q = t + i * N;
-      wv[i] = q < WQ ? W4[q] : make_float4(0.f, 0.f, 0.f, 0.f);
-    }
-#pragma unroll
-    for (int i = 0; i < IT; i++) {
-      const int q = t + i * N;
-      if (q < WQ) {
-        const float v4[4] = {wv[i].x, wv[i].y, wv[i].z, wv[i].w};
-#pragma unroll
-        for (int c = 0; c < 4; c++) {
-          const int e = 4 * q + c;
-          ws[e + e / K0] = v4[c];
-        }
-      }
-    }
+  {  // this net's weights W[net] [N, K0], row-major as they lie, by LDS-DMA (global_load_lds_dwordx4: 1 KB
+     // per wave-instruction, no VGPRs, so the first chunk's gather issues behind it; the chunk's first
+     // barrier retires it)
+    const float* Wn = p.W + (size_t)net * N * K0;
+    for (int i = t >> 6; i < N * K0 / 256; i += N / 64)
+      __builtin_amdgcn_global_load_lds((const void*)(Wn + 256 * i + 4 * (t & 63)),
+                                       (__attribute__((address_space(3))) void*)&ws[256 * i], 16, 0, 0);
   }
   const long long nsrc = p.nsrc;
   const float nan = __builtin_nanf("");
@@ -378,16 +363,12 @@ __global__ __launch_bounds__(256, 64 / R) void twin_head_kernel(TwinHeadArgs p) 
   const int net = blockIdx.x & 1, S = (int)(gridDim.x >> 1), blk = (int)(blockIdx.x >> 1), n = p.n;
   const int nchunk = (n + R - 1) / R;
   // ---- once per workgroup: W_out of this net, the log_std terms, the advantage statistics
-  {
-    constexpr int Q = 32 * K / 4 / 256;  // float4 per thread
-#pragma unroll
-    for (int i = 0; i < Q; i++) {
-      const int q = t + 256 * i, a = q / (K / 4), c4 = q - a * (K / 4);
-      if (a < A)
-        *reinterpret_cast<float4*>(&ws[a * HS + 4 * c4]) =
-            *reinterpret_cast<const float4*>(p.W + ((size_t)net * A + a) * K + 4 * c4);
-    }
-  }
+  // (by LDS-DMA, global_load_lds_dwordx4: one 1-KB row per wave-instruction, no VGPRs, so the first
+  // chunk's loads issue behind it; the chunk's first barrier retires it)
+  static_assert(K == 64 * 4, "one W_out row per wave-instruction");
+  for (int a = w; a < A; a += 4)
+    __builtin_amdgcn_global_load_lds((const void*)(p.W + ((size_t)net * A + a) * K + 4 * lane),
+                                     (__attribute__((address_space(3))) void*)&ws[a * HS], 16, 0, 0);
   if (w == 0) {
     const float ls = lane < A ? fminf(fmaxf(p.log_std[lane], p.ls_lo), p.ls_hi) : 0.f;  // networks.py:103
     if (lane < 32) ivs[lane] = lane < A ? expf(-2.f * ls) : 0.f;

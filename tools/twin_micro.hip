@@ -36,16 +36,12 @@ __global__ __launch_bounds__(256, 64 / R) void th_stamped(TwinHeadArgs p, unsign
   const int net = blockIdx.x & 1, S = (int)(gridDim.x >> 1), blk = (int)(blockIdx.x >> 1), n = p.n;
   const int nchunk = (n + R - 1) / R;
   // ---- once per workgroup: W_out of this net, the log_std terms, the advantage statistics
-  {
-    constexpr int Q = 32 * K / 4 / 256;  // float4 per thread
-#pragma unroll
-    for (int i = 0; i < Q; i++) {
-      const int q = t + 256 * i, a = q / (K / 4), c4 = q - a * (K / 4);
-      if (a < A)
-        *reinterpret_cast<float4*>(&ws[a * HS + 4 * c4]) =
-            *reinterpret_cast<const float4*>(p.W + ((size_t)net * A + a) * K + 4 * c4);
-    }
-  }
+  // (by LDS-DMA, global_load_lds_dwordx4: one 1-KB row per wave-instruction, no VGPRs, so the first
+  // chunk's loads issue behind it; the chunk's first barrier retires it)
+  static_assert(K == 64 * 4, "one W_out row per wave-instruction");
+  for (int a = w; a < A; a += 4)
+    __builtin_amdgcn_global_load_lds((const void*)(p.W + ((size_t)net * A + a) * K + 4 * lane),
+                                     (__attribute__((address_space(3))) void*)&ws[a * HS], 16, 0, 0);
   if (w == 0) {
     const float ls = lane < A ? fminf(fmaxf(p.log_std[lane], p.ls_lo), p.ls_hi) : 0.f;  // networks.py:103
     if (lane < 32) ivs[lane] = lane < A ? expf(-2.f * ls) : 0.f;
