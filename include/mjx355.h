@@ -344,6 +344,11 @@ int mjl_policy_fwd(const float* obs, const float* mean, const float* var, float 
  * matrices read from the slot (environment MJL_VJP_LEAN=0 selects the full layout; same results). */
 int mjl_env_step_record(mjlBatch* batch, int slot, const float* act, float* obs, float* rew, float* term,
                         float* trunc, void* stream);
+/* mjl_env_step_record followed by mjl_apg_post's update of every env (below), as one launch where the
+ * record keeps its rows in LDS (the implicit record on the humanoid dims), else the two launches. */
+int mjl_env_step_record_apg(mjlBatch* batch, int slot, const float* act, float* obs, float* rew, float* term,
+                            float* trunc, float gamma, float diverge_qvel, uint8_t* alive, float* disc, float* ret,
+                            float* dropped, float* grew, float* rfin, void* stream);
 int mjl_env_step_vjp_replay(mjlBatch* batch, int slot, const float* act, const float* g_qpos, const float* g_qvel,
                             const float* g_qacc_ws, const float* g_rew, const float* g_aux, float* out_qpos,
                             float* out_qvel, float* out_qacc_ws, float* out_act, float* out_aux,

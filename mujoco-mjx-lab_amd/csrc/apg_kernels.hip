@@ -49,21 +49,54 @@ __global__ void apg_obs_kernel(StateBuf S, int B, int nq, int nv, const uint8_t*
 }
 
 // after env e's step: the non-finite / divergence guard, the discount and the return
-// (apg.py _loss_and_grad, in the same order of float operations). One wave per env: lane j loads
-// qpos[j] / qvel[j] (coalesced), the finite test by ballot, max |qvel| by a wave max (fmaxf is
-// order-free: the serial loop's value); lane 0 updates the env's scalars. (A thread per env looped over
-// the env's nq + nv words: 55 strided loads per lane, 9.4 us per 2048-env launch on 8 workgroups.)
+// (apg.py _loss_and_grad, in the same order of float operations), from env e's wave: fin = this lane's
+// qpos / qvel entries are finite, vmax = their max |qvel|; the finite test by ballot, max |qvel| by a
+// wave max (fmaxf is order-free: the serial loop's value); lane 0 updates the env's scalars (r, te,
+// tr: its reward, terminated and truncated flags). Shared by apg_post_kernel and the APG record kernel
+// (adjoint.hip vjp_record_kernel, which runs it on the state it just wrote back).
+struct ApgPostArgs {
+  float gamma, diverge_qvel;
+  uint8_t* alive;  // null: no post-step update
+  float *disc, *ret, *dropped, *grew, *rfin;
+  int B;
+};
+// env e's scalars before the update (loaded where the caller can hide their latency)
+struct ApgPostEnv {
+  bool alive;
+  float disc, ret, dropped;
+};
+__device__ __forceinline__ ApgPostEnv apg_post_load(const ApgPostArgs& a, int e) {
+  return ApgPostEnv{a.alive[e] != 0, a.disc[e], a.ret[e], a.dropped[e]};
+}
+__device__ __forceinline__ void apg_post_wave(const ApgPostArgs& a, int e, int lane, bool fin, float vmax, float r,
+                                              float te, float tr, const ApgPostEnv& pe) {
+  const bool allfin = __ballot(!fin) == 0ull;
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) vmax = fmaxf(vmax, __shfl_xor(vmax, o));
+  if (lane != 0) return;
+  bool ok = isfinite(r) && allfin;
+  if (a.diverge_qvel > 0.f) ok = ok && vmax <= a.diverge_qvel;
+  bool al = pe.alive;
+  const bool bad = al && !ok;
+  if (bad) a.dropped[e] = pe.dropped + 1.f;
+  al = al && !bad;
+  const float d = al ? pe.disc : 0.f;
+  a.grew[e] = div_rn(-d, (float)a.B);
+  a.ret[e] = pe.ret + (al ? d * r : 0.f);
+  a.rfin[e] = isfinite(r) ? r : 0.f;
+  const float nd = d * a.gamma * (1.f - fmaxf(te, tr));
+  a.disc[e] = nd;
+  a.alive[e] = al && nd != 0.f;
+}
+
+// One wave per env: lane j loads qpos[j] / qvel[j] (coalesced). (A thread per env looped over the env's
+// nq + nv words: 55 strided loads per lane, 9.4 us per 2048-env launch on 8 workgroups.)
 constexpr int kPostEnvs = 4;  // envs (waves) per block
-__global__ __launch_bounds__(64 * kPostEnvs) void apg_post_kernel(StateBuf S, int B, int nq, int nv,
-                                                                  const float* __restrict__ rew,
+__global__ __launch_bounds__(64 * kPostEnvs) void apg_post_kernel(StateBuf S, int nq, int nv, const float* __restrict__ rew,
                                                                   const float* __restrict__ term,
-                                                                  const float* __restrict__ trunc, float gamma,
-                                                                  float diverge_qvel, uint8_t* __restrict__ alive,
-                                                                  float* __restrict__ disc, float* __restrict__ ret,
-                                                                  float* __restrict__ dropped, float* __restrict__ grew,
-                                                                  float* __restrict__ rfin) {
+                                                                  const float* __restrict__ trunc, ApgPostArgs a) {
   const int lane = threadIdx.x & 63, e = blockIdx.x * kPostEnvs + (threadIdx.x >> 6);
-  if (e >= B) return;  // wave-uniform
+  if (e >= a.B) return;  // wave-uniform
   bool fin = true;
   float vmax = 0.f;
   for (int j = lane; j < nq; j += 64) fin &= isfinite(S.qpos[(size_t)e * nq + j]);
@@ -72,24 +105,7 @@ __global__ __launch_bounds__(64 * kPostEnvs) void apg_post_kernel(StateBuf S, in
     fin &= isfinite(v);
     vmax = fmaxf(vmax, fabsf(v));
   }
-  const bool allfin = __ballot(!fin) == 0ull;
-#pragma unroll
-  for (int o = 32; o >= 1; o >>= 1) vmax = fmaxf(vmax, __shfl_xor(vmax, o));
-  if (lane != 0) return;
-  const float r = rew[e];
-  bool ok = isfinite(r) && allfin;
-  if (diverge_qvel > 0.f) ok = ok && vmax <= diverge_qvel;
-  bool al = alive[e] != 0;
-  const bool bad = al && !ok;
-  if (bad) dropped[e] += 1.f;
-  al = al && !bad;
-  const float d = al ? disc[e] : 0.f;
-  grew[e] = div_rn(-d, (float)B);
-  ret[e] = ret[e] + (al ? d * r : 0.f);
-  rfin[e] = isfinite(r) ? r : 0.f;
-  const float nd = d * gamma * (1.f - fmaxf(term[e], trunc[e]));
-  disc[e] = nd;
-  alive[e] = al && nd != 0.f;
+  apg_post_wave(a, e, lane, fin, vmax, rew[e], term[e], trunc[e], apg_post_load(a, e));
 }
 
 // backward of apg_obs_kernel's on w.r.t. o, accumulated: g_qpos / g_qvel += d on / d o * go

@@ -832,6 +832,20 @@ template <bool ENV, int TM = 0> static int launch_vjp(mjlBatch* B, const VjpArgs
       HIPCHK(hipGetLastError());
       return MJL_OK;
     }
+    if (V.post.alive) {  // the other record kernels leave the post-step update to its own launch
+      VjpArgs V2 = V;
+      V2.post.alive = nullptr;
+      if (B->model->nvc == 0)
+        hipLaunchKernelGGL((vjp_kernel<DHumV, ENV, TM>), grid, block, 0, (hipStream_t)stream, P, V2);
+      else
+        hipLaunchKernelGGL((vjp_kernel<DGen, ENV, TM>), grid, block, 0, (hipStream_t)stream, P, V2);
+      HIPCHK(hipGetLastError());
+      hipLaunchKernelGGL(apg_post_kernel, dim3((B->nenv + kPostEnvs - 1) / kPostEnvs), dim3(64 * kPostEnvs), 0,
+                         (hipStream_t)stream, B->s, B->model->desc.nq, B->model->desc.nv, P.rew, P.term, P.trunc,
+                         V.post);
+      HIPCHK(hipGetLastError());
+      return MJL_OK;
+    }
   }
   if (B->model->nvc == 0)
     hipLaunchKernelGGL((vjp_kernel<DHumV, ENV, TM>), grid, block, 0, (hipStream_t)stream, P, V);
@@ -910,6 +924,23 @@ int mjl_env_step_record(mjlBatch* B, int slot, const float* act, float* obs, flo
   std::memset(&V, 0, sizeof(V));
   V.act = act;
   V.slot = B->d_vtape + (size_t)slot * B->nenv * (size_t)B->vtape_stride;
+  return launch_vjp<true, 1>(B, V, stream, &P);
+}
+
+int mjl_env_step_record_apg(mjlBatch* B, int slot, const float* act, float* obs, float* rew, float* term, float* trunc,
+                            float gamma, float diverge_qvel, uint8_t* alive, float* disc, float* ret, float* dropped,
+                            float* grew, float* rfin, void* stream) {
+  if (!B || !act || !obs || !rew || !term || !trunc || !alive || !disc || !ret || !dropped || !grew || !rfin)
+    return fail(MJL_ERR_ARG, "bad argument");
+  if (!B->has_env) return fail(MJL_ERR_ARG, "mjl_env_config not called");
+  if (!B->d_vtape || slot < 0 || slot >= B->vtape_slots) return fail(MJL_ERR_ARG, "VJP tape slot %d not allocated", slot);
+  KParams P = make_params(B);
+  P.obs = obs; P.rew = rew; P.term = term; P.trunc = trunc;
+  VjpArgs V;
+  std::memset(&V, 0, sizeof(V));
+  V.act = act;
+  V.slot = B->d_vtape + (size_t)slot * B->nenv * (size_t)B->vtape_stride;
+  V.post = ApgPostArgs{gamma, diverge_qvel, alive, disc, ret, dropped, grew, rfin, B->nenv};
   return launch_vjp<true, 1>(B, V, stream, &P);
 }
 
@@ -1258,9 +1289,9 @@ extern "C" int mjl_apg_post(mjlBatch* B, const float* rew, const float* term, co
   if (!B || !rew || !term || !trunc || !alive || !disc || !ret || !dropped || !grew || !rfin)
     return fail(MJL_ERR_ARG, "bad argument");
   HIPCHK(hipSetDevice(B->device));
-  hipLaunchKernelGGL(apg_post_kernel, dim3((B->nenv + kPostEnvs - 1) / kPostEnvs), dim3(64 * kPostEnvs), 0, (hipStream_t)stream, B->s, B->nenv,
-                     B->model->desc.nq, B->model->desc.nv, rew, term, trunc, gamma, diverge_qvel, alive, disc, ret,
-                     dropped, grew, rfin);
+  const ApgPostArgs a{gamma, diverge_qvel, alive, disc, ret, dropped, grew, rfin, B->nenv};
+  hipLaunchKernelGGL(apg_post_kernel, dim3((B->nenv + kPostEnvs - 1) / kPostEnvs), dim3(64 * kPostEnvs), 0,
+                     (hipStream_t)stream, B->s, B->model->desc.nq, B->model->desc.nv, rew, term, trunc, a);
   HIPCHK(hipGetLastError());
   return MJL_OK;
 }

@@ -237,6 +237,8 @@ class APGTrainer:
         # the observation and the policy forward as one launch (and their backward as one), when the env
         # is the native one (HumanoidAPGEnv); MJL_APG_FUSED_OBS=0 keeps the separate launches
         fused = nat is not None and isinstance(env, HumanoidAPGEnv) and os.environ.get("MJL_APG_FUSED_OBS", "1") != "0"
+        # the record and the post-step update as one launch (MJL_APG_FUSED_POST=0: the two launches)
+        fused_post = taped and hasattr(env, "step_record_apg") and os.environ.get("MJL_APG_FUSED_POST", "1") != "0"
         for t in range(H):
             if not taped:
                 tape.append(env.get_state())
@@ -251,6 +253,9 @@ class APGTrainer:
                 a = self.policy(on)
                 leaves.append(on)
             acts.append(a)
+            if fused_post:  # the step, its tape slot t and the post-step update in one launch
+                env.step_record_apg(t, a.detach(), gamma, dq, alive, disc, ret, dropped_e, grew_all[t], rfin[t])
+                continue
             if taped:  # the step, leaving its forward workspace in tape slot t
                 _, r, te, tr = env.step_record(t, a.detach())
             else:
@@ -538,6 +543,18 @@ class HumanoidAPGEnv:
         act = act.to(e.obs.device, torch.float32).contiguous()
         check(lib().mjl_env_step_record(e.data.handle, int(slot), _ptr(act), _ptr(e.obs), _ptr(e.rew), _ptr(e.term),
                                         _ptr(e.trunc), _stream()))
+        return e.obs, e.rew, e.term, e.trunc
+
+    def step_record_apg(self, slot: int, act, gamma, diverge_qvel, alive, disc, ret, dropped, grew, rfin):
+        """step_record then apg_post on its outputs, as one launch where the record kernel allows it
+        (mjl_env_step_record_apg)."""
+        from ._lib import check, lib
+        from .mjx import _ptr, _stream
+        e = self.env
+        act = act.to(e.obs.device, torch.float32).contiguous()
+        check(lib().mjl_env_step_record_apg(e.data.handle, int(slot), _ptr(act), _ptr(e.obs), _ptr(e.rew),
+                                            _ptr(e.term), _ptr(e.trunc), float(gamma), float(diverge_qvel), _u8(alive),
+                                            _ptr(disc), _ptr(ret), _ptr(dropped), _ptr(grew), _ptr(rfin), _stream()))
         return e.obs, e.rew, e.term, e.trunc
 
     def step_vjp_replay(self, slot: int, act, gq, gv, gws, grew, gaux, nonfinite=None):

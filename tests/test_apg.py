@@ -442,6 +442,41 @@ def test_apg_fused_obs_policy_launches_bit_identical(monkeypatch, graph):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("solver", ["cg44", "model"])
+@pytest.mark.parametrize("graph", [False, True])
+def test_apg_fused_record_post_bit_identical(monkeypatch, graph, solver):
+    """The record + post-step update as one launch (mjl_env_step_record_apg) against the record and
+    mjl_apg_post as two (MJL_APG_FUSED_POST=0): loss, gradient, returns, cut envs and parameters bit for
+    bit over 4 updates, eager and under the update's hipGraph; with a divergence bound low enough that
+    some envs are cut by it."""
+    import mjx_amd
+    from mjx_amd import mjcf, mjx
+    from mjx_amd.config import reference_ppo_config
+    from mjx_amd.envs import HumanoidEnv, resolve_ids
+    m = mjx_amd.load_model("humanoid_mjx")
+    if solver == "cg44":
+        m.solver, m.iterations, m.ls_iterations = mjcf.SOLVER_CG, 4, 4
+    ecfg = resolve_ids(m, reference_ppo_config().env_config)
+    cfg = _cfg(batch_size=100, horizon=8, hidden_size=32)
+    cfg.diverge_qvel = 5.0
+    envs = [apg.HumanoidAPGEnv(HumanoidEnv(mjx.put_model(m), ecfg, cfg.batch_size, seed=5), "implicit")
+            for _ in range(2)]
+    trs = [apg.APGTrainer(cfg, e, device="cuda", use_graph=graph) for e in envs]
+    cut = 0.0
+    for step in range(4):
+        ms = []
+        for tr, fused in zip(trs, ("1", "0")):
+            monkeypatch.setenv("MJL_APG_FUSED_POST", fused)
+            ms.append(tr.update(step))
+        for k in ("loss", "grad_norm", "mean_reward", "return", "nonfinite_envs"):
+            assert ms[0][k] == ms[1][k], f"update {step}: {k}"
+        cut += float(ms[0]["nonfinite_envs"])
+        for p, q in zip(trs[0].policy.parameters(), trs[1].policy.parameters()):
+            assert torch.equal(p, q), f"update {step}"
+    assert cut > 0, "the divergence bound should cut some envs"
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("k0,hidden,depth,act_dim,B", [(55, 32, 2, 21, 2048), (55, 64, 3, 21, 1000), (7, 16, 1, 3, 5)])
 def test_native_apg_policy_matches_torch(k0, hidden, depth, act_dim, B):
     """mjl_small_mlp_fwd / mjl_small_mlp_bwd_input against the APGPolicy's torch forward and the
