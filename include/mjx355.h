@@ -349,6 +349,17 @@ int mjl_env_step_record(mjlBatch* batch, int slot, const float* act, float* obs,
 int mjl_env_step_record_apg(mjlBatch* batch, int slot, const float* act, float* obs, float* rew, float* term,
                             float* trunc, float gamma, float diverge_qvel, uint8_t* alive, float* disc, float* ret,
                             float* dropped, float* grew, float* rfin, void* stream);
+/* 1 if mjl_env_step_record_apg_next applies to this batch (the implicit record on the humanoid dims). */
+int mjl_env_record_fused(const mjlBatch* batch);
+/* mjl_env_step_record_apg, then, from each env's new state and alive flag, mjl_apg_obs_policy_fwd's
+ * observation (o, on, alive_snap) and small-MLP forward (ys) for the next rollout step, in the same
+ * launch (the implicit record on the humanoid dims only: MJL_ERR_UNSUPPORTED otherwise). w_t[l]: layer
+ * l's weight TRANSPOSED, [k_l, n_l] row-major; b[l], widths as mjl_small_mlp_fwd. */
+int mjl_env_step_record_apg_next(mjlBatch* batch, int slot, const float* act, float* obs, float* rew, float* term,
+                                 float* trunc, float gamma, float diverge_qvel, uint8_t* alive, float* disc, float* ret,
+                                 float* dropped, float* grew, float* rfin, const float* mean, const float* var,
+                                 int use_norm, float* o, float* on, uint8_t* alive_snap, int nl, const int* widths,
+                                 const float* const* w_t, const float* const* b, float* const* ys, void* stream);
 int mjl_env_step_vjp_replay(mjlBatch* batch, int slot, const float* act, const float* g_qpos, const float* g_qvel,
                             const float* g_qacc_ws, const float* g_rew, const float* g_aux, float* out_qpos,
                             float* out_qvel, float* out_qacc_ws, float* out_act, float* out_aux,

@@ -1754,6 +1754,7 @@ struct VjpArgs {
   long long slot_stride;
   int s_w, s_a, s_r, s_t;
   ApgPostArgs post;  // record: the APG post-step update fused into the launch (post.alive null: none)
+  ApgNextArgs next;  // record with post: the next step's observation + policy forward (next.o null: none)
 };
 
 // record mode's share of WSA: what the forward leaves there for the reverse passes
@@ -2279,8 +2280,42 @@ template <class DL, class DI> __global__ __launch_bounds__(64, 2) void vjp_recor
     }
     // (the env's scalars loaded here: loaded with the state at the start instead, they stay live across
     // the step and spill -- 80.7 against 78.2 us per record)
-    apg_post_wave(V.post, env, lane, fin, vmax, W->sc[SC_REW], W->sc[SC_TERM], W->sc[SC_TRUNC],
-                  apg_post_load(V.post, env));
+    const bool aln = apg_post_wave(V.post, env, lane, fin, vmax, W->sc[SC_REW], W->sc[SC_TERM], W->sc[SC_TRUNC],
+                                   apg_post_load(V.post, env));
+    if (V.next.o) {  // the next step's observation and policy forward from this state (one launch less)
+      const ApgNextArgs& X = V.next;
+      const bool al = __builtin_amdgcn_readlane((int)aln, 0) != 0;  // alive after this step's update
+      const int k0 = nq + nv;
+      LDSA float* h = (LDSA float*)W->J;  // [2][64]: the layer inputs (the row area is free here)
+      for (int k = lane; k < k0; k += 64) {
+        const float v = k < nq ? W->qpos[k] : W->qvel[k - nq];
+        const size_t i = (size_t)env * k0 + k;
+        X.o[i] = v;
+        const float xv = al ? v : 0.f;
+        const float in = X.use_norm ? clamp_keep_nan(div_rn(xv - X.mean[k], sqrt_rn(X.var[k]) + 1e-8f), 10.f) : xv;
+        X.on[i] = in;
+        h[k] = in;
+      }
+      if (lane == 0) X.snap[env] = al;
+      SYNC();
+      int K = k0, cur = 0;
+      for (int l = 0; l < X.P.nl; l++) {
+        const int N = X.P.n[l];
+        const float* __restrict__ wt = X.P.w[l];  // [K, N]
+        float y = 0.f;
+        if (lane < N) {  // small_mlp_fwd_kernel's sum: the bias, then k in order
+          float s = X.P.b[l][lane];
+#pragma unroll 8
+          for (int k = 0; k < K; k++) s = fmaf(wt[k * N + lane], h[cur * 64 + k], s);
+          y = tanhf(s);
+          X.P.y[l][(size_t)env * N + lane] = y;
+          h[(cur ^ 1) * 64 + lane] = y;
+        }
+        SYNC();
+        cur ^= 1;
+        K = N;
+      }
+    }
   }
 }
 

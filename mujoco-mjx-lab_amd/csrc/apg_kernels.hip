@@ -68,12 +68,13 @@ struct ApgPostEnv {
 __device__ __forceinline__ ApgPostEnv apg_post_load(const ApgPostArgs& a, int e) {
   return ApgPostEnv{a.alive[e] != 0, a.disc[e], a.ret[e], a.dropped[e]};
 }
-__device__ __forceinline__ void apg_post_wave(const ApgPostArgs& a, int e, int lane, bool fin, float vmax, float r,
+// (returns the env's new alive flag in lane 0)
+__device__ __forceinline__ bool apg_post_wave(const ApgPostArgs& a, int e, int lane, bool fin, float vmax, float r,
                                               float te, float tr, const ApgPostEnv& pe) {
   const bool allfin = __ballot(!fin) == 0ull;
 #pragma unroll
   for (int o = 32; o >= 1; o >>= 1) vmax = fmaxf(vmax, __shfl_xor(vmax, o));
-  if (lane != 0) return;
+  if (lane != 0) return false;
   bool ok = isfinite(r) && allfin;
   if (a.diverge_qvel > 0.f) ok = ok && vmax <= a.diverge_qvel;
   bool al = pe.alive;
@@ -87,6 +88,7 @@ __device__ __forceinline__ void apg_post_wave(const ApgPostArgs& a, int e, int l
   const float nd = d * a.gamma * (1.f - fmaxf(te, tr));
   a.disc[e] = nd;
   a.alive[e] = al && nd != 0.f;
+  return al && nd != 0.f;
 }
 
 // One wave per env: lane j loads qpos[j] / qvel[j] (coalesced). (A thread per env looped over the env's
@@ -159,6 +161,17 @@ struct ObsIn {
   const float *mean, *var;
   float *o, *on;
   uint8_t* snap;
+};
+// the next rollout step's observation and policy forward, fused into the APG record after its post-step
+// update (mjl_env_step_record_apg_next): mjl_apg_obs_policy_fwd's o / on / alive_snap and layer outputs
+// for this env, the same float operations; P.w[l] hold the layers' weights TRANSPOSED ([k_l, n_l], so
+// the wave's lanes read a k row coalesced); o null: none
+struct ApgNextArgs {
+  int use_norm;
+  const float *mean, *var;
+  float *o, *on;
+  uint8_t* snap;
+  SmallMlp P;
 };
 // the observation's backward fused into the policy's input backward (mjl_apg_policy_bwd_obs_vjp):
 // apg_obs_vjp_kernel on the input cotangent where small_mlp_bwd_input_kernel wrote g_x

@@ -1328,6 +1328,40 @@ extern "C" int mjl_apg_obs_policy_fwd(mjlBatch* B, const uint8_t* alive, const f
   return MJL_OK;
 }
 
+// 1 if this batch's record launch is vjp_record_kernel (the rows in LDS; the post-step update and the next
+// step's policy forward can ride along): the humanoid dims, the implicit VJP, rows not forced global
+extern "C" int mjl_env_record_fused(const mjlBatch* B) {
+  return B && B->model->nvc == 0 && !B->vjp_unrolled && !B->force_global_rows ? 1 : 0;
+}
+
+// the APG record + post-step update + the next step's observation and policy forward, in one launch
+extern "C" int mjl_env_step_record_apg_next(mjlBatch* B, int slot, const float* act, float* obs, float* rew, float* term,
+                                 float* trunc, float gamma, float diverge_qvel, uint8_t* alive, float* disc, float* ret,
+                                 float* dropped, float* grew, float* rfin, const float* mean, const float* var,
+                                 int use_norm, float* o, float* on, uint8_t* alive_snap, int nl, const int* widths,
+                                 const float* const* w_t, const float* const* b, float* const* ys, void* stream) {
+  if (!B || !act || !obs || !rew || !term || !trunc || !alive || !disc || !ret || !dropped || !grew || !rfin || !o ||
+      !on || !alive_snap || (use_norm && (!mean || !var)))
+    return fail(MJL_ERR_ARG, "bad argument");
+  if (!B->has_env) return fail(MJL_ERR_ARG, "mjl_env_config not called");
+  if (!B->d_vtape || slot < 0 || slot >= B->vtape_slots) return fail(MJL_ERR_ARG, "VJP tape slot %d not allocated", slot);
+  if (!(B->model->nvc == 0 && !B->vjp_unrolled && !B->force_global_rows))
+    return fail(MJL_ERR_UNSUPPORTED, "record_apg_next: the fused record (implicit VJP, humanoid dims) only");
+  const int nq = B->model->desc.nq, nv = B->model->desc.nv;
+  SmallMlp P;
+  int rc = small_mlp_setup(B->nenv, nq + nv, nl, widths, w_t, b, ys, P, true);
+  if (rc != MJL_OK) return rc;
+  KParams Pk = make_params(B);
+  Pk.obs = obs; Pk.rew = rew; Pk.term = term; Pk.trunc = trunc;
+  VjpArgs V;
+  std::memset(&V, 0, sizeof(V));
+  V.act = act;
+  V.slot = B->d_vtape + (size_t)slot * B->nenv * (size_t)B->vtape_stride;
+  V.post = ApgPostArgs{gamma, diverge_qvel, alive, disc, ret, dropped, grew, rfin, B->nenv};
+  V.next = ApgNextArgs{use_norm, mean, var, o, on, alive_snap, P};
+  return launch_vjp<true, 1>(B, V, stream, &Pk);
+}
+
 // mjl_small_mlp_bwd_input then mjl_apg_obs_vjp on its g_x, in one launch (k0 = nq + nv; g_x not stored)
 extern "C" int mjl_apg_policy_bwd_obs_vjp(const float* g_out, int nenv, int nq, int nv, int nl, const int* widths,
                                           const float* const* w, const float* const* ys, const float* o,

@@ -90,6 +90,25 @@ class NativeAPGPolicy:
                                            self._ptrs([b for _, b in self.params]), self._ptrs(ys), _stream()))
         return ys[-1]
 
+    def transposed_weights(self):
+        """The layers' weights as [k_l, n_l] copies (mjl_env_step_record_apg_next reads k rows coalesced)."""
+        return [w.t().contiguous() for w, _ in self.params]
+
+    def record_next(self, env, slot, act, gamma, diverge_qvel, alive, disc, ret, dropped, grew, rfin, rms, use_norm,
+                    o, on, snap, ys, w_t):
+        """HumanoidAPGEnv.step_record_apg, then forward_obs for the next step from its state, as one launch
+        (mjl_env_step_record_apg_next); returns ys[-1], the next action mean."""
+        from ._lib import check, lib
+        from .mjx import _ptr, _stream
+        e = env.env
+        act = act.to(e.obs.device, torch.float32).contiguous()
+        check(lib().mjl_env_step_record_apg_next(
+            e.data.handle, int(slot), _ptr(act), _ptr(e.obs), _ptr(e.rew), _ptr(e.term), _ptr(e.trunc), float(gamma),
+            float(diverge_qvel), _u8(alive), _ptr(disc), _ptr(ret), _ptr(dropped), _ptr(grew), _ptr(rfin),
+            _ptr(rms.mean), _ptr(rms.var), int(use_norm), _ptr(o), _ptr(on), _u8(snap), len(self.widths), self._widths,
+            self._ptrs(w_t), self._ptrs([b for _, b in self.params]), self._ptrs(ys), _stream()))
+        return ys[-1]
+
     def backward_obs_vjp(self, env, g_out, ys, o, snap, rms, use_norm, gq, gv):
         """backward_input(g_out, ys), then HumanoidAPGEnv.apg_obs_vjp on its result, as one launch
         (mjl_apg_policy_bwd_obs_vjp): gq / gv accumulate the observation's cotangent."""
@@ -237,12 +256,19 @@ class APGTrainer:
         # the observation and the policy forward as one launch (and their backward as one), when the env
         # is the native one (HumanoidAPGEnv); MJL_APG_FUSED_OBS=0 keeps the separate launches
         fused = nat is not None and isinstance(env, HumanoidAPGEnv) and os.environ.get("MJL_APG_FUSED_OBS", "1") != "0"
-        # the record and the post-step update as one launch (MJL_APG_FUSED_POST=0: the two launches)
+        # the record and the post-step update as one launch (MJL_APG_FUSED_POST=0: the two launches), and
+        # with it the next step's observation + policy forward (MJL_APG_FUSED_NEXT=0: their own launch)
         fused_post = taped and hasattr(env, "step_record_apg") and os.environ.get("MJL_APG_FUSED_POST", "1") != "0"
+        fused_next = (fused_post and fused and env.supports_record_next()
+                      and os.environ.get("MJL_APG_FUSED_NEXT", "1") != "0")
+        w_t = nat.transposed_weights() if fused_next else None
+        a_next = None
         for t in range(H):
             if not taped:
                 tape.append(env.get_state())
-            if fused:
+            if a_next is not None:  # written by the previous step's record launch
+                a, a_next = a_next, None
+            elif fused:
                 a = nat.forward_obs(env, alive, self.rms, use_norm, o_all[t], on_all[t], snap[t], [y[t] for y in ys_all])
             elif nat is not None:  # one launch; the layers' outputs kept for the reverse
                 env.apg_obs(alive, self.rms, use_norm, o_all[t], on_all[t], snap[t])
@@ -253,6 +279,11 @@ class APGTrainer:
                 a = self.policy(on)
                 leaves.append(on)
             acts.append(a)
+            if fused_next and t + 1 < H:  # the step, slot t, the post-step update and step t + 1's policy
+                a_next = nat.record_next(env, t, a.detach(), gamma, dq, alive, disc, ret, dropped_e, grew_all[t],
+                                         rfin[t], self.rms, use_norm, o_all[t + 1], on_all[t + 1], snap[t + 1],
+                                         [y[t + 1] for y in ys_all], w_t)
+                continue
             if fused_post:  # the step, its tape slot t and the post-step update in one launch
                 env.step_record_apg(t, a.detach(), gamma, dq, alive, disc, ret, dropped_e, grew_all[t], rfin[t])
                 continue
@@ -544,6 +575,12 @@ class HumanoidAPGEnv:
         check(lib().mjl_env_step_record(e.data.handle, int(slot), _ptr(act), _ptr(e.obs), _ptr(e.rew), _ptr(e.term),
                                         _ptr(e.trunc), _stream()))
         return e.obs, e.rew, e.term, e.trunc
+
+    def supports_record_next(self) -> bool:
+        """Whether the record kernel takes the next step's policy forward (mjl_env_step_record_apg_next:
+        the implicit record on the humanoid dims)."""
+        from ._lib import lib
+        return bool(lib().mjl_env_record_fused(self.env.data.handle))
 
     def step_record_apg(self, slot: int, act, gamma, diverge_qvel, alive, disc, ret, dropped, grew, rfin):
         """step_record then apg_post on its outputs, as one launch where the record kernel allows it

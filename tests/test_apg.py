@@ -442,13 +442,17 @@ def test_apg_fused_obs_policy_launches_bit_identical(monkeypatch, graph):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("nxt", ["1", "0"])
 @pytest.mark.parametrize("solver", ["cg44", "model"])
 @pytest.mark.parametrize("graph", [False, True])
-def test_apg_fused_record_post_bit_identical(monkeypatch, graph, solver):
-    """The record + post-step update as one launch (mjl_env_step_record_apg) against the record and
-    mjl_apg_post as two (MJL_APG_FUSED_POST=0): loss, gradient, returns, cut envs and parameters bit for
-    bit over 4 updates, eager and under the update's hipGraph; with a divergence bound low enough that
-    some envs are cut by it."""
+def test_apg_fused_record_post_bit_identical(monkeypatch, graph, solver, nxt):
+    """The record + post-step update as one launch (mjl_env_step_record_apg), with (nxt = "1") the next
+    step's observation + policy forward in it too (mjl_env_step_record_apg_next), against the record,
+    mjl_apg_post and mjl_apg_obs_policy_fwd as separate launches (MJL_APG_FUSED_POST=0): loss, gradient,
+    returns, cut envs and parameters bit for bit over 4 updates (the first without observation
+    normalisation), eager and under the update's hipGraph; with a divergence bound low enough that some
+    envs are cut by it."""
+    monkeypatch.setenv("MJL_APG_FUSED_NEXT", nxt)
     import mjx_amd
     from mjx_amd import mjcf, mjx
     from mjx_amd.config import reference_ppo_config
