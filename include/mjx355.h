@@ -364,6 +364,15 @@ int mjl_env_step_vjp_replay(mjlBatch* batch, int slot, const float* act, const f
                             const float* g_qacc_ws, const float* g_rew, const float* g_aux, float* out_qpos,
                             float* out_qvel, float* out_qacc_ws, float* out_act, float* out_aux,
                             float* nonfinite_count, void* stream);
+/* mjl_env_step_vjp_replay, then mjl_apg_policy_bwd_obs_vjp on its action cotangent, added to its state
+ * cotangents before they are written (the same float operations), in one launch: w, widths, ys, o,
+ * alive_snap, mean, var, use_norm as mjl_apg_policy_bwd_obs_vjp (the policy's output width = nu <= 32). */
+int mjl_env_step_vjp_replay_apg(mjlBatch* batch, int slot, const float* act, const float* g_qpos,
+                                const float* g_qvel, const float* g_qacc_ws, const float* g_rew, const float* g_aux,
+                                float* out_qpos, float* out_qvel, float* out_qacc_ws, float* out_act, float* out_aux,
+                                float* nonfinite_count, int nl, const int* widths, const float* const* w,
+                                float* const* ys, const float* o, const uint8_t* alive_snap, const float* mean,
+                                const float* var, int use_norm, void* stream);
 
 /* APG rollout bookkeeping (train_apg.py:161-209; the sweep of mjx_amd/apg.py), one launch each per
  * rollout step. alive / alive_snap: uint8 [nenv] (0/1); device pointers, float32, row-major.

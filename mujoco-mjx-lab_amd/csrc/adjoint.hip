@@ -1755,6 +1755,7 @@ struct VjpArgs {
   int s_w, s_a, s_r, s_t;
   ApgPostArgs post;  // record: the APG post-step update fused into the launch (post.alive null: none)
   ApgNextArgs next;  // record with post: the next step's observation + policy forward (next.o null: none)
+  ApgPolicyBwd pbwd; // replay (ENV): the policy + observation backward added to the state cotangents (P.nl 0: none)
 };
 
 // record mode's share of WSA: what the forward leaves there for the reverse passes
@@ -2110,9 +2111,11 @@ __global__ __launch_bounds__(64, LEAN ? 2 : 1) void vjp_kernel(KParams P, VjpArg
       return;
     }
   }
-  if (lane < nq) V.o_qpos[(size_t)env * nq + lane] = A->qposb[lane];
-  if (lane < nv) V.o_qvel[(size_t)env * nv + lane] = A->qvelb[lane];
-  if (V.o_ws && lane < nv) V.o_ws[(size_t)env * nv + lane] = A->wsb[lane];
+  // the APG policy's backward rides along (replay, ENV): the action cotangent through the policy and the
+  // observation is added to the state cotangents before they are written (as mjl_apg_policy_bwd_obs_vjp
+  // adds it to them after); the smooth-dynamics scratch (dead after the reverse passes) holds its rows
+  const bool pol = ENV && TM == 2 && V.pbwd.P.nl > 0;
+  LDSA float* gsrc = (LDSA float*)W->cinert;  // [32] action cotangent by action, [2][64] layer rows, [64] obs part
   if (lane < nu) {
     if (ENV) {  // ctrl = clip(flip ? act[perm] * sign : act, -1, 1)
       const mjlEnvConfig* c = P.env;
@@ -2120,11 +2123,58 @@ __global__ __launch_bounds__(64, LEAN ? 2 : 1) void vjp_kernel(KParams P, VjpArg
       const int src = flip ? c->act_perm[lane] : lane;
       const float sg = flip ? (float)c->act_sign[lane] : 1.f;
       const float a = V.act[(size_t)env * nu + src] * sg;
-      V.o_ctrl[(size_t)env * nu + src] = (a > -1.f && a < 1.f) ? sg * A->ctrlb[lane] : 0.f;
+      const float ga = (a > -1.f && a < 1.f) ? sg * A->ctrlb[lane] : 0.f;
+      V.o_ctrl[(size_t)env * nu + src] = ga;
+      if (pol) gsrc[src] = ga;
     } else {
       V.o_ctrl[(size_t)env * nu + lane] = A->ctrlb[lane];
     }
   }
+  float gq_add = 0.f, gv_add = 0.f;
+  if (pol) {  // small_mlp_bwd_input_kernel<true>'s sums, then apg_obs_vjp_kernel's element
+    const ApgPolicyBwd& Q = V.pbwd;
+    static_assert((10 + 10 + 6 + 6) * D::NB >= 32 + 3 * 64, "policy backward scratch (cinert..cacc)");
+    LDSA float* g = gsrc + 32;   // [2][64]
+    LDSA float* ggs = g + 128;   // [64]: the observation's cotangent by input index
+    const int L = Q.P.nl, NL = Q.P.n[L - 1], k0 = Q.P.k0;
+    SYNC();
+    if (lane < NL) {
+      const float y = Q.P.y[L - 1][(size_t)env * NL + lane];
+      g[lane] = gsrc[lane] * (1.f - y * y);
+    }
+    int cur = 0;
+    for (int l = L - 1; l >= 0; l--) {
+      const int N = Q.P.n[l], K = l ? Q.P.n[l - 1] : k0;
+      const float* __restrict__ Wl = Q.P.w[l];
+      SYNC();
+      if (lane < K) {
+        float sacc = 0.f;
+        for (int jj = 0; jj < N; jj++) sacc = fmaf(Wl[jj * K + lane], g[cur * 64 + jj], sacc);
+        if (l) {
+          const float y = Q.P.y[l - 1][(size_t)env * K + lane];
+          g[(cur ^ 1) * 64 + lane] = sacc * (1.f - y * y);
+        } else {
+          float gg = 0.f;
+          if (Q.snap[env]) {
+            gg = sacc;
+            if (Q.use_norm) {
+              const float den = sqrt_rn(Q.var[lane]) + 1e-8f;
+              const float yy = div_rn(Q.o[(size_t)env * K + lane] - Q.mean[lane], den);
+              gg = (yy >= -10.f && yy <= 10.f) ? div_rn(gg, den) : 0.f;
+            }
+          }
+          ggs[lane] = gg;
+        }
+      }
+      cur ^= 1;
+    }
+    SYNC();
+    if (lane < nq) gq_add = ggs[lane];
+    if (lane < nv) gv_add = ggs[nq + lane];
+  }
+  if (lane < nq) V.o_qpos[(size_t)env * nq + lane] = pol ? A->qposb[lane] + gq_add : A->qposb[lane];
+  if (lane < nv) V.o_qvel[(size_t)env * nv + lane] = pol ? A->qvelb[lane] + gv_add : A->qvelb[lane];
+  if (V.o_ws && lane < nv) V.o_ws[(size_t)env * nv + lane] = A->wsb[lane];
   if (ENV && lane < MJL_AUX_DIM) V.o_aux[(size_t)env * MJL_AUX_DIM + lane] = A->auxb[lane];
   }
 }

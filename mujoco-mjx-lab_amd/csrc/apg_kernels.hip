@@ -173,6 +173,15 @@ struct ApgNextArgs {
   uint8_t* snap;
   SmallMlp P;
 };
+// the policy's input backward + the observation's backward (mjl_apg_policy_bwd_obs_vjp's arithmetic) fused
+// into the APG replay's tail (mjl_env_step_vjp_replay_apg): P.w row-major as the torch weights, P.y the
+// step's layer outputs; o / alive_snap the step's observation and flags; P.nl 0: none
+struct ApgPolicyBwd {
+  int use_norm;
+  const float *o, *mean, *var;
+  const uint8_t* snap;
+  SmallMlp P;
+};
 // the observation's backward fused into the policy's input backward (mjl_apg_policy_bwd_obs_vjp):
 // apg_obs_vjp_kernel on the input cotangent where small_mlp_bwd_input_kernel wrote g_x
 struct ObsVjp {

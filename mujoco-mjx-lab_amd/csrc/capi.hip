@@ -1362,6 +1362,38 @@ extern "C" int mjl_env_step_record_apg_next(mjlBatch* B, int slot, const float* 
   return launch_vjp<true, 1>(B, V, stream, &Pk);
 }
 
+// the APG replay with the policy's input backward + the observation's backward added to its state
+// cotangents, in one launch
+extern "C" int mjl_env_step_vjp_replay_apg(mjlBatch* B, int slot, const float* act, const float* g_qpos,
+                                           const float* g_qvel, const float* g_qacc_ws, const float* g_rew,
+                                           const float* g_aux, float* out_qpos, float* out_qvel, float* out_qacc_ws,
+                                           float* out_act, float* out_aux, float* nonfinite_count, int nl,
+                                           const int* widths, const float* const* w, float* const* ys, const float* o,
+                                           const uint8_t* alive_snap, const float* mean, const float* var,
+                                           int use_norm, void* stream) {
+  if (!B || !act || !g_qpos || !g_qvel || !g_rew || !g_aux || !out_qpos || !out_qvel || !out_act || !out_aux || !o ||
+      !alive_snap || !w || !w[0] || (use_norm && (!mean || !var)))
+    return fail(MJL_ERR_ARG, "bad argument");
+  if (!B->has_env) return fail(MJL_ERR_ARG, "mjl_env_config not called");
+  if (!B->d_vtape || slot < 0 || slot >= B->vtape_slots) return fail(MJL_ERR_ARG, "VJP tape slot %d not allocated", slot);
+  const int nq = B->model->desc.nq, nv = B->model->desc.nv;
+  SmallMlp Pm;
+  const float* nob[kSmlMaxL] = {w[0], w[0], w[0], w[0]};  // biases unused by the backward
+  int rc = small_mlp_setup(B->nenv, nq + nv, nl, widths, w, nob, ys, Pm);
+  if (rc != MJL_OK) return rc;
+  if (Pm.n[nl - 1] > 32 || B->model->desc.nu != Pm.n[nl - 1])
+    return fail(MJL_ERR_ARG, "replay_apg: the policy's output width must be the action width (<= 32)");
+  VjpArgs V;
+  std::memset(&V, 0, sizeof(V));
+  V.act = act; V.g_qpos = g_qpos; V.g_qvel = g_qvel; V.g_rew = g_rew; V.g_aux = g_aux;
+  V.o_qpos = out_qpos; V.o_qvel = out_qvel; V.o_ctrl = out_act; V.o_aux = out_aux;
+  V.g_ws = g_qacc_ws; V.o_ws = out_qacc_ws;
+  V.nonfinite = nonfinite_count;
+  V.slot = B->d_vtape + (size_t)slot * B->nenv * (size_t)B->vtape_stride;
+  V.pbwd = ApgPolicyBwd{use_norm, o, mean, var, alive_snap, Pm};
+  return launch_vjp<true, 2>(B, V, stream);
+}
+
 // mjl_small_mlp_bwd_input then mjl_apg_obs_vjp on its g_x, in one launch (k0 = nq + nv; g_x not stored)
 extern "C" int mjl_apg_policy_bwd_obs_vjp(const float* g_out, int nenv, int nq, int nv, int nl, const int* widths,
                                           const float* const* w, const float* const* ys, const float* o,

@@ -28,7 +28,7 @@ EXPORTS = [
     "mjl_policy_param_floats", "mjl_policy_fwd",
     "mjl_step_vjp_full", "mjl_env_step_vjp_full", "mjl_env_fill_reset_pool",
     "mjl_apg_obs", "mjl_apg_post", "mjl_apg_obs_vjp", "mjl_env_step_record", "mjl_env_step_record_apg",
-    "mjl_env_step_record_apg_next", "mjl_env_record_fused", "mjl_env_step_vjp_replay",
+    "mjl_env_step_record_apg_next", "mjl_env_record_fused", "mjl_env_step_vjp_replay", "mjl_env_step_vjp_replay_apg",
     "mjl_ppo_loss_scratch", "mjl_ppo_surrogate", "mjl_mse", "mjl_gather_rows", "mjl_adam",
     "mjl_adam_dev",
     "mjl_colsum_batched_scratch", "mjl_colsum_batched", "mjl_tanh_bwd_colsum_batched", "mjl_slice_sum_batched",
@@ -118,6 +118,7 @@ def lib() -> C.CDLL:
     L.mjl_env_step_record.argtypes = [vp, i32, vp, vp, vp, vp, vp, vp]
     L.mjl_env_step_record_apg.argtypes = [vp, i32, vp, vp, vp, vp, vp, C.c_float, C.c_float] + [vp] * 7
     L.mjl_env_record_fused.argtypes = [vp]
+    L.mjl_env_step_vjp_replay_apg.argtypes = [vp, i32] + [vp] * 12 + [i32, vp, vp, vp, vp, vp, vp, vp, i32, vp]
     L.mjl_env_step_record_apg_next.argtypes = ([vp, i32, vp, vp, vp, vp, vp, C.c_float, C.c_float] + [vp] * 8 +
                                                [i32, vp, vp, vp, i32, vp, vp, vp, vp, vp])
     L.mjl_env_step_vjp_replay.argtypes = [vp, i32] + [vp] * 12 + [vp]

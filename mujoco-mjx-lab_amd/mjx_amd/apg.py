@@ -109,6 +109,27 @@ class NativeAPGPolicy:
             self._ptrs(w_t), self._ptrs([b for _, b in self.params]), self._ptrs(ys), _stream()))
         return ys[-1]
 
+    def replay_bwd(self, env, slot, act, gq, gv, gws, grew, gaux, nonfinite, ys, o, snap, rms, use_norm):
+        """HumanoidAPGEnv.step_vjp_replay, then backward_obs_vjp on its action cotangent, as one launch
+        (mjl_env_step_vjp_replay_apg): returns the replay's (gq, gv, gws, ga, gaux) with the policy's
+        observation path added to gq / gv."""
+        from . import abi
+        from ._lib import check, lib
+        from .mjx import _ptr, _stream
+        B, dev = env.num_envs, env.env.obs.device
+        f = lambda x, *shape: x.to(dev, torch.float32).reshape(B, *shape).contiguous()  # noqa: E731
+        act, gq, gv, gr = f(act, env.act_dim), f(gq, env.nq), f(gv, env.nv), f(grew)
+        ga = torch.zeros((B, abi.AUX_DIM), device=dev) if gaux is None else f(gaux, abi.AUX_DIM)
+        gw = None if gws is None else f(gws, env.nv)
+        oq, ov, oa, oaux = torch.empty_like(gq), torch.empty_like(gv), torch.empty_like(act), torch.empty_like(ga)
+        ow = None if gws is None else torch.empty_like(gw)
+        check(lib().mjl_env_step_vjp_replay_apg(
+            env.env.data.handle, int(slot), _ptr(act), _ptr(gq), _ptr(gv), _ptr(gw), _ptr(gr), _ptr(ga), _ptr(oq),
+            _ptr(ov), _ptr(ow), _ptr(oa), _ptr(oaux), _ptr(nonfinite), len(self.widths), self._widths,
+            self._ptrs([w for w, _ in self.params]), self._ptrs(ys), _ptr(o), _u8(snap), _ptr(rms.mean),
+            _ptr(rms.var), int(use_norm), _stream()))
+        return oq, ov, ow, oa, oaux
+
     def backward_obs_vjp(self, env, g_out, ys, o, snap, rms, use_norm, gq, gv):
         """backward_input(g_out, ys), then HumanoidAPGEnv.apg_obs_vjp on its result, as one launch
         (mjl_apg_policy_bwd_obs_vjp): gq / gv accumulate the observation's cotangent."""
@@ -301,7 +322,18 @@ class APGTrainer:
         nonfinite = torch.zeros(1, device=dev)
         gws = torch.zeros((B, env.nv), device=dev) if getattr(env, "vjp_carries_ws", False) else None
         gas = [None] * H
+        # the policy + observation backward in the replay launch (MJL_APG_FUSED_BWD=0: their own launch)
+        fused_bwd = taped and fused and os.environ.get("MJL_APG_FUSED_BWD", "1") != "0"
         for t in range(H - 1, -1, -1):
+            if fused_bwd:  # slot t's reverse passes, then the policy's and the observation's backward
+                gq, gv, gws, ga, gaux = nat.replay_bwd(env, t, acts[t].detach(), gq, gv, gws, grew_all[t], gaux,
+                                                       nonfinite, [y[t] for y in ys_all], o_all[t], snap[t], self.rms,
+                                                       use_norm)
+                gas[t] = ga
+                if self.diag is not None and not graph:
+                    e = (ga.double() ** 2).sum(1)
+                    self.diag["ga_sq"] = e if t == H - 1 else self.diag["ga_sq"] + e
+                continue
             if taped:  # the reverse passes from slot t: no state restore, no recompute
                 gq, gv, gws, ga, gaux = env.step_vjp_replay(t, acts[t].detach(), gq, gv, gws, grew_all[t], gaux,
                                                             nonfinite)

@@ -443,12 +443,14 @@ def test_apg_fused_obs_policy_launches_bit_identical(monkeypatch, graph):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("nxt", ["1", "0"])
-@pytest.mark.parametrize("solver", ["cg44", "model"])
+@pytest.mark.parametrize("solver,vjp", [("cg44", "implicit"), ("model", "implicit"), ("cg44", "unrolled")])
 @pytest.mark.parametrize("graph", [False, True])
-def test_apg_fused_record_post_bit_identical(monkeypatch, graph, solver, nxt):
+def test_apg_fused_record_post_bit_identical(monkeypatch, graph, solver, vjp, nxt):
     """The record + post-step update as one launch (mjl_env_step_record_apg), with (nxt = "1") the next
-    step's observation + policy forward in it too (mjl_env_step_record_apg_next), against the record,
-    mjl_apg_post and mjl_apg_obs_policy_fwd as separate launches (MJL_APG_FUSED_POST=0): loss, gradient,
+    step's observation + policy forward in it too (mjl_env_step_record_apg_next) and the policy +
+    observation backward in the replay (mjl_env_step_vjp_replay_apg), against the record, mjl_apg_post,
+    mjl_apg_obs_policy_fwd and mjl_apg_policy_bwd_obs_vjp as separate launches (MJL_APG_FUSED_POST=0 and
+    MJL_APG_FUSED_BWD=0 on the second trainer): loss, gradient,
     returns, cut envs and parameters bit for bit over 4 updates (the first without observation
     normalisation), eager and under the update's hipGraph; with a divergence bound low enough that some
     envs are cut by it."""
@@ -463,7 +465,7 @@ def test_apg_fused_record_post_bit_identical(monkeypatch, graph, solver, nxt):
     ecfg = resolve_ids(m, reference_ppo_config().env_config)
     cfg = _cfg(batch_size=100, horizon=8, hidden_size=32)
     cfg.diverge_qvel = 5.0
-    envs = [apg.HumanoidAPGEnv(HumanoidEnv(mjx.put_model(m), ecfg, cfg.batch_size, seed=5), "implicit")
+    envs = [apg.HumanoidAPGEnv(HumanoidEnv(mjx.put_model(m), ecfg, cfg.batch_size, seed=5), vjp)
             for _ in range(2)]
     trs = [apg.APGTrainer(cfg, e, device="cuda", use_graph=graph) for e in envs]
     cut = 0.0
@@ -471,6 +473,7 @@ def test_apg_fused_record_post_bit_identical(monkeypatch, graph, solver, nxt):
         ms = []
         for tr, fused in zip(trs, ("1", "0")):
             monkeypatch.setenv("MJL_APG_FUSED_POST", fused)
+            monkeypatch.setenv("MJL_APG_FUSED_BWD", nxt if fused == "1" else "0")
             ms.append(tr.update(step))
         for k in ("loss", "grad_norm", "mean_reward", "return", "nonfinite_envs"):
             assert ms[0][k] == ms[1][k], f"update {step}: {k}"
