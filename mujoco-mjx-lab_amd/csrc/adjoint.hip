@@ -2199,7 +2199,11 @@ template <class DL, int MW> NOINL void record_rows_global(MP m, LDSA WS<DL>* W, 
   solver_hessian<DL, true>(m, W, R, lane);  // Hc at the converged active set, into H
 }
 
-template <class DL, class DI> __global__ __launch_bounds__(64, 2) void vjp_record_kernel(KParams P, VjpArgs V) {
+// UNR: the unrolled VJP's record (MJL_OPT_VJP_UNROLLED): the solve taped as vjp_kernel's record tapes it
+// (SolveTape into slot + s_t, row accumulators in V.unr), chol(M) in the A part for CG (the reverse sweep's
+// preconditioner) in place of the factor of Hc, which it does not use.
+template <class DL, class DI, bool UNR = false>
+__global__ __launch_bounds__(64, 2) void vjp_record_kernel(KParams P, VjpArgs V) {
   constexpr int LD = DL::LD, NV = DL::NV;
   static_assert(LD == DI::LD && NV == DI::NV, "the tape image's dims are the workspace's, rows aside");
   static_assert(offsetof(WS<DL>, cinert) == offsetof(WS<DI>, cinert) && offsetof(WS<DI>, cinert) % 16 == 0,
@@ -2268,6 +2272,18 @@ template <class DL, class DI> __global__ __launch_bounds__(64, 2) void vjp_recor
     if (lane < LD) W->qacc_smooth[lane] = (lane < nv) ? x : 0.f;
     SYNC();
   }
+  SolveTape tp;  // (UNR)
+  if constexpr (UNR) {
+    tp.t = slot + V.s_t;
+    tp.acc = (GLBA float*)(V.unr + (size_t)env * V.td.stride) + V.td.tape;
+    tp.d = V.td;
+    tp.nup = tp.nls = tp.nsets = tp.overflow = 0;
+    // the A part's 1/diag and factor: chol(M) for CG (vjp_kernel's A->Lc / invdc), zero otherwise
+    constexpr int O4 = O3 + LD, O5 = O4 + LD;
+    const bool cg = m->solver != MJL_SOLVER_NEWTON;
+    for (int i = lane; i < NV * LD; i += 64) sa[O5 + i] = cg ? W->H[i] : 0.f;
+    for (int i = lane; i < LD; i += 64) sa[O4 + i] = cg ? W->invd[i] : 0.f;
+  }
   GLBA f32x4* img = (GLBA f32x4*)(slot + V.s_w);
   {  // the image's union: the smooth-dynamics scratch, before the rows take its place
     const LDSA f32x4* src = (const LDSA f32x4*)W;
@@ -2276,7 +2292,13 @@ template <class DL, class DI> __global__ __launch_bounds__(64, 2) void vjp_recor
   float* rows = (float*)(slot + V.s_r);
   if (build_rows<DL, false>(m, W, lds_rows<DL>(W), lane)) {
     const Rows<false> R = lds_rows<DL>(W);
-    solver<DL, false>(m, W, R, lane);
+    if constexpr (UNR) {
+      solver_t<DL, false>(m, W, R, lane, tp);  // the same solve, recording its tape
+      tp.finish(lane);
+      SYNC();
+    } else {
+      solver<DL, false>(m, W, R, lane);
+    }
     sensors<DL, false>(m, W, R, lane);
     {  // the rows into the slot's global layout (what vjp_kernel's record leaves there)
       const Rows<true> G = global_rows<DL>(rows, P.gmax_efc, P.gmax_con);
@@ -2289,20 +2311,31 @@ template <class DL, class DI> __global__ __launch_bounds__(64, 2) void vjp_recor
       for (int i = lane; i < ncon * CONW; i += 64) G.con[i] = R.con[i];
       for (int i = lane; i < ncon; i += 64) { G.con_pair[i] = R.con_pair[i]; G.con_efc[i] = R.con_efc[i]; }
     }
-    solver_hessian<DL, false>(m, W, R, lane);  // Hc at the converged active set, into H
+    if constexpr (!UNR) solver_hessian<DL, false>(m, W, R, lane);  // Hc at the converged active set, into H
+  } else if constexpr (UNR) {
+    const Rows<true> R = global_rows<DL>(rows, P.gmax_efc, P.gmax_con);
+    build_rows<DL, true>(m, W, R, lane);
+    solver_t<DL, true>(m, W, R, lane, tp);
+    tp.finish(lane);
+    SYNC();
+    sensors<DL, true>(m, W, R, lane);
   } else {
     record_rows_global<DL, 2>(m, W, rows, P.gmax_efc, P.gmax_con, lane);
   }
   // a', 1/diag and the factor of Hc in the row area (free now), zeroed as vjp_kernel's A part is
+  // (UNR: a' only; 1/diag and the factor went to the slot above)
+  constexpr int NAB = UNR ? LD : 2 * LD + NV * LD;
   LDSA float* ab = (LDSA float*)W->J;
-  for (int i = lane; i < 2 * LD + NV * LD; i += 64) ab[i] = 0.f;
+  for (int i = lane; i < NAB; i += 64) ab[i] = 0.f;
   SYNC();
-  chol_factor_solve<DL>(W->H, ab + 2 * LD, ab + LD, nv, W->frc_smooth, lane);
-  SYNC();
+  if constexpr (!UNR) {
+    chol_factor_solve<DL>(W->H, ab + 2 * LD, ab + LD, nv, W->frc_smooth, lane);
+    SYNC();
+  }
   integrate<DL>(m, W, lane, ab);
   STAMP(1, lane);
   SYNC();
-  for (int i = lane; i < 2 * LD + NV * LD; i += 64) sa[O3 + i] = ab[i];
+  for (int i = lane; i < NAB; i += 64) sa[O3 + i] = ab[i];
   {  // the rest of the image: the workspace up to the union
     const LDSA f32x4* src = (const LDSA f32x4*)W;
     for (int i = lane; i < U0; i += 64) img[i] = src[i];

@@ -827,8 +827,11 @@ template <bool ENV, int TM = 0> static int launch_vjp(mjlBatch* B, const VjpArgs
   // the implicit record on the humanoid dims keeps its rows in LDS (vjp_record_kernel, the same slot as
   // vjp_kernel's record); MJL_OPT_FORCE_GLOBAL_ROWS keeps the global-row record (A/B, parity tests)
   if constexpr (TM == 1 && ENV) {
-    if (B->model->nvc == 0 && !B->vjp_unrolled && !B->force_global_rows) {
-      hipLaunchKernelGGL((vjp_record_kernel<DHum, DHumV>), grid, block, 0, (hipStream_t)stream, P, V);
+    if (B->model->nvc == 0 && !B->force_global_rows) {
+      if (B->vjp_unrolled)
+        hipLaunchKernelGGL((vjp_record_kernel<DHum, DHumV, true>), grid, block, 0, (hipStream_t)stream, P, V);
+      else
+        hipLaunchKernelGGL((vjp_record_kernel<DHum, DHumV>), grid, block, 0, (hipStream_t)stream, P, V);
       HIPCHK(hipGetLastError());
       return MJL_OK;
     }
@@ -1329,9 +1332,9 @@ extern "C" int mjl_apg_obs_policy_fwd(mjlBatch* B, const uint8_t* alive, const f
 }
 
 // 1 if this batch's record launch is vjp_record_kernel (the rows in LDS; the post-step update and the next
-// step's policy forward can ride along): the humanoid dims, the implicit VJP, rows not forced global
+// step's policy forward can ride along): the humanoid dims, rows not forced global
 extern "C" int mjl_env_record_fused(const mjlBatch* B) {
-  return B && B->model->nvc == 0 && !B->vjp_unrolled && !B->force_global_rows ? 1 : 0;
+  return B && B->model->nvc == 0 && !B->force_global_rows ? 1 : 0;
 }
 
 // the APG record + post-step update + the next step's observation and policy forward, in one launch
@@ -1345,8 +1348,7 @@ extern "C" int mjl_env_step_record_apg_next(mjlBatch* B, int slot, const float* 
     return fail(MJL_ERR_ARG, "bad argument");
   if (!B->has_env) return fail(MJL_ERR_ARG, "mjl_env_config not called");
   if (!B->d_vtape || slot < 0 || slot >= B->vtape_slots) return fail(MJL_ERR_ARG, "VJP tape slot %d not allocated", slot);
-  if (!(B->model->nvc == 0 && !B->vjp_unrolled && !B->force_global_rows))
-    return fail(MJL_ERR_UNSUPPORTED, "record_apg_next: the fused record (implicit VJP, humanoid dims) only");
+  if (!mjl_env_record_fused(B)) return fail(MJL_ERR_UNSUPPORTED, "record_apg_next: the humanoid dims' record only");
   const int nq = B->model->desc.nq, nv = B->model->desc.nv;
   SmallMlp P;
   int rc = small_mlp_setup(B->nenv, nq + nv, nl, widths, w_t, b, ys, P, true);

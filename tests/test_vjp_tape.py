@@ -78,15 +78,15 @@ def test_tape_slot_bounds():
         env.step_record(2, a)
 
 
-@pytest.mark.parametrize("solver", ["cg44", "model"])
-def test_lds_row_record_equals_global_row_record(solver):
+@pytest.mark.parametrize("solver,vjp", [("cg44", "implicit"), ("model", "implicit"), ("cg44", "unrolled")])
+def test_lds_row_record_equals_global_row_record(solver, vjp):
     """The implicit record keeps its constraint rows in LDS (vjp_record_kernel) and writes the tape
     slot vjp_kernel's global-row record writes (MJL_OPT_FORCE_GLOBAL_ROWS selects that one): over 8
     steps, with env 0 posed past every hinge limit and into the floor (more rows than the LDS holds:
     the record's global fallback), the step outputs, the state and every replayed cotangent agree
     bit for bit (CG 4/4 drives that pose to NaN within a few steps in both: NaN equals NaN here)."""
     same = lambda x, y: torch.testing.assert_close(x, y, rtol=0, atol=0, equal_nan=True) is None
-    m, (lds, glb) = _pair(solver, "implicit", B=32)
+    m, (lds, glb) = _pair(solver, vjp, B=32)
     glb.env.data.set_option(abi.OPT_FORCE_GLOBAL_ROWS, 1)
     B, H = lds.num_envs, 8
     q = m.key_qpos[m.names["key"].index("supine")].copy()
@@ -121,8 +121,9 @@ def test_lds_row_record_equals_global_row_record(solver):
         gv = torch.randn((B, m.nv), generator=g, device="cuda")
         gr = torch.randn(B, generator=g, device="cuda")
         gx = torch.randn((B, abi.AUX_DIM), generator=g, device="cuda")
-        r1 = lds.step_vjp_replay(t, acts[t], gq, gv, None, gr, gx)
-        r2 = glb.step_vjp_replay(t, acts[t], gq, gv, None, gr, gx)
+        gw = torch.randn((B, m.nv), generator=g, device="cuda") if vjp == "unrolled" else None
+        r1 = lds.step_vjp_replay(t, acts[t], gq, gv, gw, gr, gx)
+        r2 = glb.step_vjp_replay(t, acts[t], gq, gv, gw, gr, gx)
         for x, y, k in zip(r1, r2, ("qpos", "qvel", "ws", "act", "aux")):
             if x is None:
                 assert y is None
