@@ -565,14 +565,22 @@ INL void adj_solver_unrolled(MP m, LDSA WT* W, LDSA AT* A, const MT& mt, Rows<tr
     const uint32_t w = __float_as_uint(mk[2 * (r >> 6) + ((r >> 5) & 1)]);
     return (w >> (r & 31)) & 1u;
   };
-  // J-bar rows += ca (x) va + cb (x) vb (ca, cb per row in scratch; va, vb in LDS); four rows per
-  // step with every load issued before the stores (a loop of single global read-modify-writes
-  // waited for each one)
+  // J-bar rows += ca (x) va + cb (x) vb (ca, cb per row in scratch; va, vb in LDS); JB rows per step
+  // with every load issued before the stores: each step is one global round trip (4 rows per step:
+  // 32-row sweeps waited 8; single read-modify-writes waited for each one)
+  constexpr int JB = 16;
   auto jbar_add = [&](LDSA const float* va, LDSA const float* vb) {
     SYNC();
     if (isd) {
       const float a = va[lane], b = vb[lane];
       int r = 0;
+      for (; r + JB <= nefc; r += JB) {
+        float c0[JB], c1[JB], jb[JB];
+#pragma unroll
+        for (int e = 0; e < JB; e++) { c0[e] = ca[r + e]; c1[e] = cb[r + e]; jb[e] = Jbar[(r + e) * LD + lane]; }
+#pragma unroll
+        for (int e = 0; e < JB; e++) Jbar[(r + e) * LD + lane] = jb[e] + (c0[e] * a + c1[e] * b);
+      }
       for (; r + 4 <= nefc; r += 4) {
         float c0[4], c1[4], jb[4];
 #pragma unroll
@@ -583,10 +591,17 @@ INL void adj_solver_unrolled(MP m, LDSA WT* W, LDSA AT* A, const MT& mt, Rows<tr
       for (; r < nefc; r++) Jbar[r * LD + lane] += ca[r] * a + cb[r] * b;
     }
   };
-  auto jt = [&](GLBA const float* c) -> float {  // (J' c)[lane], four rows' loads per step
+  auto jt = [&](GLBA const float* c) -> float {  // (J' c)[lane] in row order, JB rows' loads per step
     float x = 0.f;
     if (isd) {
       int r = 0;
+      for (; r + JB <= nefc; r += JB) {
+        float jv[JB], cv[JB];
+#pragma unroll
+        for (int e = 0; e < JB; e++) { jv[e] = R.J[(r + e) * LD + lane]; cv[e] = c[r + e]; }
+#pragma unroll
+        for (int e = 0; e < JB; e++) x += jv[e] * cv[e];
+      }
       for (; r + 4 <= nefc; r += 4) {
         float jv[4], cv[4];
 #pragma unroll
