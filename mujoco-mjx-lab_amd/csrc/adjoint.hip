@@ -1333,7 +1333,7 @@ INL void adj_mass(MP m, LDSA WT* W, LDSA AT* A, const MT& mt, bool unr, int lane
     // every dof in ascending order, the sum taking the descendants (the mask's bit loop, unrolled:
     // a root dof has all nv as descendants, and the loop waited for each iteration's LDS reads)
     float cb[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-#pragma unroll 9
+#pragma unroll  // (fully: 98.6 against 99.7 us per replay unrolled by 9)
     for (int ii = 0; ii < D::NV; ii++) {
       const bool in = (descm >> ii) & 1u;
       const float a = mbar(ii, j), c = mbar(j, ii);
