@@ -68,3 +68,18 @@ def test_batch_create_rejects_empty_and_null_without_gpu():
         assert b"bad argument" in L.mjl_last_error()
     assert L.mjl_batch_create(None, 4, 0, C.byref(b)) == 1
     L.mjl_model_destroy(h)
+
+
+def test_fused_apg_entries_reject_null_without_gpu():
+    """The fused APG entry points (record + bookkeeping + next policy, replay + policy backward) report a
+    null batch or a null buffer as an argument error before any device call; the eligibility query says
+    0 for a null batch."""
+    L = _lib.lib()
+    assert L.mjl_env_record_fused(None) == 0
+    z = [None] * 7
+    assert L.mjl_env_step_record_apg(None, 0, None, None, None, None, None, 0.99, 0.0, *z) == 1
+    assert b"bad argument" in L.mjl_last_error()
+    assert L.mjl_env_step_record_apg_next(None, 0, None, None, None, None, None, 0.99, 0.0, *([None] * 8), 0, None,
+                                          None, None, 1, None, None, None, None, None) == 1
+    assert L.mjl_env_step_vjp_replay_apg(None, 0, *([None] * 12), 1, None, None, None, None, None, None, None, 0,
+                                         None) == 1
